@@ -1,0 +1,196 @@
+"""Benchmark: LiDAR scans/s registered (C2: ~64k-point VLP-16 scan vs 1M-point feature map).
+
+One step = one pass of the hot path over one batch of B synthetic scans per GPU: LOAM feature
+extraction from the raw scans + scan-to-map registration (5 outer iterations of 5-NN matching,
+line/plane fits and a 4-iteration Ceres-equivalent LM), followed by the RCCL all-gather of the
+resulting 6-DoF poses across ranks (multi-GPU only).  Inputs (raw scans, map index) are resident
+in HBM before the timed region.  Weak scaling: B scans per GPU.
+
+Usage: python bench.py [--gpus N --steps K --warmup W --batch B]
+       (N > 1 is launched by torch.distributed.run, one rank per GPU).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "lmsf-slam_amd"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=32, help="scans per GPU per step")
+    ap.add_argument("--unique-scans", type=int, default=8, help="distinct synthetic scans per rank")
+    ap.add_argument("--map-points", type=int, default=1_000_000)
+    ap.add_argument("--cols", type=int, default=4096)
+    ap.add_argument("--outer", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "knn_traffic.json"),
+                    help="per-launch HBM bytes of the neighbour-search kernel from rocprofv3 PMC runs")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local)
+
+    from lmsf import _lib, synth
+
+    # ---------------- workload (C2), deterministic per rank: rank r registers its own scans
+    U = max(1, min(args.unique_scans, args.batch))
+    cfgc = synth.CONFIGS["C2"]
+    scene = synth.make_scene(1000 + cfgc["k"], road_length=80.0)
+    truth_u = synth.trajectory(U * world, 3000 + cfgc["k"], step=80.0 / max(U * world, 1))[rank * U:(rank + 1) * U]
+    scans_u = [synth.make_scan(scene, truth_u[i], 2000 + cfgc["k"] + 97 * (rank * U + i), n_cols=args.cols)
+               for i in range(U)]
+    edge_map, surf_map = synth.make_map(scene, args.map_points, 1000 + cfgc["k"] + 7, center_x=(0.0, 80.0),
+                                        radius=cfgc["radius"])
+    rng = np.random.default_rng(3000 + cfgc["k"] + rank)
+    slot_scan = [i % U for i in range(args.batch)]
+    guesses = np.stack([synth.perturb(truth_u[slot_scan[i]], rng) for i in range(args.batch)])
+    max_pts = max(len(s) for s in scans_u)
+
+    ctx = _lib.Context(device=local, max_batch=args.batch, max_scan_points=max_pts + 64,
+                       max_features=max_pts + 64, schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer)
+    ctx.set_map(_lib.EDGE, edge_map)
+    ctx.set_map(_lib.SURF, surf_map)
+    ctx.load_scans([scans_u[slot_scan[i]] for i in range(args.batch)])
+
+    gathered = torch.zeros((world, args.batch, 7), dtype=torch.float64, device=dev)
+
+    def step():
+        ctx.batch_launch(guesses)
+        poses, stats = ctx.batch_wait(args.batch)
+        if world > 1:
+            local_t = torch.from_numpy(poses).to(dev, non_blocking=True)
+            dist.all_gather_into_tensor(gathered, local_t.unsqueeze(0))
+        return poses, stats
+
+    for _ in range(args.warmup):
+        step()
+    ctx.kernel_stats_reset(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        poses, stats = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ks = ctx.kernel_stats()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    scans_total = args.batch * args.steps * world
+    value = scans_total / elapsed
+    # accuracy of the batch vs ground truth (sanity: registration converged)
+    terr = [synth.pose_delta(poses[i], truth_u[slot_scan[i]]) for i in range(args.batch)]
+
+    # ---------------- roofline of the neighbour-search kernel (SURVEY.md §8(d) algorithmic bytes)
+    # B_search = sum_q [16 (query float4) + 27*8 (cell ranges) + 16 * n27(q)]
+    alg_bytes = ks.queries * (16 + 27 * 8) + 16 * ks.n27_sum
+    avg_launch_ms = ks.total_ms / max(ks.launches, 1)
+    bytes_per_launch = alg_bytes / max(ks.launches, 1)
+    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if int(tj.get("batch", -1)) == args.batch and int(tj.get("map_points", -1)) == args.map_points:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "knn_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
+                "alg_bytes_per_launch": int(bytes_per_launch), "launches": int(ks.launches),
+                "queries_per_launch": int(ks.queries / max(ks.launches, 1)),
+                "mean_n27": round(ks.n27_sum / max(ks.queries, 1), 1)}
+
+    # ---------------- CPU baseline + pose delta vs CPU (rank 0, N = 1 only)
+    cpu = None
+    pose_dv = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle
+        oracle.set_threads(1)
+        reg = oracle.Registration()
+        reg.set_map(1, edge_map)
+        reg.set_map(2, surf_map)
+        reg.set_fixed_schedule(True)
+        reg.set_max_iterations(args.outer)
+        n_done, worst_t, worst_r = 0, 0.0, 0.0
+        t1 = time.perf_counter()
+        while n_done < args.batch and (n_done == 0 or time.perf_counter() - t1 < args.cpu_seconds):
+            e, s, _, _ = oracle.extract(scans_u[slot_scan[n_done]])
+            reg.set_scan(1, e)
+            reg.set_scan(2, s)
+            ox, _, _ = reg.solve(guesses[n_done])
+            dt, dr = synth.pose_delta(ox, poses[n_done])
+            worst_t, worst_r = max(worst_t, dt), max(worst_r, dr)
+            n_done += 1
+        cpu_el = time.perf_counter() - t1
+        cpu = {"value": round(n_done / cpu_el, 3), "unit": "scans/s", "cores": 1, "kind": "port",
+               "sample": f"{n_done} scans of the same C2 batch (extract + {args.outer} outer iterations, "
+                         f"kd-tree 5-NN, Ceres-LM restatement), {cpu_el:.1f} s on 1 thread of "
+                         f"{os.cpu_count()} host cores"}
+        pose_dv = {"scans": n_done, "max_m": worst_t, "max_rad": worst_r}
+
+    if rank == 0:
+        line = {
+            "metric": "LiDAR scans/sec registered (64k-pt scan, 1M-pt map)",
+            "value": round(value, 2),
+            "unit": "scans/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"C2: VLP-16 16x{args.cols} scans (~{int(np.mean([len(s) for s in scans_u]))} pts) "
+                                   f"vs {args.map_points}-pt edge+surf map, {args.outer} outer iters x Ceres-LM(4), "
+                                   f"extraction included, batch {args.batch} scans/GPU ({U} distinct)",
+                       "batch_per_gpu": args.batch, "map_points": args.map_points, "outer_iterations": args.outer,
+                       "parallelism": f"scan-sharded x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "pose_delta_vs_cpu": pose_dv,
+            "pose_error_vs_truth": {"max_m": max(t for t, _ in terr), "max_rad": max(r for _, r in terr)},
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,176 @@
+/*
+ * lmsf.h -- C ABI of the MI355X-native LOAM edge/surface registration hot path.
+ *
+ * Drop-in boundary for LMSF-Slam's feature-based registration plugin
+ * (selection string "feature_based", INC/factory/System/ML_SystemFactory.hpp:179-198;
+ * INC = src/MultiSensorFusionEstimator3D/include, REG = INC/Algorithm/PointClouds/registration,
+ * FX = INC/Algorithm/PointClouds/processing/FeatureExtract).  Every entry point below names the
+ * reference interface it replaces.  Plain pointers and sizes only; no exceptions cross the ABI;
+ * every call returns an lmsf_status (0 ok, < 0 error, message in lmsf_last_error()).
+ *
+ * Threading: a context is used by one host thread at a time and owns one HIP stream on one
+ * device; distinct contexts may run concurrently (same rule as the reference, where each
+ * tracker owns its registration object: INC/System/ML_System.hpp:248-264).
+ * Ownership: the library copies every input into device buffers it owns; no caller pointer is
+ * retained after a call returns.
+ */
+#ifndef LMSF_LMSF_H_
+#define LMSF_LMSF_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t lmsf_status;
+#define LMSF_OK 0
+#define LMSF_ERR_ARG (-1)       /* bad argument / null pointer */
+#define LMSF_ERR_HIP (-2)       /* HIP runtime failure (device missing, OOM, launch error) */
+#define LMSF_ERR_NO_MAP (-3)    /* solve before any map was set */
+#define LMSF_ERR_CAPACITY (-4)  /* input larger than the context was created for */
+#define LMSF_ERR_STATE (-5)     /* call out of order (e.g. copy features before extraction) */
+
+/* feature cloud names of the reference: "loam_edge" / "loam_surf" (FX:124-125) */
+#define LMSF_EDGE 1
+#define LMSF_SURF 2
+
+#define LMSF_SOLVER_CERES_LM 0  /* CeresEdgeSurfFeatureRegistration (REG/ceres_edgeSurfFeatureRegistration.hpp) */
+#define LMSF_SOLVER_GN 1        /* EdgeSurfFeatureRegistration, GN mode (REG/edgeSurfFeatureRegistration.hpp) */
+
+#define LMSF_SCHEDULE_REFERENCE_DECAY 0 /* optimization_count_ 10 -> 9, 8, ... 2 (ceres_...:100-101) */
+#define LMSF_SCHEDULE_FIXED 1           /* exactly max_iterations outer iterations per solve */
+
+/* termination of the last inner solve (Ceres TerminationType / GN convergence) */
+#define LMSF_TERM_MAX_ITERATIONS 0
+#define LMSF_TERM_FUNCTION_TOL 1
+#define LMSF_TERM_PARAMETER_TOL 2
+#define LMSF_TERM_GRADIENT_TOL 3
+#define LMSF_TERM_NO_RESIDUALS 4
+#define LMSF_TERM_GN_CONVERGED 5
+#define LMSF_TERM_GN_TOO_FEW 6
+
+typedef struct {
+    int32_t device;            /* HIP device ordinal */
+    int32_t solver;            /* LMSF_SOLVER_* */
+    int32_t schedule;          /* LMSF_SCHEDULE_* */
+    int32_t max_iterations;    /* initial optimization_count_ (10: ceres_...:46) */
+    int32_t max_batch;         /* registrations processed together by lmsf_batch_run */
+    int32_t max_scan_points;   /* raw points per scan (capacity) */
+    int32_t max_features;      /* edge + surf features per scan (capacity) */
+    /* LOAMFeatureProcessorBase(N_SCANS, min_distance, max_distance, edge_thresh, voxel, RemovalBadPoints)
+       (FX:36-50); the factory uses (16, 2, 80) (ML_SystemFactory.hpp:196-197). */
+    int32_t n_scans;
+    float min_distance;
+    float max_distance;
+    float edge_threshold;
+    int32_t remove_bad_points;
+    /* build-defined uniform beam model for N_SCANS not in {16, 32, 64} (0 spacing: reference
+       behaviour, every point in ring 0, FX:337-341) */
+    double beam_lo_deg;
+    double beam_spacing_deg;
+} lmsf_config;
+
+/* One correspondence (64 bytes).  kind 0: none, 1: edge (v0 = a, v1 = b: the two line points of
+ * EdgeFeatureMatch.hpp:72-73), 2: surf (v0 = unit normal, v1[0] = D: surfFeatureMatch.hpp:76-82).
+ * p is the feature in the lidar frame (the factor's curr_point, ceres_...:148-150). */
+typedef struct {
+    float px, py, pz;
+    int32_t kind;
+    double v0[3];
+    double v1[3];
+} lmsf_record;
+
+typedef struct {
+    int32_t outer_iterations;
+    int32_t edge_matches;      /* of the last outer iteration */
+    int32_t surf_matches;
+    int32_t inner_iterations;  /* summed over outer iterations */
+    int32_t evaluations;       /* residual passes summed over outer iterations */
+    int32_t termination;       /* LMSF_TERM_* of the last outer iteration */
+    double initial_cost;       /* of the last outer iteration */
+    double final_cost;
+} lmsf_solve_stats;
+
+typedef struct {
+    int64_t n_edge;
+    int64_t n_surf;
+} lmsf_feature_counts;
+
+typedef struct lmsf_ctx lmsf_ctx;
+
+/* Defaults: device 0, Ceres-LM, reference decay, 10 iterations, batch 1, VLP-16 (16, 2, 80, 1, true). */
+lmsf_status lmsf_config_init(lmsf_config* cfg);
+
+/* Registration object construction: CeresEdgeSurfFeatureRegistration("loam_edge", "loam_surf")
+ * (REG/ceres_edgeSurfFeatureRegistration.hpp:45-49) + LOAMFeatureProcessorBase ctor (FX:36-50). */
+lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out);
+void lmsf_ctx_destroy(lmsf_ctx* ctx);
+const char* lmsf_last_error(const lmsf_ctx* ctx);
+
+/* RegistrationBase::SetInputSource (REG/registration_base.hpp:31; ceres_...:56-71): set the local
+ * feature map of one kind and build its device neighbour index.  n == 0 keeps the previous map
+ * (ceres_...:60). */
+lmsf_status lmsf_set_map(lmsf_ctx* ctx, int32_t kind, const float* xyzi, size_t n);
+
+/* RegistrationBase::SetInputTarget (REG/registration_base.hpp:32; ceres_...:73-84): set the
+ * current scan's features of one kind (host arrays, copied to the device). */
+lmsf_status lmsf_set_scan(lmsf_ctx* ctx, int32_t kind, const float* xyzi, size_t n);
+
+/* SetMaxIteration (ceres_...:86-89). */
+lmsf_status lmsf_set_max_iterations(lmsf_ctx* ctx, int32_t n);
+
+/* RegistrationBase::Solve (REG/registration_base.hpp:33; ceres_...:96-130).  pose: qx qy qz qw tx
+ * ty tz (Eigen storage order of ceres_...:38-40); in = predicted map<-lidar pose, out = refined. */
+lmsf_status lmsf_solve(lmsf_ctx* ctx, double pose[7], lmsf_solve_stats* stats);
+/* Pose after every outer iteration of the last lmsf_solve (rows of 7 doubles); *n_out = rows. */
+lmsf_status lmsf_solve_trace(lmsf_ctx* ctx, double* trace, int32_t cap, int32_t* n_out);
+
+/* PointCloudProcessBase::Process (INC/Algorithm/PointClouds/processing/process_base.hpp:26-39),
+ * LOAM implementation FX:59-126: extract "loam_edge" / "loam_surf" from a raw scan.  The features
+ * stay device-resident and become the current scan target (as SetInputTarget with the
+ * processor's output container) without a host round trip. */
+lmsf_status lmsf_extract_features(lmsf_ctx* ctx, const float* xyzi, size_t n, lmsf_feature_counts* counts);
+/* Copy the current features of one kind to the host (xyzi rows, reference emission order);
+ * src (nullable) receives each feature's index in the raw scan. */
+lmsf_status lmsf_copy_features(lmsf_ctx* ctx, int32_t kind, float* out, int32_t* src, size_t cap, size_t* n_out);
+
+/* Batch throughput path: n independent registrations against the context's map (the ML_System
+ * per-LiDAR loop, INC/System/ML_System.hpp:137-156 + :248-264, run as one device pass).
+ * load_scans uploads raw scans (concatenated rows, counts[i] points each) into device slots;
+ * run extracts features for every slot and registers slot i from poses[i] (in/out). */
+lmsf_status lmsf_batch_load_scans(lmsf_ctx* ctx, const float* xyzi, const int64_t* counts, int32_t n);
+lmsf_status lmsf_batch_run(lmsf_ctx* ctx, int32_t n, double* poses, lmsf_solve_stats* stats);
+/* Same, but without blocking: poses are read back by lmsf_batch_wait. */
+lmsf_status lmsf_batch_launch(lmsf_ctx* ctx, int32_t n, const double* poses);
+lmsf_status lmsf_batch_wait(lmsf_ctx* ctx, int32_t n, double* poses, lmsf_solve_stats* stats);
+/* Features of one batch slot after lmsf_batch_run. */
+lmsf_status lmsf_batch_copy_features(lmsf_ctx* ctx, int32_t slot, int32_t kind, float* out, int32_t* src,
+                                     size_t cap, size_t* n_out);
+
+/* ---- diagnostics used by the parity tests and the roofline report (not on the reference surface) */
+/* Matching only at a pose: n_edge + n_surf records (edges first) and the 5 neighbour map indices. */
+lmsf_status lmsf_match(lmsf_ctx* ctx, const double pose[7], lmsf_record* out, int32_t* nn, size_t cap);
+/* Weighted normal-equation packet of the current records at a pose: cost, H (21 upper, row-major),
+ * g (6), count -- the quantities the device LM reduces. */
+lmsf_status lmsf_eval(lmsf_ctx* ctx, const double pose[7], double out[29]);
+/* Neighbour-search kernel accounting since the last reset: launches, summed device time (ms,
+ * HIP events on the context stream), queries, and sum over queries of n27 (map points in the
+ * 3x3x3 block of 1 m cells around each query: the algorithmic-byte figure of DESIGN.md). */
+typedef struct {
+    int64_t launches;
+    double total_ms;
+    int64_t queries;
+    int64_t n27_sum;
+} lmsf_kernel_stats;
+lmsf_status lmsf_kernel_stats_get(lmsf_ctx* ctx, lmsf_kernel_stats* out);
+lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* ctx, int32_t enable_timing);
+
+/* Library version string. */
+const char* lmsf_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LMSF_LMSF_H_ */

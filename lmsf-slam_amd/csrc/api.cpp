@@ -1,0 +1,674 @@
+// C ABI of liblmsf_hip.so: context, device memory, map index build and the registration /
+// extraction pipelines (include/lmsf/lmsf.h documents every entry point against the reference).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "lmsf_internal.h"
+
+using namespace lmsf;
+
+namespace {
+
+struct DevMap {
+    int n = 0;
+    size_t cap = 0;
+    float4* orig = nullptr;
+    float4* pts = nullptr;
+    int* cell = nullptr;
+    size_t cells_cap = 0;
+    uint32_t* counts = nullptr;
+    uint32_t* off = nullptr;
+    uint32_t* fill = nullptr;
+    void* scan_tmp = nullptr;
+    size_t scan_tmp_bytes = 0;
+    int ox = 0, oy = 0, oz = 0, nx = 0, ny = 0, nz = 0;
+
+    GridView view() const {
+        GridView g;
+        g.ox = ox; g.oy = oy; g.oz = oz; g.nx = nx; g.ny = ny; g.nz = nz;
+        g.off = off; g.pts = pts; g.orig = orig; g.n = n;
+        return g;
+    }
+};
+
+constexpr size_t kMaxCells = (size_t)1 << 30;   // 4 GiB of offsets: refuse larger map extents
+constexpr int kEventPairs = 4096;
+
+template <typename T>
+hipError_t dalloc(T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    return hipMalloc((void**)p, count * sizeof(T));
+}
+
+}  // namespace
+
+struct lmsf_ctx {
+    lmsf_config cfg;
+    std::string err;
+    hipStream_t stream = nullptr;
+    int B = 1, R = 0, F = 0, max_parts = 0, n_tiles = 0;
+    int optimization_count = 10;
+    DevMap map[3];
+    bool map_set[3] = {false, false, false};
+    // registration buffers
+    float4* feat = nullptr;
+    int* feat_src = nullptr;
+    int* n_edge = nullptr;
+    int* n_surf = nullptr;
+    int* nn = nullptr;
+    lmsf_record* rec = nullptr;
+    double* partials = nullptr;
+    double* partials_gn = nullptr;
+    double* gn_rows = nullptr;
+    SolveState* st = nullptr;
+    double* d_poses = nullptr;
+    unsigned long long* d_n27 = nullptr;
+    // extraction buffers
+    float4* raw = nullptr;
+    int* raw_count = nullptr;
+    int8_t* ring_id = nullptr;
+    int* tile_counts = nullptr;
+    int* ring_start = nullptr;
+    float4* ring_pts = nullptr;
+    int* ring_src = nullptr;
+    float4* surf_stage = nullptr;
+    int* surf_stage_src = nullptr;
+    float4* edge_stage = nullptr;
+    int* edge_stage_src = nullptr;
+    int* ring_edge_cnt = nullptr;
+    int* ring_surf_cnt = nullptr;
+    int* d_error = nullptr;
+    // host side
+    double* h_poses = nullptr;        // pinned [B*7]
+    SolveState* h_st = nullptr;       // pinned [B]
+    int* h_counts = nullptr;          // pinned [2*B]
+    std::vector<float> host_scan[3];  // SetInputTarget copies (slot 0)
+    bool scan_dirty = false;
+    bool features_on_device = false;  // slot 0 features came from lmsf_extract_features
+    int64_t slot0_ne = 0, slot0_ns = 0;
+    int last_outer = 0;
+    double last_trace[kMaxOuter][7];
+    // kernel accounting
+    bool timing = false;
+    hipEvent_t ev[2 * kEventPairs];
+    int ev_used = 0;
+    double knn_ms = 0.0;
+    int64_t knn_launches = 0, knn_queries = 0;
+
+    lmsf_status fail(lmsf_status code, const char* fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+
+    BatchView bview(int nb) const {
+        BatchView v;
+        v.B = nb;
+        v.feat_stride = F;
+        v.feat = feat;
+        v.n_edge = n_edge;
+        v.n_surf = n_surf;
+        v.nn = nn;
+        v.rec = rec;
+        v.partials = partials;
+        v.max_parts = max_parts;
+        v.st = st;
+        v.n27 = timing ? d_n27 : nullptr;
+        v.gn_rows = gn_rows;
+        v.partials_gn = partials_gn;
+        return v;
+    }
+
+    ExtractView eview(int nb) const {
+        ExtractView e;
+        e.B = nb;
+        e.raw_stride = R;
+        e.raw = raw;
+        e.raw_count = raw_count;
+        e.ring_id = ring_id;
+        e.n_tiles = n_tiles;
+        e.tile_counts = tile_counts;
+        e.ring_start = ring_start;
+        e.ring_pts = ring_pts;
+        e.ring_src = ring_src;
+        e.surf_stage = surf_stage;
+        e.surf_stage_src = surf_stage_src;
+        e.edge_stage = edge_stage;
+        e.edge_stage_src = edge_stage_src;
+        e.ring_edge_cnt = ring_edge_cnt;
+        e.ring_surf_cnt = ring_surf_cnt;
+        e.feat = feat;
+        e.feat_src = feat_src;
+        e.feat_stride = F;
+        e.n_edge = n_edge;
+        e.n_surf = n_surf;
+        e.error = d_error;
+        e.n_scans = cfg.n_scans;
+        e.min_d = cfg.min_distance;
+        e.max_d = cfg.max_distance;
+        e.edge_thresh = cfg.edge_threshold;
+        e.remove_bad = cfg.remove_bad_points;
+        e.beam_lo = cfg.beam_lo_deg;
+        e.beam_spacing = cfg.beam_spacing_deg;
+        return e;
+    }
+};
+
+#define HIPCHK(ctx, expr)                                                                          \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return (ctx)->fail(LMSF_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                               __FILE__, __LINE__);                                                \
+    } while (0)
+
+namespace {
+
+lmsf_status build_map(lmsf_ctx* c, int kind, const float* xyzi, size_t n) {
+    DevMap& m = c->map[kind];
+    hipStream_t s = c->stream;
+    if (n > (size_t)INT32_MAX) return c->fail(LMSF_ERR_CAPACITY, "map too large (%zu points)", n);
+    if (n > m.cap) {
+        hipFree(m.orig); hipFree(m.pts); hipFree(m.cell);
+        m.orig = nullptr; m.pts = nullptr; m.cell = nullptr;
+        HIPCHK(c, dalloc(&m.orig, n));
+        HIPCHK(c, dalloc(&m.pts, n));
+        HIPCHK(c, dalloc(&m.cell, n));
+        m.cap = n;
+    }
+    HIPCHK(c, hipMemcpyAsync(m.orig, xyzi, n * sizeof(float4), hipMemcpyHostToDevice, s));
+    int* d_bbox = c->d_error + 4;  // scratch ints after the error word
+    const int init[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
+    HIPCHK(c, hipMemcpyAsync(d_bbox, init, sizeof init, hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_map_bbox(m.orig, (int)n, d_bbox, s));
+    int bb[6];
+    HIPCHK(c, hipMemcpyAsync(bb, d_bbox, sizeof bb, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const int nx = bb[3] - bb[0] + 1, ny = bb[4] - bb[1] + 1, nz = bb[5] - bb[2] + 1;
+    const size_t cells = (size_t)nx * ny * nz;
+    if (nx <= 0 || ny <= 0 || nz <= 0 || cells > kMaxCells)
+        return c->fail(LMSF_ERR_CAPACITY, "map extent of %d x %d x %d cells exceeds the dense grid limit", nx, ny, nz);
+    if (cells + 1 > m.cells_cap) {
+        hipFree(m.counts); hipFree(m.off); hipFree(m.fill); hipFree(m.scan_tmp);
+        m.counts = m.off = m.fill = nullptr;
+        m.scan_tmp = nullptr;
+        HIPCHK(c, dalloc(&m.counts, cells + 1));
+        HIPCHK(c, dalloc(&m.off, cells + 1));
+        HIPCHK(c, dalloc(&m.fill, cells + 1));
+        m.scan_tmp_bytes = 0;
+        HIPCHK(c, exclusive_scan_u32(m.counts, m.off, cells + 1, nullptr, m.scan_tmp_bytes, s));
+        HIPCHK(c, hipMalloc(&m.scan_tmp, std::max<size_t>(m.scan_tmp_bytes, 16)));
+        m.cells_cap = cells + 1;
+    }
+    m.ox = bb[0]; m.oy = bb[1]; m.oz = bb[2];
+    m.nx = nx; m.ny = ny; m.nz = nz;
+    HIPCHK(c, hipMemsetAsync(m.counts, 0, (cells + 1) * sizeof(uint32_t), s));
+    HIPCHK(c, hipMemsetAsync(m.fill, 0, (cells + 1) * sizeof(uint32_t), s));
+    HIPCHK(c, launch_map_count(m.orig, (int)n, m.ox, m.oy, m.oz, nx, ny, nz, m.cell, m.counts, s));
+    size_t tb = m.scan_tmp_bytes;
+    HIPCHK(c, exclusive_scan_u32(m.counts, m.off, cells + 1, m.scan_tmp, tb, s));
+    HIPCHK(c, launch_map_scatter(m.orig, (int)n, m.cell, m.off, m.fill, m.pts, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    m.n = (int)n;
+    c->map_set[kind] = true;
+    return LMSF_OK;
+}
+
+// Upload SetInputTarget copies of slot 0 when they changed.
+lmsf_status sync_slot0_features(lmsf_ctx* c) {
+    if (!c->scan_dirty) return LMSF_OK;
+    const size_t ne = c->host_scan[LMSF_EDGE].size() / 4, ns = c->host_scan[LMSF_SURF].size() / 4;
+    if (ne + ns > (size_t)c->F) return c->fail(LMSF_ERR_CAPACITY, "%zu features exceed max_features %d", ne + ns, c->F);
+    if (ne) HIPCHK(c, hipMemcpyAsync(c->feat, c->host_scan[LMSF_EDGE].data(), ne * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    if (ns) HIPCHK(c, hipMemcpyAsync(c->feat + ne, c->host_scan[LMSF_SURF].data(), ns * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    c->h_counts[0] = (int)ne;
+    c->h_counts[1] = (int)ns;
+    HIPCHK(c, hipMemcpyAsync(c->n_edge, &c->h_counts[0], sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->n_surf, &c->h_counts[1], sizeof(int), hipMemcpyHostToDevice, c->stream));
+    c->slot0_ne = (int64_t)ne;
+    c->slot0_ns = (int64_t)ns;
+    c->scan_dirty = false;
+    c->features_on_device = false;
+    return LMSF_OK;
+}
+
+// Enqueue the registration of slots [0, nb): outer iterations of match + solver control.
+lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
+    const BatchView bv = c->bview(nb);
+    const GridView ge = c->map[LMSF_EDGE].view(), gs = c->map[LMSF_SURF].view();
+    hipStream_t s = c->stream;
+    const bool gn = c->cfg.solver == LMSF_SOLVER_GN;
+    for (int o = 0; o < iters; ++o) {
+        const bool t = c->timing && c->ev_used + 2 <= 2 * kEventPairs;
+        if (t) HIPCHK(c, hipEventRecord(c->ev[c->ev_used], s));
+        HIPCHK(c, launch_knn(ge, gs, bv, gn ? 1 : 0, s));
+        if (t) {
+            HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 1], s));
+            c->ev_used += 2;
+        }
+        c->knn_launches++;
+        HIPCHK(c, launch_fit_eval(ge, gs, bv, c->cfg.solver, s));
+        if (gn) {
+            HIPCHK(c, launch_gn_solve(bv, o, s));
+        } else {
+            HIPCHK(c, launch_lm_begin(bv, s));
+            for (int i = 0; i < 4; ++i) {
+                HIPCHK(c, launch_lm_eval(bv, s));
+                HIPCHK(c, launch_lm_step(bv, o, i == 3 ? 1 : 0, s));
+            }
+        }
+    }
+    return LMSF_OK;
+}
+
+void fill_stats(const SolveState& S, lmsf_solve_stats* st) {
+    st->outer_iterations = S.outer_run;
+    st->edge_matches = S.edge_matches;
+    st->surf_matches = S.surf_matches;
+    st->inner_iterations = S.inner_total;
+    st->evaluations = S.evals_total;
+    st->termination = S.term;
+    st->initial_cost = S.initial_cost;
+    st->final_cost = S.cost;
+}
+
+lmsf_status collect_timing(lmsf_ctx* c) {
+    if (!c->timing) return LMSF_OK;
+    for (int i = 0; i + 1 < c->ev_used; i += 2) {
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
+        c->knn_ms += ms;
+    }
+    c->ev_used = 0;
+    return LMSF_OK;
+}
+
+int outer_iterations_for_solve(lmsf_ctx* c) {
+    if (c->cfg.solver == LMSF_SOLVER_CERES_LM && c->cfg.schedule == LMSF_SCHEDULE_REFERENCE_DECAY) {
+        if (c->optimization_count > 2) c->optimization_count--;   // ceres_...:100-101
+    }
+    return std::min(c->optimization_count, kMaxOuter);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* lmsf_version(void) { return "lmsf-mi355x 0.1 (gfx950)"; }
+
+lmsf_status lmsf_config_init(lmsf_config* cfg) {
+    if (!cfg) return LMSF_ERR_ARG;
+    std::memset(cfg, 0, sizeof *cfg);
+    cfg->device = 0;
+    cfg->solver = LMSF_SOLVER_CERES_LM;
+    cfg->schedule = LMSF_SCHEDULE_REFERENCE_DECAY;
+    cfg->max_iterations = 10;
+    cfg->max_batch = 1;
+    cfg->max_scan_points = 1 << 17;
+    cfg->max_features = 1 << 17;
+    cfg->n_scans = 16;
+    cfg->min_distance = 2.f;
+    cfg->max_distance = 80.f;
+    cfg->edge_threshold = 1.f;
+    cfg->remove_bad_points = 1;
+    cfg->beam_lo_deg = 0.0;
+    cfg->beam_spacing_deg = 0.0;
+    return LMSF_OK;
+}
+
+void lmsf_ctx_destroy(lmsf_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->cfg.device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (auto& m : c->map) {
+        hipFree(m.orig); hipFree(m.pts); hipFree(m.cell); hipFree(m.counts); hipFree(m.off); hipFree(m.fill);
+        hipFree(m.scan_tmp);
+    }
+    void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nn, c->rec, c->partials, c->partials_gn,
+                    c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
+                    c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->edge_stage,
+                    c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->d_error};
+    for (void* p : bufs) hipFree(p);
+    if (c->h_poses) hipHostFree(c->h_poses);
+    if (c->h_st) hipHostFree(c->h_st);
+    if (c->h_counts) hipHostFree(c->h_counts);
+    for (int i = 0; i < 2 * kEventPairs; ++i)
+        if (c->ev[i]) hipEventDestroy(c->ev[i]);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
+    if (!cfg || !out) return LMSF_ERR_ARG;
+    *out = nullptr;
+    if (cfg->max_batch < 1 || cfg->max_scan_points < 1 || cfg->max_features < 1 || cfg->n_scans < 1 ||
+        cfg->n_scans > kMaxRings || cfg->max_iterations < 0)
+        return LMSF_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || cfg->device < 0 || cfg->device >= ndev) return LMSF_ERR_HIP;
+    lmsf_ctx* c = new lmsf_ctx();
+    std::memset(c->ev, 0, sizeof c->ev);
+    c->cfg = *cfg;
+    c->optimization_count = cfg->max_iterations;
+    c->B = cfg->max_batch;
+    c->R = cfg->max_scan_points;
+    c->F = std::max(cfg->max_features, cfg->max_scan_points);
+    c->max_parts = (c->F + kFitBlock - 1) / kFitBlock;
+    c->n_tiles = (c->R + kTile - 1) / kTile;
+    auto bail = [&](lmsf_status code) {
+        lmsf_ctx_destroy(c);
+        return code;
+    };
+#define CHK(expr) \
+    do {          \
+        if ((expr) != hipSuccess) return bail(LMSF_ERR_HIP); \
+    } while (0)
+    CHK(hipSetDevice(cfg->device));
+    CHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    const size_t B = c->B, F = c->F, R = c->R;
+    CHK(dalloc(&c->feat, B * F));
+    CHK(dalloc(&c->feat_src, B * F));
+    CHK(dalloc(&c->n_edge, B));
+    CHK(dalloc(&c->n_surf, B));
+    CHK(dalloc(&c->nn, B * F * 5));
+    CHK(dalloc(&c->rec, B * F));
+    CHK(dalloc(&c->partials, B * c->max_parts * kPacket));
+    CHK(dalloc(&c->st, B));
+    CHK(dalloc(&c->d_poses, B * 7));
+    CHK(dalloc(&c->d_n27, kCounterShards * 16));
+    if (cfg->solver == LMSF_SOLVER_GN) {
+        CHK(dalloc(&c->partials_gn, B * c->max_parts * kPacket));
+        CHK(dalloc(&c->gn_rows, B * F * 4));
+    }
+    CHK(dalloc(&c->raw, B * R));
+    CHK(dalloc(&c->raw_count, B));
+    CHK(dalloc(&c->ring_id, B * R));
+    CHK(dalloc(&c->tile_counts, B * kMaxRings * c->n_tiles));
+    CHK(dalloc(&c->ring_start, B * (kMaxRings + 1)));
+    CHK(dalloc(&c->ring_pts, B * R));
+    CHK(dalloc(&c->ring_src, B * R));
+    CHK(dalloc(&c->surf_stage, B * R));
+    CHK(dalloc(&c->surf_stage_src, B * R));
+    CHK(dalloc(&c->edge_stage, B * kMaxRings * kEdgePerRing));
+    CHK(dalloc(&c->edge_stage_src, B * kMaxRings * kEdgePerRing));
+    CHK(dalloc(&c->ring_edge_cnt, B * kMaxRings));
+    CHK(dalloc(&c->ring_surf_cnt, B * kMaxRings));
+    CHK(dalloc(&c->d_error, 16));
+    CHK(hipMemset(c->d_error, 0, 16 * sizeof(int)));
+    CHK(hipMemset(c->n_edge, 0, B * sizeof(int)));
+    CHK(hipMemset(c->n_surf, 0, B * sizeof(int)));
+    CHK(hipMemset(c->d_n27, 0, kCounterShards * 16 * sizeof(unsigned long long)));
+    CHK(hipHostMalloc((void**)&c->h_poses, B * 7 * sizeof(double), hipHostMallocDefault));
+    CHK(hipHostMalloc((void**)&c->h_st, B * sizeof(SolveState), hipHostMallocDefault));
+    CHK(hipHostMalloc((void**)&c->h_counts, 2 * B * sizeof(int), hipHostMallocDefault));
+#undef CHK
+    *out = c;
+    return LMSF_OK;
+}
+
+const char* lmsf_last_error(const lmsf_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+lmsf_status lmsf_set_map(lmsf_ctx* c, int32_t kind, const float* xyzi, size_t n) {
+    if (!c || (kind != LMSF_EDGE && kind != LMSF_SURF)) return LMSF_ERR_ARG;
+    if (n == 0) return LMSF_OK;  // empty source ignored (ceres_...:60)
+    if (!xyzi) return c->fail(LMSF_ERR_ARG, "null map pointer");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    return build_map(c, kind, xyzi, n);
+}
+
+lmsf_status lmsf_set_scan(lmsf_ctx* c, int32_t kind, const float* xyzi, size_t n) {
+    if (!c || (kind != LMSF_EDGE && kind != LMSF_SURF)) return LMSF_ERR_ARG;
+    if (n && !xyzi) return c->fail(LMSF_ERR_ARG, "null scan pointer");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (c->features_on_device) {  // keep the other kind extracted on the device
+        const int other = kind == LMSF_EDGE ? LMSF_SURF : LMSF_EDGE;
+        const int64_t no = other == LMSF_EDGE ? c->slot0_ne : c->slot0_ns;
+        const float4* src = c->feat + (other == LMSF_EDGE ? 0 : c->slot0_ne);
+        c->host_scan[other].resize((size_t)no * 4);
+        if (no)
+            HIPCHK(c, hipMemcpyAsync(c->host_scan[other].data(), src, no * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->features_on_device = false;
+    }
+    c->host_scan[kind].assign(xyzi, xyzi + 4 * n);
+    c->scan_dirty = true;
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_set_max_iterations(lmsf_ctx* c, int32_t n) {
+    if (!c || n < 0) return LMSF_ERR_ARG;
+    c->optimization_count = n;
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
+    if (!c || !pose) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (!c->map_set[LMSF_EDGE] && !c->map_set[LMSF_SURF])
+        return c->fail(LMSF_ERR_NO_MAP, "Solve before SetInputSource: no map");
+    lmsf_status rc = sync_slot0_features(c);
+    if (rc) return rc;
+    const int iters = outer_iterations_for_solve(c);
+    std::memcpy(c->h_poses, pose, 7 * sizeof(double));
+    HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_state_init(c->bview(1), c->d_poses, c->stream));
+    rc = enqueue_register(c, 1, iters);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    rc = collect_timing(c);
+    if (rc) return rc;
+    const SolveState& S = c->h_st[0];
+    std::memcpy(pose, S.x, 7 * sizeof(double));
+    c->last_outer = std::min(S.outer_run, kMaxOuter);
+    std::memcpy(c->last_trace, S.trace, sizeof c->last_trace);
+    if (stats) fill_stats(S, stats);
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_solve_trace(lmsf_ctx* c, double* trace, int32_t cap, int32_t* n_out) {
+    if (!c || (!trace && cap > 0)) return LMSF_ERR_ARG;
+    const int n = std::min(cap, c->last_outer);
+    for (int i = 0; i < n; ++i) std::memcpy(trace + 7 * i, c->last_trace[i], 7 * sizeof(double));
+    if (n_out) *n_out = c->last_outer;
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf_feature_counts* counts) {
+    if (!c || (n && !xyzi)) return LMSF_ERR_ARG;
+    if (n > (size_t)c->R) return c->fail(LMSF_ERR_CAPACITY, "%zu points exceed max_scan_points %d", n, c->R);
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    const int64_t counts_in[1] = {(int64_t)n};
+    lmsf_status rc = lmsf_batch_load_scans(c, xyzi, counts_in, 1);
+    if (rc) return rc;
+    HIPCHK(c, hipMemsetAsync(c->d_error, 0, sizeof(int), c->stream));
+    HIPCHK(c, launch_extract(c->eview(1), c->stream));
+    int hc[3];
+    HIPCHK(c, hipMemcpyAsync(&hc[0], c->n_edge, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&hc[1], c->n_surf, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&hc[2], c->d_error, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (hc[2]) return c->fail(LMSF_ERR_CAPACITY, "ring or sector larger than the extraction kernel supports (flags %d)", hc[2]);
+    c->slot0_ne = hc[0];
+    c->slot0_ns = hc[1];
+    c->features_on_device = true;
+    c->scan_dirty = false;
+    c->host_scan[LMSF_EDGE].clear();
+    c->host_scan[LMSF_SURF].clear();
+    if (counts) { counts->n_edge = hc[0]; counts->n_surf = hc[1]; }
+    return LMSF_OK;
+}
+
+static lmsf_status copy_slot_features(lmsf_ctx* c, int slot, int32_t kind, float* out, int32_t* src, size_t cap,
+                                      size_t* n_out) {
+    int hc[2];
+    HIPCHK(c, hipMemcpyAsync(&hc[0], c->n_edge + slot, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&hc[1], c->n_surf + slot, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t n = kind == LMSF_EDGE ? hc[0] : hc[1];
+    const size_t off = (size_t)slot * c->F + (kind == LMSF_EDGE ? 0 : hc[0]);
+    if (n_out) *n_out = n;
+    if (n > cap) return c->fail(LMSF_ERR_CAPACITY, "output capacity %zu < %zu features", cap, n);
+    if (n && out) HIPCHK(c, hipMemcpyAsync(out, c->feat + off, n * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    if (n && src) HIPCHK(c, hipMemcpyAsync(src, c->feat_src + off, n * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_copy_features(lmsf_ctx* c, int32_t kind, float* out, int32_t* src, size_t cap, size_t* n_out) {
+    if (!c || (kind != LMSF_EDGE && kind != LMSF_SURF)) return LMSF_ERR_ARG;
+    if (!c->features_on_device) return c->fail(LMSF_ERR_STATE, "no extracted features on the device");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    return copy_slot_features(c, 0, kind, out, src, cap, n_out);
+}
+
+lmsf_status lmsf_batch_copy_features(lmsf_ctx* c, int32_t slot, int32_t kind, float* out, int32_t* src, size_t cap,
+                                     size_t* n_out) {
+    if (!c || slot < 0 || slot >= c->B || (kind != LMSF_EDGE && kind != LMSF_SURF)) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    return copy_slot_features(c, slot, kind, out, src, cap, n_out);
+}
+
+lmsf_status lmsf_batch_load_scans(lmsf_ctx* c, const float* xyzi, const int64_t* counts, int32_t n) {
+    if (!c || !counts || n < 1 || n > c->B) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    size_t off = 0;
+    for (int i = 0; i < n; ++i) {
+        if (counts[i] < 0 || counts[i] > c->R)
+            return c->fail(LMSF_ERR_CAPACITY, "scan %d has %lld points (max_scan_points %d)", i, (long long)counts[i], c->R);
+        if (counts[i])
+            HIPCHK(c, hipMemcpyAsync(c->raw + (size_t)i * c->R, xyzi + 4 * off, counts[i] * sizeof(float4),
+                                     hipMemcpyHostToDevice, c->stream));
+        c->h_counts[i] = (int)counts[i];
+        off += (size_t)counts[i];
+    }
+    HIPCHK(c, hipMemcpyAsync(c->raw_count, c->h_counts, n * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_batch_launch(lmsf_ctx* c, int32_t n, const double* poses) {
+    if (!c || !poses || n < 1 || n > c->B) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (!c->map_set[LMSF_EDGE] && !c->map_set[LMSF_SURF]) return c->fail(LMSF_ERR_NO_MAP, "no map set");
+    std::memcpy(c->h_poses, poses, (size_t)n * 7 * sizeof(double));
+    HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, (size_t)n * 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_extract(c->eview(n), c->stream));
+    HIPCHK(c, launch_state_init(c->bview(n), c->d_poses, c->stream));
+    // every slot behaves as one Solve on a fresh registration object (ceres_...:100-101)
+    int iters = c->optimization_count;
+    if (c->cfg.solver == LMSF_SOLVER_CERES_LM && c->cfg.schedule == LMSF_SCHEDULE_REFERENCE_DECAY && iters > 2) --iters;
+    iters = std::min(iters, kMaxOuter);
+    c->features_on_device = false;
+    return enqueue_register(c, n, iters);
+}
+
+lmsf_status lmsf_batch_wait(lmsf_ctx* c, int32_t n, double* poses, lmsf_solve_stats* stats) {
+    if (!c || !poses || n < 1 || n > c->B) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, (size_t)n * sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
+    int herr = 0;
+    HIPCHK(c, hipMemcpyAsync(&herr, c->d_error, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    lmsf_status rc = collect_timing(c);
+    if (rc) return rc;
+    for (int i = 0; i < n; ++i) {
+        std::memcpy(poses + 7 * i, c->h_st[i].x, 7 * sizeof(double));
+        if (stats) fill_stats(c->h_st[i], &stats[i]);
+    }
+    if (herr) return c->fail(LMSF_ERR_CAPACITY, "ring or sector larger than the extraction kernel supports (flags %d)", herr);
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_batch_run(lmsf_ctx* c, int32_t n, double* poses, lmsf_solve_stats* stats) {
+    lmsf_status rc = lmsf_batch_launch(c, n, poses);
+    if (rc) return rc;
+    return lmsf_batch_wait(c, n, poses, stats);
+}
+
+lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int32_t* nn, size_t cap) {
+    if (!c || !pose) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    lmsf_status rc = sync_slot0_features(c);
+    if (rc) return rc;
+    const size_t nq = (size_t)(c->slot0_ne + c->slot0_ns);
+    if (nq > cap) return c->fail(LMSF_ERR_CAPACITY, "output capacity %zu < %zu queries", cap, nq);
+    std::memcpy(c->h_poses, pose, 7 * sizeof(double));
+    HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    const BatchView bv = c->bview(1);
+    HIPCHK(c, launch_state_init(bv, c->d_poses, c->stream));
+    const GridView ge = c->map[LMSF_EDGE].view(), gs = c->map[LMSF_SURF].view();
+    HIPCHK(c, launch_knn(ge, gs, bv, 0, c->stream));
+    HIPCHK(c, launch_fit_eval(ge, gs, bv, LMSF_SOLVER_CERES_LM, c->stream));
+    if (nq && out) HIPCHK(c, hipMemcpyAsync(out, c->rec, nq * sizeof(lmsf_record), hipMemcpyDeviceToHost, c->stream));
+    if (nq && nn) HIPCHK(c, hipMemcpyAsync(nn, c->nn, nq * 5 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_eval(lmsf_ctx* c, const double pose[7], double out[29]) {
+    if (!c || !pose || !out) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    const int nq = (int)(c->slot0_ne + c->slot0_ns);
+    const int nparts = (nq + kEvalBlock - 1) / kEvalBlock;
+    std::memcpy(c->h_poses, pose, 7 * sizeof(double));
+    HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_eval_at(c->bview(1), c->d_poses, nullptr, c->stream));
+    std::vector<double> parts((size_t)std::max(nparts, 1) * kPacket, 0.0);
+    if (nparts)
+        HIPCHK(c, hipMemcpyAsync(parts.data(), c->partials, (size_t)nparts * kPacket * sizeof(double),
+                                 hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < 29; ++i) {
+        double s = 0.0;
+        for (int p = 0; p < nparts; ++p) s += parts[(size_t)p * kPacket + i];
+        out[i] = s;
+    }
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* c, int32_t enable_timing) {
+    if (!c) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (enable_timing && !c->ev[0]) {
+        for (int i = 0; i < 2 * kEventPairs; ++i) HIPCHK(c, hipEventCreate(&c->ev[i]));
+    }
+    c->timing = enable_timing != 0;
+    c->ev_used = 0;
+    c->knn_ms = 0.0;
+    c->knn_launches = 0;
+    c->knn_queries = 0;
+    HIPCHK(c, hipMemset(c->d_n27, 0, kCounterShards * 16 * sizeof(unsigned long long)));
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_kernel_stats_get(lmsf_ctx* c, lmsf_kernel_stats* out) {
+    if (!c || !out) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    lmsf_status rc = collect_timing(c);
+    if (rc) return rc;
+    std::vector<unsigned long long> sh((size_t)kCounterShards * 16, 0);
+    HIPCHK(c, hipMemcpy(sh.data(), c->d_n27, sh.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long n27 = 0, q = 0;
+    for (int i = 0; i < kCounterShards; ++i) { n27 += sh[(size_t)i * 16]; q += sh[(size_t)i * 16 + 1]; }
+    out->launches = c->knn_launches;
+    out->total_ms = c->knn_ms;
+    out->queries = (int64_t)q;
+    out->n27_sum = (int64_t)n27;
+    return LMSF_OK;
+}
+
+}  // extern "C"

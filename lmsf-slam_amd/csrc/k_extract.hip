@@ -1,0 +1,405 @@
+// LOAM edge / surf feature extraction on gfx950.
+//
+// Replaces LOAMFeatureProcessorBase::Process (FX/LOAMFeatureProcessor_base.hpp:59-126, FX =
+// src/MultiSensorFusionEstimator3D/include/Algorithm/PointClouds/processing/FeatureExtract) and
+// reproduces its output exactly: same ring assignment (splitScan :290-343, float/double
+// evaluation order of the C++ expressions), same bad-point automaton including the `j += 4`
+// skips (checkBadEdgePoint :216-282), same sectors, same greedy edge pick with disable marks
+// leaking across sectors (featureExtractionFromSector :145-207), surf points in ascending
+// curvature order.  The unstable std::sort of the reference is canonicalised to (c, index).
+//
+// Kernels (per batch of scans, one HIP stream):
+//   ring_count   tiles of kTile raw points: ring id per point, per-tile ring histogram
+//   ring_offsets per scan: exclusive scan (ring-major) -> stable ring-ordered positions
+//   ring_scatter stable multisplit (wave ballots) into ring order
+//   ring_features one workgroup per ring: automaton (wave-ballot walk), 6 sectors of
+//                 {curvature, LDS bitonic sort, wave-ballot greedy pick, block-scan compaction}
+//   concat       per scan: edges (ring order) then surfs (ring order) into the feature array
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "lmsf_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace lmsf {
+
+namespace {
+
+__device__ __forceinline__ int ring_of(const ExtractView& ev, float4 p) {
+    const float s = p.x * p.x + p.y * p.y;                       // float expression (FX:300-301)
+    const double distance = sqrt((double)s);
+    if (distance > (double)ev.max_d || distance < (double)ev.min_d) return -1;   // FX:302
+    const double angle = atan((double)p.z / distance) * 180 / M_PI;              // FX:307
+    const bool bad = isnan(angle);   // int(NaN) is INT_MIN on the reference's x86 host
+    const int n = ev.n_scans;
+    int id;
+    if (n == 16) {
+        if (bad) return -1;
+        id = (int)((angle + 15) / 2 + 0.5);
+        if (id > n - 1 || id < 0) return -1;
+    } else if (n == 32) {
+        if (bad) return -1;
+        id = (int)((angle + 92.0 / 3.0) * 3.0 / 4.0);
+        if (id > n - 1 || id < 0) return -1;    // FX:320 lower-bound bug is UB: rejected here
+    } else if (n == 64) {
+        if (bad) return -1;
+        if (angle >= -8.83) id = (int)((2 - angle) * 3.0 + 0.5);
+        else id = n / 2 + (int)((-8.83 - angle) * 2.0 + 0.5);
+        if (angle > 2 || angle < -24.33 || id > 63 || id < 0) return -1;
+    } else if (ev.beam_spacing > 0) {
+        if (bad) return -1;
+        id = (int)((angle - ev.beam_lo) / ev.beam_spacing + 0.5);
+        if (id > n - 1 || id < 0) return -1;
+    } else {
+        id = 0;  // "wrong scan number" (FX:337-341)
+    }
+    return id;
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt(int lane) {
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void ring_count_kernel(ExtractView ev) {
+    __shared__ int cnt[kMaxRings];
+    const int b = blockIdx.y, t = blockIdx.x;
+    const int n = ev.raw_count[b];
+    if (t * kTile >= n && t > 0) return;
+    for (int r = threadIdx.x; r < ev.n_scans; r += 256) cnt[r] = 0;
+    __syncthreads();
+    const float4* raw = ev.raw + (size_t)b * ev.raw_stride;
+    int8_t* rid = ev.ring_id + (size_t)b * ev.raw_stride;
+    for (int k = threadIdx.x; k < kTile; k += 256) {
+        const int i = t * kTile + k;
+        if (i < n) {
+            const int r = ring_of(ev, raw[i]);
+            rid[i] = (int8_t)r;
+            if (r >= 0) atomicAdd(&cnt[r], 1);
+        }
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < ev.n_scans; r += 256)
+        ev.tile_counts[((size_t)b * kMaxRings + r) * ev.n_tiles + t] = cnt[r];
+}
+
+// Exclusive scan of tile_counts in (ring, tile) order, in place -> tile offsets; ring_start.
+__global__ __launch_bounds__(256) void ring_offsets_kernel(ExtractView ev) {
+    __shared__ int part[256];
+    const int b = blockIdx.x;
+    const int n = ev.raw_count[b];
+    const int nt = max((n + kTile - 1) / kTile, 1);
+    const int E = ev.n_scans * nt;
+    int* tc = ev.tile_counts + (size_t)b * kMaxRings * ev.n_tiles;
+    const int per = (E + 255) / 256;
+    const int lo = threadIdx.x * per, hi = min(lo + per, E);
+    int s = 0;
+    for (int e = lo; e < hi; ++e) s += tc[(e / nt) * ev.n_tiles + (e % nt)];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int i = 0; i < 256; ++i) { int v = part[i]; part[i] = acc; acc += v; }
+    }
+    __syncthreads();
+    int acc = part[threadIdx.x];
+    for (int e = lo; e < hi; ++e) {
+        int* c = &tc[(e / nt) * ev.n_tiles + (e % nt)];
+        const int v = *c;
+        *c = acc;
+        if (e % nt == 0) ev.ring_start[(size_t)b * (kMaxRings + 1) + e / nt] = acc;
+        acc += v;
+    }
+    if (hi == E && lo < hi) ev.ring_start[(size_t)b * (kMaxRings + 1) + ev.n_scans] = acc;
+    if (E == 0 && threadIdx.x == 0) ev.ring_start[(size_t)b * (kMaxRings + 1) + ev.n_scans] = 0;
+}
+
+// Stable multisplit of one tile into ring order (input order preserved inside each ring).
+__global__ __launch_bounds__(256) void ring_scatter_kernel(ExtractView ev) {
+    __shared__ int wcnt[4][kMaxRings];
+    __shared__ int running[kMaxRings];
+    const int b = blockIdx.y, t = blockIdx.x;
+    const int n = ev.raw_count[b];
+    if (t * kTile >= n) return;
+    const int nt = (n + kTile - 1) / kTile;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int r = threadIdx.x; r < kMaxRings; r += 256) running[r] = 0;
+    const float4* raw = ev.raw + (size_t)b * ev.raw_stride;
+    const int8_t* rid = ev.ring_id + (size_t)b * ev.raw_stride;
+    const int* toff = ev.tile_counts + (size_t)b * kMaxRings * ev.n_tiles;
+    float4* out = ev.ring_pts + (size_t)b * ev.raw_stride;
+    int* osrc = ev.ring_src + (size_t)b * ev.raw_stride;
+    (void)nt;
+    for (int c0 = 0; c0 < kTile; c0 += 256) {
+        for (int k = threadIdx.x; k < 4 * kMaxRings; k += 256) wcnt[k / kMaxRings][k % kMaxRings] = 0;
+        __syncthreads();
+        const int i = t * kTile + c0 + threadIdx.x;
+        const int r = i < n ? (int)rid[i] : -1;
+        int rank = 0;
+        unsigned long long remaining = __ballot(r >= 0);
+        while (remaining) {
+            const int leader = __ffsll((long long)remaining) - 1;
+            const int rl = __shfl(r, leader, 64);
+            const unsigned long long m = __ballot(r == rl);
+            if (r == rl) rank = __popcll(m & lanemask_lt(lane));
+            if (lane == leader) wcnt[wave][rl] = __popcll(m);
+            remaining &= ~m;
+        }
+        __syncthreads();
+        if (r >= 0) {
+            int base = running[r];
+            for (int w = 0; w < wave; ++w) base += wcnt[w][r];
+            const int dst = toff[(size_t)r * ev.n_tiles + t] + base + rank;
+            out[dst] = raw[i];
+            osrc[dst] = i;
+        }
+        __syncthreads();
+        for (int rr = threadIdx.x; rr < ev.n_scans; rr += 256)
+            running[rr] += wcnt[0][rr] + wcnt[1][rr] + wcnt[2][rr] + wcnt[3][rr];
+        __syncthreads();
+    }
+}
+
+// One workgroup per (ring, scan).
+__global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
+    __shared__ uint8_t dis[kRingMax];
+    __shared__ uint8_t flag[kRingMax];
+    __shared__ double key[kSortMax];
+    __shared__ int kidx[kSortMax];
+    __shared__ int scan_part[256];
+    __shared__ int sh_ec, sh_sc, sh_err;
+    const int r = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int* rs = ev.ring_start + (size_t)b * (kMaxRings + 1);
+    const int start = rs[r];
+    const int size = rs[r + 1] - start;
+    int* ecnt = ev.ring_edge_cnt + (size_t)b * kMaxRings;
+    int* scnt = ev.ring_surf_cnt + (size_t)b * kMaxRings;
+    if (size < 20 || size > kRingMax) {   // FX:71
+        if (tid == 0) {
+            ecnt[r] = 0;
+            scnt[r] = 0;
+            if (size > kRingMax) atomicOr(ev.error, 1);
+        }
+        return;
+    }
+    const float4* pts = ev.ring_pts + (size_t)b * ev.raw_stride + start;
+    const int* psrc = ev.ring_src + (size_t)b * ev.raw_stride + start;
+    for (int j = tid; j < size; j += 256) { dis[j] = 0; flag[j] = 0; }
+    if (tid == 0) { sh_ec = 0; sh_sc = 0; sh_err = 0; }
+    __syncthreads();
+    const int jmax = size - 7;  // checkBadEdgePoint visits j in [5, size - 7]
+    if (ev.remove_bad) {
+        for (int j = 5 + tid; j <= jmax; j += 256) {
+            const float4 a = pts[j], c = pts[j + 1];
+            const double angle_curr = atan2((double)a.x, (double)a.y);
+            const double angle_after = atan2((double)c.x, (double)c.y);
+            double delta_angle = fabs(angle_curr - angle_after);
+            if (delta_angle > M_PI) delta_angle = M_PI * 2 - delta_angle;
+            uint8_t e = 0;
+            if (delta_angle > 0.0175) {
+                e = 1;
+            } else {
+                const float sc = a.x * a.x + a.y * a.y + a.z * a.z;
+                const float sa = c.x * c.x + c.y * c.y + c.z * c.z;
+                const double dc = sqrt((double)sc), da = sqrt((double)sa);
+                const double ang = dc < da ? atan2(dc * delta_angle, da - dc) : atan2(da * delta_angle, dc - da);
+                if (ang <= 0.17) e = dc < da ? 2 : 3;
+            }
+            flag[j] = e;
+        }
+        __syncthreads();
+        // sequential skip automaton (next j = j + 5 after event 1 / 2, else j + 1), 64 at a time
+        if (tid < 64) {
+            int pos = 5;
+            while (pos <= jmax) {
+                const int j = pos + lane;
+                const int e = j <= jmax ? (int)flag[j] : 0;
+                const unsigned long long m = __ballot(e == 1 || e == 2);
+                const int f = m ? (__ffsll((long long)m) - 1) : 64;
+                if (lane < f && e == 3) {
+#pragma unroll
+                    for (int k = 0; k <= 5; ++k) dis[j - k] = 1;
+                }
+                if (lane == f) {
+                    if (e == 1) {
+#pragma unroll
+                        for (int k = -5; k <= 5; ++k) dis[j + k] = 1;
+                    } else {
+#pragma unroll
+                        for (int k = 1; k <= 5; ++k) dis[j + k] = 1;
+                    }
+                }
+                pos = m ? pos + f + 5 : pos + 64;
+            }
+        }
+        __syncthreads();
+        for (int j = tid; j < size; j += 256) flag[j] = 0;   // reuse as is_edge
+        __syncthreads();
+    }
+    const int total_points = size - 10;
+    const int sector_length = total_points / 6;          // (int)((total/6) + 0.5) with int division
+    const double thresh = (double)ev.edge_thresh;
+    float4* estage = ev.edge_stage + ((size_t)b * kMaxRings + r) * kEdgePerRing;
+    int* estage_src = ev.edge_stage_src + ((size_t)b * kMaxRings + r) * kEdgePerRing;
+    float4* sstage = ev.surf_stage + (size_t)b * ev.raw_stride + start;
+    int* sstage_src = ev.surf_stage_src + (size_t)b * ev.raw_stride + start;
+    for (int k = 0; k < 6; ++k) {
+        const int s0 = 5 + sector_length * k;
+        const int e0 = (k == 5) ? size - 6 : s0 + sector_length - 1;
+        const int n = e0 - s0 + 1;
+        if (n > kSortMax) {
+            if (tid == 0) { atomicOr(ev.error, 2); sh_err = 1; }
+            break;
+        }
+        int npow = 1;
+        while (npow < n) npow <<= 1;
+        for (int i = tid; i < npow; i += 256) {
+            if (i < n) {
+                const int j = s0 + i;
+                const float4 m5 = pts[j - 5], m4 = pts[j - 4], m3 = pts[j - 3], m2 = pts[j - 2], m1 = pts[j - 1];
+                const float4 p0 = pts[j];
+                const float4 q1 = pts[j + 1], q2 = pts[j + 2], q3 = pts[j + 3], q4 = pts[j + 4], q5 = pts[j + 5];
+                const float fx = m5.x + m4.x + m3.x + m2.x + m1.x - 10 * p0.x + q1.x + q2.x + q3.x + q4.x + q5.x;
+                const float fy = m5.y + m4.y + m3.y + m2.y + m1.y - 10 * p0.y + q1.y + q2.y + q3.y + q4.y + q5.y;
+                const float fz = m5.z + m4.z + m3.z + m2.z + m1.z - 10 * p0.z + q1.z + q2.z + q3.z + q4.z + q5.z;
+                const double dx = fx, dy = fy, dz = fz;
+                key[i] = dx * dx + dy * dy + dz * dz;
+                kidx[i] = j;
+            } else {
+                key[i] = __builtin_huge_val();
+                kidx[i] = 0x7fffffff;
+            }
+        }
+        __syncthreads();
+        // bitonic sort ascending by (c, index)
+        for (int kk = 2; kk <= npow; kk <<= 1) {
+            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                for (int i = tid; i < npow; i += 256) {
+                    const int ixj = i ^ jj;
+                    if (ixj > i) {
+                        const double ka = key[i], kb = key[ixj];
+                        const int ia = kidx[i], ib = kidx[ixj];
+                        const bool a_gt_b = ka > kb || (ka == kb && ia > ib);
+                        const bool up = (i & kk) == 0;
+                        if (up == a_gt_b) {
+                            key[i] = kb; key[ixj] = ka;
+                            kidx[i] = ib; kidx[ixj] = ia;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        // greedy edge pick, largest curvature first (FX:157-195), one wave
+        if (tid < 64) {
+            int pos = n - 1, picked = 0, ec = sh_ec;
+            while (pos >= 0) {
+                const int cand = pos - lane;
+                const bool elig = cand >= 0 && dis[kidx[cand]] == 0;
+                const unsigned long long m = __ballot(elig);
+                if (!m) { pos -= 64; continue; }
+                const int f = __ffsll((long long)m) - 1;
+                const double c = key[pos - f];
+                const int ind = kidx[pos - f];
+                if (c <= thresh) break;
+                ++picked;
+                if (picked > 20) break;
+                if (lane == 0) {
+                    estage[ec] = pts[ind];
+                    estage_src[ec] = psrc[ind];
+                    flag[ind] = 1;
+                }
+                if (lane >= 1 && lane <= 5) dis[min(ind + lane, size - 1)] = 1;
+                if (lane >= 6 && lane <= 10) dis[max(ind - (lane - 5), 0)] = 1;
+                ++ec;
+                pos = pos - f - 1;
+            }
+            if (lane == 0) sh_ec = ec;
+        }
+        __syncthreads();
+        // surf: every sector point not picked as edge, ascending curvature (FX:197-206)
+        const int per = (n + 255) / 256;
+        const int lo = tid * per, hi = min(lo + per, n);
+        int cntv = 0;
+        for (int i = lo; i < hi; ++i) cntv += flag[kidx[i]] == 0;
+        scan_part[tid] = cntv;
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0;
+            for (int i = 0; i < 256; ++i) { const int v = scan_part[i]; scan_part[i] = acc; acc += v; }
+        }
+        __syncthreads();
+        int o = sh_sc + scan_part[tid];
+        for (int i = lo; i < hi; ++i) {
+            const int ind = kidx[i];
+            if (flag[ind] == 0) {
+                sstage[o] = pts[ind];
+                sstage_src[o] = psrc[ind];
+                ++o;
+            }
+        }
+        __syncthreads();
+        if (tid == 255) sh_sc = o;  // thread 255's running offset is the sector's total
+        __syncthreads();
+    }
+    if (tid == 0) {
+        ecnt[r] = sh_err ? 0 : sh_ec;
+        scnt[r] = sh_err ? 0 : sh_sc;
+    }
+}
+
+// Concatenate per-ring stages: edges of ring 0..N-1, then surfs of ring 0..N-1 (FX:124-125 order).
+__global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
+    __shared__ int epre[kMaxRings + 1], spre[kMaxRings + 1];
+    const int b = blockIdx.y;
+    const int nr = ev.n_scans;
+    if (threadIdx.x == 0) {
+        int e = 0, s = 0;
+        for (int r = 0; r < nr; ++r) {
+            epre[r] = e; spre[r] = s;
+            e += ev.ring_edge_cnt[(size_t)b * kMaxRings + r];
+            s += ev.ring_surf_cnt[(size_t)b * kMaxRings + r];
+        }
+        epre[nr] = e; spre[nr] = s;
+        if (blockIdx.x == 0) {
+            ev.n_edge[b] = e;
+            ev.n_surf[b] = s;
+        }
+    }
+    __syncthreads();
+    const int ne = epre[nr], ns = spre[nr];
+    const int* rs = ev.ring_start + (size_t)b * (kMaxRings + 1);
+    float4* feat = ev.feat + (size_t)b * ev.feat_stride;
+    int* fsrc = ev.feat_src + (size_t)b * ev.feat_stride;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < ne + ns; i += gridDim.x * 256) {
+        if (i < ne) {
+            int lo = 0, hi = nr - 1;  // last ring with epre[r] <= i
+            while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (epre[mid] <= i) lo = mid; else hi = mid - 1; }
+            const size_t src = ((size_t)b * kMaxRings + lo) * kEdgePerRing + (i - epre[lo]);
+            feat[i] = ev.edge_stage[src];
+            fsrc[i] = ev.edge_stage_src[src];
+        } else {
+            const int k = i - ne;
+            int lo = 0, hi = nr - 1;
+            while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (spre[mid] <= k) lo = mid; else hi = mid - 1; }
+            const size_t src = (size_t)b * ev.raw_stride + rs[lo] + (k - spre[lo]);
+            feat[i] = ev.surf_stage[src];
+            fsrc[i] = ev.surf_stage_src[src];
+        }
+    }
+}
+
+hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
+    hipLaunchKernelGGL(ring_count_kernel, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
+    hipLaunchKernelGGL(ring_offsets_kernel, dim3(ev.B), dim3(256), 0, s, ev);
+    hipLaunchKernelGGL(ring_scatter_kernel, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
+    hipLaunchKernelGGL(ring_features_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
+    const int cblocks = min(64, (ev.raw_stride + 255) / 256);
+    hipLaunchKernelGGL(concat_kernel, dim3(max(cblocks, 1), ev.B), dim3(256), 0, s, ev);
+    return hipGetLastError();
+}
+
+}  // namespace lmsf

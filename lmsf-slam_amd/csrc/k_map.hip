@@ -1,0 +1,96 @@
+// Device neighbour index of a LOAM feature map: dense 1 m cell grid with cell-sorted points.
+//
+// Replaces FeatureMatch::SetSearchTarget -> pcl::KdTreeFLANN::setInputCloud
+// (REG/FeatureMatch/FeatureMatchBase.hpp:40-44), rebuilt whenever the local map changes
+// (INC/LidarTracker/LidarTrackerLocalMap.hpp:229).  Cell edge = the 1 m match radius
+// (search_thresh_ = 1.0, FeatureMatchBase.hpp:29), so every map point with d^2 < 1 to a query
+// lies in the 3x3x3 cells around the query's cell; cell = floor(coord) - origin is exact in float.
+// Layout in HBM: float4 pts[n] sorted by linear cell (x fastest: the 3 x-neighbours of a cell are
+// one contiguous range), uint32 off[cells + 1]; w of each sorted point = its original index.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "lmsf_internal.h"
+
+namespace lmsf {
+
+__global__ void map_bbox_kernel(const float4* pts, int n, int* bbox) {
+    int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float4 p = pts[i];
+        const float c[3] = {floorf(p.x), floorf(p.y), floorf(p.z)};
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            // coordinates beyond +-2^30 m are clamped (they cannot be matched anyway)
+            const int v = (int)fminf(fmaxf(c[d], -1073741824.f), 1073741824.f);
+            lo[d] = min(lo[d], v);
+            hi[d] = max(hi[d], v);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            lo[d] = min(lo[d], __shfl_xor(lo[d], o, 64));
+            hi[d] = max(hi[d], __shfl_xor(hi[d], o, 64));
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            atomicMin(&bbox[d], lo[d]);
+            atomicMax(&bbox[3 + d], hi[d]);
+        }
+    }
+}
+
+__global__ void map_count_kernel(const float4* pts, int n, int ox, int oy, int oz, int nx, int ny, int nz,
+                                 int* cell, uint32_t* counts) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = pts[i];
+    const int cx = (int)fminf(fmaxf(floorf(p.x), -1073741824.f), 1073741824.f) - ox;
+    const int cy = (int)fminf(fmaxf(floorf(p.y), -1073741824.f), 1073741824.f) - oy;
+    const int cz = (int)fminf(fmaxf(floorf(p.z), -1073741824.f), 1073741824.f) - oz;
+    const int c = (cz * ny + cy) * nx + cx;
+    cell[i] = c;
+    atomicAdd(&counts[c], 1u);
+}
+
+// Scatter into cell order.  Order inside a cell is arbitrary: the search ranks candidates by the
+// total order (d2, original index), so results do not depend on it.
+__global__ void map_scatter_kernel(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
+                                   float4* sorted) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int c = cell[i];
+    const uint32_t pos = off[c] + atomicAdd(&fill[c], 1u);
+    const float4 p = pts[i];
+    sorted[pos] = make_float4(p.x, p.y, p.z, __int_as_float(i));
+}
+
+hipError_t launch_map_bbox(const float4* pts, int n, int* bbox, hipStream_t s) {
+    const int blocks = min((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(map_bbox_kernel, dim3(max(blocks, 1)), dim3(256), 0, s, pts, n, bbox);
+    return hipGetLastError();
+}
+
+hipError_t launch_map_count(const float4* pts, int n, int ox, int oy, int oz, int nx, int ny, int nz, int* cell,
+                            uint32_t* counts, hipStream_t s) {
+    hipLaunchKernelGGL(map_count_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pts, n, ox, oy, oz, nx, ny, nz,
+                       cell, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_map_scatter(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
+                              float4* sorted, hipStream_t s) {
+    hipLaunchKernelGGL(map_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pts, n, cell, off, fill, sorted);
+    return hipGetLastError();
+}
+
+hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, void* tmp, size_t& tmp_bytes,
+                              hipStream_t s) {
+    return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, out, n, s);
+}
+
+}  // namespace lmsf

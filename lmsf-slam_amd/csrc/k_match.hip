@@ -1,0 +1,402 @@
+// Correspondence search and residual evaluation for LOAM edge/surf registration on gfx950.
+//
+// Replaces, per outer iteration of CeresEdgeSurfFeatureRegistration::Solve
+// (REG/ceres_edgeSurfFeatureRegistration.hpp:105-125; REG = src/MultiSensorFusionEstimator3D/
+// include/Algorithm/PointClouds/registration):
+//   pointAssociateToMap (:235-244)  -> knn_kernel (query = float(q * p + t), double math)
+//   KdTreeFLANN::nearestKSearch(5) + sqd[4] < 1.0 (FeatureMatch/EdgeFeatureMatch.hpp:38-40,
+//       FeatureMatch/surfFeatureMatch.hpp:37-42) -> knn_kernel over a dense 1 m cell grid
+//   PCA line / QR plane fits (EdgeFeatureMatch.hpp:44-80, surfFeatureMatch.hpp:46-82) and the
+//       first Ceres evaluation of every factor (ceres_factor/*.hpp) -> fit_eval_kernel
+//   later Ceres residual evaluations at LM candidates -> lm_eval_kernel
+// Memory roofline: HBM/L2 gather of float4 map points; no MFMA (no dense contraction here).
+#include <hip/hip_runtime.h>
+
+#include "devmath.h"
+#include "lmsf_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace lmsf {
+
+namespace {
+
+constexpr int kTeam = 16;                       // lanes cooperating on one query
+constexpr int kTeamsPerBlock = 256 / kTeam;
+constexpr uint64_t kSentinel = (uint64_t)0x3f800000u << 32;  // key of d2 == 1.0f, idx 0
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo = __shfl_xor(lo, m, kTeam);
+    hi = __shfl_xor(hi, m, kTeam);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ int shfl_int(int v, int src) { return __shfl(v, src, kTeam); }
+
+__device__ __forceinline__ void insert5(uint64_t key, uint64_t (&k)[5]) {
+    if (key < k[4]) {
+        k[4] = key;
+        if (k[4] < k[3]) { uint64_t t = k[3]; k[3] = k[4]; k[4] = t; }
+        if (k[3] < k[2]) { uint64_t t = k[2]; k[2] = k[3]; k[3] = t; }
+        if (k[2] < k[1]) { uint64_t t = k[1]; k[1] = k[2]; k[2] = t; }
+        if (k[1] < k[0]) { uint64_t t = k[0]; k[0] = k[1]; k[1] = t; }
+    }
+}
+
+// World-frame query of a lidar-frame feature: double transform rounded to float
+// (pointAssociateToMap, ceres_...:235-244).
+__device__ __forceinline__ float3 associate(const Pose& P, float4 p) {
+    d3 w = transform(P, mk((double)p.x, (double)p.y, (double)p.z));
+    return make_float3((float)w.x, (float)w.y, (float)w.z);
+}
+
+}  // namespace
+
+// One team of kTeam lanes per query.  The 27 cells around the query cell are enumerated as 9
+// x-rows (each row = 3 consecutive cells = one contiguous range of the cell-sorted points); the
+// team strides over the flattened candidate list with coalesced float4 loads, keeps a per-lane
+// sorted top-5 of (d2 bits, map index) keys with d2 < 1, then merges the lanes' lists.
+__global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, BatchView bv, int skip_converged) {
+    __shared__ unsigned long long blk_n27;
+    __shared__ unsigned int blk_q;
+    const int b = blockIdx.y;
+    if (threadIdx.x == 0) { blk_n27 = 0; blk_q = 0; }
+    __syncthreads();
+    const int ne = bv.n_edge[b], ns = bv.n_surf[b];
+    const int team = threadIdx.x / kTeam, lane = threadIdx.x % kTeam;
+    const int q = blockIdx.x * kTeamsPerBlock + team;
+    const bool active = q < ne + ns && !(skip_converged && bv.st[b].gn_converged);
+    if (active) {
+        const bool is_edge = q < ne;
+        const GridView& g = is_edge ? ge : gs;
+        const Pose P = load_pose(bv.st[b].x);
+        const float4 p = bv.feat[(size_t)b * bv.feat_stride + q];
+        const float3 w = associate(P, p);
+        // rows: lanes 0..8 each resolve one (dy, dz) row of three x-cells
+        int rstart = 0, rlen = 0;
+        const float fx = floorf(w.x), fy = floorf(w.y), fz = floorf(w.z);
+        const bool inside = g.n > 0 && fx >= (float)(g.ox - 2) && fx <= (float)(g.ox + g.nx + 1) &&
+                            fy >= (float)(g.oy - 2) && fy <= (float)(g.oy + g.ny + 1) &&
+                            fz >= (float)(g.oz - 2) && fz <= (float)(g.oz + g.nz + 1);
+        if (inside && lane < 9) {
+            const int cx = (int)fx - g.ox, cy = (int)fy - g.oy + (lane % 3) - 1, cz = (int)fz - g.oz + (lane / 3) - 1;
+            const int xa = max(cx - 1, 0), xb = min(cx + 1, g.nx - 1);
+            if (cy >= 0 && cy < g.ny && cz >= 0 && cz < g.nz && xa <= xb) {
+                const size_t row = ((size_t)cz * g.ny + cy) * g.nx;
+                rstart = (int)g.off[row + xa];
+                rlen = (int)g.off[row + xb + 1] - rstart;
+            }
+        }
+        int st[9], pre[10];
+        pre[0] = 0;
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+            st[r] = shfl_int(rstart, r);
+            pre[r + 1] = pre[r] + shfl_int(rlen, r);
+        }
+        const int total = pre[9];
+        uint64_t k[5] = {kSentinel, kSentinel, kSentinel, kSentinel, kSentinel};
+        // current row r: candidates [rpre, rend) map to pts[rbase + (v - rpre)]
+        int r = 0, rpre = 0, rend = pre[1], rbase = st[0];
+        for (int v = lane; v < total; v += kTeam) {
+            while (v >= rend) {
+                ++r;
+                rpre = rend;
+                int e = pre[9], s0 = st[8];
+#pragma unroll
+                for (int j = 8; j >= 1; --j) {   // static-index selects keep pre[]/st[] in registers
+                    e = (r + 1 == j) ? pre[j] : e;
+                    s0 = (r == j - 1) ? st[j - 1] : s0;
+                }
+                rend = e;
+                rbase = s0;
+            }
+            const float4 m = g.pts[rbase + (v - rpre)];
+            const float dx = w.x - m.x, dy = w.y - m.y, dz = w.z - m.z;
+            const float d2 = dx * dx + dy * dy + dz * dz;
+            const uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)__float_as_int(m.w);
+            insert5(key, k);
+        }
+        // merge: five rounds of team-min; the owning lane pops its head
+        uint64_t res[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            uint64_t mn = k[0];
+#pragma unroll
+            for (int o = kTeam / 2; o >= 1; o >>= 1) {
+                uint64_t t = shfl_xor_u64(mn, o);
+                mn = t < mn ? t : mn;
+            }
+            res[i] = mn;
+            if (k[0] == mn) { k[0] = k[1]; k[1] = k[2]; k[2] = k[3]; k[3] = k[4]; k[4] = kSentinel; }
+        }
+        if (lane < 5) {
+            uint64_t mine = res[0];
+#pragma unroll
+            for (int i = 1; i < 5; ++i) mine = (lane == i) ? res[i] : mine;
+            bv.nn[((size_t)b * bv.feat_stride + q) * 5 + lane] = mine < kSentinel ? (int)(uint32_t)mine : -1;
+        }
+        if (lane == 0 && bv.n27) {
+            atomicAdd(&blk_n27, (unsigned long long)total);
+            atomicAdd(&blk_q, 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && bv.n27 && blk_q) {
+        // 64 counter shards on separate 128-B lines: one word serialises ~1e5 block updates
+        unsigned long long* shard = bv.n27 + (size_t)((blockIdx.x + blockIdx.y) & (kCounterShards - 1)) * 16;
+        atomicAdd(shard, blk_n27);
+        atomicAdd(shard + 1, (unsigned long long)blk_q);
+    }
+}
+
+// ---------------------------------------------------------------- fits (double precision)
+
+// EdgeFeatureMatch::Match body after the 5-NN (EdgeFeatureMatch.hpp:44-80).
+__device__ bool edge_fit(const float4* mp, const int* nn, d3& a, d3& b) {
+    d3 pts[5];
+    d3 center = mk(0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const float4 p = mp[nn[j]];
+        pts[j] = mk((double)p.x, (double)p.y, (double)p.z);
+        center = center + pts[j];
+    }
+    center = mk(center.x / 5.0, center.y / 5.0, center.z / 5.0);
+    double cov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        d3 e = pts[j] - center;
+        const double ev[3] = {e.x, e.y, e.z};
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) cov[r * 3 + c] = cov[r * 3 + c] + ev[r] * ev[c];
+    }
+    double d[3], v[9];
+    jacobi_eig<3>(cov, d, v);
+    int i0, i1, i2;
+    order3(d, i0, i1, i2);
+    const double l1 = pick3(d, i1), l2 = pick3(d, i2);
+    if (!(l2 > 3 * l1)) return false;
+    const double c0[3] = {v[0], v[3], v[6]}, c1[3] = {v[1], v[4], v[7]}, c2[3] = {v[2], v[5], v[8]};
+    d3 u = i2 == 0 ? mk(c0[0], c0[1], c0[2]) : (i2 == 1 ? mk(c1[0], c1[1], c1[2]) : mk(c2[0], c2[1], c2[2]));
+    a = smul(0.1, u) + center;
+    b = smul(-0.1, u) + center;
+    return true;
+}
+
+// SurfFeatureMatch::Match body after the 5-NN (surfFeatureMatch.hpp:46-82).
+__device__ bool surf_fit(const float4* mp, const int* nn, float3 q, d3& n_out, double& D_out,
+                         double& gn_res) {
+    double A[15], bb[5], x[3];
+    float4 p[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        p[j] = mp[nn[j]];
+        A[j * 3 + 0] = p[j].x; A[j * 3 + 1] = p[j].y; A[j * 3 + 2] = p[j].z;
+        bb[j] = -1.0;
+    }
+    colpiv_qr_solve<5, 3>(A, bb, x);
+    d3 n = mk(x[0], x[1], x[2]);
+    double nn_ = norm(n);
+    double D = 1 / nn_;
+    double z = sqnorm(n);
+    if (z > 0.0) {
+        double s = sqrt(z);
+        n = mk(n.x / s, n.y / s, n.z / s);
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        if (fabs(n.x * (double)p[j].x + n.y * (double)p[j].y + n.z * (double)p[j].z + D) > 0.2) return false;
+    const d3 cp = mk((double)q.x, (double)q.y, (double)q.z);
+    const float distance = (float)(dot(n, cp) + D);
+    gn_res = fabs((double)distance);
+    if (distance >= 0) { n_out = n; D_out = D; } else { n_out = mk(-n.x, -n.y, -n.z); D_out = -D; }
+    return true;
+}
+
+// Block reduction of a kPacket-double packet: wave butterfly, then 4 wave sums in LDS.
+// Fixed order -> deterministic.
+__device__ __forceinline__ void block_reduce_packet(double* P, double* out) {
+    __shared__ double red[4][kPacket];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < kPacket; ++i) {
+        double v = P[i];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        P[i] = v;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < kPacket; ++i) red[wave][i] = P[i];
+    }
+    __syncthreads();
+    if (threadIdx.x < kPacket) {
+        const int i = threadIdx.x;
+        out[i] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+    }
+}
+
+// One thread per query: line / plane fit from the 5 neighbours, record write, and the
+// Huber-weighted normal-equation packet at the linearisation pose (Ceres' first evaluation).
+__global__ __launch_bounds__(256) void fit_eval_kernel(GridView ge, GridView gs, BatchView bv, int solver) {
+    const int b = blockIdx.y;
+    const int ne = bv.n_edge[b], ns = bv.n_surf[b];
+    const int nq = ne + ns;
+    if (blockIdx.x * kFitBlock >= nq) return;
+    if (solver == LMSF_SOLVER_GN && bv.st[b].gn_converged) return;
+    const int q = blockIdx.x * kFitBlock + threadIdx.x;
+    double P[kPacket];
+#pragma unroll
+    for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
+    if (q < nq) {
+        const bool is_edge = q < ne;
+        const size_t slot = (size_t)b * bv.feat_stride + q;
+        const float4 p = bv.feat[slot];
+        const Pose Ps = load_pose(bv.st[b].x);
+        lmsf_record r;
+        r.px = p.x; r.py = p.y; r.pz = p.z;
+        r.kind = 0;
+        r.v0[0] = r.v0[1] = r.v0[2] = 0.0;
+        r.v1[0] = r.v1[1] = r.v1[2] = 0.0;
+        int nn[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) nn[j] = bv.nn[slot * 5 + j];
+        double gn_grad[3] = {0, 0, 0}, gn_res = 0.0;
+        if (nn[4] >= 0) {
+            const float3 w = associate(Ps, p);
+            if (is_edge) {
+                d3 a, bpt;
+                if (edge_fit(ge.orig, nn, a, bpt)) {
+                    r.kind = LMSF_EDGE;
+                    r.v0[0] = a.x; r.v0[1] = a.y; r.v0[2] = a.z;
+                    r.v1[0] = bpt.x; r.v1[1] = bpt.y; r.v1[2] = bpt.z;
+                    if (solver == LMSF_SOLVER_GN) {  // EdgeCostFactorInfo residuals_ / norm_
+                        const d3 cp = mk((double)w.x, (double)w.y, (double)w.z);
+                        d3 nu = cross(cp - a, cp - bpt);
+                        d3 de = a - bpt;
+                        gn_res = norm(nu) / norm(de);
+                        d3 gg = cross(de, nu);
+                        double gnn = norm(gg);
+                        gn_grad[0] = gnn > 0 ? gg.x / gnn : gg.x;
+                        gn_grad[1] = gnn > 0 ? gg.y / gnn : gg.y;
+                        gn_grad[2] = gnn > 0 ? gg.z / gnn : gg.z;
+                    }
+                }
+            } else {
+                d3 n;
+                double D;
+                if (surf_fit(gs.orig, nn, w, n, D, gn_res)) {
+                    r.kind = LMSF_SURF;
+                    r.v0[0] = n.x; r.v0[1] = n.y; r.v0[2] = n.z;
+                    r.v1[0] = D;
+                    gn_grad[0] = n.x; gn_grad[1] = n.y; gn_grad[2] = n.z;
+                }
+            }
+        }
+        bv.rec[slot] = r;
+        if (solver == LMSF_SOLVER_GN) {
+            double* gr = bv.gn_rows + slot * 4;
+            gr[0] = gn_grad[0]; gr[1] = gn_grad[1]; gr[2] = gn_grad[2]; gr[3] = r.kind ? gn_res : -1.0;
+        } else if (r.kind != 0) {
+            double J[6], res;
+            const d3 pp = mk((double)p.x, (double)p.y, (double)p.z);
+            if (r.kind == LMSF_EDGE)
+                res = edge_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), mk(r.v1[0], r.v1[1], r.v1[2]), J);
+            else
+                res = surf_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), r.v1[0], J);
+            huber_accumulate(P, res, J);
+        }
+        if (r.kind == LMSF_EDGE) P[29] = 1.0;
+        if (r.kind == LMSF_SURF) P[30] = 1.0;
+    }
+    block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + blockIdx.x) * kPacket);
+}
+
+// LM candidate evaluation over the fixed correspondences (Ceres re-evaluates the same residual
+// blocks at every trial point).  kEvalPerThread records per thread.
+__global__ __launch_bounds__(256) void lm_eval_kernel(BatchView bv) {
+    const int b = blockIdx.y;
+    const int nq = bv.n_edge[b] + bv.n_surf[b];
+    if (blockIdx.x * kEvalBlock >= nq) return;
+    if (!bv.st[b].need_eval) return;
+    const Pose Ps = load_pose(bv.st[b].xc);
+    double P[kPacket];
+#pragma unroll
+    for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
+#pragma unroll
+    for (int k = 0; k < kEvalPerThread; ++k) {
+        const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
+        if (q < nq) {
+            const lmsf_record r = bv.rec[(size_t)b * bv.feat_stride + q];
+            if (r.kind != 0) {
+                double J[6], res;
+                const d3 pp = mk((double)r.px, (double)r.py, (double)r.pz);
+                if (r.kind == LMSF_EDGE)
+                    res = edge_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), mk(r.v1[0], r.v1[1], r.v1[2]), J);
+                else
+                    res = surf_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), r.v1[0], J);
+                huber_accumulate(P, res, J);
+            }
+        }
+    }
+    block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + blockIdx.x) * kPacket);
+}
+
+// Diagnostics: evaluate slot 0's records at an arbitrary pose into partials of slot 0.
+__global__ __launch_bounds__(256) void eval_at_kernel(BatchView bv, const double* pose) {
+    const int nq = bv.n_edge[0] + bv.n_surf[0];
+    if (blockIdx.x * kEvalBlock >= nq) return;
+    const Pose Ps = load_pose(pose);
+    double P[kPacket];
+#pragma unroll
+    for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
+#pragma unroll
+    for (int k = 0; k < kEvalPerThread; ++k) {
+        const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
+        if (q < nq) {
+            const lmsf_record r = bv.rec[q];
+            if (r.kind != 0) {
+                double J[6], res;
+                const d3 pp = mk((double)r.px, (double)r.py, (double)r.pz);
+                if (r.kind == LMSF_EDGE)
+                    res = edge_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), mk(r.v1[0], r.v1[1], r.v1[2]), J);
+                else
+                    res = surf_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), r.v1[0], J);
+                huber_accumulate(P, res, J);
+            }
+        }
+    }
+    block_reduce_packet(P, bv.partials + (size_t)blockIdx.x * kPacket);
+}
+
+hipError_t launch_knn(const GridView& edge, const GridView& surf, const BatchView& bv, int skip_converged,
+                      hipStream_t s) {
+    dim3 grid((bv.feat_stride + kTeamsPerBlock - 1) / kTeamsPerBlock, bv.B);
+    hipLaunchKernelGGL(knn_kernel, grid, dim3(256), 0, s, edge, surf, bv, skip_converged);
+    return hipGetLastError();
+}
+
+hipError_t launch_fit_eval(const GridView& edge, const GridView& surf, const BatchView& bv, int solver,
+                           hipStream_t s) {
+    dim3 grid((bv.feat_stride + kFitBlock - 1) / kFitBlock, bv.B);
+    hipLaunchKernelGGL(fit_eval_kernel, grid, dim3(256), 0, s, edge, surf, bv, solver);
+    return hipGetLastError();
+}
+
+hipError_t launch_lm_eval(const BatchView& bv, hipStream_t s) {
+    dim3 grid((bv.feat_stride + kEvalBlock - 1) / kEvalBlock, bv.B);
+    hipLaunchKernelGGL(lm_eval_kernel, grid, dim3(256), 0, s, bv);
+    return hipGetLastError();
+}
+
+hipError_t launch_eval_at(const BatchView& bv, const double* pose_dev, double* out_dev, hipStream_t s) {
+    (void)out_dev;
+    dim3 grid((bv.feat_stride + kEvalBlock - 1) / kEvalBlock, 1);
+    hipLaunchKernelGGL(eval_at_kernel, grid, dim3(256), 0, s, bv, pose_dev);
+    return hipGetLastError();
+}
+
+}  // namespace lmsf

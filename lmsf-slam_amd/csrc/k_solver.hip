@@ -1,0 +1,451 @@
+// Device-resident solver control for LOAM registration (one 64-lane workgroup per registration).
+//
+// Restates, without any host round trip per step, ceres::Solve as configured in
+// CeresEdgeSurfFeatureRegistration::Solve (REG/ceres_edgeSurfFeatureRegistration.hpp:107-123:
+// TRUST_REGION / LEVENBERG_MARQUARDT, DENSE_QR, max_num_iterations = 4, HuberLoss(0.1),
+// PoseSE3Parameterization) on the reduced 6x6 normal equations, and the GN alternative
+// EdgeSurfFeatureRegistration::GNOptimization (REG/edgeSurfFeatureRegistration.hpp:218-330).
+// Ceres semantics restated (external, Ceres Solver 1.x): jacobi scaling s = 1/(1+sqrt(diag JtJ))
+// fixed at the first evaluation; LM diagonal clamp(diag, 1e-6, 1e32)/radius; step valid iff the
+// model decrease is positive; parameter tolerance 1e-8, function tolerance 1e-6, gradient
+// tolerance 1e-10, min_relative_decrease 1e-3; radius update max(1/3, 1-(2rho-1)^3) on success,
+// radius /= mu, mu *= 2 on rejection; initial radius 1e4, max 1e16.
+#include <hip/hip_runtime.h>
+
+#include "devmath.h"
+#include "lmsf_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace lmsf {
+
+namespace {
+
+constexpr int kMaxInner = 4;  // options.max_num_iterations (ceres_...:118)
+
+// Sum the first `nparts` packets of slot b in a fixed order; result valid in every lane.
+__device__ void reduce_parts(const BatchView& bv, int b, int nparts, double* tot) {
+    const int lane = threadIdx.x;
+    const double* base = bv.partials + (size_t)b * bv.max_parts * kPacket;
+#pragma unroll
+    for (int i = 0; i < kPacket; ++i) {
+        double v = 0.0;
+        for (int p = lane; p < nparts; p += 64) v += base[(size_t)p * kPacket + i];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        tot[i] = v;
+    }
+}
+
+__device__ double norm7(const double* x) {
+    double s = 0.0;
+    for (int i = 0; i < 7; ++i) s += x[i] * x[i];
+    return sqrt(s);
+}
+
+__device__ double grad_max_norm(const double* x, const double* g) {
+    double ng[6], xp[7];
+    for (int i = 0; i < 6; ++i) ng[i] = -g[i];
+    pose_plus(x, ng, xp);
+    double m = 0.0;
+    for (int i = 0; i < 7; ++i) m = fmax(m, fabs(x[i] - xp[i]));
+    return m;
+}
+
+__device__ bool chol_solve6(const double* A, const double* b, double* x) {
+    double L[36];
+    for (int i = 0; i < 36; ++i) L[i] = 0.0;
+    for (int j = 0; j < 6; ++j) {
+        double s = A[j * 6 + j];
+        for (int k = 0; k < j; ++k) s -= L[j * 6 + k] * L[j * 6 + k];
+        if (!(s > 0.0)) return false;
+        double ljj = sqrt(s);
+        L[j * 6 + j] = ljj;
+        for (int i = j + 1; i < 6; ++i) {
+            double t = A[i * 6 + j];
+            for (int k = 0; k < j; ++k) t -= L[i * 6 + k] * L[j * 6 + k];
+            L[i * 6 + j] = t / ljj;
+        }
+    }
+    double y[6];
+    for (int i = 0; i < 6; ++i) {
+        double t = b[i];
+        for (int k = 0; k < i; ++k) t -= L[i * 6 + k] * y[k];
+        y[i] = t / L[i * 6 + i];
+    }
+    for (int i = 5; i >= 0; --i) {
+        double t = y[i];
+        for (int k = i + 1; k < 6; ++k) t -= L[k * 6 + i] * x[k];
+        x[i] = t / L[i * 6 + i];
+    }
+    for (int i = 0; i < 6; ++i)
+        if (!isfinite(x[i])) return false;
+    return true;
+}
+
+// ComputeTrustRegionStep + HandleInvalidStep loop: leaves a candidate awaiting evaluation, or
+// terminates (max iterations / min radius).
+__device__ void compute_step(SolveState& S) {
+    while (true) {
+        if (S.iteration >= kMaxInner) { S.done = 1; S.term = LMSF_TERM_MAX_ITERATIONS; return; }
+        if (S.radius < 1e-32) { S.done = 1; S.term = LMSF_TERM_PARAMETER_TOL; return; }
+        ++S.iteration;
+        double A[36], Hs[36], gs[6], nb[6], step[6];
+        for (int i = 0; i < 6; ++i) {
+            gs[i] = S.g[i] * S.s[i];
+            for (int j = 0; j < 6; ++j) {
+                const int a = i <= j ? hidx(i, j) : hidx(j, i);
+                Hs[i * 6 + j] = S.H[a] * S.s[i] * S.s[j];
+                A[i * 6 + j] = Hs[i * 6 + j];
+            }
+        }
+        for (int i = 0; i < 6; ++i) {
+            const double dg = fmin(fmax(Hs[i * 6 + i], 1e-6), 1e32);
+            A[i * 6 + i] += dg / S.radius;
+            nb[i] = -gs[i];
+        }
+        const bool ok = chol_solve6(A, nb, step);
+        double mcc = 0.0;
+        if (ok) {
+            double sg = 0.0, sHs = 0.0;
+            for (int i = 0; i < 6; ++i) {
+                sg += step[i] * gs[i];
+                double t = 0.0;
+                for (int j = 0; j < 6; ++j) t += Hs[i * 6 + j] * step[j];
+                sHs += step[i] * t;
+            }
+            mcc = -(sg + 0.5 * sHs);
+        }
+        if (!ok || !(mcc > 0.0)) {  // StepIsInvalid == StepRejected(0)
+            S.radius = S.radius / S.decrease;
+            S.decrease *= 2.0;
+            continue;
+        }
+        double delta[6];
+        for (int i = 0; i < 6; ++i) delta[i] = step[i] * S.s[i];
+        pose_plus(S.x, delta, S.xc);
+        S.mcc = mcc;
+        S.need_eval = 1;
+        return;
+    }
+}
+
+__device__ void finish_outer(SolveState& S, int outer) {
+    if (outer < kMaxOuter)
+        for (int i = 0; i < 7; ++i) S.trace[outer][i] = S.x[i];
+    S.inner_total += S.iteration;
+    S.evals_total += S.evals;
+    S.outer_run = outer + 1;
+}
+
+}  // namespace
+
+// Initialise slot states from host poses (qx qy qz qw tx ty tz).
+__global__ void state_init_kernel(BatchView bv, const double* poses) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= bv.B) return;
+    SolveState& S = bv.st[b];
+    for (int i = 0; i < 7; ++i) S.x[i] = poses[b * 7 + i];
+    S.inner_total = S.evals_total = S.outer_run = 0;
+    S.gn_converged = 0;
+    S.done = 1;
+    S.need_eval = 0;
+    S.iteration = 0;
+    S.evals = 0;
+    S.term = LMSF_TERM_MAX_ITERATIONS;
+    S.initial_cost = S.cost = 0.0;
+    S.edge_matches = S.surf_matches = S.nmatch = 0;
+}
+
+// After fit_eval: IterationZero (evaluate at x0, jacobi scaling, gradient check) + first step.
+__global__ __launch_bounds__(64) void lm_begin_kernel(BatchView bv) {
+    const int b = blockIdx.x;
+    const int nq = bv.n_edge[b] + bv.n_surf[b];
+    const int nparts = (nq + kFitBlock - 1) / kFitBlock;
+    double tot[kPacket];
+    reduce_parts(bv, b, nparts, tot);
+    if (threadIdx.x != 0) return;
+    SolveState& S = bv.st[b];
+    S.iteration = 0;
+    S.need_eval = 0;
+    S.done = 0;
+    S.evals = 1;
+    S.nmatch = (int)tot[28];
+    S.edge_matches = (int)tot[29];
+    S.surf_matches = (int)tot[30];
+    S.cost = tot[0];
+    S.initial_cost = tot[0];
+    for (int i = 0; i < 21; ++i) S.H[i] = tot[1 + i];
+    for (int i = 0; i < 6; ++i) S.g[i] = tot[22 + i];
+    if (S.nmatch == 0) {  // no residual blocks: pose unchanged
+        S.done = 1;
+        S.term = LMSF_TERM_NO_RESIDUALS;
+        return;
+    }
+    for (int j = 0; j < 6; ++j) S.s[j] = 1.0 / (1.0 + sqrt(S.H[hidx(j, j)]));
+    S.radius = 1e4;
+    S.decrease = 2.0;
+    S.x_norm = norm7(S.x);
+    if (grad_max_norm(S.x, S.g) <= 1e-10) {
+        S.done = 1;
+        S.term = LMSF_TERM_GRADIENT_TOL;
+        return;
+    }
+    compute_step(S);
+}
+
+// After lm_eval at the candidate: step acceptance (ParameterToleranceReached,
+// FunctionToleranceReached, IsStepSuccessful, HandleSuccessfulStep / StepRejected) + next step.
+__global__ __launch_bounds__(64) void lm_step_kernel(BatchView bv, int outer, int is_last) {
+    const int b = blockIdx.x;
+    SolveState& S = bv.st[b];
+    if (!S.need_eval) {
+        if (is_last && threadIdx.x == 0) finish_outer(S, outer);
+        return;
+    }
+    const int nq = bv.n_edge[b] + bv.n_surf[b];
+    const int nparts = (nq + kEvalBlock - 1) / kEvalBlock;
+    double tot[kPacket];
+    reduce_parts(bv, b, nparts, tot);
+    if (threadIdx.x != 0) return;
+    S.need_eval = 0;
+    ++S.evals;
+    const double cost_c = isfinite(tot[0]) ? tot[0] : 1.7976931348623157e308;
+    double dx[7];
+    for (int i = 0; i < 7; ++i) dx[i] = S.x[i] - S.xc[i];
+    if (norm7(dx) <= 1e-8 * (S.x_norm + 1e-8)) {
+        S.done = 1;
+        S.term = LMSF_TERM_PARAMETER_TOL;
+    } else {
+        const double cost_change = S.cost - cost_c;
+        if (fabs(cost_change) <= 1e-6 * S.cost) {
+            S.done = 1;
+            S.term = LMSF_TERM_FUNCTION_TOL;
+        } else {
+            const double rel = cost_change / S.mcc;
+            if (rel > 1e-3) {
+                const double f = 1.0 - pow(2.0 * rel - 1.0, 3.0);
+                S.radius = S.radius / fmax(1.0 / 3.0, f);
+                S.radius = fmin(1e16, S.radius);
+                S.decrease = 2.0;
+                for (int i = 0; i < 7; ++i) S.x[i] = S.xc[i];
+                S.x_norm = norm7(S.x);
+                S.cost = cost_c;
+                for (int i = 0; i < 21; ++i) S.H[i] = tot[1 + i];
+                for (int i = 0; i < 6; ++i) S.g[i] = tot[22 + i];
+                if (S.iteration >= kMaxInner) {
+                    S.done = 1;
+                    S.term = LMSF_TERM_MAX_ITERATIONS;
+                } else if (grad_max_norm(S.x, S.g) <= 1e-10) {
+                    S.done = 1;
+                    S.term = LMSF_TERM_GRADIENT_TOL;
+                } else {
+                    compute_step(S);
+                }
+            } else {
+                S.radius = S.radius / S.decrease;
+                S.decrease *= 2.0;
+                compute_step(S);
+            }
+        }
+    }
+    if (is_last) finish_outer(S, outer);
+}
+
+// ---------------------------------------------------------------- GN (edgeSurfFeatureRegistration)
+// gn_accum writes JtJ (upper 21 at [1..21]), JtR ([22..27]) and per-block match counts
+// ([29] edge, [30] surf) into partials_gn; fit_eval's own partials carry the per-block counts
+// used to rank matches.
+
+__device__ void gn_record_trace(SolveState& S, int outer) {
+    if (outer < kMaxOuter)
+        for (int i = 0; i < 7; ++i) S.trace[outer][i] = S.x[i];
+    S.outer_run = outer + 1;
+}
+
+__global__ __launch_bounds__(64) void gn_solve_kernel(BatchView bv, int outer) {
+    const int b = blockIdx.x;
+    SolveState& S = bv.st[b];
+    if (S.gn_converged) return;
+    const int nq = bv.n_edge[b] + bv.n_surf[b];
+    const int nparts = (nq + kFitBlock - 1) / kFitBlock;
+    double tot[kPacket];
+    BatchView g = bv;
+    g.partials = bv.partials_gn;
+    reduce_parts(g, b, nparts, tot);
+    if (threadIdx.x != 0) return;
+    S.edge_matches = (int)tot[29];
+    S.surf_matches = (int)tot[30];
+    const int e16 = (int)(uint16_t)(int)tot[29], s16 = (int)(uint16_t)(int)tot[30];
+    S.inner_total += 1;
+    if (e16 + s16 < 10) {  // edgeSurf...:221-225: no update this iteration
+        S.term = LMSF_TERM_GN_TOO_FEW;
+        gn_record_trace(S, outer);
+        return;
+    }
+    double JTJ[36], JTR[6];
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) JTJ[i * 6 + j] = tot[1 + (i <= j ? hidx(i, j) : hidx(j, i))];
+    for (int i = 0; i < 6; ++i) JTR[i] = tot[22 + i];
+    double A[36], nb[6], X[6];
+    for (int i = 0; i < 36; ++i) A[i] = JTJ[i];
+    for (int i = 0; i < 6; ++i) nb[i] = -JTR[i];
+    colpiv_qr_solve<6, 6>(A, nb, X);
+    if (outer == 0) {  // degeneracy check at iterCount == 0 (edgeSurf...:280-304)
+        double a2[36], d[6], V[36];
+        for (int i = 0; i < 36; ++i) a2[i] = JTJ[i];
+        jacobi_eig<6>(a2, d, V);
+        int ord[6] = {0, 1, 2, 3, 4, 5};
+        for (int i = 1; i < 6; ++i) {
+            int k = ord[i], j = i;
+            while (j > 0 && d[ord[j - 1]] > d[k]) { ord[j] = ord[j - 1]; --j; }
+            ord[j] = k;
+        }
+        double ds[6], Vs[36], V2[36];
+        for (int c = 0; c < 6; ++c) {
+            ds[c] = d[ord[c]];
+            for (int r = 0; r < 6; ++r) Vs[r * 6 + c] = V[r * 6 + ord[c]];
+        }
+        for (int i = 0; i < 36; ++i) V2[i] = Vs[i];
+        S.gn_degenerate = 0;
+        for (int i = 5; i >= 0; i--) {
+            if (ds[i] < 100.0) {
+                for (int c = 0; c < 6; ++c) V2[i * 6 + c] = 0.0;   // rows zeroed (:293)
+                S.gn_degenerate = 1;
+            } else {
+                break;
+            }
+        }
+        // Map = V^-1 V2 with V^-1 = V^T (orthogonal eigenvectors; Eigen uses an LU inverse)
+        for (int a = 0; a < 6; ++a)
+            for (int c = 0; c < 6; ++c) {
+                double t = 0.0;
+                for (int k = 0; k < 6; ++k) t += Vs[k * 6 + a] * V2[k * 6 + c];
+                S.gn_map[a * 6 + c] = t;
+            }
+    }
+    if (S.gn_degenerate) {
+        double Y[6];
+        for (int a = 0; a < 6; ++a) {
+            double t = 0.0;
+            for (int k = 0; k < 6; ++k) t += S.gn_map[a * 6 + k] * X[k];
+            Y[a] = t;
+        }
+        for (int a = 0; a < 6; ++a) X[a] = Y[a];
+    }
+    // t += X[3:6]; q = q * AngleAxis(|dr|/2, dr/|dr|) (edgeSurf...:312-321)
+    S.x[4] += X[3]; S.x[5] += X[4]; S.x[6] += X[5];
+    const d3 dr = mk(X[0], X[1], X[2]);
+    const double drn = norm(dr);
+    const d3 axis = drn > 0 ? mk(dr.x / drn, dr.y / drn, dr.z / drn) : dr;
+    const double ha = 0.5 * (drn / 2);
+    const double sh = sin(ha);
+    dq dqq; dqq.x = sh * axis.x; dqq.y = sh * axis.y; dqq.z = sh * axis.z; dqq.w = cos(ha);
+    dq q; q.x = S.x[0]; q.y = S.x[1]; q.z = S.x[2]; q.w = S.x[3];
+    dq qn = qmul(q, dqq);
+    S.x[0] = qn.x; S.x[1] = qn.y; S.x[2] = qn.z; S.x[3] = qn.w;
+    const float deltaR = (float)(drn / 2);
+    const float deltaT = (float)sqrt(pow(X[3] * 100, 2.0) + pow(X[4] * 100, 2.0) + pow(X[5] * 100, 2.0));
+    if (deltaR < 0.0009f && deltaT < 0.05f) {
+        S.gn_converged = 1;
+        S.term = LMSF_TERM_GN_CONVERGED;
+    } else {
+        S.term = LMSF_TERM_MAX_ITERATIONS;
+    }
+    gn_record_trace(S, outer);
+}
+
+// GN accumulation: J row = grad^T [-R [p]x, I] (edgeSurf...:255-265) over the first
+// (count mod 65536) matches of each kind in query order (uint16_t counters, :58-59).
+__global__ __launch_bounds__(256) void gn_accum_kernel(BatchView bv) {
+    const int b = blockIdx.y;
+    SolveState& S = bv.st[b];
+    const int ne = bv.n_edge[b], ns = bv.n_surf[b];
+    const int nq = ne + ns;
+    if (blockIdx.x * kFitBlock >= nq) return;
+    if (S.gn_converged) return;
+    __shared__ int wcnt[2][4];
+    __shared__ int base_e, base_s;
+    __shared__ double red[4][kPacket];
+    const int q = blockIdx.x * kFitBlock + threadIdx.x;
+    const size_t slot = (size_t)b * bv.feat_stride + q;
+    const double* gr = bv.gn_rows + slot * 4;
+    const bool valid = q < nq && gr[3] >= 0.0;
+    const bool is_edge = q < ne;
+    if (threadIdx.x == 0) {  // matches in earlier blocks (fit_eval's per-block counts)
+        double e = 0.0, s = 0.0;
+        const double* pb = bv.partials + (size_t)b * bv.max_parts * kPacket;
+        for (int p = 0; p < (int)blockIdx.x; ++p) { e += pb[(size_t)p * kPacket + 29]; s += pb[(size_t)p * kPacket + 30]; }
+        base_e = (int)e;
+        base_s = (int)s;
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long me = __ballot(valid && is_edge), ms = __ballot(valid && !is_edge);
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    if (lane == 0) { wcnt[0][wave] = __popcll(me); wcnt[1][wave] = __popcll(ms); }
+    __syncthreads();
+    int rank = 0;
+    for (int w = 0; w < wave; ++w) rank += is_edge ? wcnt[0][w] : wcnt[1][w];
+    rank += __popcll((is_edge ? me : ms) & below) + (is_edge ? base_e : base_s);
+    double P[kPacket];
+    for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
+    if (valid && rank < 65536) {
+        const float4 p4 = bv.feat[slot];
+        const d3 p = mk((double)p4.x, (double)p4.y, (double)p4.z);
+        double R[9];
+        dq qq; qq.x = S.x[0]; qq.y = S.x[1]; qq.z = S.x[2]; qq.w = S.x[3];
+        qmat(qq, R);
+        const double sk[9] = {0., -p.z, p.y, p.z, 0., -p.x, -p.y, p.x, 0.};
+        double M[9];
+        for (int a = 0; a < 3; ++a)
+            for (int c = 0; c < 3; ++c)
+                M[a * 3 + c] = (-R[a * 3 + 0]) * sk[0 * 3 + c] + (-R[a * 3 + 1]) * sk[1 * 3 + c] + (-R[a * 3 + 2]) * sk[2 * 3 + c];
+        double J[6];
+        for (int c = 0; c < 3; ++c) J[c] = gr[0] * M[0 * 3 + c] + gr[1] * M[1 * 3 + c] + gr[2] * M[2 * 3 + c];
+        J[3] = gr[0]; J[4] = gr[1]; J[5] = gr[2];
+        const double res = gr[3];
+        for (int i = 0; i < 6; ++i)
+            for (int j = i; j < 6; ++j) P[1 + hidx(i, j)] += J[i] * J[j];
+        for (int i = 0; i < 6; ++i) P[22 + i] += J[i] * res;
+    }
+    if (valid) { if (is_edge) P[29] = 1.0; else P[30] = 1.0; }
+    for (int i = 0; i < kPacket; ++i) {
+        double v = P[i];
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        P[i] = v;
+    }
+    if (lane == 0)
+        for (int i = 0; i < kPacket; ++i) red[wave][i] = P[i];
+    __syncthreads();
+    if (threadIdx.x < kPacket) {
+        const int i = threadIdx.x;
+        bv.partials_gn[((size_t)b * bv.max_parts + blockIdx.x) * kPacket + i] =
+            ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+    }
+}
+
+hipError_t launch_state_init(const BatchView& bv, const double* poses, hipStream_t s) {
+    hipLaunchKernelGGL(state_init_kernel, dim3((bv.B + 63) / 64), dim3(64), 0, s, bv, poses);
+    return hipGetLastError();
+}
+
+hipError_t launch_lm_begin(const BatchView& bv, hipStream_t s) {
+    hipLaunchKernelGGL(lm_begin_kernel, dim3(bv.B), dim3(64), 0, s, bv);
+    return hipGetLastError();
+}
+
+hipError_t launch_lm_step(const BatchView& bv, int outer, int is_last, hipStream_t s) {
+    hipLaunchKernelGGL(lm_step_kernel, dim3(bv.B), dim3(64), 0, s, bv, outer, is_last);
+    return hipGetLastError();
+}
+
+hipError_t launch_gn_solve(const BatchView& bv, int outer, hipStream_t s) {
+    dim3 grid((bv.feat_stride + kFitBlock - 1) / kFitBlock, bv.B);
+    hipLaunchKernelGGL(gn_accum_kernel, grid, dim3(256), 0, s, bv);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(gn_solve_kernel, dim3(bv.B), dim3(64), 0, s, bv, outer);
+    return hipGetLastError();
+}
+
+}  // namespace lmsf

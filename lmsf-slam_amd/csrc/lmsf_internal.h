@@ -1,0 +1,117 @@
+// Internal device/host interfaces of liblmsf_hip.so (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/lmsf/lmsf.h"
+
+namespace lmsf {
+
+constexpr int kMaxOuter = 32;        // trace rows kept per solve
+constexpr int kPacket = 32;          // doubles per partial packet (29 used + edge/surf counts)
+constexpr int kFitBlock = 256;       // queries per fit/eval block (one per thread)
+constexpr int kEvalPerThread = 4;    // records per thread in the LM evaluation kernel
+constexpr int kEvalBlock = 256 * kEvalPerThread;
+constexpr int kRingMax = 8192;       // points per ring handled by the extraction kernel
+constexpr int kSortMax = 2048;       // points per sector (ring / 6 + 5, padded to a power of two)
+constexpr int kMaxRings = 128;
+constexpr int kEdgePerRing = 120;    // 20 per sector x 6 sectors (FX:172)
+constexpr int kTile = 2048;          // raw points per ring-split tile
+constexpr int kCounterShards = 64;   // candidate / query counters, 16 u64 (128 B) apart
+
+// Dense cell grid over one feature map: cell = floor(coord) - origin, 1 m cells (the match
+// radius: search_thresh_ = 1.0 squared metres, REG/FeatureMatch/FeatureMatchBase.hpp:29).
+struct GridView {
+    int ox, oy, oz;
+    int nx, ny, nz;
+    const uint32_t* off;   // nx*ny*nz + 1 exclusive offsets into pts
+    const float4* pts;     // points sorted by cell; w = original index (int bits)
+    const float4* orig;    // points in the caller's order (x, y, z, intensity)
+    int n;
+};
+
+// Per-registration solver state (device resident, one per batch slot).
+struct SolveState {
+    double x[7];       // accepted pose (qx qy qz qw tx ty tz)
+    double xc[7];      // candidate pose awaiting evaluation
+    double H[21];
+    double g[6];
+    double s[6];       // Jacobi scaling, fixed per ceres::Solve
+    double cost, radius, decrease, mcc, x_norm, initial_cost;
+    int iteration, need_eval, done, term;
+    int evals, nmatch, edge_matches, surf_matches;
+    int inner_total, evals_total, outer_run, gn_converged;
+    int gn_degenerate, pad0, pad1, pad2;
+    double gn_map[36];
+    double trace[kMaxOuter][7];
+};
+
+struct BatchView {
+    int B;                   // slots in this launch
+    int feat_stride;         // features per slot (capacity)
+    const float4* feat;      // [B][feat_stride]: edges then surfs
+    const int* n_edge;       // [B]
+    const int* n_surf;       // [B]
+    int* nn;                 // [B][feat_stride][5]
+    lmsf_record* rec;        // [B][feat_stride]
+    double* partials;        // [B][max_parts][kPacket]
+    int max_parts;
+    SolveState* st;          // [B]
+    unsigned long long* n27; // [kCounterShards][16]: [0] candidates, [1] queries (may be null)
+    double* gn_rows;         // [B][feat_stride][4] grad + residual (GN only)
+    double* partials_gn;     // [B][max_parts][kPacket] (GN only)
+};
+
+// ---- launchers (each enqueues on `stream`, never synchronises)
+hipError_t launch_map_bbox(const float4* pts, int n, int* bbox, hipStream_t s);
+hipError_t launch_map_count(const float4* pts, int n, int ox, int oy, int oz, int nx, int ny, int nz,
+                            int* cell, uint32_t* counts, hipStream_t s);
+hipError_t launch_map_scatter(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
+                              float4* sorted, hipStream_t s);
+hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, void* tmp, size_t& tmp_bytes, hipStream_t s);
+
+hipError_t launch_knn(const GridView& edge, const GridView& surf, const BatchView& bv, int skip_converged,
+                      hipStream_t s);
+hipError_t launch_fit_eval(const GridView& edge, const GridView& surf, const BatchView& bv, int solver,
+                           hipStream_t s);
+hipError_t launch_lm_begin(const BatchView& bv, hipStream_t s);
+hipError_t launch_lm_eval(const BatchView& bv, hipStream_t s);
+hipError_t launch_lm_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
+hipError_t launch_gn_solve(const BatchView& bv, int outer, hipStream_t s);
+hipError_t launch_state_init(const BatchView& bv, const double* poses, hipStream_t s);
+// Standalone evaluation at one pose (diagnostics): packet of slot 0 into out29 (device).
+hipError_t launch_eval_at(const BatchView& bv, const double* pose_dev, double* out_dev, hipStream_t s);
+
+// ---- feature extraction (LOAMFeatureProcessorBase::Process)
+struct ExtractView {
+    int B;
+    int raw_stride;              // raw points per slot (capacity)
+    const float4* raw;           // [B][raw_stride]
+    const int* raw_count;        // [B]
+    int8_t* ring_id;             // [B][raw_stride]  (-1 rejected)
+    int n_tiles;                 // tiles per slot (capacity)
+    int* tile_counts;            // [B][kMaxRings][n_tiles]
+    int* ring_start;             // [B][kMaxRings + 1]
+    float4* ring_pts;            // [B][raw_stride] ring-ordered points
+    int* ring_src;               // [B][raw_stride] raw index of each ring-ordered point
+    float4* surf_stage;          // [B][raw_stride]   per ring at ring_start
+    int* surf_stage_src;         // [B][raw_stride]
+    float4* edge_stage;          // [B][kMaxRings * kEdgePerRing]
+    int* edge_stage_src;         // [B][kMaxRings * kEdgePerRing]
+    int* ring_edge_cnt;          // [B][kMaxRings]
+    int* ring_surf_cnt;          // [B][kMaxRings]
+    float4* feat;                // [B][feat_stride] output (edges then surfs)
+    int* feat_src;               // [B][feat_stride]
+    int feat_stride;
+    int* n_edge;                 // [B]
+    int* n_surf;                 // [B]
+    int* error;                  // [1] capacity flags
+    // parameters
+    int n_scans;
+    float min_d, max_d, edge_thresh;
+    int remove_bad;
+    double beam_lo, beam_spacing;
+};
+hipError_t launch_extract(const ExtractView& ev, hipStream_t s);
+
+}  // namespace lmsf

@@ -1,0 +1,235 @@
+"""ctypes binding of liblmsf_hip.so (the C ABI declared in include/lmsf/lmsf.h).
+
+The HIP library is the product path: there is no CPU fallback.  Importing this module on a
+machine without the built library raises immediately; calling into it without a GPU returns
+LMSF_ERR_HIP, which is raised as LmsfError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # lmsf-slam_amd/
+LIB_PATH = os.path.join(PKG_ROOT, "liblmsf_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "lmsf", "lmsf.h")
+
+OK, ERR_ARG, ERR_HIP, ERR_NO_MAP, ERR_CAPACITY, ERR_STATE = 0, -1, -2, -3, -4, -5
+EDGE, SURF = 1, 2
+SOLVER_CERES_LM, SOLVER_GN = 0, 1
+SCHEDULE_REFERENCE_DECAY, SCHEDULE_FIXED = 0, 1
+TERM_NAMES = {0: "max_iterations", 1: "function_tol", 2: "parameter_tol", 3: "gradient_tol",
+              4: "no_residuals", 5: "gn_converged", 6: "gn_too_few"}
+
+RECORD_DTYPE = np.dtype([("p", np.float32, 3), ("kind", np.int32), ("v0", np.float64, 3), ("v1", np.float64, 3)])
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("solver", C.c_int32), ("schedule", C.c_int32),
+                ("max_iterations", C.c_int32), ("max_batch", C.c_int32), ("max_scan_points", C.c_int32),
+                ("max_features", C.c_int32), ("n_scans", C.c_int32), ("min_distance", C.c_float),
+                ("max_distance", C.c_float), ("edge_threshold", C.c_float), ("remove_bad_points", C.c_int32),
+                ("beam_lo_deg", C.c_double), ("beam_spacing_deg", C.c_double)]
+
+
+class SolveStats(C.Structure):
+    _fields_ = [("outer_iterations", C.c_int32), ("edge_matches", C.c_int32), ("surf_matches", C.c_int32),
+                ("inner_iterations", C.c_int32), ("evaluations", C.c_int32), ("termination", C.c_int32),
+                ("initial_cost", C.c_double), ("final_cost", C.c_double)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class FeatureCounts(C.Structure):
+    _fields_ = [("n_edge", C.c_int64), ("n_surf", C.c_int64)]
+
+
+class KernelStats(C.Structure):
+    _fields_ = [("launches", C.c_int64), ("total_ms", C.c_double), ("queries", C.c_int64), ("n27_sum", C.c_int64)]
+
+
+class LmsfError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"lmsf error {code}: {msg}")
+        self.code = code
+
+
+# every entry point of include/lmsf/lmsf.h: name -> (restype, argtypes)
+_P = C.c_void_p
+_SIGS = {
+    "lmsf_config_init": (C.c_int32, [C.POINTER(Config)]),
+    "lmsf_ctx_create": (C.c_int32, [C.POINTER(Config), C.POINTER(_P)]),
+    "lmsf_ctx_destroy": (None, [_P]),
+    "lmsf_last_error": (C.c_char_p, [_P]),
+    "lmsf_set_map": (C.c_int32, [_P, C.c_int32, _P, C.c_size_t]),
+    "lmsf_set_scan": (C.c_int32, [_P, C.c_int32, _P, C.c_size_t]),
+    "lmsf_set_max_iterations": (C.c_int32, [_P, C.c_int32]),
+    "lmsf_solve": (C.c_int32, [_P, _P, C.POINTER(SolveStats)]),
+    "lmsf_solve_trace": (C.c_int32, [_P, _P, C.c_int32, C.POINTER(C.c_int32)]),
+    "lmsf_extract_features": (C.c_int32, [_P, _P, C.c_size_t, C.POINTER(FeatureCounts)]),
+    "lmsf_copy_features": (C.c_int32, [_P, C.c_int32, _P, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "lmsf_batch_load_scans": (C.c_int32, [_P, _P, _P, C.c_int32]),
+    "lmsf_batch_run": (C.c_int32, [_P, C.c_int32, _P, _P]),
+    "lmsf_batch_launch": (C.c_int32, [_P, C.c_int32, _P]),
+    "lmsf_batch_wait": (C.c_int32, [_P, C.c_int32, _P, _P]),
+    "lmsf_batch_copy_features": (C.c_int32, [_P, C.c_int32, C.c_int32, _P, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "lmsf_match": (C.c_int32, [_P, _P, _P, _P, C.c_size_t]),
+    "lmsf_eval": (C.c_int32, [_P, _P, _P]),
+    "lmsf_kernel_stats_get": (C.c_int32, [_P, C.POINTER(KernelStats)]),
+    "lmsf_kernel_stats_reset": (C.c_int32, [_P, C.c_int32]),
+    "lmsf_version": (C.c_char_p, []),
+}
+
+_lib = None
+
+
+def load():
+    """Load liblmsf_hip.so (raises if it has not been built: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `make -C lmsf-slam_amd` "
+                              "(__graft_entry__.build()); the HIP path has no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def default_config(**kw) -> Config:
+    cfg = Config()
+    load().lmsf_config_init(C.byref(cfg))
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+def _f4(a):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    if a.ndim != 2 or a.shape[1] != 4:
+        raise ValueError("points must be (N, 4) float32 x y z intensity")
+    return a
+
+
+class Context:
+    """One lmsf_ctx: a registration object + feature processor bound to one device stream."""
+
+    def __init__(self, **cfg):
+        self.cfg = default_config(**cfg)
+        h = C.c_void_p()
+        rc = load().lmsf_ctx_create(C.byref(self.cfg), C.byref(h))
+        if rc != OK:
+            raise LmsfError(rc, "lmsf_ctx_create failed (no HIP device or bad config)")
+        self.h = h
+
+    def _check(self, rc):
+        if rc != OK:
+            raise LmsfError(rc, load().lmsf_last_error(self.h).decode(errors="replace"))
+        return rc
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().lmsf_ctx_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    # ---- reference surface
+    def set_map(self, kind, pts):
+        p = _f4(pts)
+        self._check(load().lmsf_set_map(self.h, kind, p.ctypes.data, p.shape[0]))
+
+    def set_scan(self, kind, pts):
+        p = _f4(pts) if len(pts) else np.zeros((0, 4), np.float32)
+        self._check(load().lmsf_set_scan(self.h, kind, p.ctypes.data, p.shape[0]))
+
+    def set_max_iterations(self, n):
+        self._check(load().lmsf_set_max_iterations(self.h, int(n)))
+
+    def solve(self, pose):
+        x = np.ascontiguousarray(pose, dtype=np.float64).copy()
+        st = SolveStats()
+        self._check(load().lmsf_solve(self.h, x.ctypes.data, C.byref(st)))
+        return x, st
+
+    def trace(self, cap=32):
+        out = np.zeros((cap, 7), np.float64)
+        n = C.c_int32()
+        self._check(load().lmsf_solve_trace(self.h, out.ctypes.data, cap, C.byref(n)))
+        return out[:min(n.value, cap)].copy()
+
+    def extract(self, pts):
+        p = _f4(pts) if len(pts) else np.zeros((0, 4), np.float32)
+        fc = FeatureCounts()
+        self._check(load().lmsf_extract_features(self.h, p.ctypes.data, p.shape[0], C.byref(fc)))
+        return fc.n_edge, fc.n_surf
+
+    def copy_features(self, kind, slot=None):
+        n = C.c_size_t()
+        cap = int(self.cfg.max_scan_points) if slot is not None else max(int(self.cfg.max_features),
+                                                                          int(self.cfg.max_scan_points))
+        out = np.zeros((cap, 4), np.float32)
+        src = np.zeros(cap, np.int32)
+        if slot is None:
+            self._check(load().lmsf_copy_features(self.h, kind, out.ctypes.data, src.ctypes.data, cap, C.byref(n)))
+        else:
+            self._check(load().lmsf_batch_copy_features(self.h, slot, kind, out.ctypes.data, src.ctypes.data, cap,
+                                                         C.byref(n)))
+        return out[:n.value].copy(), src[:n.value].copy()
+
+    # ---- batch path
+    def load_scans(self, scans):
+        counts = np.array([len(s) for s in scans], np.int64)
+        cat = np.ascontiguousarray(np.concatenate([_f4(s) for s in scans], 0)) if counts.sum() else np.zeros((0, 4), np.float32)
+        self._check(load().lmsf_batch_load_scans(self.h, cat.ctypes.data, counts.ctypes.data, len(scans)))
+
+    def batch_run(self, poses):
+        x = np.ascontiguousarray(poses, dtype=np.float64).copy()
+        n = x.shape[0]
+        st = (SolveStats * n)()
+        self._check(load().lmsf_batch_run(self.h, n, x.ctypes.data, C.cast(st, C.c_void_p)))
+        return x, list(st)
+
+    def batch_launch(self, poses):
+        x = np.ascontiguousarray(poses, dtype=np.float64)
+        self._check(load().lmsf_batch_launch(self.h, x.shape[0], x.ctypes.data))
+
+    def batch_wait(self, n):
+        x = np.zeros((n, 7), np.float64)
+        st = (SolveStats * n)()
+        self._check(load().lmsf_batch_wait(self.h, n, x.ctypes.data, C.cast(st, C.c_void_p)))
+        return x, list(st)
+
+    # ---- diagnostics
+    def match(self, pose, n_queries):
+        rec = np.zeros(n_queries, RECORD_DTYPE)
+        nn = np.zeros((n_queries, 5), np.int32)
+        x = np.ascontiguousarray(pose, dtype=np.float64)
+        self._check(load().lmsf_match(self.h, x.ctypes.data, rec.ctypes.data, nn.ctypes.data, n_queries))
+        return rec, nn
+
+    def eval(self, pose):
+        out = np.zeros(29, np.float64)
+        x = np.ascontiguousarray(pose, dtype=np.float64)
+        self._check(load().lmsf_eval(self.h, x.ctypes.data, out.ctypes.data))
+        return out
+
+    def kernel_stats_reset(self, timing=True):
+        self._check(load().lmsf_kernel_stats_reset(self.h, int(timing)))
+
+    def kernel_stats(self):
+        ks = KernelStats()
+        self._check(load().lmsf_kernel_stats_get(self.h, C.byref(ks)))
+        return ks
+
+
+def header_symbols(path=HEADER_PATH):
+    """Function names declared in include/lmsf/lmsf.h (for the ABI export test)."""
+    import re
+    text = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:lmsf_status|void|const char\*)\s+(lmsf_\w+)\s*\(", text, re.M)))
