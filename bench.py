@@ -27,7 +27,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=32, help="scans per GPU per step")
+    ap.add_argument("--batch", type=int, default=64, help="scans per GPU per step")
     ap.add_argument("--unique-scans", type=int, default=8, help="distinct synthetic scans per rank")
     ap.add_argument("--map-points", type=int, default=1_000_000)
     ap.add_argument("--cols", type=int, default=4096)

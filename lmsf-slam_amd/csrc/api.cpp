@@ -62,7 +62,7 @@ struct lmsf_ctx {
     int* feat_src = nullptr;
     int* n_edge = nullptr;
     int* n_surf = nullptr;
-    int* nn = nullptr;
+    float4* nnp = nullptr;
     lmsf_record* rec = nullptr;
     double* partials = nullptr;
     double* partials_gn = nullptr;
@@ -119,7 +119,8 @@ struct lmsf_ctx {
         v.feat = feat;
         v.n_edge = n_edge;
         v.n_surf = n_surf;
-        v.nn = nn;
+        v.nnp = nnp;
+        v.fit_per_thread = fit_per_thread_default();
         v.rec = rec;
         v.partials = partials;
         v.max_parts = max_parts;
@@ -335,7 +336,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
         hipFree(m.orig); hipFree(m.pts); hipFree(m.cell); hipFree(m.counts); hipFree(m.off); hipFree(m.fill);
         hipFree(m.scan_tmp);
     }
-    void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nn, c->rec, c->partials, c->partials_gn,
+    void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->rec, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->edge_stage,
                     c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->d_error};
@@ -364,7 +365,7 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     c->B = cfg->max_batch;
     c->R = cfg->max_scan_points;
     c->F = std::max(cfg->max_features, cfg->max_scan_points);
-    c->max_parts = (c->F + kFitBlock - 1) / kFitBlock;
+    c->max_parts = (c->F + 255) / 256;   // worst case: one query per fit thread
     c->n_tiles = (c->R + kTile - 1) / kTile;
     auto bail = [&](lmsf_status code) {
         lmsf_ctx_destroy(c);
@@ -381,7 +382,7 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->feat_src, B * F));
     CHK(dalloc(&c->n_edge, B));
     CHK(dalloc(&c->n_surf, B));
-    CHK(dalloc(&c->nn, B * F * 5));
+    CHK(dalloc(&c->nnp, B * F * 5));
     CHK(dalloc(&c->rec, B * F));
     CHK(dalloc(&c->partials, B * c->max_parts * kPacket));
     CHK(dalloc(&c->st, B));
@@ -612,8 +613,16 @@ lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int3
     HIPCHK(c, launch_knn(ge, gs, bv, 0, c->stream));
     HIPCHK(c, launch_fit_eval(ge, gs, bv, LMSF_SOLVER_CERES_LM, c->stream));
     if (nq && out) HIPCHK(c, hipMemcpyAsync(out, c->rec, nq * sizeof(lmsf_record), hipMemcpyDeviceToHost, c->stream));
-    if (nq && nn) HIPCHK(c, hipMemcpyAsync(nn, c->nn, nq * 5 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    std::vector<float4> pts(nn ? nq * 5 : 0);
+    if (nq && nn) HIPCHK(c, hipMemcpyAsync(pts.data(), c->nnp, nq * 5 * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nn) {  // neighbour points carry their map index in w (-1: rank not found with d^2 < 1)
+        for (size_t i = 0; i < nq * 5; ++i) {
+            int32_t v;
+            std::memcpy(&v, &pts[i].w, sizeof v);
+            nn[i] = v;
+        }
+    }
     return LMSF_OK;
 }
 

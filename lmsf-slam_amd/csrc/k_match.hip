@@ -21,25 +21,28 @@ namespace lmsf {
 
 namespace {
 
-constexpr int kTeam = 16;                       // lanes cooperating on one query
-constexpr int kTeamsPerBlock = 256 / kTeam;
 constexpr uint64_t kSentinel = (uint64_t)0x3f800000u << 32;  // key of d2 == 1.0f, idx 0
 
+template <int T>
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
     uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-    lo = __shfl_xor(lo, m, kTeam);
-    hi = __shfl_xor(hi, m, kTeam);
+    lo = __shfl_xor(lo, m, T);
+    hi = __shfl_xor(hi, m, T);
     return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ int shfl_int(int v, int src) { return __shfl(v, src, kTeam); }
 
-__device__ __forceinline__ void insert5(uint64_t key, uint64_t (&k)[5]) {
+// sorted insertion of (key, position) into a lane's ascending top-5
+__device__ __forceinline__ void insert5(uint64_t key, int pos, uint64_t (&k)[5], int (&p)[5]) {
     if (key < k[4]) {
         k[4] = key;
-        if (k[4] < k[3]) { uint64_t t = k[3]; k[3] = k[4]; k[4] = t; }
-        if (k[3] < k[2]) { uint64_t t = k[2]; k[2] = k[3]; k[3] = t; }
-        if (k[2] < k[1]) { uint64_t t = k[1]; k[1] = k[2]; k[2] = t; }
-        if (k[1] < k[0]) { uint64_t t = k[0]; k[0] = k[1]; k[1] = t; }
+        p[4] = pos;
+#pragma unroll
+        for (int i = 4; i >= 1; --i) {
+            if (k[i] < k[i - 1]) {
+                uint64_t t = k[i - 1]; k[i - 1] = k[i]; k[i] = t;
+                int u = p[i - 1]; p[i - 1] = p[i]; p[i] = u;
+            }
+        }
     }
 }
 
@@ -52,19 +55,38 @@ __device__ __forceinline__ float3 associate(const Pose& P, float4 p) {
 
 }  // namespace
 
-// One team of kTeam lanes per query.  The 27 cells around the query cell are enumerated as 9
+// Block id -> (query block, scan).  With remap, the 8 XCDs (blocks are dealt round-robin: b and
+// b + 8 share one) each walk one contiguous eighth of the logical block range, so the queries an
+// XCD has in flight are neighbours along the same rings and reuse that XCD's 4 MB L2.  Speed
+// only: the mapping is a bijection and results do not depend on placement.
+__device__ __forceinline__ void block_coords(int remap, int gx, int& x, int& b) {
+    const int L = blockIdx.x, total = gridDim.x;
+    int logical = L;
+    if (remap) {
+        const int q = total >> 3, r = total & 7, xcd = L & 7, k = L >> 3;
+        logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+    }
+    b = logical / gx;
+    x = logical - b * gx;
+}
+
+// One team of T lanes per query.  The 27 cells around the query cell are enumerated as 9
 // x-rows (each row = 3 consecutive cells = one contiguous range of the cell-sorted points); the
 // team strides over the flattened candidate list with coalesced float4 loads, keeps a per-lane
-// sorted top-5 of (d2 bits, map index) keys with d2 < 1, then merges the lanes' lists.
-__global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, BatchView bv, int skip_converged) {
+// sorted top-5 of (d2 bits, map index) keys with d2 < 1 (plus each key's position in the sorted
+// array), then merges the lanes' lists.  Output: sorted-array positions of the 5 neighbours.
+template <int T>
+__global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, BatchView bv, int skip_converged,
+                                                  int gx, int remap) {
     __shared__ unsigned long long blk_n27;
     __shared__ unsigned int blk_q;
-    const int b = blockIdx.y;
+    int bx, b;
+    block_coords(remap, gx, bx, b);
     if (threadIdx.x == 0) { blk_n27 = 0; blk_q = 0; }
     __syncthreads();
     const int ne = bv.n_edge[b], ns = bv.n_surf[b];
-    const int team = threadIdx.x / kTeam, lane = threadIdx.x % kTeam;
-    const int q = blockIdx.x * kTeamsPerBlock + team;
+    const int team = threadIdx.x / T, lane = threadIdx.x % T;
+    const int q = bx * (256 / T) + team;
     const bool active = q < ne + ns && !(skip_converged && bv.st[b].gn_converged);
     if (active) {
         const bool is_edge = q < ne;
@@ -72,33 +94,41 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Batc
         const Pose P = load_pose(bv.st[b].x);
         const float4 p = bv.feat[(size_t)b * bv.feat_stride + q];
         const float3 w = associate(P, p);
-        // rows: lanes 0..8 each resolve one (dy, dz) row of three x-cells
-        int rstart = 0, rlen = 0;
         const float fx = floorf(w.x), fy = floorf(w.y), fz = floorf(w.z);
         const bool inside = g.n > 0 && fx >= (float)(g.ox - 2) && fx <= (float)(g.ox + g.nx + 1) &&
                             fy >= (float)(g.oy - 2) && fy <= (float)(g.oy + g.ny + 1) &&
                             fz >= (float)(g.oz - 2) && fz <= (float)(g.oz + g.nz + 1);
-        if (inside && lane < 9) {
-            const int cx = (int)fx - g.ox, cy = (int)fy - g.oy + (lane % 3) - 1, cz = (int)fz - g.oz + (lane / 3) - 1;
-            const int xa = max(cx - 1, 0), xb = min(cx + 1, g.nx - 1);
-            if (cy >= 0 && cy < g.ny && cz >= 0 && cz < g.nz && xa <= xb) {
-                const size_t row = ((size_t)cz * g.ny + cy) * g.nx;
-                rstart = (int)g.off[row + xa];
-                rlen = (int)g.off[row + xb + 1] - rstart;
+        // rows: lane l resolves (dy, dz) rows l, l + T, ... of the 9
+        constexpr int REPS = (9 + T - 1) / T;
+        int rs_[REPS], rl_[REPS];
+#pragma unroll
+        for (int rep = 0; rep < REPS; ++rep) {
+            rs_[rep] = 0;
+            rl_[rep] = 0;
+            const int rr = lane + rep * T;
+            if (inside && rr < 9) {
+                const int cx = (int)fx - g.ox, cy = (int)fy - g.oy + (rr % 3) - 1, cz = (int)fz - g.oz + (rr / 3) - 1;
+                const int xa = max(cx - 1, 0), xb = min(cx + 1, g.nx - 1);
+                if (cy >= 0 && cy < g.ny && cz >= 0 && cz < g.nz && xa <= xb) {
+                    const size_t row = ((size_t)cz * g.ny + cy) * g.nx;
+                    rs_[rep] = (int)g.off[row + xa];
+                    rl_[rep] = (int)g.off[row + xb + 1] - rs_[rep];
+                }
             }
         }
         int st[9], pre[10];
         pre[0] = 0;
 #pragma unroll
         for (int r = 0; r < 9; ++r) {
-            st[r] = shfl_int(rstart, r);
-            pre[r + 1] = pre[r] + shfl_int(rlen, r);
+            st[r] = T == 1 ? rs_[r] : __shfl(rs_[r / T], r % T, T);
+            pre[r + 1] = pre[r] + (T == 1 ? rl_[r] : __shfl(rl_[r / T], r % T, T));
         }
         const int total = pre[9];
         uint64_t k[5] = {kSentinel, kSentinel, kSentinel, kSentinel, kSentinel};
+        int kp[5] = {0, 0, 0, 0, 0};   // sorted-array position of each kept key
         // current row r: candidates [rpre, rend) map to pts[rbase + (v - rpre)]
         int r = 0, rpre = 0, rend = pre[1], rbase = st[0];
-        for (int v = lane; v < total; v += kTeam) {
+        for (int v = lane; v < total; v += T) {
             while (v >= rend) {
                 ++r;
                 rpre = rend;
@@ -111,31 +141,41 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Batc
                 rend = e;
                 rbase = s0;
             }
-            const float4 m = g.pts[rbase + (v - rpre)];
+            const int pos = rbase + (v - rpre);
+            const float4 m = g.pts[pos];
             const float dx = w.x - m.x, dy = w.y - m.y, dz = w.z - m.z;
             const float d2 = dx * dx + dy * dy + dz * dz;
             const uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)__float_as_int(m.w);
-            insert5(key, k);
+            insert5(key, pos, k, kp);
         }
-        // merge: five rounds of team-min; the owning lane pops its head
+        // merge: five rounds of team-min; the owning lane pops its head and donates its position
         uint64_t res[5];
+        int rpos[5];
+        const int tbase = (threadIdx.x & 63) & ~(T - 1);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
             uint64_t mn = k[0];
 #pragma unroll
-            for (int o = kTeam / 2; o >= 1; o >>= 1) {
-                uint64_t t = shfl_xor_u64(mn, o);
+            for (int o = T / 2; o >= 1; o >>= 1) {
+                uint64_t t = shfl_xor_u64<T>(mn, o);
                 mn = t < mn ? t : mn;
             }
+            const unsigned long long own = __ballot(k[0] == mn);
+            const int owner = __ffsll((long long)((own >> tbase) & ((T == 64) ? ~0ull : ((1ull << T) - 1)))) - 1;
             res[i] = mn;
-            if (k[0] == mn) { k[0] = k[1]; k[1] = k[2]; k[2] = k[3]; k[3] = k[4]; k[4] = kSentinel; }
+            rpos[i] = __shfl(kp[0], owner < 0 ? 0 : owner, T);
+            if (k[0] == mn) {
+                k[0] = k[1]; k[1] = k[2]; k[2] = k[3]; k[3] = k[4]; k[4] = kSentinel;
+                kp[0] = kp[1]; kp[1] = kp[2]; kp[2] = kp[3]; kp[3] = kp[4];
+            }
         }
-        if (lane < 5) {
-            uint64_t mine = res[0];
+        // every rank written (lane i % T writes rank i; teams smaller than 5 write several): the
+        // neighbour point itself (just touched, L1/L2 resident), so the fit reads 80 contiguous bytes
+        float4* nn_out = bv.nnp + ((size_t)b * bv.feat_stride + q) * 5;
 #pragma unroll
-            for (int i = 1; i < 5; ++i) mine = (lane == i) ? res[i] : mine;
-            bv.nn[((size_t)b * bv.feat_stride + q) * 5 + lane] = mine < kSentinel ? (int)(uint32_t)mine : -1;
-        }
+        for (int i = 0; i < 5; ++i)
+            if (i % T == lane)
+                nn_out[i] = res[i] < kSentinel ? g.pts[rpos[i]] : make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
         if (lane == 0 && bv.n27) {
             atomicAdd(&blk_n27, (unsigned long long)total);
             atomicAdd(&blk_q, 1u);
@@ -144,7 +184,7 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Batc
     __syncthreads();
     if (threadIdx.x == 0 && bv.n27 && blk_q) {
         // 64 counter shards on separate 128-B lines: one word serialises ~1e5 block updates
-        unsigned long long* shard = bv.n27 + (size_t)((blockIdx.x + blockIdx.y) & (kCounterShards - 1)) * 16;
+        unsigned long long* shard = bv.n27 + (size_t)(blockIdx.x & (kCounterShards - 1)) * 16;
         atomicAdd(shard, blk_n27);
         atomicAdd(shard + 1, (unsigned long long)blk_q);
     }
@@ -153,12 +193,12 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Batc
 // ---------------------------------------------------------------- fits (double precision)
 
 // EdgeFeatureMatch::Match body after the 5-NN (EdgeFeatureMatch.hpp:44-80).
-__device__ bool edge_fit(const float4* mp, const int* nn, d3& a, d3& b) {
+__device__ bool edge_fit(const float4* np, d3& a, d3& b) {
     d3 pts[5];
     d3 center = mk(0, 0, 0);
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-        const float4 p = mp[nn[j]];
+        const float4 p = np[j];
         pts[j] = mk((double)p.x, (double)p.y, (double)p.z);
         center = center + pts[j];
     }
@@ -187,13 +227,10 @@ __device__ bool edge_fit(const float4* mp, const int* nn, d3& a, d3& b) {
 }
 
 // SurfFeatureMatch::Match body after the 5-NN (surfFeatureMatch.hpp:46-82).
-__device__ bool surf_fit(const float4* mp, const int* nn, float3 q, d3& n_out, double& D_out,
-                         double& gn_res) {
+__device__ bool surf_fit(const float4* p, float3 q, d3& n_out, double& D_out, double& gn_res) {
     double A[15], bb[5], x[3];
-    float4 p[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-        p[j] = mp[nn[j]];
         A[j * 3 + 0] = p[j].x; A[j * 3 + 1] = p[j].y; A[j * 3 + 2] = p[j].z;
         bb[j] = -1.0;
     }
@@ -239,37 +276,29 @@ __device__ __forceinline__ void block_reduce_packet(double* P, double* out) {
     }
 }
 
-// One thread per query: line / plane fit from the 5 neighbours, record write, and the
-// Huber-weighted normal-equation packet at the linearisation pose (Ceres' first evaluation).
-__global__ __launch_bounds__(256) void fit_eval_kernel(GridView ge, GridView gs, BatchView bv, int solver) {
-    const int b = blockIdx.y;
-    const int ne = bv.n_edge[b], ns = bv.n_surf[b];
-    const int nq = ne + ns;
-    if (blockIdx.x * kFitBlock >= nq) return;
-    if (solver == LMSF_SOLVER_GN && bv.st[b].gn_converged) return;
-    const int q = blockIdx.x * kFitBlock + threadIdx.x;
-    double P[kPacket];
-#pragma unroll
-    for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
-    if (q < nq) {
+// Line / plane fit of one query from its 5 neighbours, record write, and its Huber-weighted
+// normal-equation contribution at the linearisation pose (Ceres' first evaluation).
+__device__ __forceinline__ void fit_one(const BatchView& bv, int solver, int b, int q, int ne, const Pose& Ps,
+                                        double* P) {
+    {
         const bool is_edge = q < ne;
         const size_t slot = (size_t)b * bv.feat_stride + q;
         const float4 p = bv.feat[slot];
-        const Pose Ps = load_pose(bv.st[b].x);
         lmsf_record r;
         r.px = p.x; r.py = p.y; r.pz = p.z;
         r.kind = 0;
         r.v0[0] = r.v0[1] = r.v0[2] = 0.0;
         r.v1[0] = r.v1[1] = r.v1[2] = 0.0;
-        int nn[5];
+        // the 5 neighbour points, written contiguously by knn
+        float4 np[5];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) nn[j] = bv.nn[slot * 5 + j];
+        for (int j = 0; j < 5; ++j) np[j] = bv.nnp[slot * 5 + j];
         double gn_grad[3] = {0, 0, 0}, gn_res = 0.0;
-        if (nn[4] >= 0) {
+        if (__float_as_int(np[4].w) >= 0) {
             const float3 w = associate(Ps, p);
             if (is_edge) {
                 d3 a, bpt;
-                if (edge_fit(ge.orig, nn, a, bpt)) {
+                if (edge_fit(np, a, bpt)) {
                     r.kind = LMSF_EDGE;
                     r.v0[0] = a.x; r.v0[1] = a.y; r.v0[2] = a.z;
                     r.v1[0] = bpt.x; r.v1[1] = bpt.y; r.v1[2] = bpt.z;
@@ -288,7 +317,7 @@ __global__ __launch_bounds__(256) void fit_eval_kernel(GridView ge, GridView gs,
             } else {
                 d3 n;
                 double D;
-                if (surf_fit(gs.orig, nn, w, n, D, gn_res)) {
+                if (surf_fit(np, w, n, D, gn_res)) {
                     r.kind = LMSF_SURF;
                     r.v0[0] = n.x; r.v0[1] = n.y; r.v0[2] = n.z;
                     r.v1[0] = D;
@@ -309,8 +338,27 @@ __global__ __launch_bounds__(256) void fit_eval_kernel(GridView ge, GridView gs,
                 res = surf_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), r.v1[0], J);
             huber_accumulate(P, res, J);
         }
-        if (r.kind == LMSF_EDGE) P[29] = 1.0;
-        if (r.kind == LMSF_SURF) P[30] = 1.0;
+        if (r.kind == LMSF_EDGE) P[29] += 1.0;
+        if (r.kind == LMSF_SURF) P[30] += 1.0;
+    }
+}
+
+// FPT queries per thread (block = 256 * FPT queries): one packet reduction per block.
+template <int FPT>
+__global__ __launch_bounds__(256) void fit_eval_kernel(BatchView bv, int solver) {
+    const int b = blockIdx.y;
+    const int ne = bv.n_edge[b], ns = bv.n_surf[b];
+    const int nq = ne + ns;
+    if (blockIdx.x * 256 * FPT >= nq) return;
+    if (solver == LMSF_SOLVER_GN && bv.st[b].gn_converged) return;
+    const Pose Ps = load_pose(bv.st[b].x);
+    double P[kPacket];
+#pragma unroll
+    for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
+#pragma unroll
+    for (int k = 0; k < FPT; ++k) {
+        const int q = blockIdx.x * 256 * FPT + k * 256 + threadIdx.x;
+        if (q < nq) fit_one(bv, solver, b, q, ne, Ps, P);
     }
     block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + blockIdx.x) * kPacket);
 }
@@ -372,18 +420,66 @@ __global__ __launch_bounds__(256) void eval_at_kernel(BatchView bv, const double
     block_reduce_packet(P, bv.partials + (size_t)blockIdx.x * kPacket);
 }
 
+// Team size and XCD remap are tunables (LMSF_KNN_TEAM = 8 | 16 | 32, LMSF_XCD_REMAP = 0 | 1) for
+// A/B measurement; defaults are the measured best.
+static int knn_team() {
+    static int t = [] {
+        const char* e = getenv("LMSF_KNN_TEAM");
+        int v = e ? atoi(e) : 1;
+        return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 1;
+    }();
+    return t;
+}
+static int knn_remap() {
+    static int r = [] {
+        const char* e = getenv("LMSF_XCD_REMAP");
+        return e ? atoi(e) : 1;
+    }();
+    return r;
+}
+
 hipError_t launch_knn(const GridView& edge, const GridView& surf, const BatchView& bv, int skip_converged,
                       hipStream_t s) {
-    dim3 grid((bv.feat_stride + kTeamsPerBlock - 1) / kTeamsPerBlock, bv.B);
-    hipLaunchKernelGGL(knn_kernel, grid, dim3(256), 0, s, edge, surf, bv, skip_converged);
+    const int T = knn_team(), remap = knn_remap();
+    const int gx = (bv.feat_stride + (256 / T) - 1) / (256 / T);
+    const dim3 grid(gx * bv.B);
+    if (T == 8)
+        hipLaunchKernelGGL(knn_kernel<8>, grid, dim3(256), 0, s, edge, surf, bv, skip_converged, gx, remap);
+    else if (T == 1)
+        hipLaunchKernelGGL(knn_kernel<1>, grid, dim3(256), 0, s, edge, surf, bv, skip_converged, gx, remap);
+    else if (T == 2)
+        hipLaunchKernelGGL(knn_kernel<2>, grid, dim3(256), 0, s, edge, surf, bv, skip_converged, gx, remap);
+    else if (T == 4)
+        hipLaunchKernelGGL(knn_kernel<4>, grid, dim3(256), 0, s, edge, surf, bv, skip_converged, gx, remap);
+    else if (T == 32)
+        hipLaunchKernelGGL(knn_kernel<32>, grid, dim3(256), 0, s, edge, surf, bv, skip_converged, gx, remap);
+    else
+        hipLaunchKernelGGL(knn_kernel<16>, grid, dim3(256), 0, s, edge, surf, bv, skip_converged, gx, remap);
     return hipGetLastError();
 }
 
 hipError_t launch_fit_eval(const GridView& edge, const GridView& surf, const BatchView& bv, int solver,
                            hipStream_t s) {
-    dim3 grid((bv.feat_stride + kFitBlock - 1) / kFitBlock, bv.B);
-    hipLaunchKernelGGL(fit_eval_kernel, grid, dim3(256), 0, s, edge, surf, bv, solver);
+    (void)edge;
+    (void)surf;
+    const int per_block = 256 * bv.fit_per_thread;
+    dim3 grid((bv.feat_stride + per_block - 1) / per_block, bv.B);
+    switch (bv.fit_per_thread) {
+        case 1: hipLaunchKernelGGL(fit_eval_kernel<1>, grid, dim3(256), 0, s, bv, solver); break;
+        case 2: hipLaunchKernelGGL(fit_eval_kernel<2>, grid, dim3(256), 0, s, bv, solver); break;
+        default: hipLaunchKernelGGL(fit_eval_kernel<4>, grid, dim3(256), 0, s, bv, solver); break;
+    }
     return hipGetLastError();
+}
+
+// Queries per thread of fit_eval (LMSF_FIT_PER_THREAD = 1 | 2 | 4, for A/B measurement).
+int fit_per_thread_default() {
+    static int v = [] {
+        const char* e = getenv("LMSF_FIT_PER_THREAD");
+        int x = e ? atoi(e) : 2;
+        return (x == 1 || x == 2 || x == 4) ? x : 2;
+    }();
+    return v;
 }
 
 hipError_t launch_lm_eval(const BatchView& bv, hipStream_t s) {

@@ -161,7 +161,8 @@ __global__ void state_init_kernel(BatchView bv, const double* poses) {
 __global__ __launch_bounds__(64) void lm_begin_kernel(BatchView bv) {
     const int b = blockIdx.x;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
-    const int nparts = (nq + kFitBlock - 1) / kFitBlock;
+    const int fb = 256 * bv.fit_per_thread;
+    const int nparts = (nq + fb - 1) / fb;
     double tot[kPacket];
     reduce_parts(bv, b, nparts, tot);
     if (threadIdx.x != 0) return;
@@ -268,7 +269,8 @@ __global__ __launch_bounds__(64) void gn_solve_kernel(BatchView bv, int outer) {
     SolveState& S = bv.st[b];
     if (S.gn_converged) return;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
-    const int nparts = (nq + kFitBlock - 1) / kFitBlock;
+    const int fb = 256 * bv.fit_per_thread;
+    const int nparts = (nq + fb - 1) / fb;
     double tot[kPacket];
     BatchView g = bv;
     g.partials = bv.partials_gn;
@@ -362,16 +364,12 @@ __global__ __launch_bounds__(256) void gn_accum_kernel(BatchView bv) {
     SolveState& S = bv.st[b];
     const int ne = bv.n_edge[b], ns = bv.n_surf[b];
     const int nq = ne + ns;
-    if (blockIdx.x * kFitBlock >= nq) return;
+    const int fb = 256 * bv.fit_per_thread;
+    if (blockIdx.x * fb >= nq) return;
     if (S.gn_converged) return;
     __shared__ int wcnt[2][4];
     __shared__ int base_e, base_s;
     __shared__ double red[4][kPacket];
-    const int q = blockIdx.x * kFitBlock + threadIdx.x;
-    const size_t slot = (size_t)b * bv.feat_stride + q;
-    const double* gr = bv.gn_rows + slot * 4;
-    const bool valid = q < nq && gr[3] >= 0.0;
-    const bool is_edge = q < ne;
     if (threadIdx.x == 0) {  // matches in earlier blocks (fit_eval's per-block counts)
         double e = 0.0, s = 0.0;
         const double* pb = bv.partials + (size_t)b * bv.max_parts * kPacket;
@@ -380,15 +378,27 @@ __global__ __launch_bounds__(256) void gn_accum_kernel(BatchView bv) {
         base_s = (int)s;
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const unsigned long long me = __ballot(valid && is_edge), ms = __ballot(valid && !is_edge);
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    double P[kPacket];
+    for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
+    for (int chunk = 0; chunk < bv.fit_per_thread; ++chunk) {
+    const int q = blockIdx.x * fb + chunk * 256 + threadIdx.x;
+    const size_t slot = (size_t)b * bv.feat_stride + q;
+    const double* gr = bv.gn_rows + slot * 4;
+    const bool valid = q < nq && gr[3] >= 0.0;
+    const bool is_edge = q < ne;
+    __syncthreads();   // previous chunk's wcnt / base reads are complete
+    const unsigned long long me = __ballot(valid && is_edge), ms = __ballot(valid && !is_edge);
     if (lane == 0) { wcnt[0][wave] = __popcll(me); wcnt[1][wave] = __popcll(ms); }
     __syncthreads();
     int rank = 0;
     for (int w = 0; w < wave; ++w) rank += is_edge ? wcnt[0][w] : wcnt[1][w];
     rank += __popcll((is_edge ? me : ms) & below) + (is_edge ? base_e : base_s);
-    double P[kPacket];
-    for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        base_e += wcnt[0][0] + wcnt[0][1] + wcnt[0][2] + wcnt[0][3];
+        base_s += wcnt[1][0] + wcnt[1][1] + wcnt[1][2] + wcnt[1][3];
+    }
     if (valid && rank < 65536) {
         const float4 p4 = bv.feat[slot];
         const d3 p = mk((double)p4.x, (double)p4.y, (double)p4.z);
@@ -408,7 +418,8 @@ __global__ __launch_bounds__(256) void gn_accum_kernel(BatchView bv) {
             for (int j = i; j < 6; ++j) P[1 + hidx(i, j)] += J[i] * J[j];
         for (int i = 0; i < 6; ++i) P[22 + i] += J[i] * res;
     }
-    if (valid) { if (is_edge) P[29] = 1.0; else P[30] = 1.0; }
+    if (valid) { if (is_edge) P[29] += 1.0; else P[30] += 1.0; }
+    }  // chunk
     for (int i = 0; i < kPacket; ++i) {
         double v = P[i];
         for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -440,7 +451,8 @@ hipError_t launch_lm_step(const BatchView& bv, int outer, int is_last, hipStream
 }
 
 hipError_t launch_gn_solve(const BatchView& bv, int outer, hipStream_t s) {
-    dim3 grid((bv.feat_stride + kFitBlock - 1) / kFitBlock, bv.B);
+    const int fb = 256 * bv.fit_per_thread;
+    dim3 grid((bv.feat_stride + fb - 1) / fb, bv.B);
     hipLaunchKernelGGL(gn_accum_kernel, grid, dim3(256), 0, s, bv);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -9,7 +9,8 @@ namespace lmsf {
 
 constexpr int kMaxOuter = 32;        // trace rows kept per solve
 constexpr int kPacket = 32;          // doubles per partial packet (29 used + edge/surf counts)
-constexpr int kFitBlock = 256;       // queries per fit/eval block (one per thread)
+constexpr int kFitMaxPerThread = 4;  // queries per thread in the fit / first-evaluation kernel (1..4)
+constexpr int kFitBlockMax = 256 * kFitMaxPerThread;
 constexpr int kEvalPerThread = 4;    // records per thread in the LM evaluation kernel
 constexpr int kEvalBlock = 256 * kEvalPerThread;
 constexpr int kRingMax = 8192;       // points per ring handled by the extraction kernel
@@ -52,7 +53,8 @@ struct BatchView {
     const float4* feat;      // [B][feat_stride]: edges then surfs
     const int* n_edge;       // [B]
     const int* n_surf;       // [B]
-    int* nn;                 // [B][feat_stride][5]
+    float4* nnp;             // [B][feat_stride][5] neighbour points (w = map index bits, -1: none)
+    int fit_per_thread;      // queries per thread of fit_eval (partials per kFitThreads*fpt queries)
     lmsf_record* rec;        // [B][feat_stride]
     double* partials;        // [B][max_parts][kPacket]
     int max_parts;
@@ -78,6 +80,7 @@ hipError_t launch_lm_begin(const BatchView& bv, hipStream_t s);
 hipError_t launch_lm_eval(const BatchView& bv, hipStream_t s);
 hipError_t launch_lm_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
 hipError_t launch_gn_solve(const BatchView& bv, int outer, hipStream_t s);
+int fit_per_thread_default();
 hipError_t launch_state_init(const BatchView& bv, const double* poses, hipStream_t s);
 // Standalone evaluation at one pose (diagnostics): packet of slot 0 into out29 (device).
 hipError_t launch_eval_at(const BatchView& bv, const double* pose_dev, double* out_dev, hipStream_t s);
