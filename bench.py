@@ -56,7 +56,7 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
 
-    from lmsf import _lib, synth
+    from lmsf import _lib, multi, synth
 
     # ---------------- workload (C2), deterministic per rank: rank r registers its own scans
     U = max(1, min(args.unique_scans, args.batch))
@@ -84,8 +84,7 @@ def main():
         ctx.batch_launch(guesses)
         poses, stats = ctx.batch_wait(args.batch)
         if world > 1:
-            local_t = torch.from_numpy(poses).to(dev, non_blocking=True)
-            dist.all_gather_into_tensor(gathered, local_t.unsqueeze(0))
+            multi.gather_poses(poses, gathered, dev)     # RCCL all-gather of the 6-DoF poses
         return poses, stats
 
     for _ in range(args.warmup):
@@ -103,9 +102,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ks = ctx.kernel_stats()
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = multi.max_over_ranks(elapsed, dev)
 
     scans_total = args.batch * args.steps * world
     value = scans_total / elapsed

@@ -370,14 +370,16 @@ class Workload:
 
 
 def make_workload(config: str = "C2", n_scans: int = 4, map_points: int | None = None,
-                  n_cols: int | None = None, road_length: float = 80.0) -> Workload:
+                  n_cols: int | None = None, road_length: float = 80.0, radius: float | None = None) -> Workload:
+    """Scene, ground-truth trajectory, perturbed initial guesses, scans and the feature map.
+    `radius` / `road_length` shrink the mapped region for small test maps (keeps density)."""
     c = CONFIGS[config]
     k = c["k"]
-    scene = make_scene(1000 + k, road_length=road_length)
+    scene = make_scene(1000 + k, road_length=80.0)
     truth = trajectory(n_scans, 3000 + k, step=road_length / max(n_scans, 1))
     rng = np.random.default_rng(3000 + k)
     guess = np.stack([perturb(p, rng) for p in truth]) if n_scans else np.zeros((0, 7))
     scans = [make_scan(scene, truth[i], 2000 + k + 97 * i, n_cols=n_cols or c["n_cols"]) for i in range(n_scans)]
     em, sm = make_map(scene, map_points or c["map_points"], 1000 + k + 7, center_x=(0.0, road_length),
-                      radius=c["radius"])
+                      radius=radius or c["radius"])
     return Workload(scene, em, sm, scans, truth, guess)

@@ -1,0 +1,245 @@
+"""CPU checks of the oracle (the parity checker) against independent implementations.
+
+The reference has no runnable tests or golden vectors for this path, so
+the CPU restatement is pinned here by: scipy cKDTree (exact k-NN), numpy eigh (PCA line),
+numpy lstsq (plane fit), finite differences (Jacobians / gradient), closed-form SE(3) algebra
+(Plus), the reference's own commented-out known-answer test re-created on synthetic clouds
+(feature_registration_test.cpp:73-112: yaw 5 deg, t = (0.9, 0.4, 0.5)), and the committed
+golden fixtures under tests/golden/.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import pose_err
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    """C1-shaped scans (1800 columns) against a 100k-point map of a 40 m region: fast on one thread."""
+    from lmsf import synth
+    return synth.make_workload("C1", n_scans=2, map_points=100_000, n_cols=1800, road_length=20.0, radius=40.0)
+
+
+def test_kdtree_exact_vs_brute_and_scipy(oracle_mod):
+    from scipy.spatial import cKDTree
+    rng = np.random.default_rng(5)
+    pts = np.zeros((20000, 4), np.float32)
+    pts[:, :3] = rng.uniform(-20, 20, (20000, 3)).astype(np.float32)
+    pts[10000:10100, :3] = pts[:100, :3]              # exact duplicates -> distance ties
+    pts[:, :3] = np.round(pts[:, :3] * 4) / 4         # lattice values -> many equal distances
+    q = np.zeros((3000, 4), np.float32)
+    q[:, :3] = rng.uniform(-20, 20, (3000, 3)).astype(np.float32)
+    q[:500, :3] = pts[rng.integers(0, 20000, 500), :3]
+    m = oracle_mod.KdMap(pts)
+    i1, d1 = m.knn(q, 5)
+    i2, d2 = oracle_mod.brute_knn(pts, q, 5)
+    np.testing.assert_array_equal(i1, i2)
+    np.testing.assert_array_equal(d1, d2)
+    # scipy: same distance multiset (float64 distances; ties may be ordered differently)
+    dd, _ = cKDTree(pts[:, :3].astype(np.float64)).query(q[:, :3].astype(np.float64), k=5)
+    np.testing.assert_allclose(np.sqrt(d1.astype(np.float64)), dd, rtol=1e-5, atol=1e-5)
+    # ties are broken by ascending index
+    tie = d1[:, 1:] == d1[:, :-1]
+    assert tie.any() and (i1[:, 1:][tie] > i1[:, :-1][tie]).all()
+
+
+def _registration(oracle_mod, wl, scan_idx, solver=0):
+    e, s, _, _ = oracle_mod.extract(wl.scans[scan_idx])
+    reg = oracle_mod.Registration(solver)
+    reg.set_map(1, wl.edge_map)
+    reg.set_map(2, wl.surf_map)
+    reg.set_scan(1, e)
+    reg.set_scan(2, s)
+    return reg, e, s
+
+
+def test_edge_line_fit_vs_numpy(oracle_mod, tiny):
+    from lmsf import synth
+    reg, e, s = _registration(oracle_mod, tiny, 0)
+    rec, nn = reg.match(tiny.guess[0])
+    idx = np.nonzero(rec["kind"] == 1)[0]
+    assert len(idx) > 10
+    for i in idx[:200]:
+        P = tiny.edge_map[nn[i], :3].astype(np.float64)
+        c = P.mean(0)
+        w, V = np.linalg.eigh((P - c).T @ (P - c))
+        u = V[:, 2]
+        a, b = rec["v0"][i], rec["v1"][i]
+        np.testing.assert_allclose((a + b) / 2, c, atol=1e-9)
+        d = (a - b) / 0.2
+        assert abs(abs(d @ u) - 1.0) < 1e-9                      # same principal direction (sign free)
+        assert w[2] > 3 * w[1]                                    # linearity test passed (EdgeFeatureMatch.hpp:68)
+
+
+def test_surf_plane_fit_vs_lstsq(oracle_mod, tiny):
+    from lmsf import synth
+    reg, e, s = _registration(oracle_mod, tiny, 1)
+    rec, nn = reg.match(tiny.guess[1])
+    ne = len(e)
+    idx = ne + np.nonzero(rec["kind"][ne:] == 2)[0]
+    assert len(idx) > 1000
+    for i in idx[:500]:
+        A = tiny.surf_map[nn[i], :3].astype(np.float64)
+        x, *_ = np.linalg.lstsq(A, -np.ones(5), rcond=None)
+        D = 1.0 / np.linalg.norm(x)
+        n = x / np.linalg.norm(x)
+        got_n, got_D = rec["v0"][i], rec["v1"][i][0]
+        if got_n @ n < 0:
+            n, D = -n, -D
+        np.testing.assert_allclose(got_n, n, atol=1e-7)
+        assert abs(got_D - D) < 1e-6 * max(1.0, abs(D))
+        assert np.all(np.abs(A @ got_n + got_D) <= 0.2)          # plane validity (surfFeatureMatch.hpp:57-65)
+
+
+def _rotvec_to_mat(w):
+    th = np.linalg.norm(w)
+    if th < 1e-15:
+        return np.eye(3)
+    k = w / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + math.sin(th) * K + (1 - math.cos(th)) * K @ K
+
+
+def test_pose_plus_closed_form(oracle_mod):
+    from lmsf import synth
+    rng = np.random.default_rng(1)
+    for _ in range(50):
+        x = np.concatenate([synth.axis_angle_quat(rng.normal(0, 1, 3)), rng.normal(0, 10, 3)])
+        d = np.concatenate([rng.normal(0, 0.3, 3), rng.normal(0, 1, 3)])
+        out = oracle_mod.pose_plus(x, d)
+        w, u = d[:3], d[3:]
+        Rd = _rotvec_to_mat(w)
+        th = np.linalg.norm(w)
+        K = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
+        J = np.eye(3) + (1 - math.cos(th)) / th ** 2 * K + (th - math.sin(th)) / th ** 3 * K @ K
+        np.testing.assert_allclose(synth.quat_to_mat(out[:4]), Rd @ synth.quat_to_mat(x[:4]), atol=1e-12)
+        np.testing.assert_allclose(out[4:], Rd @ x[4:] + J @ u, atol=1e-10)
+    # small-angle branch (theta < 1e-10): Taylor factor, J = dq.matrix()
+    out = oracle_mod.pose_plus(np.array([0, 0, 0, 1.0, 1, 2, 3]), np.array([1e-12, 0, 0, 0.5, 0, 0]))
+    np.testing.assert_allclose(out[4:], [1.5, 2 - 3e-12, 3 + 2e-12], atol=1e-14)
+
+
+def test_gradient_and_hessian_vs_finite_differences(oracle_mod, tiny):
+    reg, e, s = _registration(oracle_mod, tiny, 0)
+    x0 = tiny.guess[0]
+    rec, _ = reg.match(x0)
+    rec = rec[rec["kind"] > 0]
+    P = oracle_mod.eval_records(rec, x0)
+    g = P[22:28]
+    h = 1e-7
+    num = np.zeros(6)
+    for k in range(6):
+        dp, dm = np.zeros(6), np.zeros(6)
+        dp[k], dm[k] = h, -h
+        cp = oracle_mod.eval_records(rec, oracle_mod.pose_plus(x0, dp))[0]
+        cm = oracle_mod.eval_records(rec, oracle_mod.pose_plus(x0, dm))[0]
+        num[k] = (cp - cm) / (2 * h)
+    np.testing.assert_allclose(g, num, rtol=2e-4, atol=1e-6 * np.abs(g).max())
+    assert P[28] == len(rec)
+    H = np.zeros((6, 6))
+    k = 1
+    for i in range(6):
+        for j in range(i, 6):
+            H[i, j] = H[j, i] = P[k]
+            k += 1
+    assert np.all(np.linalg.eigvalsh(H) > 0)                      # Gauss-Newton Hessian is SPD
+
+
+def test_extraction_invariants(oracle_mod, tiny):
+    scan = tiny.scans[0]
+    e, s, ei, si = oracle_mod.extract(scan)
+    assert len(e) > 0 and len(s) > 0.8 * len(scan)
+    assert len(set(ei.tolist()) | set(si.tolist())) == len(ei) + len(si)   # each point at most once
+    np.testing.assert_array_equal(e, scan[ei])
+    np.testing.assert_array_equal(s, scan[si])
+    # deterministic
+    e2, s2, ei2, si2 = oracle_mod.extract(scan)
+    np.testing.assert_array_equal(ei, ei2)
+    np.testing.assert_array_equal(si, si2)
+    # at most 20 edges per sector: 16 rings x 6 sectors
+    assert len(e) <= 16 * 6 * 20
+    # range gate 2 <= sqrt(x^2 + y^2) <= 80 (float expression as in splitScan)
+    d = np.sqrt((scan[:, 0] * scan[:, 0] + scan[:, 1] * scan[:, 1]).astype(np.float64))
+    used = np.concatenate([ei, si])
+    assert np.all((d[used] >= 2.0) & (d[used] <= 80.0))
+    # no bad-point removal and threshold 0.1 -> more edges
+    e3, *_ = oracle_mod.extract(scan, remove_bad_points=False, edge_threshold=0.1)
+    assert len(e3) >= len(e)
+    # empty / tiny inputs
+    e4, s4, _, _ = oracle_mod.extract(np.zeros((0, 4), np.float32))
+    assert len(e4) == len(s4) == 0
+    e5, s5, _, _ = oracle_mod.extract(scan[:50])
+    assert len(e5) == 0 and len(s5) == 0
+
+
+@pytest.mark.parametrize("solver", [0, 1])
+def test_known_answer_transform(oracle_mod, tiny, solver):
+    """feature_registration_test.cpp:73-112 re-created: target = source transformed by yaw 5 deg,
+    t = (0.9, 0.4, 0.5); solving from identity recovers the inverse transform."""
+    from lmsf import synth
+    c = tiny.truth[0][4:]
+    near = lambda m: m[np.linalg.norm(m[:, :3] - c, axis=1) < 30.0]
+    edge_src, surf_src = near(tiny.edge_map), near(tiny.surf_map)
+    T = np.concatenate([synth.quat_from_rpy(0, 0, math.radians(5)), [0.9, 0.4, 0.5]])
+    reg = oracle_mod.Registration(solver)
+    reg.set_map(1, edge_src)
+    reg.set_map(2, surf_src)
+    rng = np.random.default_rng(3)
+    reg.set_scan(1, synth.transform_points(T, edge_src[rng.permutation(len(edge_src))[:2000]]))
+    reg.set_scan(2, synth.transform_points(T, surf_src[rng.permutation(len(surf_src))[:20000]]))
+    reg.set_fixed_schedule(True)
+    # GN rotates by |dtheta|/2 per step (AngleAxis(norm/2, ...), edgeSurfFeatureRegistration.hpp:317),
+    # so it needs more iterations and its convergence gate (:326) stops ~3e-3 rad short
+    reg.set_max_iterations(10 if solver == 0 else 30)
+    x, tr, st = reg.solve(np.array([0, 0, 0, 1.0, 0, 0, 0]), trace_cap=32)
+    R = synth.quat_to_mat(T[:4])
+    inv = np.concatenate([synth.quat_from_rpy(0, 0, -math.radians(5)), -R.T @ T[4:]])
+    dt, dr = pose_err(x, inv)
+    if solver == 0:
+        assert dt < 2e-3 and dr < 2e-4, (dt, dr, st.termination)
+    else:
+        assert st.termination == 5 and dt < 5e-3 and dr < 5e-3, (dt, dr, st.termination)
+
+
+def test_registration_converges_and_schedule(oracle_mod, tiny):
+    reg, e, s = _registration(oracle_mod, tiny, 0)
+    x, tr, st = reg.solve(tiny.guess[0])       # reference decay: 10 -> 9 outer iterations
+    assert st.outer_iterations == 9 and len(tr) == 9
+    dt, dr = pose_err(x, tiny.truth[0])
+    assert dt < 0.05 and dr < 0.01
+    x2, tr2, st2 = reg.solve(tiny.guess[0])
+    assert st2.outer_iterations == 8
+    reg.set_max_iterations(2)
+    assert reg.solve(tiny.guess[0])[2].outer_iterations == 2    # no decrement at 2
+
+
+def test_golden_fixtures_reproduced(oracle_mod):
+    """Fixtures generated by tests/golden/make_golden.py (oracle outputs + numpy cross-checks)."""
+    path = os.path.join(GOLDEN, "c1_small.npz")
+    assert os.path.exists(path), "run tests/golden/make_golden.py"
+    g = np.load(path)
+    e, s, ei, si = oracle_mod.extract(g["scan"])
+    np.testing.assert_array_equal(ei, g["edge_src"])
+    np.testing.assert_array_equal(si, g["surf_src"])
+    reg = oracle_mod.Registration()
+    reg.set_map(1, g["edge_map"])
+    reg.set_map(2, g["surf_map"])
+    reg.set_scan(1, e)
+    reg.set_scan(2, s)
+    rec, nn = reg.match(g["guess"])
+    np.testing.assert_array_equal(nn, g["nn"])
+    np.testing.assert_array_equal(rec["kind"], g["kind"])
+    np.testing.assert_array_equal(rec["v0"], g["v0"])
+    np.testing.assert_array_equal(rec["v1"], g["v1"])
+    reg.set_fixed_schedule(True)
+    reg.set_max_iterations(5)
+    x, tr, st = reg.solve(g["guess"])
+    np.testing.assert_allclose(tr, g["trace"], rtol=0, atol=1e-12)
+    # independent numpy pins stored in the fixture
+    np.testing.assert_allclose(g["np_edge_dir_dot"], 1.0, atol=1e-9)
+    np.testing.assert_allclose(g["np_plane_err"], 0.0, atol=1e-7)
