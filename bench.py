@@ -115,12 +115,13 @@ def main():
     avg_launch_ms = ks.total_ms / max(ks.launches, 1)
     bytes_per_launch = alg_bytes / max(ks.launches, 1)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
-    traffic = None
+    traffic, l2_hit = None, None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             if int(tj.get("batch", -1)) == args.batch and int(tj.get("map_points", -1)) == args.map_points:
                 traffic = tj.get("hbm_bytes_per_launch")
+                l2_hit = tj.get("l2_hit_rate")
         except Exception:
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -128,7 +129,11 @@ def main():
                 "kernel": "knn_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
                 "alg_bytes_per_launch": int(bytes_per_launch), "launches": int(ks.launches),
                 "queries_per_launch": int(ks.queries / max(ks.launches, 1)),
-                "mean_n27": round(ks.n27_sum / max(ks.queries, 1), 1)}
+                "mean_n27": round(ks.n27_sum / max(ks.queries, 1), 1),
+                "measured_hbm_gbs": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic and avg_launch_ms else None,
+                "l2_hit_rate": round(l2_hit, 3) if l2_hit is not None else None,
+                "note": "achieved = SURVEY 8(d) algorithmic bytes / launch time; the 1M-pt map + cell index "
+                        "(~27 MB) is L2/Infinity-Cache resident, so measured HBM traffic (PMC) is far lower"}
 
     # ---------------- CPU baseline + pose delta vs CPU (rank 0, N = 1 only)
     cpu = None
