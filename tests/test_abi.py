@@ -88,6 +88,25 @@ def test_factory_selection_strings(lib):
         R.make_registration("feature_based")  # the CPU path is the oracle, not a product fallback
 
 
+def build_facade_example(out_dir):
+    """Compile tests/cpp/facade_example.cpp (a C++ caller of the reference-shaped facade) and link
+    it against liblmsf_hip.so."""
+    lib_dir = os.path.join(REPO, "lmsf-slam_amd")
+    exe = os.path.join(str(out_dir), "facade_example")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-I", os.path.join(REPO, "include"),
+                    os.path.join(REPO, "tests", "cpp", "facade_example.cpp"), "-L", lib_dir, "-llmsf_hip",
+                    f"-Wl,-rpath,{lib_dir}", "-o", exe], check=True)
+    return exe
+
+
+def test_cpp_facade_builds_and_links(lib, tmp_path):
+    exe = build_facade_example(tmp_path)
+    assert os.path.exists(exe)
+    out = subprocess.run(["nm", "-u", exe], capture_output=True, text=True).stdout
+    for s in ("lmsf_ctx_create", "lmsf_set_map", "lmsf_set_scan", "lmsf_solve", "lmsf_extract_features"):
+        assert s in out
+
+
 def test_lmsf_header_compiles_as_c_and_cpp(tmp_path):
     src = tmp_path / "t.c"
     src.write_text('#include "lmsf/lmsf.h"\nint main(void){ lmsf_config c; return lmsf_config_init(&c); }\n')

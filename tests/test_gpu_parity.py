@@ -260,6 +260,36 @@ def test_n27_accounting(lib, oracle_mod, small_workload):
     assert abs(ks.n27_sum - expect) <= 1e-4 * expect
 
 
+def test_cpp_facade(lib, oracle_mod, small_workload, tmp_path):
+    """A C++ program written against RegistrationBase / PointCloudProcessBase (include/lmsf/lmsf.hpp)
+    reproduces the oracle: default factory settings, reference decay schedule (10 -> 9 iterations)."""
+    import subprocess
+    from test_abi import build_facade_example
+    wl = small_workload
+    exe = build_facade_example(tmp_path)
+    paths = []
+    for name, arr in (("scan", wl.scans[0]), ("edge", wl.edge_map), ("surf", wl.surf_map)):
+        p = tmp_path / f"{name}.bin"
+        np.ascontiguousarray(arr, np.float32).tofile(p)
+        paths.append(str(p))
+    g = wl.guess[0]
+    out = subprocess.run([exe, *paths, *[repr(float(v)) for v in g], "10"], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    f = out.stdout.split()
+    ne, ns, x, outer = int(f[0]), int(f[1]), np.array([float(v) for v in f[2:9]]), int(f[9])
+    e, s = _features(oracle_mod, wl.scans[0])
+    assert (ne, ns) == (len(e), len(s)) and outer == 9
+    reg = oracle_mod.Registration()
+    reg.set_map(1, wl.edge_map)
+    reg.set_map(2, wl.surf_map)
+    reg.set_scan(1, e)
+    reg.set_scan(2, s)
+    ox, _, _ = reg.solve(g)
+    dt, dr = pose_err(x, ox)
+    assert dt <= POSE_TOL and dr <= POSE_TOL
+
+
 def test_reference_interface(lib, oracle_mod, small_workload):
     """The Python mirror of RegistrationBase / PointCloudProcessBase drives the same library."""
     from lmsf import registration as R
