@@ -167,6 +167,49 @@ typedef struct {
 lmsf_status lmsf_kernel_stats_get(lmsf_ctx* ctx, lmsf_kernel_stats* out);
 lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* ctx, int32_t enable_timing);
 
+/* ---- scan-to-local-map tracker: LidarTrackerLocalMap<P, RegistrationBase<P>>
+ * (INC/LidarTracker/LidarTrackerLocalMap.hpp:42-263) over one context's registration.
+ * The local map implementation is absent from the reference snapshot (factory/Map/LocalMap_factory.hpp,
+ * included at :15); the build defines "sliding_Localmap" as a window of the last `window_frames`
+ * keyframes per feature kind, concatenated oldest -> newest, rebuilt on the device at every
+ * keyframe (MOTION and TIME updates both append).  Poses are row-major 4x4 Isometry3d matrices. */
+typedef struct lmsf_tracker lmsf_tracker;
+typedef struct {
+    int32_t window_frames;     /* keyframes kept per feature map (build-defined, default 20) */
+    double threshold_trans;    /* THRESHOLD_TRANS_ = 0.3 m   (LidarTrackerLocalMap.hpp:65) */
+    double threshold_rot;      /* THRESHOLD_ROT_   = 0.1 rad */
+    double time_interval;      /* TIME_INTERVAL_   = 10 s */
+} lmsf_tracker_config;
+
+#define LMSF_UPDATE_NONE 0    /* LocalMapUpdataType NO_UPDATA */
+#define LMSF_UPDATE_MOTION 1  /* MOTION_UPDATA */
+#define LMSF_UPDATE_TIME 2    /* TIME_UPDATA */
+
+typedef struct {
+    int32_t initialized;       /* 1 when this call only seeded the local map (first call, :112-122) */
+    int32_t update_type;       /* LMSF_UPDATE_* decided by needUpdataLocalMap (:239-262) */
+    int64_t local_map_edge;    /* local map sizes after the call */
+    int64_t local_map_surf;
+    lmsf_solve_stats solve;
+} lmsf_tracker_result;
+
+lmsf_status lmsf_tracker_config_init(lmsf_tracker_config* cfg);
+/* SetRegistration + SetLocalMap({"loam_edge", "loam_surf"}, "sliding_Localmap") on context ctx. */
+lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, lmsf_tracker** out);
+void lmsf_tracker_destroy(lmsf_tracker* t);
+/* LidarTrackerLocalMap::Solve (:107-160): features of the current scan, timestamp (s), deltaT
+ * in/out (identity in => constant-velocity prediction; out = motion increment). */
+lmsf_status lmsf_tracker_solve(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf, size_t n_surf,
+                               double timestamp, double deltaT[16], lmsf_tracker_result* res);
+/* RegistrationLocalMap (:168-177): register features against the local map from pose (in/out),
+ * no tracker state change (the dual-LiDAR refine of INC/System/ML_System.hpp:303-307). */
+lmsf_status lmsf_tracker_register(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf,
+                                  size_t n_surf, double pose[16], lmsf_solve_stats* stats);
+/* GetCurrPoseInLocalFrame (:182-185). */
+lmsf_status lmsf_tracker_pose(const lmsf_tracker* t, double T[16]);
+/* GetLocalMap (:187-195): copy one feature map of the window to the host. */
+lmsf_status lmsf_tracker_local_map(lmsf_tracker* t, int32_t kind, float* out, size_t cap, size_t* n_out);
+
 /* Library version string. */
 const char* lmsf_version(void);
 

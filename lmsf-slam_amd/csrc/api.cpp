@@ -188,7 +188,8 @@ lmsf_status build_map(lmsf_ctx* c, int kind, const float* xyzi, size_t n) {
         HIPCHK(c, dalloc(&m.cell, n));
         m.cap = n;
     }
-    HIPCHK(c, hipMemcpyAsync(m.orig, xyzi, n * sizeof(float4), hipMemcpyHostToDevice, s));
+    // host or device source (unified addressing): the tracker rebuilds from device-resident maps
+    HIPCHK(c, hipMemcpyAsync(m.orig, xyzi, n * sizeof(float4), hipMemcpyDefault, s));
     int* d_bbox = c->d_error + 4;  // scratch ints after the error word
     const int init[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
     HIPCHK(c, hipMemcpyAsync(d_bbox, init, sizeof init, hipMemcpyHostToDevice, s));
@@ -681,3 +682,29 @@ lmsf_status lmsf_kernel_stats_get(lmsf_ctx* c, lmsf_kernel_stats* out) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- internal (tracker.cpp)
+namespace lmsf {
+
+hipStream_t ctx_stream(lmsf_ctx* c) { return c->stream; }
+int ctx_device(const lmsf_ctx* c) { return c->cfg.device; }
+int ctx_feature_capacity(const lmsf_ctx* c) { return c->F; }
+lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg) { return c->fail(code, "%s", msg); }
+
+// SetInputSource from device-resident points (local-map rebuild without a host round trip).
+lmsf_status ctx_set_map_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n) {
+    if (n == 0) return LMSF_OK;
+    return build_map(c, kind, reinterpret_cast<const float*>(d_pts), n);
+}
+
+// Current slot-0 features on the device (after SetInputTarget / extraction): edges then surfs.
+lmsf_status ctx_slot0_features(lmsf_ctx* c, const float4** d_feat, int64_t* ne, int64_t* ns) {
+    lmsf_status rc = sync_slot0_features(c);
+    if (rc) return rc;
+    *d_feat = c->feat;
+    *ne = c->slot0_ne;
+    *ns = c->slot0_ns;
+    return LMSF_OK;
+}
+
+}  // namespace lmsf

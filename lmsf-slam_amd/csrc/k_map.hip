@@ -69,6 +69,29 @@ __global__ void map_scatter_kernel(const float4* pts, int n, const int* cell, co
     sorted[pos] = make_float4(p.x, p.y, p.z, __int_as_float(i));
 }
 
+// pcl::transformPointCloud with an Eigen::Matrix4d (PCL 1.7 transforms.hpp): per point
+// out = float(t(r,0) x + t(r,1) y + t(r,2) z + t(r,3)) evaluated in double, fields copied.
+// Used by LidarTrackerLocalMap::updateLocalMap (INC/LidarTracker/LidarTrackerLocalMap.hpp:217).
+__global__ void transform_kernel(const float4* in, int n, Affine34 M, float4* out) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = in[i];
+    const double x = p.x, y = p.y, z = p.z;
+    float4 o;
+    o.x = (float)(M.m[0] * x + M.m[1] * y + M.m[2] * z + M.m[3]);
+    o.y = (float)(M.m[4] * x + M.m[5] * y + M.m[6] * z + M.m[7]);
+    o.z = (float)(M.m[8] * x + M.m[9] * y + M.m[10] * z + M.m[11]);
+    o.w = p.w;
+    out[i] = o;
+}
+
+hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(transform_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, M, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_map_bbox(const float4* pts, int n, int* bbox, hipStream_t s) {
     const int blocks = min((n + 255) / 256, 1024);
     hipLaunchKernelGGL(map_bbox_kernel, dim3(max(blocks, 1)), dim3(256), 0, s, pts, n, bbox);

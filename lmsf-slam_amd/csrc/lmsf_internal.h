@@ -117,4 +117,16 @@ struct ExtractView {
 };
 hipError_t launch_extract(const ExtractView& ev, hipStream_t s);
 
+// ---- local map maintenance (tracker.cpp)
+struct Affine34 { double m[12]; };   // row-major 3x4 of an Isometry3d matrix
+// pcl::transformPointCloud(cloud, out, Matrix4d) per point: float(m00 x + m01 y + m02 z + m03), double math
+hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hipStream_t s);
+
+hipStream_t ctx_stream(lmsf_ctx* c);
+int ctx_device(const lmsf_ctx* c);
+int ctx_feature_capacity(const lmsf_ctx* c);
+lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg);
+lmsf_status ctx_set_map_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n);
+lmsf_status ctx_slot0_features(lmsf_ctx* c, const float4** d_feat, int64_t* ne, int64_t* ns);
+
 }  // namespace lmsf

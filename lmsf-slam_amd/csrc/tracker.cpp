@@ -1,0 +1,337 @@
+// Scan-to-local-map tracker on the MI355X registration context.
+//
+// Restates LidarTrackerLocalMap (INC/LidarTracker/LidarTrackerLocalMap.hpp:42-263, INC =
+// src/MultiSensorFusionEstimator3D/include): first scan seeds the local map (:112-122), constant
+// velocity prediction `prev * motion_increment` when deltaT is exactly identity (:125-129),
+// RegistrationLocalMap (:168-177), motion increment (:133-135), keyframe gate needUpdataLocalMap
+// (:239-262: dt > 10 s -> TIME, |dp| > 0.3 m or 2 acos(|q.w|) > 0.1 rad -> MOTION), and
+// updateLocalMap (:205-232: transformPointCloud, add frame, SetInputSource(local map)).
+// The local-map class itself is missing from the reference snapshot (factory/Map/LocalMap_factory.hpp);
+// "sliding_Localmap" is defined here as a device-resident window of the last W keyframes.
+// Isometry arithmetic follows Eigen's Isometry3d (linear * linear, linear * t + t; inverse = R^T,
+// -R^T t) and its quaternion <-> matrix conversions (the Ceres path converts at Solve, ceres_...:103, :128).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "lmsf_internal.h"
+
+using namespace lmsf;
+
+namespace {
+
+struct Iso {
+    double R[9];
+    double t[3];
+};
+
+Iso iso_identity() {
+    Iso I;
+    for (int i = 0; i < 9; ++i) I.R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    I.t[0] = I.t[1] = I.t[2] = 0.0;
+    return I;
+}
+
+Iso iso_mul(const Iso& A, const Iso& B) {
+    Iso C;
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) C.R[3 * i + j] = A.R[3 * i] * B.R[j] + A.R[3 * i + 1] * B.R[3 + j] + A.R[3 * i + 2] * B.R[6 + j];
+        C.t[i] = A.R[3 * i] * B.t[0] + A.R[3 * i + 1] * B.t[1] + A.R[3 * i + 2] * B.t[2] + A.t[i];
+    }
+    return C;
+}
+
+Iso iso_inverse(const Iso& A) {
+    Iso B;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) B.R[3 * i + j] = A.R[3 * j + i];
+    for (int i = 0; i < 3; ++i)
+        B.t[i] = (-B.R[3 * i]) * A.t[0] + (-B.R[3 * i + 1]) * A.t[1] + (-B.R[3 * i + 2]) * A.t[2];
+    return B;
+}
+
+Iso iso_from16(const double* m) {
+    Iso T;
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) T.R[3 * i + j] = m[4 * i + j];
+        T.t[i] = m[4 * i + 3];
+    }
+    return T;
+}
+
+void iso_to16(const Iso& T, double* m) {
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) m[4 * i + j] = T.R[3 * i + j];
+        m[4 * i + 3] = T.t[i];
+    }
+    m[12] = m[13] = m[14] = 0.0;
+    m[15] = 1.0;
+}
+
+bool is_identity16(const double* m) {   // deltaT.matrix() == Identity().matrix() (exact)
+    for (int i = 0; i < 16; ++i)
+        if (m[i] != ((i % 5 == 0) ? 1.0 : 0.0)) return false;
+    return true;
+}
+
+// Eigen::Quaterniond(Matrix3d) (quaternionbase_assign_impl, Shepperd) -> (x, y, z, w)
+void quat_from_R(const double* m, double* q) {
+    const double tr = m[0] + m[4] + m[8];
+    if (tr > 0) {
+        double t = std::sqrt(tr + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m[7] - m[5]) * t;
+        q[1] = (m[2] - m[6]) * t;
+        q[2] = (m[3] - m[1]) * t;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[4 * i]) i = 2;
+        const int j = (i + 1) % 3, k = (i + 2) % 3;
+        double t = std::sqrt(m[4 * i] - m[4 * j] - m[4 * k] + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m[3 * k + j] - m[3 * j + k]) * t;
+        q[j] = (m[3 * j + i] + m[3 * i + j]) * t;
+        q[k] = (m[3 * k + i] + m[3 * i + k]) * t;
+    }
+}
+
+// Eigen QuaternionBase::toRotationMatrix
+void R_from_quat(const double* q, double* R) {
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z, twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x, tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+
+struct Window {
+    std::vector<float4*> slots;
+    std::vector<int> sizes;
+    int head = 0, count = 0;
+    float4* concat = nullptr;
+    size_t total = 0;
+};
+
+}  // namespace
+
+struct lmsf_tracker {
+    lmsf_ctx* ctx = nullptr;
+    lmsf_tracker_config cfg{};
+    bool init = false;
+    Iso curr, prev, motion, last_kf;
+    double last_kf_time = 0.0;
+    Window win[3];
+    int cap = 0;   // points per keyframe slot
+};
+
+namespace {
+
+lmsf_status fail(lmsf_tracker* t, lmsf_status code, const char* msg) { return ctx_fail(t->ctx, code, msg); }
+
+#define TCHK(t, expr)                                               \
+    do {                                                            \
+        hipError_t e_ = (expr);                                     \
+        if (e_ != hipSuccess) return fail((t), LMSF_ERR_HIP, #expr); \
+    } while (0)
+
+// updateLocalMap (:205-232) for every kind with a non-empty cloud.
+lmsf_status update_local_map(lmsf_tracker* t, const Iso& T) {
+    const float4* feat;
+    int64_t ne, ns;
+    lmsf_status rc = ctx_slot0_features(t->ctx, &feat, &ne, &ns);
+    if (rc) return rc;
+    hipStream_t s = ctx_stream(t->ctx);
+    Affine34 M;
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) M.m[4 * i + j] = T.R[3 * i + j];
+        M.m[4 * i + 3] = T.t[i];
+    }
+    for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) {
+        const int64_t n = kind == LMSF_EDGE ? ne : ns;
+        if (n == 0) continue;                                   // :213
+        if (n > t->cap) return fail(t, LMSF_ERR_CAPACITY, "keyframe larger than the tracker slot capacity");
+        const float4* src = feat + (kind == LMSF_EDGE ? 0 : ne);
+        Window& w = t->win[kind];
+        const int W = (int)w.slots.size();
+        int slot;
+        if (w.count < W) {
+            slot = (w.head + w.count) % W;
+            ++w.count;
+        } else {                                                  // window full: evict the oldest
+            slot = w.head;
+            w.head = (w.head + 1) % W;
+        }
+        TCHK(t, launch_transform(src, (int)n, M, w.slots[slot], s));
+        w.sizes[slot] = (int)n;
+        size_t off = 0;
+        for (int i = 0; i < w.count; ++i) {
+            const int k = (w.head + i) % W;
+            TCHK(t, hipMemcpyAsync(w.concat + off, w.slots[k], (size_t)w.sizes[k] * sizeof(float4),
+                                   hipMemcpyDeviceToDevice, s));
+            off += (size_t)w.sizes[k];
+        }
+        w.total = off;
+        rc = ctx_set_map_device(t->ctx, kind, w.concat, off);   // SetInputSource(GetLocalMap())
+        if (rc) return rc;
+    }
+    return LMSF_OK;
+}
+
+lmsf_status set_features(lmsf_tracker* t, const float* edge, size_t ne, const float* surf, size_t ns) {
+    lmsf_status rc = lmsf_set_scan(t->ctx, LMSF_EDGE, edge, ne);
+    if (rc) return rc;
+    return lmsf_set_scan(t->ctx, LMSF_SURF, surf, ns);
+}
+
+// RegistrationLocalMap (:168-177) -> Solve: T -> (q, t) -> T.linear() = q.toRotationMatrix()
+lmsf_status register_pose(lmsf_tracker* t, Iso& T, lmsf_solve_stats* st) {
+    double x[7];
+    quat_from_R(T.R, x);
+    x[4] = T.t[0]; x[5] = T.t[1]; x[6] = T.t[2];
+    lmsf_status rc = lmsf_solve(t->ctx, x, st);
+    if (rc) return rc;
+    R_from_quat(x, T.R);
+    T.t[0] = x[4]; T.t[1] = x[5]; T.t[2] = x[6];
+    return LMSF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+lmsf_status lmsf_tracker_config_init(lmsf_tracker_config* cfg) {
+    if (!cfg) return LMSF_ERR_ARG;
+    cfg->window_frames = 20;
+    cfg->threshold_trans = 0.3;
+    cfg->threshold_rot = 0.1;
+    cfg->time_interval = 10.0;
+    return LMSF_OK;
+}
+
+void lmsf_tracker_destroy(lmsf_tracker* t) {
+    if (!t) return;
+    hipSetDevice(ctx_device(t->ctx));
+    hipStreamSynchronize(ctx_stream(t->ctx));
+    for (auto& w : t->win) {
+        for (float4* p : w.slots) hipFree(p);
+        hipFree(w.concat);
+    }
+    delete t;
+}
+
+lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, lmsf_tracker** out) {
+    if (!ctx || !cfg || !out || cfg->window_frames < 1) return LMSF_ERR_ARG;
+    *out = nullptr;
+    lmsf_tracker* t = new lmsf_tracker();
+    t->ctx = ctx;
+    t->cfg = *cfg;
+    t->cap = ctx_feature_capacity(ctx);
+    if (hipSetDevice(ctx_device(ctx)) != hipSuccess) { delete t; return LMSF_ERR_HIP; }
+    for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) {
+        Window& w = t->win[kind];
+        w.slots.assign(cfg->window_frames, nullptr);
+        w.sizes.assign(cfg->window_frames, 0);
+        for (auto& p : w.slots)
+            if (hipMalloc((void**)&p, (size_t)t->cap * sizeof(float4)) != hipSuccess) { lmsf_tracker_destroy(t); return LMSF_ERR_HIP; }
+        if (hipMalloc((void**)&w.concat, (size_t)t->cap * cfg->window_frames * sizeof(float4)) != hipSuccess) {
+            lmsf_tracker_destroy(t);
+            return LMSF_ERR_HIP;
+        }
+    }
+    t->curr = t->prev = t->motion = t->last_kf = iso_identity();
+    *out = t;
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_tracker_solve(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf, size_t n_surf,
+                               double timestamp, double deltaT[16], lmsf_tracker_result* res) {
+    if (!t || !deltaT || (n_edge && !edge) || (n_surf && !surf)) return LMSF_ERR_ARG;
+    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    lmsf_tracker_result r;
+    std::memset(&r, 0, sizeof r);
+    lmsf_status rc = set_features(t, edge, n_edge, surf, n_surf);
+    if (rc) return rc;
+    if (!t->init) {                                                   // :112-122
+        rc = update_local_map(t, iso_identity());
+        if (rc) return rc;
+        t->curr = t->prev = t->motion = t->last_kf = iso_identity();
+        t->last_kf_time = timestamp;
+        t->init = true;
+        r.initialized = 1;
+        r.update_type = LMSF_UPDATE_MOTION;
+    } else {
+        if (is_identity16(deltaT)) t->curr = iso_mul(t->prev, t->motion);   // :125-129
+        else t->curr = iso_mul(t->prev, iso_from16(deltaT));
+        rc = register_pose(t, t->curr, &r.solve);                      // :131
+        if (rc) return rc;
+        t->motion = iso_mul(iso_inverse(t->prev), t->curr);             // :133
+        iso_to16(t->motion, deltaT);
+        t->prev = t->curr;
+        // needUpdataLocalMap (:239-262)
+        int type = LMSF_UPDATE_NONE;
+        if (timestamp - t->last_kf_time > t->cfg.time_interval) {
+            type = LMSF_UPDATE_TIME;
+        } else {
+            const Iso d = iso_mul(iso_inverse(t->last_kf), t->curr);
+            const double dt = std::sqrt(d.t[0] * d.t[0] + d.t[1] * d.t[1] + d.t[2] * d.t[2]);
+            double q[4];
+            quat_from_R(d.R, q);
+            const double qn = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+            const double angle = std::acos(q[3] / qn) * 2;
+            if (dt > t->cfg.threshold_trans || angle > t->cfg.threshold_rot) type = LMSF_UPDATE_MOTION;
+        }
+        r.update_type = type;
+        if (type) {
+            t->last_kf = t->curr;
+            t->last_kf_time = timestamp;
+            rc = update_local_map(t, t->curr);
+            if (rc) return rc;
+        }
+    }
+    r.local_map_edge = (int64_t)t->win[LMSF_EDGE].total;
+    r.local_map_surf = (int64_t)t->win[LMSF_SURF].total;
+    if (res) *res = r;
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_tracker_register(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf,
+                                  size_t n_surf, double pose[16], lmsf_solve_stats* stats) {
+    if (!t || !pose) return LMSF_ERR_ARG;
+    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    lmsf_status rc = set_features(t, edge, n_edge, surf, n_surf);
+    if (rc) return rc;
+    Iso T = iso_from16(pose);
+    lmsf_solve_stats st;
+    rc = register_pose(t, T, &st);
+    if (rc) return rc;
+    iso_to16(T, pose);
+    if (stats) *stats = st;
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_tracker_pose(const lmsf_tracker* t, double T[16]) {
+    if (!t || !T) return LMSF_ERR_ARG;
+    iso_to16(t->curr, T);
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_tracker_local_map(lmsf_tracker* t, int32_t kind, float* out, size_t cap, size_t* n_out) {
+    if (!t || (kind != LMSF_EDGE && kind != LMSF_SURF)) return LMSF_ERR_ARG;
+    const Window& w = t->win[kind];
+    if (n_out) *n_out = w.total;
+    if (!out) return LMSF_OK;
+    if (w.total > cap) return fail(t, LMSF_ERR_CAPACITY, "output capacity smaller than the local map");
+    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    hipStream_t s = ctx_stream(t->ctx);
+    TCHK(t, hipMemcpyAsync(out, w.concat, w.total * sizeof(float4), hipMemcpyDeviceToHost, s));
+    TCHK(t, hipStreamSynchronize(s));
+    return LMSF_OK;
+}
+
+}  // extern "C"

@@ -17,6 +17,7 @@ HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "lmsf", "lmsf.h
 
 OK, ERR_ARG, ERR_HIP, ERR_NO_MAP, ERR_CAPACITY, ERR_STATE = 0, -1, -2, -3, -4, -5
 EDGE, SURF = 1, 2
+UPDATE_NONE, UPDATE_MOTION, UPDATE_TIME = 0, 1, 2
 SOLVER_CERES_LM, SOLVER_GN = 0, 1
 SCHEDULE_REFERENCE_DECAY, SCHEDULE_FIXED = 0, 1
 TERM_NAMES = {0: "max_iterations", 1: "function_tol", 2: "parameter_tol", 3: "gradient_tol",
@@ -50,6 +51,16 @@ class KernelStats(C.Structure):
     _fields_ = [("launches", C.c_int64), ("total_ms", C.c_double), ("queries", C.c_int64), ("n27_sum", C.c_int64)]
 
 
+class TrackerConfig(C.Structure):
+    _fields_ = [("window_frames", C.c_int32), ("threshold_trans", C.c_double), ("threshold_rot", C.c_double),
+                ("time_interval", C.c_double)]
+
+
+class TrackerResult(C.Structure):
+    _fields_ = [("initialized", C.c_int32), ("update_type", C.c_int32), ("local_map_edge", C.c_int64),
+                ("local_map_surf", C.c_int64), ("solve", SolveStats)]
+
+
 class LmsfError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"lmsf error {code}: {msg}")
@@ -80,6 +91,13 @@ _SIGS = {
     "lmsf_kernel_stats_get": (C.c_int32, [_P, C.POINTER(KernelStats)]),
     "lmsf_kernel_stats_reset": (C.c_int32, [_P, C.c_int32]),
     "lmsf_version": (C.c_char_p, []),
+    "lmsf_tracker_config_init": (C.c_int32, [C.POINTER(TrackerConfig)]),
+    "lmsf_tracker_create": (C.c_int32, [_P, C.POINTER(TrackerConfig), C.POINTER(_P)]),
+    "lmsf_tracker_destroy": (None, [_P]),
+    "lmsf_tracker_solve": (C.c_int32, [_P, _P, C.c_size_t, _P, C.c_size_t, C.c_double, _P, C.POINTER(TrackerResult)]),
+    "lmsf_tracker_register": (C.c_int32, [_P, _P, C.c_size_t, _P, C.c_size_t, _P, C.POINTER(SolveStats)]),
+    "lmsf_tracker_pose": (C.c_int32, [_P, _P]),
+    "lmsf_tracker_local_map": (C.c_int32, [_P, C.c_int32, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
 }
 
 _lib = None
@@ -226,6 +244,59 @@ class Context:
         ks = KernelStats()
         self._check(load().lmsf_kernel_stats_get(self.h, C.byref(ks)))
         return ks
+
+
+def _pts(a):
+    return _f4(a) if len(a) else np.zeros((0, 4), np.float32)
+
+
+class Tracker:
+    """lmsf_tracker: LidarTrackerLocalMap over a Context (poses are 4x4 row-major matrices)."""
+
+    def __init__(self, ctx: Context, window_frames=20, threshold_trans=0.3, threshold_rot=0.1, time_interval=10.0):
+        cfg = TrackerConfig()
+        load().lmsf_tracker_config_init(C.byref(cfg))
+        cfg.window_frames, cfg.threshold_trans = window_frames, threshold_trans
+        cfg.threshold_rot, cfg.time_interval = threshold_rot, time_interval
+        self.ctx = ctx
+        h = C.c_void_p()
+        ctx._check(load().lmsf_tracker_create(ctx.h, C.byref(cfg), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().lmsf_tracker_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def solve(self, edge, surf, timestamp, deltaT=None):
+        e, s = _pts(edge), _pts(surf)
+        d = np.ascontiguousarray(np.eye(4) if deltaT is None else deltaT, dtype=np.float64).copy()
+        r = TrackerResult()
+        self.ctx._check(load().lmsf_tracker_solve(self.h, e.ctypes.data, e.shape[0], s.ctypes.data, s.shape[0],
+                                                  float(timestamp), d.ctypes.data, C.byref(r)))
+        return d, r
+
+    def register(self, edge, surf, pose):
+        e, s = _pts(edge), _pts(surf)
+        T = np.ascontiguousarray(pose, dtype=np.float64).copy()
+        st = SolveStats()
+        self.ctx._check(load().lmsf_tracker_register(self.h, e.ctypes.data, e.shape[0], s.ctypes.data, s.shape[0],
+                                                     T.ctypes.data, C.byref(st)))
+        return T, st
+
+    def pose(self):
+        T = np.zeros((4, 4))
+        self.ctx._check(load().lmsf_tracker_pose(self.h, T.ctypes.data))
+        return T
+
+    def local_map(self, kind):
+        n = C.c_size_t()
+        self.ctx._check(load().lmsf_tracker_local_map(self.h, kind, None, 0, C.byref(n)))
+        out = np.zeros((n.value, 4), np.float32)
+        self.ctx._check(load().lmsf_tracker_local_map(self.h, kind, out.ctypes.data, n.value, C.byref(n)))
+        return out
 
 
 def header_symbols(path=HEADER_PATH):

@@ -36,6 +36,44 @@ def c2_workload():
     return synth.make_workload("C2", n_scans=2, map_points=1_000_000)
 
 
+HDL64_ELEV = np.concatenate([np.linspace(2.0, -8.33, 32), np.linspace(-8.83, -24.33, 32)])
+
+
+@pytest.fixture(scope="session")
+def sequence_workload():
+    """10 consecutive 64-beam scans (HDL-64 ring formula, 1024 columns), 10 Hz at 2.5 m/s:
+    the tracker builds its own map from the first scan.  A 16-beam first scan is too sparse
+    vertically to seed a scan-to-map tracker in this synthetic canyon (it drifts), 64 beams hold."""
+    from types import SimpleNamespace
+    from lmsf import synth
+    scene = synth.make_scene(1001)
+    truth = synth.trajectory(10, 3001, step=0.25)
+    scans = [synth.make_scan(scene, truth[i], 2001 + 97 * i, n_cols=1024, elev_deg=HDL64_ELEV)
+             for i in range(len(truth))]
+    return SimpleNamespace(scans=scans, truth=truth, n_scans=64, dt=0.1)
+
+
+def relative_truth(truth):
+    """Ground-truth poses relative to the first scan (the tracker's local frame), 4x4."""
+    from lmsf import synth
+    mats = []
+    for p in truth:
+        T = np.eye(4)
+        T[:3, :3] = synth.quat_to_mat(p[:4])
+        T[:3, 3] = p[4:]
+        mats.append(T)
+    T0i = np.linalg.inv(mats[0])
+    return [T0i @ T for T in mats]
+
+
+def mat_err(A, B):
+    import math
+    dt = float(np.linalg.norm(A[:3, 3] - B[:3, 3]))
+    R = A[:3, :3].T @ B[:3, :3]
+    c = max(-1.0, min(1.0, (np.trace(R) - 1) / 2))
+    return dt, math.acos(c)
+
+
 def pose_err(a, b):
     from lmsf import synth
     return synth.pose_delta(a, b)

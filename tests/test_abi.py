@@ -50,10 +50,39 @@ def test_config_defaults_match_reference_factory(lib):
     assert (c.max_iterations, c.solver, c.schedule) == (10, lib.SOLVER_CERES_LM, lib.SCHEDULE_REFERENCE_DECAY)
 
 
-def test_struct_layouts(lib):
+def test_struct_layouts(lib, tmp_path):
+    """Every ctypes mirror has the C compiler's size and field offsets (include/lmsf/lmsf.h)."""
     assert lib.RECORD_DTYPE.itemsize == 64
-    assert ctypes.sizeof(lib.SolveStats) == 6 * 4 + 2 * 8
-    assert ctypes.sizeof(lib.Config) == 12 * 4 + 2 * 8
+    structs = {"lmsf_config": lib.Config, "lmsf_solve_stats": lib.SolveStats,
+               "lmsf_feature_counts": lib.FeatureCounts, "lmsf_kernel_stats": lib.KernelStats,
+               "lmsf_tracker_config": lib.TrackerConfig, "lmsf_tracker_result": lib.TrackerResult}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "lmsf/lmsf.h"', 'int main(void) {']
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f in py._fields_:
+            lines.append(f'printf("{cname} {f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    lines.append('printf("lmsf_record size %zu\\n", sizeof(lmsf_record)); return 0; }')
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = {}
+    for ln in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        s, f, v = ln.split()
+        got[(s, f)] = int(v)
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for f in py._fields_:
+            assert got[(cname, f[0])] == getattr(py, f[0]).offset, (cname, f[0])
+    assert got[("lmsf_record", "size")] == 64
+
+
+def test_tracker_config_defaults(lib):
+    """LidarTrackerLocalMap: THRESHOLD_TRANS 0.3 m, THRESHOLD_ROT 0.1 rad, TIME_INTERVAL 10 s
+    (LidarTrackerLocalMap.hpp:65); window = the sliding local map's frame count."""
+    c = lib.TrackerConfig()
+    assert lib.load().lmsf_tracker_config_init(ctypes.byref(c)) == lib.OK
+    assert (c.window_frames, c.threshold_trans, c.threshold_rot, c.time_interval) == (20, 0.3, 0.1, 10.0)
 
 
 def test_no_silent_fallback_without_device(lib):

@@ -290,6 +290,74 @@ def test_cpp_facade(lib, oracle_mod, small_workload, tmp_path):
     assert dt <= POSE_TOL and dr <= POSE_TOL
 
 
+def test_tracker_sequence_parity(lib, oracle_mod, sequence_workload):
+    """lmsf_tracker (device-resident sliding-window local map) vs oracle/tracker.py on a 10-scan
+    64-beam sequence: same update decisions and map sizes, poses <= 1e-4, tracking within 5 cm."""
+    import tracker as OT
+    from conftest import mat_err, relative_truth
+    wl = sequence_workload
+    rel = relative_truth(wl.truth)
+    ctx = _ctx(lib, n_scans=wl.n_scans)
+    gt = lib.Tracker(ctx, window_frames=3)
+    ot = OT.Tracker(window_frames=3)
+    types = []
+    for i, scan in enumerate(wl.scans):
+        e, s, _, _ = oracle_mod.extract(scan, n_scans=wl.n_scans)
+        ctx.extract(scan)
+        ge, _ = ctx.copy_features(lib.EDGE)
+        gs, _ = ctx.copy_features(lib.SURF)
+        assert ge.tobytes() == e.tobytes() and gs.tobytes() == s.tobytes()
+        gd, r = gt.solve(ge, gs, wl.dt * i)
+        od, otyp, _ = ot.solve(e, s, wl.dt * i)
+        assert r.update_type == otyp, i
+        assert bool(r.initialized) == (i == 0)
+        assert (r.local_map_edge, r.local_map_surf) == (len(ot.local_map(1)), len(ot.local_map(2)))
+        dt, dr = mat_err(gt.pose(), ot.curr)
+        assert dt <= POSE_TOL and dr <= POSE_TOL, (i, dt, dr)
+        np.testing.assert_allclose(gd, od, atol=POSE_TOL)
+        dt, dr = mat_err(gt.pose(), rel[i])
+        assert dt < 0.05 and dr < 0.01, (i, dt, dr)
+        types.append(otyp)
+    assert 0 in types[1:] and 1 in types[1:]
+    for kind in (lib.EDGE, lib.SURF):
+        np.testing.assert_allclose(gt.local_map(kind), ot.local_map(kind), atol=1e-4)
+    # refine (dual-LiDAR / external prediction path): register against the current local map
+    T0 = rel[-1].copy()
+    T0[:3, 3] += (0.05, -0.03, 0.02)
+    e, s, _, _ = oracle_mod.extract(wl.scans[-1], n_scans=wl.n_scans)
+    GT, st = gt.register(e, s, T0)
+    OTp, _ = ot._register({1: e, 2: s}, T0)
+    dt, dr = mat_err(GT, OTp)
+    assert dt <= POSE_TOL and dr <= POSE_TOL and st.outer_iterations > 0
+    gt.close()
+
+
+def test_tracker_time_gate_and_capacity(lib, oracle_mod, sequence_workload):
+    """TIME keyframes after time_interval; window eviction keeps only the newest W frames;
+    a keyframe larger than the slot capacity is an error, not a truncation."""
+    wl = sequence_workload
+    ctx = _ctx(lib, n_scans=wl.n_scans)
+    gt = lib.Tracker(ctx, window_frames=2, threshold_trans=1e9, threshold_rot=1e9, time_interval=0.15)
+    kf_sizes = []
+    types = []
+    for i, scan in enumerate(wl.scans[:5]):
+        e, s, _, _ = oracle_mod.extract(scan, n_scans=wl.n_scans)
+        _, r = gt.solve(e, s, 0.1 * i)
+        types.append(r.update_type)
+        if r.update_type != lib.UPDATE_NONE:
+            kf_sizes.append(len(s))
+        assert r.local_map_surf == sum(kf_sizes[-2:])
+    assert types == [lib.UPDATE_MOTION, lib.UPDATE_NONE, lib.UPDATE_TIME, lib.UPDATE_NONE, lib.UPDATE_TIME]
+    gt.close()
+    small = _ctx(lib, n_scans=wl.n_scans, max_features=1000)
+    t2 = lib.Tracker(small, window_frames=2)
+    e, s, _, _ = oracle_mod.extract(wl.scans[0], n_scans=wl.n_scans)
+    assert len(s) > 1000
+    with pytest.raises(lib.LmsfError):
+        t2.solve(e[:500], s, 0.0)
+    t2.close()
+
+
 def test_reference_interface(lib, oracle_mod, small_workload):
     """The Python mirror of RegistrationBase / PointCloudProcessBase drives the same library."""
     from lmsf import registration as R

@@ -218,6 +218,27 @@ def test_registration_converges_and_schedule(oracle_mod, tiny):
     assert reg.solve(tiny.guess[0])[2].outer_iterations == 2    # no decrement at 2
 
 
+def test_oracle_tracker_follows_trajectory(oracle_mod, sequence_workload):
+    """LidarTrackerLocalMap restated: first scan seeds the map, constant-velocity prediction,
+    keyframe gate (0.3 m / 0.1 rad / 10 s), sliding-window local map."""
+    import tracker as OT
+    from conftest import mat_err, relative_truth
+    wl = sequence_workload
+    rel = relative_truth(wl.truth)
+    tr = OT.Tracker(window_frames=3)
+    kinds = []
+    for i, scan in enumerate(wl.scans):
+        e, s, _, _ = oracle_mod.extract(scan, n_scans=wl.n_scans)
+        d, typ, st = tr.solve(e, s, wl.dt * i)
+        kinds.append(typ)
+        dt, dr = mat_err(tr.curr, rel[i])
+        assert dt < 0.05 and dr < 0.01, (i, dt, dr)
+    # 0.25 m per scan: every other scan crosses the 0.3 m keyframe gate
+    assert kinds[0] == 1 and 0 in kinds[1:] and 1 in kinds[1:]
+    assert len(tr.win[2]) == 3                                      # window capped
+    assert np.allclose(d, tr.motion) and np.array_equal(tr.prev, tr.curr)
+
+
 def test_golden_fixtures_reproduced(oracle_mod):
     """Fixtures generated by tests/golden/make_golden.py (oracle outputs + numpy cross-checks)."""
     path = os.path.join(GOLDEN, "c1_small.npz")
