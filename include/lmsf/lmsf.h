@@ -111,7 +111,8 @@ const char* lmsf_last_error(const lmsf_ctx* ctx);
 
 /* RegistrationBase::SetInputSource (REG/registration_base.hpp:31; ceres_...:56-71): set the local
  * feature map of one kind and build its device neighbour index.  n == 0 keeps the previous map
- * (ceres_...:60). */
+ * (ceres_...:60).  xyzi may be host or device memory of the context's GPU (e.g. a map received by
+ * an RCCL broadcast). */
 lmsf_status lmsf_set_map(lmsf_ctx* ctx, int32_t kind, const float* xyzi, size_t n);
 
 /* RegistrationBase::SetInputTarget (REG/registration_base.hpp:32; ceres_...:73-84): set the
@@ -130,15 +131,16 @@ lmsf_status lmsf_solve_trace(lmsf_ctx* ctx, double* trace, int32_t cap, int32_t*
 /* PointCloudProcessBase::Process (INC/Algorithm/PointClouds/processing/process_base.hpp:26-39),
  * LOAM implementation FX:59-126: extract "loam_edge" / "loam_surf" from a raw scan.  The features
  * stay device-resident and become the current scan target (as SetInputTarget with the
- * processor's output container) without a host round trip. */
+ * processor's output container) without a host round trip.  xyzi: host or device memory. */
 lmsf_status lmsf_extract_features(lmsf_ctx* ctx, const float* xyzi, size_t n, lmsf_feature_counts* counts);
-/* Copy the current features of one kind to the host (xyzi rows, reference emission order);
- * src (nullable) receives each feature's index in the raw scan. */
+/* Copy the current features of one kind (xyzi rows, reference emission order) to host or device
+ * memory; src (nullable) receives each feature's index in the raw scan. */
 lmsf_status lmsf_copy_features(lmsf_ctx* ctx, int32_t kind, float* out, int32_t* src, size_t cap, size_t* n_out);
 
 /* Batch throughput path: n independent registrations against the context's map (the ML_System
  * per-LiDAR loop, INC/System/ML_System.hpp:137-156 + :248-264, run as one device pass).
- * load_scans uploads raw scans (concatenated rows, counts[i] points each) into device slots;
+ * load_scans copies raw scans (concatenated rows, counts[i] points each; host or device memory)
+ * into device slots;
  * run extracts features for every slot and registers slot i from poses[i] (in/out). */
 lmsf_status lmsf_batch_load_scans(lmsf_ctx* ctx, const float* xyzi, const int64_t* counts, int32_t n);
 lmsf_status lmsf_batch_run(lmsf_ctx* ctx, int32_t n, double* poses, lmsf_solve_stats* stats);
@@ -179,6 +181,10 @@ typedef struct {
     double threshold_trans;    /* THRESHOLD_TRANS_ = 0.3 m   (LidarTrackerLocalMap.hpp:65) */
     double threshold_rot;      /* THRESHOLD_ROT_   = 0.1 rad */
     double time_interval;      /* TIME_INTERVAL_   = 10 s */
+    int32_t manual_map_update; /* 0 (reference): a keyframe is appended inside solve.  1: solve only
+                                  decides (res->update_type, keyframe pose/time); the caller appends
+                                  keyframes with lmsf_tracker_add_keyframe and rebuilds once with
+                                  lmsf_tracker_commit_map (multi-stream map stitching) */
 } lmsf_tracker_config;
 
 #define LMSF_UPDATE_NONE 0    /* LocalMapUpdataType NO_UPDATA */
@@ -207,8 +213,25 @@ lmsf_status lmsf_tracker_register(lmsf_tracker* t, const float* edge, size_t n_e
                                   size_t n_surf, double pose[16], lmsf_solve_stats* stats);
 /* GetCurrPoseInLocalFrame (:182-185). */
 lmsf_status lmsf_tracker_pose(const lmsf_tracker* t, double T[16]);
-/* GetLocalMap (:187-195): copy one feature map of the window to the host. */
+/* GetLocalMap (:187-195): copy one feature map of the window (prior map first, then keyframes
+ * oldest -> newest) to host or device memory. */
 lmsf_status lmsf_tracker_local_map(lmsf_tracker* t, int32_t kind, float* out, size_t cap, size_t* n_out);
+
+/* Extensions for the multi-stream configurations (not on the reference surface):
+ * solve_extracted = lmsf_tracker_solve on the features lmsf_extract_features left on the device;
+ * set_initial_pose = before the first scan: the local frame's pose of the first scan (default
+ *                   identity = the reference's "first scan defines the local frame");
+ * set_prior_map   = a static map (local frame) kept in front of the keyframe window (shared map
+ *                   replicated on every GPU; xyzi host or device memory; index rebuilt at once);
+ * add_keyframe    = transform features by pose (local <- lidar) and push them into the window
+ *                   (evicting the oldest); any thread's stream may contribute, in a fixed order;
+ * commit_map      = rebuild the device neighbour index of every kind the window changed. */
+lmsf_status lmsf_tracker_solve_extracted(lmsf_tracker* t, double timestamp, double deltaT[16], lmsf_tracker_result* res);
+lmsf_status lmsf_tracker_set_initial_pose(lmsf_tracker* t, const double pose[16]);
+lmsf_status lmsf_tracker_set_prior_map(lmsf_tracker* t, int32_t kind, const float* xyzi, size_t n);
+lmsf_status lmsf_tracker_add_keyframe(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf,
+                                      size_t n_surf, const double pose[16]);
+lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t);
 
 /* Library version string. */
 const char* lmsf_version(void);

@@ -522,8 +522,8 @@ static lmsf_status copy_slot_features(lmsf_ctx* c, int slot, int32_t kind, float
     const size_t off = (size_t)slot * c->F + (kind == LMSF_EDGE ? 0 : hc[0]);
     if (n_out) *n_out = n;
     if (n > cap) return c->fail(LMSF_ERR_CAPACITY, "output capacity %zu < %zu features", cap, n);
-    if (n && out) HIPCHK(c, hipMemcpyAsync(out, c->feat + off, n * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
-    if (n && src) HIPCHK(c, hipMemcpyAsync(src, c->feat_src + off, n * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    if (n && out) HIPCHK(c, hipMemcpyAsync(out, c->feat + off, n * sizeof(float4), hipMemcpyDefault, c->stream));
+    if (n && src) HIPCHK(c, hipMemcpyAsync(src, c->feat_src + off, n * sizeof(int), hipMemcpyDefault, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return LMSF_OK;
 }
@@ -551,7 +551,7 @@ lmsf_status lmsf_batch_load_scans(lmsf_ctx* c, const float* xyzi, const int64_t*
             return c->fail(LMSF_ERR_CAPACITY, "scan %d has %lld points (max_scan_points %d)", i, (long long)counts[i], c->R);
         if (counts[i])
             HIPCHK(c, hipMemcpyAsync(c->raw + (size_t)i * c->R, xyzi + 4 * off, counts[i] * sizeof(float4),
-                                     hipMemcpyHostToDevice, c->stream));
+                                     hipMemcpyDefault, c->stream));   // host or device source
         c->h_counts[i] = (int)counts[i];
         off += (size_t)counts[i];
     }
@@ -689,6 +689,7 @@ namespace lmsf {
 hipStream_t ctx_stream(lmsf_ctx* c) { return c->stream; }
 int ctx_device(const lmsf_ctx* c) { return c->cfg.device; }
 int ctx_feature_capacity(const lmsf_ctx* c) { return c->F; }
+bool ctx_features_on_device(const lmsf_ctx* c) { return c->features_on_device; }
 lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg) { return c->fail(code, "%s", msg); }
 
 // SetInputSource from device-resident points (local-map rebuild without a host round trip).

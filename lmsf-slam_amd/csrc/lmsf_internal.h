@@ -125,6 +125,7 @@ hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hi
 hipStream_t ctx_stream(lmsf_ctx* c);
 int ctx_device(const lmsf_ctx* c);
 int ctx_feature_capacity(const lmsf_ctx* c);
+bool ctx_features_on_device(const lmsf_ctx* c);
 lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg);
 lmsf_status ctx_set_map_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n);
 lmsf_status ctx_slot0_features(lmsf_ctx* c, const float4** d_feat, int64_t* ne, int64_t* ns);

@@ -110,12 +110,18 @@ void R_from_quat(const double* q, double* R) {
     R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
 }
 
+// One feature kind's local map: [prior | keyframe W-ring oldest -> newest] in one device buffer
+// that the context's neighbour index is built from.
 struct Window {
     std::vector<float4*> slots;
     std::vector<int> sizes;
     int head = 0, count = 0;
+    float4* prior = nullptr;
+    size_t prior_n = 0;
     float4* concat = nullptr;
+    size_t concat_cap = 0;
     size_t total = 0;
+    bool dirty = false;
 };
 
 }  // namespace
@@ -124,10 +130,11 @@ struct lmsf_tracker {
     lmsf_ctx* ctx = nullptr;
     lmsf_tracker_config cfg{};
     bool init = false;
-    Iso curr, prev, motion, last_kf;
+    Iso origin, curr, prev, motion, last_kf;
     double last_kf_time = 0.0;
     Window win[3];
-    int cap = 0;   // points per keyframe slot
+    float4* stage = nullptr;   // host/device keyframe input staged before the transform
+    int cap = 0;               // points per keyframe slot
 };
 
 namespace {
@@ -140,36 +147,48 @@ lmsf_status fail(lmsf_tracker* t, lmsf_status code, const char* msg) { return ct
         if (e_ != hipSuccess) return fail((t), LMSF_ERR_HIP, #expr); \
     } while (0)
 
-// updateLocalMap (:205-232) for every kind with a non-empty cloud.
-lmsf_status update_local_map(lmsf_tracker* t, const Iso& T) {
-    const float4* feat;
-    int64_t ne, ns;
-    lmsf_status rc = ctx_slot0_features(t->ctx, &feat, &ne, &ns);
-    if (rc) return rc;
-    hipStream_t s = ctx_stream(t->ctx);
+Affine34 affine(const Iso& T) {
     Affine34 M;
     for (int i = 0; i < 3; ++i) {
         for (int j = 0; j < 3; ++j) M.m[4 * i + j] = T.R[3 * i + j];
         M.m[4 * i + 3] = T.t[i];
     }
+    return M;
+}
+
+// AddFrameForMotion / AddFrameForTime of one kind: pcl::transformPointCloud(cloud, T) into the
+// next window slot (evicting the oldest when full).  src is device memory.
+lmsf_status push_frame(lmsf_tracker* t, int kind, const float4* src, int64_t n, const Iso& T) {
+    if (n == 0) return LMSF_OK;                                   // :213
+    if (n > t->cap) return fail(t, LMSF_ERR_CAPACITY, "keyframe larger than the tracker slot capacity");
+    Window& w = t->win[kind];
+    const int W = (int)w.slots.size();
+    int slot;
+    if (w.count < W) {
+        slot = (w.head + w.count) % W;
+        ++w.count;
+    } else {                                                      // window full: evict the oldest
+        slot = w.head;
+        w.head = (w.head + 1) % W;
+    }
+    TCHK(t, launch_transform(src, (int)n, affine(T), w.slots[slot], ctx_stream(t->ctx)));
+    w.sizes[slot] = (int)n;
+    w.dirty = true;
+    return LMSF_OK;
+}
+
+// SetInputSource(GetLocalMap()) (:229) for every kind whose window changed.
+lmsf_status commit(lmsf_tracker* t) {
+    hipStream_t s = ctx_stream(t->ctx);
     for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) {
-        const int64_t n = kind == LMSF_EDGE ? ne : ns;
-        if (n == 0) continue;                                   // :213
-        if (n > t->cap) return fail(t, LMSF_ERR_CAPACITY, "keyframe larger than the tracker slot capacity");
-        const float4* src = feat + (kind == LMSF_EDGE ? 0 : ne);
         Window& w = t->win[kind];
+        if (!w.dirty) continue;
         const int W = (int)w.slots.size();
-        int slot;
-        if (w.count < W) {
-            slot = (w.head + w.count) % W;
-            ++w.count;
-        } else {                                                  // window full: evict the oldest
-            slot = w.head;
-            w.head = (w.head + 1) % W;
-        }
-        TCHK(t, launch_transform(src, (int)n, M, w.slots[slot], s));
-        w.sizes[slot] = (int)n;
         size_t off = 0;
+        if (w.prior_n) {
+            TCHK(t, hipMemcpyAsync(w.concat, w.prior, w.prior_n * sizeof(float4), hipMemcpyDeviceToDevice, s));
+            off = w.prior_n;
+        }
         for (int i = 0; i < w.count; ++i) {
             const int k = (w.head + i) % W;
             TCHK(t, hipMemcpyAsync(w.concat + off, w.slots[k], (size_t)w.sizes[k] * sizeof(float4),
@@ -177,10 +196,24 @@ lmsf_status update_local_map(lmsf_tracker* t, const Iso& T) {
             off += (size_t)w.sizes[k];
         }
         w.total = off;
-        rc = ctx_set_map_device(t->ctx, kind, w.concat, off);   // SetInputSource(GetLocalMap())
+        w.dirty = false;
+        lmsf_status rc = ctx_set_map_device(t->ctx, kind, w.concat, off);
         if (rc) return rc;
     }
     return LMSF_OK;
+}
+
+// updateLocalMap (:205-232) with the current scan's features (context slot 0).
+lmsf_status update_local_map(lmsf_tracker* t, const Iso& T) {
+    const float4* feat;
+    int64_t ne, ns;
+    lmsf_status rc = ctx_slot0_features(t->ctx, &feat, &ne, &ns);
+    if (rc) return rc;
+    rc = push_frame(t, LMSF_EDGE, feat, ne, T);
+    if (rc) return rc;
+    rc = push_frame(t, LMSF_SURF, feat + ne, ns, T);
+    if (rc) return rc;
+    return commit(t);
 }
 
 lmsf_status set_features(lmsf_tracker* t, const float* edge, size_t ne, const float* surf, size_t ns) {
@@ -211,6 +244,7 @@ lmsf_status lmsf_tracker_config_init(lmsf_tracker_config* cfg) {
     cfg->threshold_trans = 0.3;
     cfg->threshold_rot = 0.1;
     cfg->time_interval = 10.0;
+    cfg->manual_map_update = 0;
     return LMSF_OK;
 }
 
@@ -221,7 +255,9 @@ void lmsf_tracker_destroy(lmsf_tracker* t) {
     for (auto& w : t->win) {
         for (float4* p : w.slots) hipFree(p);
         hipFree(w.concat);
+        hipFree(w.prior);
     }
+    hipFree(t->stage);
     delete t;
 }
 
@@ -239,28 +275,40 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
         w.sizes.assign(cfg->window_frames, 0);
         for (auto& p : w.slots)
             if (hipMalloc((void**)&p, (size_t)t->cap * sizeof(float4)) != hipSuccess) { lmsf_tracker_destroy(t); return LMSF_ERR_HIP; }
-        if (hipMalloc((void**)&w.concat, (size_t)t->cap * cfg->window_frames * sizeof(float4)) != hipSuccess) {
+        w.concat_cap = (size_t)t->cap * cfg->window_frames;
+        if (hipMalloc((void**)&w.concat, w.concat_cap * sizeof(float4)) != hipSuccess) {
             lmsf_tracker_destroy(t);
             return LMSF_ERR_HIP;
         }
     }
-    t->curr = t->prev = t->motion = t->last_kf = iso_identity();
+    if (hipMalloc((void**)&t->stage, (size_t)t->cap * sizeof(float4)) != hipSuccess) {
+        lmsf_tracker_destroy(t);
+        return LMSF_ERR_HIP;
+    }
+    t->origin = t->curr = t->prev = t->motion = t->last_kf = iso_identity();
     *out = t;
     return LMSF_OK;
 }
 
-lmsf_status lmsf_tracker_solve(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf, size_t n_surf,
-                               double timestamp, double deltaT[16], lmsf_tracker_result* res) {
-    if (!t || !deltaT || (n_edge && !edge) || (n_surf && !surf)) return LMSF_ERR_ARG;
-    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+}  // extern "C"
+
+namespace {
+
+// Solve (:107-160) on the features currently in the context's slot 0.
+lmsf_status solve_current(lmsf_tracker* t, double timestamp, double deltaT[16], lmsf_tracker_result* res) {
     lmsf_tracker_result r;
     std::memset(&r, 0, sizeof r);
-    lmsf_status rc = set_features(t, edge, n_edge, surf, n_surf);
-    if (rc) return rc;
+    lmsf_status rc;
+    const bool manual = t->cfg.manual_map_update != 0;
     if (!t->init) {                                                   // :112-122
-        rc = update_local_map(t, iso_identity());
-        if (rc) return rc;
-        t->curr = t->prev = t->motion = t->last_kf = iso_identity();
+        // the local frame is the first scan's frame (origin = identity, as the reference) unless
+        // lmsf_tracker_set_initial_pose placed it in a shared map's frame
+        t->curr = t->prev = t->last_kf = t->origin;
+        t->motion = iso_identity();
+        if (!manual) {
+            rc = update_local_map(t, t->origin);
+            if (rc) return rc;
+        }
         t->last_kf_time = timestamp;
         t->init = true;
         r.initialized = 1;
@@ -290,14 +338,93 @@ lmsf_status lmsf_tracker_solve(lmsf_tracker* t, const float* edge, size_t n_edge
         if (type) {
             t->last_kf = t->curr;
             t->last_kf_time = timestamp;
-            rc = update_local_map(t, t->curr);
-            if (rc) return rc;
+            if (!manual) {
+                rc = update_local_map(t, t->curr);
+                if (rc) return rc;
+            }
         }
     }
     r.local_map_edge = (int64_t)t->win[LMSF_EDGE].total;
     r.local_map_surf = (int64_t)t->win[LMSF_SURF].total;
     if (res) *res = r;
     return LMSF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+lmsf_status lmsf_tracker_solve(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf, size_t n_surf,
+                               double timestamp, double deltaT[16], lmsf_tracker_result* res) {
+    if (!t || !deltaT || (n_edge && !edge) || (n_surf && !surf)) return LMSF_ERR_ARG;
+    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    lmsf_status rc = set_features(t, edge, n_edge, surf, n_surf);
+    if (rc) return rc;
+    return solve_current(t, timestamp, deltaT, res);
+}
+
+lmsf_status lmsf_tracker_solve_extracted(lmsf_tracker* t, double timestamp, double deltaT[16], lmsf_tracker_result* res) {
+    if (!t || !deltaT) return LMSF_ERR_ARG;
+    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    if (!ctx_features_on_device(t->ctx)) return fail(t, LMSF_ERR_STATE, "no extracted features on the device");
+    return solve_current(t, timestamp, deltaT, res);
+}
+
+lmsf_status lmsf_tracker_set_initial_pose(lmsf_tracker* t, const double pose[16]) {
+    if (!t || !pose) return LMSF_ERR_ARG;
+    if (t->init) return fail(t, LMSF_ERR_STATE, "initial pose after the first scan");
+    t->origin = iso_from16(pose);
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_tracker_set_prior_map(lmsf_tracker* t, int32_t kind, const float* xyzi, size_t n) {
+    if (!t || (kind != LMSF_EDGE && kind != LMSF_SURF) || (n && !xyzi)) return LMSF_ERR_ARG;
+    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    Window& w = t->win[kind];
+    hipStream_t s = ctx_stream(t->ctx);
+    TCHK(t, hipStreamSynchronize(s));
+    const size_t need = n + (size_t)t->cap * w.slots.size();
+    if (need > w.concat_cap) {
+        TCHK(t, hipFree(w.concat));
+        w.concat = nullptr;
+        w.concat_cap = 0;
+        TCHK(t, hipMalloc((void**)&w.concat, need * sizeof(float4)));
+        w.concat_cap = need;
+    }
+    TCHK(t, hipFree(w.prior));
+    w.prior = nullptr;
+    w.prior_n = 0;
+    if (n) {
+        TCHK(t, hipMalloc((void**)&w.prior, n * sizeof(float4)));
+        TCHK(t, hipMemcpyAsync(w.prior, xyzi, n * sizeof(float4), hipMemcpyDefault, s));
+        w.prior_n = n;
+    }
+    w.dirty = true;
+    return commit(t);
+}
+
+lmsf_status lmsf_tracker_add_keyframe(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf,
+                                      size_t n_surf, const double pose[16]) {
+    if (!t || !pose || (n_edge && !edge) || (n_surf && !surf)) return LMSF_ERR_ARG;
+    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    hipStream_t s = ctx_stream(t->ctx);
+    const Iso T = iso_from16(pose);
+    const float* src[3] = {nullptr, edge, surf};
+    const size_t cnt[3] = {0, n_edge, n_surf};
+    for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) {
+        if (cnt[kind] == 0) continue;
+        if (cnt[kind] > (size_t)t->cap) return fail(t, LMSF_ERR_CAPACITY, "keyframe larger than the tracker slot capacity");
+        TCHK(t, hipMemcpyAsync(t->stage, src[kind], cnt[kind] * sizeof(float4), hipMemcpyDefault, s));
+        lmsf_status rc = push_frame(t, kind, t->stage, (int64_t)cnt[kind], T);
+        if (rc) return rc;
+    }
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t) {
+    if (!t) return LMSF_ERR_ARG;
+    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    return commit(t);
 }
 
 lmsf_status lmsf_tracker_register(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf,

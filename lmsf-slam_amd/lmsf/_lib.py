@@ -53,7 +53,7 @@ class KernelStats(C.Structure):
 
 class TrackerConfig(C.Structure):
     _fields_ = [("window_frames", C.c_int32), ("threshold_trans", C.c_double), ("threshold_rot", C.c_double),
-                ("time_interval", C.c_double)]
+                ("time_interval", C.c_double), ("manual_map_update", C.c_int32)]
 
 
 class TrackerResult(C.Structure):
@@ -98,6 +98,11 @@ _SIGS = {
     "lmsf_tracker_register": (C.c_int32, [_P, _P, C.c_size_t, _P, C.c_size_t, _P, C.POINTER(SolveStats)]),
     "lmsf_tracker_pose": (C.c_int32, [_P, _P]),
     "lmsf_tracker_local_map": (C.c_int32, [_P, C.c_int32, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "lmsf_tracker_solve_extracted": (C.c_int32, [_P, C.c_double, _P, C.POINTER(TrackerResult)]),
+    "lmsf_tracker_set_initial_pose": (C.c_int32, [_P, _P]),
+    "lmsf_tracker_set_prior_map": (C.c_int32, [_P, C.c_int32, _P, C.c_size_t]),
+    "lmsf_tracker_add_keyframe": (C.c_int32, [_P, _P, C.c_size_t, _P, C.c_size_t, _P]),
+    "lmsf_tracker_commit_map": (C.c_int32, [_P]),
 }
 
 _lib = None
@@ -159,8 +164,8 @@ class Context:
 
     # ---- reference surface
     def set_map(self, kind, pts):
-        p = _f4(pts)
-        self._check(load().lmsf_set_map(self.h, kind, p.ctypes.data, p.shape[0]))
+        p, n, keep = _buf(pts)
+        self._check(load().lmsf_set_map(self.h, kind, p, n))
 
     def set_scan(self, kind, pts):
         p = _f4(pts) if len(pts) else np.zeros((0, 4), np.float32)
@@ -182,9 +187,9 @@ class Context:
         return out[:min(n.value, cap)].copy()
 
     def extract(self, pts):
-        p = _f4(pts) if len(pts) else np.zeros((0, 4), np.float32)
+        p, n, keep = _buf(pts)
         fc = FeatureCounts()
-        self._check(load().lmsf_extract_features(self.h, p.ctypes.data, p.shape[0], C.byref(fc)))
+        self._check(load().lmsf_extract_features(self.h, p, n, C.byref(fc)))
         return fc.n_edge, fc.n_surf
 
     def copy_features(self, kind, slot=None):
@@ -199,6 +204,13 @@ class Context:
             self._check(load().lmsf_batch_copy_features(self.h, slot, kind, out.ctypes.data, src.ctypes.data, cap,
                                                          C.byref(n)))
         return out[:n.value].copy(), src[:n.value].copy()
+
+    def copy_features_into(self, kind, out):
+        """Copy the extracted features of one kind into a preallocated (cap, 4) float32 torch tensor
+        (device memory: a device-to-device copy); returns the feature count."""
+        n = C.c_size_t()
+        self._check(load().lmsf_copy_features(self.h, kind, out.data_ptr(), None, int(out.shape[0]), C.byref(n)))
+        return n.value
 
     # ---- batch path
     def load_scans(self, scans):
@@ -250,14 +262,27 @@ def _pts(a):
     return _f4(a) if len(a) else np.zeros((0, 4), np.float32)
 
 
+def _buf(a):
+    """(pointer, rows, keep-alive) of an (n, 4) float32 xyzi array: numpy (host) or a torch tensor
+    (host or device memory; the C ABI copies with hipMemcpyDefault)."""
+    if hasattr(a, "data_ptr"):
+        if a.dtype != __import__("torch").float32 or a.dim() != 2 or a.shape[1] != 4 or not a.is_contiguous():
+            raise ValueError("expected a contiguous (n, 4) float32 tensor")
+        return (a.data_ptr() if a.shape[0] else None), int(a.shape[0]), a
+    p = _pts(a)
+    return p.ctypes.data, p.shape[0], p
+
+
 class Tracker:
     """lmsf_tracker: LidarTrackerLocalMap over a Context (poses are 4x4 row-major matrices)."""
 
-    def __init__(self, ctx: Context, window_frames=20, threshold_trans=0.3, threshold_rot=0.1, time_interval=10.0):
+    def __init__(self, ctx: Context, window_frames=20, threshold_trans=0.3, threshold_rot=0.1, time_interval=10.0,
+                 manual_map_update=False):
         cfg = TrackerConfig()
         load().lmsf_tracker_config_init(C.byref(cfg))
         cfg.window_frames, cfg.threshold_trans = window_frames, threshold_trans
         cfg.threshold_rot, cfg.time_interval = threshold_rot, time_interval
+        cfg.manual_map_update = int(bool(manual_map_update))
         self.ctx = ctx
         h = C.c_void_p()
         ctx._check(load().lmsf_tracker_create(ctx.h, C.byref(cfg), C.byref(h)))
@@ -297,6 +322,30 @@ class Tracker:
         out = np.zeros((n.value, 4), np.float32)
         self.ctx._check(load().lmsf_tracker_local_map(self.h, kind, out.ctypes.data, n.value, C.byref(n)))
         return out
+
+    # ---- multi-stream extensions
+    def solve_extracted(self, timestamp, deltaT=None):
+        d = np.ascontiguousarray(np.eye(4) if deltaT is None else deltaT, dtype=np.float64).copy()
+        r = TrackerResult()
+        self.ctx._check(load().lmsf_tracker_solve_extracted(self.h, float(timestamp), d.ctypes.data, C.byref(r)))
+        return d, r
+
+    def set_initial_pose(self, T):
+        T = np.ascontiguousarray(T, dtype=np.float64)
+        self.ctx._check(load().lmsf_tracker_set_initial_pose(self.h, T.ctypes.data))
+
+    def set_prior_map(self, kind, pts):
+        p, n, keep = _buf(pts)
+        self.ctx._check(load().lmsf_tracker_set_prior_map(self.h, kind, p, n))
+
+    def add_keyframe(self, edge, surf, pose):
+        pe, ne, ke = _buf(edge)
+        ps, ns, ks = _buf(surf)
+        T = np.ascontiguousarray(pose, dtype=np.float64)
+        self.ctx._check(load().lmsf_tracker_add_keyframe(self.h, pe, ne, ps, ns, T.ctypes.data))
+
+    def commit_map(self):
+        self.ctx._check(load().lmsf_tracker_commit_map(self.h))
 
 
 def header_symbols(path=HEADER_PATH):

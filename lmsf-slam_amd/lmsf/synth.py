@@ -352,11 +352,38 @@ def transform_points(pose, pts):
 
 
 # ----------------------------------------------------------------------------- configs
+BEAMS128_DEG = np.linspace(-25.0, 15.0, 128)          # C5: 128 beams evenly in [-25, 15] deg
+HDL64_DEG = np.concatenate([np.linspace(2.0, -8.33, 32), np.linspace(-8.83, -24.33, 32)])
+# C3 sub-lidar extrinsic primary <- sub (qx qy qz qw tx ty tz),
+# config/MultiLidar_system/loam_feature_multi_lidar_system.yaml:73-74 ("PS-Calib")
+DUAL_EXTRINSIC = np.array([0.34087, -0.0101817, 0.0147921, 0.945613, 0.0334837, -0.540249, -0.141798])
+
 CONFIGS = {
-    # name: (n_beams, n_cols, map_points, map_radius, config index for seeds)
-    "C1": dict(n_cols=1800, map_points=200_000, radius=60.0, k=1),
-    "C2": dict(n_cols=4096, map_points=1_000_000, radius=100.0, k=2),
+    # n_cols per revolution, map points, map slab radius, seed index k; elev = beam table,
+    # extract = lmsf_config overrides the extraction needs for that beam table
+    "C1": dict(n_cols=1800, map_points=200_000, radius=60.0, k=1, elev=VLP16_FIRING_DEG, extract={}),
+    "C2": dict(n_cols=4096, map_points=1_000_000, radius=100.0, k=2, elev=VLP16_FIRING_DEG, extract={}),
+    "C3": dict(n_cols=4096, map_points=1_000_000, radius=100.0, k=3, elev=VLP16_FIRING_DEG, extract={}),
+    "C4": dict(n_cols=4096, map_points=5_000_000, radius=100.0, k=4, elev=VLP16_FIRING_DEG, extract={}),
+    "C5": dict(n_cols=2048, map_points=10_000_000, radius=100.0, k=5, elev=BEAMS128_DEG,
+               extract=dict(n_scans=128, beam_lo_deg=-25.0, beam_spacing_deg=40.0 / 127)),
 }
+
+
+def unit_extrinsic(x):
+    """Normalised copy of a (q, t) pose (the YAML quaternion is rounded to 6 digits)."""
+    y = np.array(x, dtype=np.float64)
+    y[:4] /= np.linalg.norm(y[:4])
+    return y
+
+
+def compose(a, b):
+    """(q, t) poses: a * b."""
+    R = quat_to_mat(a[:4])
+    out = np.empty(7)
+    out[:4] = quat_mul(a[:4], b[:4])
+    out[4:] = R @ np.asarray(b[4:]) + np.asarray(a[4:])
+    return out
 
 
 @dataclasses.dataclass
@@ -379,7 +406,8 @@ def make_workload(config: str = "C2", n_scans: int = 4, map_points: int | None =
     truth = trajectory(n_scans, 3000 + k, step=road_length / max(n_scans, 1))
     rng = np.random.default_rng(3000 + k)
     guess = np.stack([perturb(p, rng) for p in truth]) if n_scans else np.zeros((0, 7))
-    scans = [make_scan(scene, truth[i], 2000 + k + 97 * i, n_cols=n_cols or c["n_cols"]) for i in range(n_scans)]
+    scans = [make_scan(scene, truth[i], 2000 + k + 97 * i, n_cols=n_cols or c["n_cols"], elev_deg=c["elev"])
+             for i in range(n_scans)]
     em, sm = make_map(scene, map_points or c["map_points"], 1000 + k + 7, center_x=(0.0, road_length),
                       radius=radius or c["radius"])
     return Workload(scene, em, sm, scans, truth, guess)

@@ -79,29 +79,57 @@ def transform_cloud(pts, T):
 
 
 class Tracker:
-    def __init__(self, window_frames=20, threshold_trans=0.3, threshold_rot=0.1, time_interval=10.0, solver=0):
+    """Extensions mirrored from include/lmsf/lmsf.h (multi-stream configurations, not reference
+    surface): `origin` (lmsf_tracker_set_initial_pose), `prior` maps in front of the window
+    (lmsf_tracker_set_prior_map), manual keyframe mode (add_keyframe + commit)."""
+
+    def __init__(self, window_frames=20, threshold_trans=0.3, threshold_rot=0.1, time_interval=10.0, solver=0,
+                 manual_map_update=False):
         self.reg = O.Registration(solver)
         self.W = window_frames
         self.th_t, self.th_r, self.dt_kf = threshold_trans, threshold_rot, time_interval
+        self.manual = manual_map_update
         self.init = False
+        self.origin = np.eye(4)
         self.curr = self.prev = self.motion = self.last_kf = np.eye(4)
         self.last_kf_time = 0.0
         self.win = {1: deque(), 2: deque()}
+        self.prior = {1: None, 2: None}
+        self.dirty = {1: False, 2: False}
 
     def local_map(self, kind):
+        parts = ([self.prior[kind]] if self.prior[kind] is not None else []) + list(self.win[kind])
+        return np.concatenate(parts, 0) if parts else np.zeros((0, 4), np.float32)
+
+    def set_prior_map(self, kind, pts):
+        self.prior[kind] = np.asarray(pts, np.float32) if len(pts) else None
+        self.dirty[kind] = True
+        self.commit()
+
+    def _push(self, kind, f, T):
+        if len(f) == 0:
+            return
         w = self.win[kind]
-        return np.concatenate(list(w), 0) if w else np.zeros((0, 4), np.float32)
+        if len(w) == self.W:
+            w.popleft()
+        w.append(transform_cloud(f, T))
+        self.dirty[kind] = True
+
+    def commit(self):
+        for kind in (1, 2):
+            if self.dirty[kind]:
+                m = self.local_map(kind)
+                if len(m):
+                    self.reg.set_map(kind, m)
+                self.dirty[kind] = False
+
+    def add_keyframe(self, edge, surf, T):
+        self._push(1, edge, T)
+        self._push(2, surf, T)
 
     def _update_local_map(self, feats, T):
-        for kind in (1, 2):
-            f = feats[kind]
-            if len(f) == 0:
-                continue
-            w = self.win[kind]
-            if len(w) == self.W:
-                w.popleft()
-            w.append(transform_cloud(f, T))
-            self.reg.set_map(kind, self.local_map(kind))
+        self.add_keyframe(feats[1], feats[2], T)
+        self.commit()
 
     def _register(self, feats, T):
         self.reg.set_scan(1, feats[1])
@@ -117,8 +145,10 @@ class Tracker:
         feats = {1: edge, 2: surf}
         deltaT = np.eye(4) if deltaT is None else np.asarray(deltaT, dtype=np.float64)
         if not self.init:
-            self._update_local_map(feats, np.eye(4))
-            self.curr = self.prev = self.motion = self.last_kf = np.eye(4)
+            self.curr = self.prev = self.last_kf = self.origin.copy()
+            self.motion = np.eye(4)
+            if not self.manual:
+                self._update_local_map(feats, self.origin)
             self.last_kf_time = timestamp
             self.init = True
             return deltaT, 1, None
@@ -141,5 +171,6 @@ class Tracker:
         if typ:
             self.last_kf = self.curr
             self.last_kf_time = timestamp
-            self._update_local_map(feats, self.curr)
+            if not self.manual:
+                self._update_local_map(feats, self.curr)
         return self.motion.copy(), typ, st

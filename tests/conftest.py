@@ -50,7 +50,17 @@ def sequence_workload():
     truth = synth.trajectory(10, 3001, step=0.25)
     scans = [synth.make_scan(scene, truth[i], 2001 + 97 * i, n_cols=1024, elev_deg=HDL64_ELEV)
              for i in range(len(truth))]
-    return SimpleNamespace(scans=scans, truth=truth, n_scans=64, dt=0.1)
+    # world-frame prior map of the same stretch (multi-stream shared-map tests)
+    edge_map, surf_map = synth.make_map(scene, 150_000, 1008, center_x=(0.0, 2.5), radius=35.0)
+    return SimpleNamespace(scans=scans, truth=truth, n_scans=64, dt=0.1, edge_map=edge_map, surf_map=surf_map)
+
+
+def pose_matrix(p):
+    from lmsf import synth
+    T = np.eye(4)
+    T[:3, :3] = synth.quat_to_mat(p[:4])
+    T[:3, 3] = p[4:]
+    return T
 
 
 def relative_truth(truth):

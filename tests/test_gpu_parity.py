@@ -349,13 +349,68 @@ def test_tracker_time_gate_and_capacity(lib, oracle_mod, sequence_workload):
         assert r.local_map_surf == sum(kf_sizes[-2:])
     assert types == [lib.UPDATE_MOTION, lib.UPDATE_NONE, lib.UPDATE_TIME, lib.UPDATE_NONE, lib.UPDATE_TIME]
     gt.close()
-    small = _ctx(lib, n_scans=wl.n_scans, max_features=1000)
+    small = _ctx(lib, n_scans=wl.n_scans, max_features=1000, max_scan_points=1000)   # capacity = max of both
     t2 = lib.Tracker(small, window_frames=2)
     e, s, _, _ = oracle_mod.extract(wl.scans[0], n_scans=wl.n_scans)
     assert len(s) > 1000
     with pytest.raises(lib.LmsfError):
         t2.solve(e[:500], s, 0.0)
     t2.close()
+
+
+def test_tracker_shared_map_streams(lib, oracle_mod, sequence_workload):
+    """C4 flow on one GPU: two streams (scans 0-4 and 5-9) with a shared world-frame prior map,
+    initial poses in that frame, keyframes exchanged in stream order and committed once per step
+    (device-tensor keyframe buffers), against two oracle trackers doing the same."""
+    import torch
+    import tracker as OT
+    from conftest import mat_err, pose_matrix
+    wl = sequence_workload
+    streams = [list(range(0, 5)), list(range(5, 10))]
+    ctxs = [_ctx(lib, n_scans=wl.n_scans) for _ in streams]
+    gts = [lib.Tracker(c, window_frames=4, manual_map_update=True) for c in ctxs]
+    ots = [OT.Tracker(window_frames=4, manual_map_update=True) for _ in streams]
+    dev = torch.device("cuda", 0)
+    for s, idx in enumerate(streams):
+        T0 = pose_matrix(wl.truth[idx[0]])
+        gts[s].set_initial_pose(T0)
+        ots[s].origin = T0.copy()
+        gts[s].set_prior_map(lib.EDGE, torch.from_numpy(wl.edge_map).to(dev))
+        gts[s].set_prior_map(lib.SURF, wl.surf_map)
+        ots[s].set_prior_map(1, wl.edge_map)
+        ots[s].set_prior_map(2, wl.surf_map)
+    buf = {k: torch.zeros((70000, 4), dtype=torch.float32, device=dev) for k in (lib.EDGE, lib.SURF)}
+    for step in range(5):
+        kfs_g, kfs_o = [], []
+        for s, idx in enumerate(streams):
+            scan = wl.scans[idx[step]]
+            e, su, _, _ = oracle_mod.extract(scan, n_scans=wl.n_scans)
+            ctxs[s].extract(torch.from_numpy(scan).to(dev))
+            _, r = gts[s].solve_extracted(wl.dt * step)
+            _, otyp, _ = ots[s].solve(e, su, wl.dt * step)
+            assert r.update_type == otyp
+            dt, dr = mat_err(gts[s].pose(), ots[s].curr)
+            assert dt <= POSE_TOL and dr <= POSE_TOL, (step, s, dt, dr)
+            dt, dr = mat_err(gts[s].pose(), pose_matrix(wl.truth[idx[step]]))
+            assert dt < 0.05 and dr < 0.01, (step, s, dt, dr)
+            if otyp:
+                ne = ctxs[s].copy_features_into(lib.EDGE, buf[lib.EDGE])
+                ns = ctxs[s].copy_features_into(lib.SURF, buf[lib.SURF])
+                assert (ne, ns) == (len(e), len(su))
+                kfs_g.append((buf[lib.EDGE][:ne].clone(), buf[lib.SURF][:ns].clone(), gts[s].pose()))
+                kfs_o.append((e, su, ots[s].curr.copy()))
+        for g, o in zip(kfs_g, kfs_o):              # every stream appends every keyframe, same order
+            for s in range(len(streams)):
+                gts[s].add_keyframe(*g)
+                ots[s].add_keyframe(*o)
+        for s in range(len(streams)):
+            gts[s].commit_map()
+            ots[s].commit()
+            assert len(gts[s].local_map(lib.SURF)) == len(ots[s].local_map(2))
+    np.testing.assert_allclose(gts[0].local_map(lib.SURF), gts[1].local_map(lib.SURF), atol=0)
+    np.testing.assert_allclose(gts[0].local_map(lib.EDGE), ots[0].local_map(1), atol=1e-4)
+    for t in gts:
+        t.close()
 
 
 def test_reference_interface(lib, oracle_mod, small_workload):
