@@ -108,6 +108,18 @@ _SIGS = {
 _lib = None
 
 
+def _share_torch_hip_runtime():
+    """PyTorch-ROCm bundles its own libamdhip64 / libhsa-runtime64 (SONAME libamdhip64.so.7, as
+    /opt/rocm's).  glibc reuses an already-loaded library by SONAME, but torch asks for
+    "libamdhip64.so", which does not match /opt/rocm's copy: loading liblmsf first would put two HIP
+    runtimes in the process (torch then fails to initialise, and device pointers cannot be passed
+    between torch/RCCL buffers and the library).  Loading torch first gives one runtime."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load():
     """Load liblmsf_hip.so (raises if it has not been built: there is no fallback path)."""
     global _lib
@@ -115,6 +127,7 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: build it with `make -C lmsf-slam_amd` "
                               "(__graft_entry__.build()); the HIP path has no CPU fallback")
+        _share_torch_hip_runtime()
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name)

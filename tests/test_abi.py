@@ -6,6 +6,7 @@ import ctypes
 import math
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -142,3 +143,15 @@ def test_lmsf_header_compiles_as_c_and_cpp(tmp_path):
     for comp, flag in (("gcc", "-std=c99"), ("g++", "-std=c++17")):
         subprocess.run([comp, flag, "-fsyntax-only", "-I", os.path.join(REPO, "include"), "-x",
                         "c" if comp == "gcc" else "c++", str(src)], check=True)
+
+
+def test_single_hip_runtime_in_process():
+    """Loading the library never adds a second HIP runtime next to PyTorch's (see _lib.load)."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from lmsf import _lib; _lib.load()\n"
+            "import torch\n"
+            "libs = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}\n"
+            "print(len(libs))\n") % os.path.join(REPO, "lmsf-slam_amd")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "1"
