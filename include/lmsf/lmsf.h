@@ -227,11 +227,31 @@ lmsf_status lmsf_tracker_local_map(lmsf_tracker* t, int32_t kind, float* out, si
  *                   (evicting the oldest); any thread's stream may contribute, in a fixed order;
  * commit_map      = rebuild the device neighbour index of every kind the window changed. */
 lmsf_status lmsf_tracker_solve_extracted(lmsf_tracker* t, double timestamp, double deltaT[16], lmsf_tracker_result* res);
+/* lmsf_tracker_register on the device-extracted features (C3: the sub-LiDAR scan is extracted on
+ * the primary tracker's context after its Solve, then registered against the primary local map). */
+lmsf_status lmsf_tracker_register_extracted(lmsf_tracker* t, double pose[16], lmsf_solve_stats* stats);
 lmsf_status lmsf_tracker_set_initial_pose(lmsf_tracker* t, const double pose[16]);
 lmsf_status lmsf_tracker_set_prior_map(lmsf_tracker* t, int32_t kind, const float* xyzi, size_t n);
 lmsf_status lmsf_tracker_add_keyframe(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf,
                                       size_t n_surf, const double pose[16]);
 lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t);
+
+/* ---- dual-LiDAR extrinsic initialisation (C3): Algorithm::HandEyeCalibrationBase
+ * (INC/Algorithm/calibration/handeye_calibration_base.hpp:36-244) as driven by
+ * MultiLidarSystem::process phase 0 (INC/System/ML_System.hpp:268-281).  Host-only arithmetic
+ * (no device needed).  Poses are row-major 4x4 inter-frame motions (tracker deltaT outputs). */
+typedef struct lmsf_handeye lmsf_handeye;
+lmsf_status lmsf_handeye_create(lmsf_handeye** out);
+void lmsf_handeye_destroy(lmsf_handeye* h);
+/* AddPose (:71-106): *ok = the reference's return value (motion accepted and >= 3 pairs stored). */
+lmsf_status lmsf_handeye_add_pose(lmsf_handeye* h, const double primary[16], const double sub[16], int32_t* ok);
+/* CalibExRotation (:113-148); singular_values (nullable) = the 4 singular values, descending. */
+lmsf_status lmsf_handeye_calib_rotation(lmsf_handeye* h, int32_t* ok, double singular_values[4]);
+/* CalibExTranslation (:150-184). */
+lmsf_status lmsf_handeye_calib_translation(lmsf_handeye* h, int32_t* ok);
+/* GetCalibResult (:187-196): primary <- sub extrinsic. */
+lmsf_status lmsf_handeye_result(const lmsf_handeye* h, double T[16], int32_t* ok);
+lmsf_status lmsf_handeye_pair_count(const lmsf_handeye* h, int32_t* n);
 
 /* Library version string. */
 const char* lmsf_version(void);

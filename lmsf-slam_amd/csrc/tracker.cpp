@@ -442,6 +442,19 @@ lmsf_status lmsf_tracker_register(lmsf_tracker* t, const float* edge, size_t n_e
     return LMSF_OK;
 }
 
+lmsf_status lmsf_tracker_register_extracted(lmsf_tracker* t, double pose[16], lmsf_solve_stats* stats) {
+    if (!t || !pose) return LMSF_ERR_ARG;
+    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    if (!ctx_features_on_device(t->ctx)) return fail(t, LMSF_ERR_STATE, "no extracted features on the device");
+    Iso T = iso_from16(pose);
+    lmsf_solve_stats st;
+    lmsf_status rc = register_pose(t, T, &st);
+    if (rc) return rc;
+    iso_to16(T, pose);
+    if (stats) *stats = st;
+    return LMSF_OK;
+}
+
 lmsf_status lmsf_tracker_pose(const lmsf_tracker* t, double T[16]) {
     if (!t || !T) return LMSF_ERR_ARG;
     iso_to16(t->curr, T);

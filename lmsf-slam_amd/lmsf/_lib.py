@@ -99,10 +99,18 @@ _SIGS = {
     "lmsf_tracker_pose": (C.c_int32, [_P, _P]),
     "lmsf_tracker_local_map": (C.c_int32, [_P, C.c_int32, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "lmsf_tracker_solve_extracted": (C.c_int32, [_P, C.c_double, _P, C.POINTER(TrackerResult)]),
+    "lmsf_tracker_register_extracted": (C.c_int32, [_P, _P, C.POINTER(SolveStats)]),
     "lmsf_tracker_set_initial_pose": (C.c_int32, [_P, _P]),
     "lmsf_tracker_set_prior_map": (C.c_int32, [_P, C.c_int32, _P, C.c_size_t]),
     "lmsf_tracker_add_keyframe": (C.c_int32, [_P, _P, C.c_size_t, _P, C.c_size_t, _P]),
     "lmsf_tracker_commit_map": (C.c_int32, [_P]),
+    "lmsf_handeye_create": (C.c_int32, [C.POINTER(_P)]),
+    "lmsf_handeye_destroy": (None, [_P]),
+    "lmsf_handeye_add_pose": (C.c_int32, [_P, _P, _P, C.POINTER(C.c_int32)]),
+    "lmsf_handeye_calib_rotation": (C.c_int32, [_P, C.POINTER(C.c_int32), _P]),
+    "lmsf_handeye_calib_translation": (C.c_int32, [_P, C.POINTER(C.c_int32)]),
+    "lmsf_handeye_result": (C.c_int32, [_P, _P, C.POINTER(C.c_int32)]),
+    "lmsf_handeye_pair_count": (C.c_int32, [_P, C.POINTER(C.c_int32)]),
 }
 
 _lib = None
@@ -343,6 +351,12 @@ class Tracker:
         self.ctx._check(load().lmsf_tracker_solve_extracted(self.h, float(timestamp), d.ctypes.data, C.byref(r)))
         return d, r
 
+    def register_extracted(self, pose):
+        T = np.ascontiguousarray(pose, dtype=np.float64).copy()
+        st = SolveStats()
+        self.ctx._check(load().lmsf_tracker_register_extracted(self.h, T.ctypes.data, C.byref(st)))
+        return T, st
+
     def set_initial_pose(self, T):
         T = np.ascontiguousarray(T, dtype=np.float64)
         self.ctx._check(load().lmsf_tracker_set_initial_pose(self.h, T.ctypes.data))
@@ -366,3 +380,55 @@ def header_symbols(path=HEADER_PATH):
     import re
     text = open(path).read()
     return sorted(set(re.findall(r"^\s*(?:lmsf_status|void|const char\*)\s+(lmsf_\w+)\s*\(", text, re.M)))
+
+
+class HandEye:
+    """lmsf_handeye: HandEyeCalibrationBase (host arithmetic; usable without a GPU)."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        rc = load().lmsf_handeye_create(C.byref(h))
+        if rc != OK:
+            raise LmsfError(rc, "lmsf_handeye_create failed")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().lmsf_handeye_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    @staticmethod
+    def _rc(rc):
+        if rc != OK:
+            raise LmsfError(rc, "lmsf_handeye call failed")
+
+    def add_pose(self, primary, sub):
+        a = np.ascontiguousarray(primary, dtype=np.float64)
+        b = np.ascontiguousarray(sub, dtype=np.float64)
+        ok = C.c_int32()
+        self._rc(load().lmsf_handeye_add_pose(self.h, a.ctypes.data, b.ctypes.data, C.byref(ok)))
+        return bool(ok.value)
+
+    def calib_rotation(self):
+        ok = C.c_int32()
+        sv = np.zeros(4)
+        self._rc(load().lmsf_handeye_calib_rotation(self.h, C.byref(ok), sv.ctypes.data))
+        return bool(ok.value), sv
+
+    def calib_translation(self):
+        ok = C.c_int32()
+        self._rc(load().lmsf_handeye_calib_translation(self.h, C.byref(ok)))
+        return bool(ok.value)
+
+    def result(self):
+        T = np.zeros((4, 4))
+        ok = C.c_int32()
+        self._rc(load().lmsf_handeye_result(self.h, T.ctypes.data, C.byref(ok)))
+        return T if ok.value else None
+
+    def pair_count(self):
+        n = C.c_int32()
+        self._rc(load().lmsf_handeye_pair_count(self.h, C.byref(n)))
+        return n.value
