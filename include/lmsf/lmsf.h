@@ -173,11 +173,15 @@ lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* ctx, int32_t enable_timing);
  * (INC/LidarTracker/LidarTrackerLocalMap.hpp:42-263) over one context's registration.
  * The local map implementation is absent from the reference snapshot (factory/Map/LocalMap_factory.hpp,
  * included at :15); the build defines "sliding_Localmap" as a window of the last `window_frames`
- * keyframes per feature kind, concatenated oldest -> newest, rebuilt on the device at every
- * keyframe (MOTION and TIME updates both append).  Poses are row-major 4x4 Isometry3d matrices. */
+ * keyframes per feature kind, concatenated oldest -> newest and VoxelGrid-downsampled (leaf per
+ * kind), rebuilt on the device at every keyframe (MOTION and TIME updates both append).  Without
+ * the downsampling a 16-beam keyframe's 5-NN sets lie on one ring (degenerate plane fits) and
+ * tracking drifts by decimetres per frame.  Poses are row-major 4x4 Isometry3d matrices. */
 typedef struct lmsf_tracker lmsf_tracker;
 typedef struct {
-    int32_t window_frames;     /* keyframes kept per feature map (build-defined, default 20) */
+    int32_t window_frames;     /* keyframes kept per feature map: 10, the LOAM MultiLidar config's
+                                  tracker.local_map_type.sliding_window.size
+                                  (config/MultiLidar_system/loam_feature_multi_lidar_system.yaml:28-29) */
     double threshold_trans;    /* THRESHOLD_TRANS_ = 0.3 m   (LidarTrackerLocalMap.hpp:65) */
     double threshold_rot;      /* THRESHOLD_ROT_   = 0.1 rad */
     double time_interval;      /* TIME_INTERVAL_   = 10 s */
@@ -185,6 +189,8 @@ typedef struct {
                                   decides (res->update_type, keyframe pose/time); the caller appends
                                   keyframes with lmsf_tracker_add_keyframe and rebuilds once with
                                   lmsf_tracker_commit_map (multi-stream map stitching) */
+    double leaf_edge;          /* VoxelGrid leaf of the keyframe window, per kind (build-defined: */
+    double leaf_surf;          /* 0.2 / 0.4 m, LOAM's mapping resolutions; 0 = no downsampling) */
 } lmsf_tracker_config;
 
 #define LMSF_UPDATE_NONE 0    /* LocalMapUpdataType NO_UPDATA */
@@ -235,6 +241,12 @@ lmsf_status lmsf_tracker_set_prior_map(lmsf_tracker* t, int32_t kind, const floa
 lmsf_status lmsf_tracker_add_keyframe(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf,
                                       size_t n_surf, const double pose[16]);
 lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t);
+
+/* VoxelGridFilter::Filter (INC/Algorithm/PointClouds/processing/Filter/voxel_grid.hpp:25-34,
+ * filter_base.hpp:34-45; pcl::VoxelGrid centroids, ascending voxel index, input returned unchanged
+ * when the voxel index would overflow int32).  in/out: host or device memory; *n_out = voxels. */
+lmsf_status lmsf_voxel_filter(lmsf_ctx* ctx, const float* xyzi, size_t n, float leaf, float* out, size_t cap,
+                              size_t* n_out);
 
 /* ---- dual-LiDAR extrinsic initialisation (C3): Algorithm::HandEyeCalibrationBase
  * (INC/Algorithm/calibration/handeye_calibration_base.hpp:36-244) as driven by

@@ -101,6 +101,11 @@ struct lmsf_ctx {
     int ev_used = 0;
     double knn_ms = 0.0;
     int64_t knn_launches = 0, knn_queries = 0;
+    // lmsf_voxel_filter workspace (grown on demand)
+    VoxelFilter voxel;
+    float4* vox_in = nullptr;
+    float4* vox_out = nullptr;
+    size_t vox_cap = 0;
 
     lmsf_status fail(lmsf_status code, const char* fmt, ...) {
         char buf[512];
@@ -342,6 +347,9 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->edge_stage,
                     c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->d_error};
     for (void* p : bufs) hipFree(p);
+    c->voxel.release();
+    hipFree(c->vox_in);
+    hipFree(c->vox_out);
     if (c->h_poses) hipHostFree(c->h_poses);
     if (c->h_st) hipHostFree(c->h_st);
     if (c->h_counts) hipHostFree(c->h_counts);
@@ -524,6 +532,31 @@ static lmsf_status copy_slot_features(lmsf_ctx* c, int slot, int32_t kind, float
     if (n > cap) return c->fail(LMSF_ERR_CAPACITY, "output capacity %zu < %zu features", cap, n);
     if (n && out) HIPCHK(c, hipMemcpyAsync(out, c->feat + off, n * sizeof(float4), hipMemcpyDefault, c->stream));
     if (n && src) HIPCHK(c, hipMemcpyAsync(src, c->feat_src + off, n * sizeof(int), hipMemcpyDefault, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_voxel_filter(lmsf_ctx* c, const float* xyzi, size_t n, float leaf, float* out, size_t cap,
+                              size_t* n_out) {
+    if (!c || (n && (!xyzi || !out)) || !(leaf > 0.f) || n > (size_t)INT32_MAX) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (n_out) *n_out = 0;
+    if (n == 0) return LMSF_OK;
+    if (n > c->vox_cap) {
+        HIPCHK(c, hipFree(c->vox_in));
+        HIPCHK(c, hipFree(c->vox_out));
+        c->vox_in = c->vox_out = nullptr;
+        c->vox_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->vox_in, n * sizeof(float4)));
+        HIPCHK(c, hipMalloc((void**)&c->vox_out, n * sizeof(float4)));
+        c->vox_cap = n;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->vox_in, xyzi, n * sizeof(float4), hipMemcpyDefault, c->stream));
+    int nv = 0;
+    HIPCHK(c, c->voxel.run(c->vox_in, (int)n, leaf, c->vox_out, &nv, c->stream));
+    if (n_out) *n_out = (size_t)nv;
+    if ((size_t)nv > cap) return c->fail(LMSF_ERR_CAPACITY, "output capacity %zu < %d voxels", cap, nv);
+    HIPCHK(c, hipMemcpyAsync(out, c->vox_out, (size_t)nv * sizeof(float4), hipMemcpyDefault, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return LMSF_OK;
 }

@@ -1,0 +1,166 @@
+// Voxel-grid downsampling (pcl::VoxelGrid, INC/Algorithm/PointClouds/processing/Filter/voxel_grid.hpp:25-34
+// via Algorithm::VoxelGridFilter::Filter, filter_base.hpp:34-45), used by the build-defined
+// "sliding_Localmap" (the window of keyframes is downsampled per feature kind) and
+// exported as lmsf_voxel_filter.
+//
+// PCL semantics kept: voxel = (int)floor(p * (1/leaf)) in float; voxels emitted in ascending
+// linear index (x fastest, then y, then z, relative to the minimum voxel); each output point is
+// the centroid of every field of the voxel's points; when div_x*div_y*div_z exceeds INT32_MAX
+// PCL refuses ("integer indices would overflow") and returns the input unchanged -- so does this.
+// PCL accumulates the centroid in float in std::sort order (unspecified inside a voxel); here the
+// sort is a stable radix sort (ties by input index) and sums are double -> deterministic, and the
+// CPU oracle (oracle/voxel.cpp) reproduces it bit for bit.
+//
+// Roofline: HBM-bound byte work (one read of the cloud for the bounding box, keys 8 B + index 4 B
+// written and radix-sorted, one gather of 16 B per point, 16 B per voxel out).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "lmsf_internal.h"
+
+namespace lmsf {
+
+__device__ __forceinline__ int vox_coord(float v, float inv) {
+    return (int)fminf(fmaxf(floorf(v * inv), -1073741824.f), 1073741824.f);
+}
+
+__global__ void voxel_bbox_kernel(const float4* pts, int n, float inv, int* bbox) {
+    int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float4 p = pts[i];
+        const int c[3] = {vox_coord(p.x, inv), vox_coord(p.y, inv), vox_coord(p.z, inv)};
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = min(lo[d], c[d]);
+            hi[d] = max(hi[d], c[d]);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            lo[d] = min(lo[d], __shfl_xor(lo[d], o, 64));
+            hi[d] = max(hi[d], __shfl_xor(hi[d], o, 64));
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            atomicMin(&bbox[d], lo[d]);
+            atomicMax(&bbox[3 + d], hi[d]);
+        }
+    }
+}
+
+__global__ void voxel_key_kernel(const float4* pts, int n, float inv, const int* bbox, uint32_t dx, uint32_t dy,
+                                 uint32_t* keys, int* idx) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = pts[i];
+    const uint32_t cx = (uint32_t)(vox_coord(p.x, inv) - bbox[0]);
+    const uint32_t cy = (uint32_t)(vox_coord(p.y, inv) - bbox[1]);
+    const uint32_t cz = (uint32_t)(vox_coord(p.z, inv) - bbox[2]);
+    keys[i] = (cz * dy + cy) * dx + cx;        // < 2^31 (checked on the host)
+    idx[i] = i;
+}
+
+// start[s] = first sorted position of voxel s (heads scanned into segment ids).
+__global__ void voxel_head_kernel(const uint32_t* keys, int n, uint32_t* head) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    head[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+
+__global__ void voxel_start_kernel(const uint32_t* head, const uint32_t* seg, int n, int* start, int* nseg) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (head[i]) start[seg[i]] = i;
+    if (i == n - 1) {
+        *nseg = (int)(seg[i] + head[i]);
+        start[seg[i] + head[i]] = n;
+    }
+}
+
+__global__ void voxel_mean_kernel(const float4* pts, const int* idx_sorted, const int* start, const int* nseg,
+                                  float4* out) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= *nseg) return;
+    const int a = start[s], b = start[s + 1];
+    double sx = 0, sy = 0, sz = 0, sw = 0;
+    for (int k = a; k < b; ++k) {                  // input order inside the voxel
+        const float4 p = pts[idx_sorted[k]];
+        sx += p.x;
+        sy += p.y;
+        sz += p.z;
+        sw += p.w;
+    }
+    const double c = (double)(b - a);
+    out[s] = make_float4((float)(sx / c), (float)(sy / c), (float)(sz / c), (float)(sw / c));
+}
+
+void VoxelFilter::release() {
+    void* bufs[] = {keys, keys_sorted, idx, idx_sorted, head, seg, start, bbox, nseg, tmp};
+    for (void* p : bufs) hipFree(p);
+    *this = VoxelFilter();
+}
+
+hipError_t VoxelFilter::reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    release();
+    hipError_t e;
+#define VALLOC(p, bytes) if ((e = hipMalloc((void**)&(p), (bytes))) != hipSuccess) return e
+    VALLOC(keys, n * sizeof(uint32_t));
+    VALLOC(keys_sorted, n * sizeof(uint32_t));
+    VALLOC(idx, n * sizeof(int));
+    VALLOC(idx_sorted, n * sizeof(int));
+    VALLOC(head, n * sizeof(uint32_t));
+    VALLOC(seg, n * sizeof(uint32_t));
+    VALLOC(start, (n + 1) * sizeof(int));
+    VALLOC(bbox, 8 * sizeof(int));
+    VALLOC(nseg, sizeof(int));
+    size_t sort_b = 0, scan_b = 0;
+    hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, keys, keys_sorted, idx, idx_sorted, (int)n);
+    hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, head, seg, (int)n);
+    tmp_bytes = sort_b > scan_b ? sort_b : scan_b;
+    VALLOC(tmp, tmp_bytes);
+#undef VALLOC
+    cap = n;
+    return hipSuccess;
+}
+
+hipError_t VoxelFilter::run(const float4* in, int n, float leaf, float4* out, int* n_out, hipStream_t s) {
+    *n_out = 0;
+    if (n <= 0) return hipSuccess;
+    hipError_t e = reserve((size_t)n);
+    if (e != hipSuccess) return e;
+    const float inv = 1.0f / leaf;
+    const int init[6] = {INT_MAX, INT_MAX, INT_MAX, INT_MIN, INT_MIN, INT_MIN};
+    int hb[6];
+    if ((e = hipMemcpyAsync(bbox, init, sizeof init, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(voxel_bbox_kernel, dim3(min(max((n + 255) / 256, 1), 1024)), dim3(256), 0, s, in, n, inv, bbox);
+    if ((e = hipMemcpyAsync(hb, bbox, sizeof hb, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    const int64_t dx = (int64_t)hb[3] - hb[0] + 1, dy = (int64_t)hb[4] - hb[1] + 1, dz = (int64_t)hb[5] - hb[2] + 1;
+    if (dx * dy * dz > (int64_t)INT32_MAX) {      // PCL: indices would overflow -> input unchanged
+        if ((e = hipMemcpyAsync(out, in, (size_t)n * sizeof(float4), hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+        *n_out = n;
+        return hipStreamSynchronize(s);
+    }
+    int bits = 1;
+    while (bits < 31 && (int64_t{1} << bits) < dx * dy * dz) ++bits;
+    const dim3 g((n + 255) / 256), b(256);
+    hipLaunchKernelGGL(voxel_key_kernel, g, b, 0, s, in, n, inv, bbox, (uint32_t)dx, (uint32_t)dy, keys, idx);
+    size_t tb = tmp_bytes;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys_sorted, idx, idx_sorted, n, 0, bits, s)) != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(voxel_head_kernel, g, b, 0, s, keys_sorted, n, head);
+    tb = tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, head, seg, n, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(voxel_start_kernel, g, b, 0, s, head, seg, n, start, nseg);
+    hipLaunchKernelGGL(voxel_mean_kernel, g, b, 0, s, in, idx_sorted, start, nseg, out);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(n_out, nseg, sizeof(int), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    return hipStreamSynchronize(s);
+}
+
+}  // namespace lmsf

@@ -122,6 +122,18 @@ struct Affine34 { double m[12]; };   // row-major 3x4 of an Isometry3d matrix
 // pcl::transformPointCloud(cloud, out, Matrix4d) per point: float(m00 x + m01 y + m02 z + m03), double math
 hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hipStream_t s);
 
+// pcl::VoxelGrid centroid downsampling on the device (k_voxel.hip); workspace grows on demand.
+// run() synchronises the stream (the output count is returned to the host).
+struct VoxelFilter {
+    uint32_t *keys = nullptr, *keys_sorted = nullptr, *head = nullptr, *seg = nullptr;
+    int *idx = nullptr, *idx_sorted = nullptr, *start = nullptr, *bbox = nullptr, *nseg = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0, cap = 0;
+    hipError_t reserve(size_t n);
+    hipError_t run(const float4* in, int n, float leaf, float4* out, int* n_out, hipStream_t s);
+    void release();
+};
+
 hipStream_t ctx_stream(lmsf_ctx* c);
 int ctx_device(const lmsf_ctx* c);
 int ctx_feature_capacity(const lmsf_ctx* c);

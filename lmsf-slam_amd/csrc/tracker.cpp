@@ -7,7 +7,8 @@
 // (:239-262: dt > 10 s -> TIME, |dp| > 0.3 m or 2 acos(|q.w|) > 0.1 rad -> MOTION), and
 // updateLocalMap (:205-232: transformPointCloud, add frame, SetInputSource(local map)).
 // The local-map class itself is missing from the reference snapshot (factory/Map/LocalMap_factory.hpp);
-// "sliding_Localmap" is defined here as a device-resident window of the last W keyframes.
+// "sliding_Localmap" is defined here as a device-resident window of the last W keyframes
+// (W = 10, the config's sliding_window.size), VoxelGrid-downsampled per kind (0.2 / 0.4 m).
 // Isometry arithmetic follows Eigen's Isometry3d (linear * linear, linear * t + t; inverse = R^T,
 // -R^T t) and its quaternion <-> matrix conversions (the Ceres path converts at Solve, ceres_...:103, :128).
 #include <hip/hip_runtime.h>
@@ -118,9 +119,11 @@ struct Window {
     int head = 0, count = 0;
     float4* prior = nullptr;
     size_t prior_n = 0;
-    float4* concat = nullptr;
+    float4* wcat = nullptr;        // keyframes concatenated (input of the voxel filter)
+    float4* concat = nullptr;      // [prior | downsampled window] = the registration map
     size_t concat_cap = 0;
     size_t total = 0;
+    double leaf = 0.0;
     bool dirty = false;
 };
 
@@ -133,6 +136,7 @@ struct lmsf_tracker {
     Iso origin, curr, prev, motion, last_kf;
     double last_kf_time = 0.0;
     Window win[3];
+    VoxelFilter voxel;
     float4* stage = nullptr;   // host/device keyframe input staged before the transform
     int cap = 0;               // points per keyframe slot
 };
@@ -184,17 +188,22 @@ lmsf_status commit(lmsf_tracker* t) {
         Window& w = t->win[kind];
         if (!w.dirty) continue;
         const int W = (int)w.slots.size();
-        size_t off = 0;
-        if (w.prior_n) {
+        if (w.prior_n)
             TCHK(t, hipMemcpyAsync(w.concat, w.prior, w.prior_n * sizeof(float4), hipMemcpyDeviceToDevice, s));
-            off = w.prior_n;
-        }
+        float4* dst = w.leaf > 0 ? w.wcat : w.concat + w.prior_n;
+        size_t nw = 0;
         for (int i = 0; i < w.count; ++i) {
             const int k = (w.head + i) % W;
-            TCHK(t, hipMemcpyAsync(w.concat + off, w.slots[k], (size_t)w.sizes[k] * sizeof(float4),
+            TCHK(t, hipMemcpyAsync(dst + nw, w.slots[k], (size_t)w.sizes[k] * sizeof(float4),
                                    hipMemcpyDeviceToDevice, s));
-            off += (size_t)w.sizes[k];
+            nw += (size_t)w.sizes[k];
         }
+        if (w.leaf > 0 && nw) {                                   // VoxelGrid of the window
+            int nv = 0;
+            TCHK(t, t->voxel.run(w.wcat, (int)nw, (float)w.leaf, w.concat + w.prior_n, &nv, s));
+            nw = (size_t)nv;
+        }
+        const size_t off = w.prior_n + nw;
         w.total = off;
         w.dirty = false;
         lmsf_status rc = ctx_set_map_device(t->ctx, kind, w.concat, off);
@@ -240,11 +249,13 @@ extern "C" {
 
 lmsf_status lmsf_tracker_config_init(lmsf_tracker_config* cfg) {
     if (!cfg) return LMSF_ERR_ARG;
-    cfg->window_frames = 20;
+    cfg->window_frames = 10;
     cfg->threshold_trans = 0.3;
     cfg->threshold_rot = 0.1;
     cfg->time_interval = 10.0;
     cfg->manual_map_update = 0;
+    cfg->leaf_edge = 0.2;
+    cfg->leaf_surf = 0.4;
     return LMSF_OK;
 }
 
@@ -255,14 +266,16 @@ void lmsf_tracker_destroy(lmsf_tracker* t) {
     for (auto& w : t->win) {
         for (float4* p : w.slots) hipFree(p);
         hipFree(w.concat);
+        hipFree(w.wcat);
         hipFree(w.prior);
     }
+    t->voxel.release();
     hipFree(t->stage);
     delete t;
 }
 
 lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, lmsf_tracker** out) {
-    if (!ctx || !cfg || !out || cfg->window_frames < 1) return LMSF_ERR_ARG;
+    if (!ctx || !cfg || !out || cfg->window_frames < 1 || cfg->leaf_edge < 0 || cfg->leaf_surf < 0) return LMSF_ERR_ARG;
     *out = nullptr;
     lmsf_tracker* t = new lmsf_tracker();
     t->ctx = ctx;
@@ -276,7 +289,9 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
         for (auto& p : w.slots)
             if (hipMalloc((void**)&p, (size_t)t->cap * sizeof(float4)) != hipSuccess) { lmsf_tracker_destroy(t); return LMSF_ERR_HIP; }
         w.concat_cap = (size_t)t->cap * cfg->window_frames;
-        if (hipMalloc((void**)&w.concat, w.concat_cap * sizeof(float4)) != hipSuccess) {
+        w.leaf = kind == LMSF_EDGE ? cfg->leaf_edge : cfg->leaf_surf;
+        if (hipMalloc((void**)&w.concat, w.concat_cap * sizeof(float4)) != hipSuccess ||
+            (w.leaf > 0 && hipMalloc((void**)&w.wcat, w.concat_cap * sizeof(float4)) != hipSuccess)) {
             lmsf_tracker_destroy(t);
             return LMSF_ERR_HIP;
         }

@@ -53,7 +53,8 @@ class KernelStats(C.Structure):
 
 class TrackerConfig(C.Structure):
     _fields_ = [("window_frames", C.c_int32), ("threshold_trans", C.c_double), ("threshold_rot", C.c_double),
-                ("time_interval", C.c_double), ("manual_map_update", C.c_int32)]
+                ("time_interval", C.c_double), ("manual_map_update", C.c_int32), ("leaf_edge", C.c_double),
+                ("leaf_surf", C.c_double)]
 
 
 class TrackerResult(C.Structure):
@@ -104,6 +105,7 @@ _SIGS = {
     "lmsf_tracker_set_prior_map": (C.c_int32, [_P, C.c_int32, _P, C.c_size_t]),
     "lmsf_tracker_add_keyframe": (C.c_int32, [_P, _P, C.c_size_t, _P, C.c_size_t, _P]),
     "lmsf_tracker_commit_map": (C.c_int32, [_P]),
+    "lmsf_voxel_filter": (C.c_int32, [_P, _P, C.c_size_t, C.c_float, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "lmsf_handeye_create": (C.c_int32, [C.POINTER(_P)]),
     "lmsf_handeye_destroy": (None, [_P]),
     "lmsf_handeye_add_pose": (C.c_int32, [_P, _P, _P, C.POINTER(C.c_int32)]),
@@ -233,6 +235,14 @@ class Context:
         self._check(load().lmsf_copy_features(self.h, kind, out.data_ptr(), None, int(out.shape[0]), C.byref(n)))
         return n.value
 
+    def voxel_filter(self, pts, leaf):
+        """lmsf_voxel_filter (pcl::VoxelGrid centroids) of an (n, 4) cloud; returns a numpy array."""
+        p, n, keep = _buf(pts)
+        out = np.zeros((max(n, 1), 4), np.float32)
+        m = C.c_size_t()
+        self._check(load().lmsf_voxel_filter(self.h, p, n, float(leaf), out.ctypes.data, out.shape[0], C.byref(m)))
+        return out[:m.value].copy()
+
     # ---- batch path
     def load_scans(self, scans):
         counts = np.array([len(s) for s in scans], np.int64)
@@ -297,13 +307,14 @@ def _buf(a):
 class Tracker:
     """lmsf_tracker: LidarTrackerLocalMap over a Context (poses are 4x4 row-major matrices)."""
 
-    def __init__(self, ctx: Context, window_frames=20, threshold_trans=0.3, threshold_rot=0.1, time_interval=10.0,
-                 manual_map_update=False):
+    def __init__(self, ctx: Context, window_frames=10, threshold_trans=0.3, threshold_rot=0.1, time_interval=10.0,
+                 manual_map_update=False, leaf_edge=0.2, leaf_surf=0.4):
         cfg = TrackerConfig()
         load().lmsf_tracker_config_init(C.byref(cfg))
         cfg.window_frames, cfg.threshold_trans = window_frames, threshold_trans
         cfg.threshold_rot, cfg.time_interval = threshold_rot, time_interval
         cfg.manual_map_update = int(bool(manual_map_update))
+        cfg.leaf_edge, cfg.leaf_surf = leaf_edge, leaf_surf
         self.ctx = ctx
         h = C.c_void_p()
         ctx._check(load().lmsf_tracker_create(ctx.h, C.byref(cfg), C.byref(h)))

@@ -1,0 +1,90 @@
+"""Dual-LiDAR front end (configuration C3): MultiLidarSystem::process for NUM_OF_LIDAR = 2
+(INC/System/ML_System.hpp:232-323, INC = src/MultiSensorFusionEstimator3D/include) on the HIP path.
+
+* phase 0 (EXTRINSIC_CALIB_STATUS_ == 0, :243-281): each LiDAR runs its own tracker; the two
+  inter-frame motions feed the hand-eye initialisation (lmsf_handeye); once rotation and
+  translation are calibrated the system moves to phase 1;
+* phase 1 (:284-322): only the primary LiDAR is tracked; the sub LiDAR's features are registered
+  against the primary tracker's local map from primary * extrinsic (RegistrationLocalMap, :304-305)
+  and the extrinsic becomes primary^-1 * sub (:306).
+
+Both scans are extracted on the device; in phase 1 the sub scan is extracted on the primary
+tracker's context after the primary Solve, so its features never leave HBM.  The reference then
+falls through to a second Solve of tracker 0 on the already moved-from feature container
+(:331-334); that defect is not reproduced.  Poses are 4x4 row-major matrices.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+
+
+def iso_mul(A, B):
+    """Eigen Isometry3d product: linear * linear, linear * t + t."""
+    C = np.eye(4)
+    C[:3, :3] = A[:3, :3] @ B[:3, :3]
+    C[:3, 3] = A[:3, :3] @ B[:3, 3] + A[:3, 3]
+    return C
+
+
+def iso_inv(A):
+    B = np.eye(4)
+    B[:3, :3] = A[:3, :3].T
+    B[:3, 3] = -B[:3, :3] @ A[:3, 3]
+    return B
+
+
+class DualLidarSystem:
+    def __init__(self, ctx_primary: _lib.Context, ctx_sub: _lib.Context | None = None, extrinsic=None,
+                 **tracker_kw):
+        self.ctx = [ctx_primary, ctx_sub]
+        self.trackers = [_lib.Tracker(ctx_primary, **tracker_kw)]
+        if extrinsic is None:
+            if ctx_sub is None:
+                raise ValueError("extrinsic initialisation (phase 0) needs a context for the sub LiDAR")
+            self.trackers.append(_lib.Tracker(ctx_sub, **tracker_kw))
+            self.handeye = _lib.HandEye()
+            self.status = 0
+            self.extrinsic = np.eye(4)
+        else:
+            self.handeye = None
+            self.status = 1
+            self.extrinsic = np.asarray(extrinsic, dtype=np.float64).copy()
+        self.pose = [np.eye(4), np.eye(4)]       # pose_lidar_cur_
+        self.last = {}
+
+    def process(self, scan_primary, scan_sub, timestamp):
+        """One synchronized frame; returns (primary pose, sub pose) in the tracker's local frame."""
+        if self.status == 0:
+            deltas = []
+            for i, scan in enumerate((scan_primary, scan_sub)):
+                self.ctx[i].extract(scan)
+                d, r = self.trackers[i].solve_extracted(timestamp)
+                self.pose[i] = iso_mul(self.pose[i], d)
+                deltas.append(d)
+            if self.handeye.add_pose(deltas[0], deltas[1]):              # :268-281
+                ok_r, sv = self.handeye.calib_rotation()
+                self.last["rot_cov"] = sv
+                if ok_r and self.handeye.calib_translation():
+                    self.extrinsic = self.handeye.result()
+                    self.status = 1
+            return self.pose[0], self.pose[1]
+        t0 = self.trackers[0]
+        self.ctx[0].extract(scan_primary)
+        d, r = t0.solve_extracted(timestamp)                              # :296-297
+        primary = t0.pose()                                               # :299
+        sub0 = iso_mul(primary, self.extrinsic)                                   # :301
+        self.pose[0] = iso_mul(self.pose[0], d)                                   # :302
+        self.ctx[0].extract(scan_sub)
+        sub, st = t0.register_extracted(sub0)                             # :304-305
+        self.extrinsic = iso_mul(iso_inv(primary), sub)                     # :306
+        self.pose[1] = iso_mul(self.pose[0], self.extrinsic)                      # :307
+        self.last = {"primary_update": r.update_type, "refine": st}
+        return primary, sub
+
+    def close(self):
+        for t in self.trackers:
+            t.close()
+        if self.handeye is not None:
+            self.handeye.close()

@@ -387,6 +387,27 @@ def compose(a, b):
 
 
 @dataclasses.dataclass
+class DualSequence:
+    scene: Scene
+    truth: np.ndarray        # primary LiDAR world <- lidar poses (q, t)
+    extrinsic: np.ndarray    # primary <- sub (q, t), normalised PS-Calib value
+    primary: list            # raw scans, primary frame
+    sub: list                # raw scans, sub frame
+
+
+def make_dual_sequence(n: int, n_cols: int = 4096, step: float = 0.5, k: int = 3, start_x: float = 0.0,
+                       elev=VLP16_FIRING_DEG) -> DualSequence:
+    """C3: two rigidly mounted 16-beam LiDARs (MultiLidar_system config: lidar_num 2, n_scans 16)
+    at the reference's PS-Calib extrinsic, 10 Hz frames along the road."""
+    scene = make_scene(1000 + k)
+    truth = trajectory(n, 3000 + k, step=step, start_x=start_x)
+    X = unit_extrinsic(DUAL_EXTRINSIC)
+    prim = [make_scan(scene, truth[i], 2000 + k + 97 * i, n_cols=n_cols, elev_deg=elev) for i in range(n)]
+    sub = [make_scan(scene, compose(truth[i], X), 2500 + k + 97 * i, n_cols=n_cols, elev_deg=elev) for i in range(n)]
+    return DualSequence(scene, truth, X, prim, sub)
+
+
+@dataclasses.dataclass
 class Workload:
     scene: Scene
     edge_map: np.ndarray

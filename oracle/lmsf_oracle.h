@@ -69,6 +69,10 @@ int lmsfo_map_knn(const lmsfo_map* m, const float* q, int64_t nq, int k, int32_t
 int lmsfo_brute_knn(const float* map_xyzi, int64_t n, const float* q, int64_t nq, int k,
                     int32_t* idx, float* d2);
 
+/* pcl::VoxelGrid centroid downsampling (oracle/voxel.cpp); out holds up to n points.
+ * Returns the number of voxels written. */
+int64_t lmsfo_voxel_filter(const float* xyzi, int64_t n, float leaf, float* out);
+
 /* Registration object = CeresEdgeSurfFeatureRegistration (REG/ceres_edgeSurfFeatureRegistration.hpp)
  * or EdgeSurfFeatureRegistration in GN mode (REG/edgeSurfFeatureRegistration.hpp). */
 enum { LMSFO_SOLVER_CERES_LM = 0, LMSFO_SOLVER_GN = 1 };

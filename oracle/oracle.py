@@ -71,8 +71,18 @@ def lib():
         L.lmsfo_eval.argtypes = [C.c_void_p, C.c_int64, dp, dp]
         L.lmsfo_pose_plus.argtypes = [dp, dp, dp]
         L.lmsfo_set_num_threads.argtypes = [C.c_int]
+        L.lmsfo_voxel_filter.restype = C.c_int64
+        L.lmsfo_voxel_filter.argtypes = [fp, C.c_int64, C.c_float, fp]
         _lib = L
     return _lib
+
+
+def voxel_filter(points, leaf):
+    """pcl::VoxelGrid restatement (oracle/voxel.cpp)."""
+    p = _f32(points)
+    out = np.zeros((max(len(p), 1), 4), np.float32)
+    m = lib().lmsfo_voxel_filter(p, len(p), float(leaf), out)
+    return out[:m].copy()
 
 
 def set_threads(n: int):

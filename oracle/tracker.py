@@ -4,7 +4,9 @@ Follows INC/LidarTracker/LidarTrackerLocalMap.hpp:107-262 (INC = src/MultiSensor
 include) on top of the oracle registration (oracle.Registration, which keeps the reference's
 per-object optimization_count_ decay across Solve calls).  The local map class is absent from the
 reference snapshot; this restates the build-defined "sliding_Localmap" (DESIGN.md): a window of the
-last W keyframes per feature kind, concatenated oldest -> newest, every keyframe appended.
+last W = 10 keyframes per feature kind (the LOAM MultiLidar config's sliding_window.size),
+concatenated oldest -> newest and VoxelGrid-downsampled (0.2 m edge / 0.4 m surf), every keyframe
+appended.
 Parity vs the reference: unpinned (see lmsf_oracle.h).
 """
 from __future__ import annotations
@@ -83,8 +85,8 @@ class Tracker:
     surface): `origin` (lmsf_tracker_set_initial_pose), `prior` maps in front of the window
     (lmsf_tracker_set_prior_map), manual keyframe mode (add_keyframe + commit)."""
 
-    def __init__(self, window_frames=20, threshold_trans=0.3, threshold_rot=0.1, time_interval=10.0, solver=0,
-                 manual_map_update=False):
+    def __init__(self, window_frames=10, threshold_trans=0.3, threshold_rot=0.1, time_interval=10.0, solver=0,
+                 manual_map_update=False, leaf_edge=0.2, leaf_surf=0.4):
         self.reg = O.Registration(solver)
         self.W = window_frames
         self.th_t, self.th_r, self.dt_kf = threshold_trans, threshold_rot, time_interval
@@ -96,9 +98,14 @@ class Tracker:
         self.win = {1: deque(), 2: deque()}
         self.prior = {1: None, 2: None}
         self.dirty = {1: False, 2: False}
+        self.leaf = {1: leaf_edge, 2: leaf_surf}
 
     def local_map(self, kind):
-        parts = ([self.prior[kind]] if self.prior[kind] is not None else []) + list(self.win[kind])
+        """[prior | VoxelGrid(window keyframes, oldest -> newest)] (the build's sliding_Localmap)."""
+        parts = [self.prior[kind]] if self.prior[kind] is not None else []
+        if self.win[kind]:
+            w = np.concatenate(list(self.win[kind]), 0)
+            parts.append(O.voxel_filter(w, self.leaf[kind]) if self.leaf[kind] > 0 else w)
         return np.concatenate(parts, 0) if parts else np.zeros((0, 4), np.float32)
 
     def set_prior_map(self, kind, pts):

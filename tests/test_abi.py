@@ -80,10 +80,13 @@ def test_struct_layouts(lib, tmp_path):
 
 def test_tracker_config_defaults(lib):
     """LidarTrackerLocalMap: THRESHOLD_TRANS 0.3 m, THRESHOLD_ROT 0.1 rad, TIME_INTERVAL 10 s
-    (LidarTrackerLocalMap.hpp:65); window = the sliding local map's frame count."""
+    (LidarTrackerLocalMap.hpp:65); window 10 = tracker.local_map_type.sliding_window.size
+    (config/MultiLidar_system/loam_feature_multi_lidar_system.yaml:28-29); voxel leaves and the
+    manual mode are build-defined."""
     c = lib.TrackerConfig()
     assert lib.load().lmsf_tracker_config_init(ctypes.byref(c)) == lib.OK
-    assert (c.window_frames, c.threshold_trans, c.threshold_rot, c.time_interval) == (20, 0.3, 0.1, 10.0)
+    assert (c.window_frames, c.threshold_trans, c.threshold_rot, c.time_interval) == (10, 0.3, 0.1, 10.0)
+    assert (c.manual_map_update, c.leaf_edge, c.leaf_surf) == (0, 0.2, 0.4)
 
 
 def test_no_silent_fallback_without_device(lib):

@@ -337,7 +337,8 @@ def test_tracker_time_gate_and_capacity(lib, oracle_mod, sequence_workload):
     a keyframe larger than the slot capacity is an error, not a truncation."""
     wl = sequence_workload
     ctx = _ctx(lib, n_scans=wl.n_scans)
-    gt = lib.Tracker(ctx, window_frames=2, threshold_trans=1e9, threshold_rot=1e9, time_interval=0.15)
+    gt = lib.Tracker(ctx, window_frames=2, threshold_trans=1e9, threshold_rot=1e9, time_interval=0.15,
+                     leaf_edge=0.0, leaf_surf=0.0)    # raw window: sizes add up
     kf_sizes = []
     types = []
     for i, scan in enumerate(wl.scans[:5]):
@@ -356,6 +357,21 @@ def test_tracker_time_gate_and_capacity(lib, oracle_mod, sequence_workload):
     with pytest.raises(lib.LmsfError):
         t2.solve(e[:500], s, 0.0)
     t2.close()
+
+
+def test_voxel_filter_bitexact(lib, oracle_mod, small_workload):
+    """lmsf_voxel_filter (radix-sorted voxel keys + ordered double centroids) == oracle/voxel.cpp."""
+    import torch
+    ctx = _ctx(lib)
+    e, s, _, _ = oracle_mod.extract(small_workload.scans[0])
+    for pts in (s, e, small_workload.surf_map[:200_000]):
+        for leaf in (0.1, 0.4, 1.0):
+            want = oracle_mod.voxel_filter(pts, leaf)
+            assert ctx.voxel_filter(pts, leaf).tobytes() == want.tobytes()
+    got = ctx.voxel_filter(torch.from_numpy(s).to("cuda:0"), 0.4)            # device input
+    assert got.tobytes() == oracle_mod.voxel_filter(s, 0.4).tobytes()
+    far = np.array([[0, 0, 0, 0], [1e4, 1e4, 1e4, 1]], np.float32)
+    assert ctx.voxel_filter(far, 0.01).tobytes() == far.tobytes()
 
 
 def test_tracker_shared_map_streams(lib, oracle_mod, sequence_workload):
@@ -411,6 +427,39 @@ def test_tracker_shared_map_streams(lib, oracle_mod, sequence_workload):
     np.testing.assert_allclose(gts[0].local_map(lib.EDGE), ots[0].local_map(1), atol=1e-4)
     for t in gts:
         t.close()
+
+
+def test_dual_lidar_refine_parity(lib, oracle_mod):
+    """C3 phase 1 (ML_System.hpp:284-322): primary tracker Solve, sub-LiDAR features extracted on
+    the same context and registered against the primary local map from primary * extrinsic,
+    extrinsic = primary^-1 * sub -- against the oracle tracker doing the same."""
+    import tracker as OT
+    from conftest import mat_err, pose_matrix, relative_truth
+    from lmsf import dual, synth
+    ds = synth.make_dual_sequence(6, n_cols=1800, step=0.5)
+    X = pose_matrix(ds.extrinsic)
+    X0 = X @ pose_matrix(np.concatenate([synth.axis_angle_quat(np.radians([0.5, -0.5, 0.5])), [0.03, -0.02, 0.02]]))
+    rel = relative_truth(ds.truth)
+    sysg = dual.DualLidarSystem(_ctx(lib), extrinsic=X0)
+    ot = OT.Tracker()
+    ext = X0.copy()
+    for i in range(len(ds.truth)):
+        prim_g, sub_g = sysg.process(ds.primary[i], ds.sub[i], 0.1 * i)
+        ep, sp, _, _ = oracle_mod.extract(ds.primary[i])
+        es, ss, _, _ = oracle_mod.extract(ds.sub[i])
+        _, typ, _ = ot.solve(ep, sp, 0.1 * i)
+        prim_o = ot.curr.copy()
+        sub_o, _ = ot._register({1: es, 2: ss}, dual.iso_mul(prim_o, ext))
+        ext = dual.iso_mul(dual.iso_inv(prim_o), sub_o)
+        assert sysg.last["primary_update"] == typ
+        for a, b in ((prim_g, prim_o), (sub_g, sub_o), (sysg.extrinsic, ext)):
+            dt, dr = mat_err(a, b)
+            assert dt <= POSE_TOL and dr <= POSE_TOL, (i, dt, dr)
+        dt, dr = mat_err(prim_g, rel[i])
+        assert dt < 0.05 and dr < 0.01
+    dt, dr = mat_err(sysg.extrinsic, X)
+    assert dt < 0.03 and dr < 0.005                   # refined from 6 cm / 0.9 deg
+    sysg.close()
 
 
 def test_reference_interface(lib, oracle_mod, small_workload):

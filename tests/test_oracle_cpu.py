@@ -264,3 +264,36 @@ def test_golden_fixtures_reproduced(oracle_mod):
     # independent numpy pins stored in the fixture
     np.testing.assert_allclose(g["np_edge_dir_dot"], 1.0, atol=1e-9)
     np.testing.assert_allclose(g["np_plane_err"], 0.0, atol=1e-7)
+
+
+def _numpy_voxel(p, leaf):
+    """Independent numpy restatement of pcl::VoxelGrid (float voxel coords, z-major index order)."""
+    inv = np.float32(1.0) / np.float32(leaf)
+    c = np.floor(p[:, :3].astype(np.float32) * inv).astype(np.int64)
+    c -= c.min(0)
+    d = c.max(0) + 1
+    key = c[:, 0] + c[:, 1] * d[0] + c[:, 2] * d[0] * d[1]
+    order = np.lexsort((np.arange(len(p)), key))
+    ks = key[order]
+    starts = np.flatnonzero(np.r_[True, ks[1:] != ks[:-1]])
+    out = []
+    for a, b in zip(starts, np.r_[starts[1:], len(p)]):
+        s = np.zeros(4)
+        for i in order[a:b]:
+            s += p[i].astype(np.float64)      # sequential double sums, input order inside a voxel
+        out.append((s / (b - a)).astype(np.float32))
+    return np.array(out, np.float32).reshape(-1, 4)
+
+
+def test_oracle_voxel_filter(oracle_mod):
+    rng = np.random.default_rng(4)
+    p = np.concatenate([rng.uniform(-20, 20, (3000, 3)), rng.random((3000, 1))], 1).astype(np.float32)
+    p[:500, :3] = np.round(p[:500, :3] * 2.5) / 2.5          # points exactly on voxel boundaries
+    for leaf in (0.2, 0.4, 1.0, 3.0):
+        got = oracle_mod.voxel_filter(p, leaf)
+        assert got.tobytes() == _numpy_voxel(p, leaf).tobytes()
+    assert len(oracle_mod.voxel_filter(p[:0], 0.4)) == 0
+    assert oracle_mod.voxel_filter(p[:1], 0.4).tobytes() == p[:1].tobytes()
+    # PCL refuses when the voxel index would overflow int32: input returned unchanged
+    far = np.array([[0, 0, 0, 0], [1e4, 1e4, 1e4, 1]], np.float32)
+    assert oracle_mod.voxel_filter(far, 0.01).tobytes() == far.tobytes()
