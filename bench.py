@@ -1,12 +1,23 @@
-"""Benchmark: LiDAR scans/s registered (C2: ~64k-point VLP-16 scan vs 1M-point feature map).
+"""Benchmark of the MI355X LOAM registration hot path (BASELINE.json configs).
 
-One step = one pass of the hot path over one batch of B synthetic scans per GPU: LOAM feature
-extraction from the raw scans + scan-to-map registration (5 outer iterations of 5-NN matching,
-line/plane fits and a 4-iteration Ceres-equivalent LM), followed by the RCCL all-gather of the
-resulting 6-DoF poses across ranks (multi-GPU only).  Inputs (raw scans, map index) are resident
+Default (the driver's line): C2 -- LiDAR scans/s registered, ~64k-point VLP-16 scans vs a
+1M-point feature map.  One step = one pass of the hot path over one batch of B synthetic scans per
+GPU: LOAM feature extraction from the raw scans + scan-to-map registration (5 outer iterations of
+5-NN matching, line/plane fits and a 4-iteration Ceres-equivalent LM), followed by the RCCL
+all-gather of the resulting 6-DoF poses across ranks.  Inputs (raw scans, map index) are resident
 in HBM before the timed region.  Weak scaling: B scans per GPU.
 
-Usage: python bench.py [--gpus N --steps K --warmup W --batch B]
+Other configurations (`--config`), each its own JSON line:
+  C3  dual-LiDAR frames/s: per frame two 16-beam 4096-column scans (~2 x 63k points), primary
+      tracker Solve + sub-LiDAR online extrinsic refine against the primary local map
+      (MultiLidarSystem phase 1); one independent system per GPU (weak scaling).
+  C4  tracking scans/s: one scan stream per GPU tracked against a shared 5M-point map (RCCL
+      broadcast from rank 0) plus the stitched window of every stream's keyframes (RCCL
+      all-gather of poses every step, of keyframe features when a stream keyframes).
+  C5  scan pairs/s: 1,000 re-registrations of 128-beam 2048-column scans (~254k points) against a
+      10M-point map, pairs partitioned i mod N, one all-gather of the poses (strong scaling).
+
+Usage: python bench.py [--config C2|C3|C4|C5] [--gpus N --steps K --warmup W ...]
        (N > 1 is launched by torch.distributed.run, one rank per GPU).
 """
 import argparse
@@ -21,136 +32,225 @@ sys.path.insert(0, os.path.join(REPO, "lmsf-slam_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
+DEFAULTS = {   # per configuration: batch (scans per launch), map points, columns, steps, warmup
+    "C2": dict(batch=64, map_points=1_000_000, cols=4096, steps=10, warmup=2),
+    "C3": dict(batch=1, map_points=0, cols=4096, steps=20, warmup=3),
+    "C4": dict(batch=1, map_points=5_000_000, cols=4096, steps=20, warmup=3),
+    "C5": dict(batch=125, map_points=10_000_000, cols=2048, steps=2, warmup=1),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2", choices=sorted(DEFAULTS))
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=64, help="scans per GPU per step")
-    ap.add_argument("--unique-scans", type=int, default=8, help="distinct synthetic scans per rank")
-    ap.add_argument("--map-points", type=int, default=1_000_000)
-    ap.add_argument("--cols", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--batch", type=int, default=None, help="scans per GPU per launch")
+    ap.add_argument("--unique-scans", type=int, default=None, help="distinct synthetic scans per rank")
+    ap.add_argument("--map-points", type=int, default=None)
+    ap.add_argument("--cols", type=int, default=None)
     ap.add_argument("--outer", type=int, default=5)
+    ap.add_argument("--pairs", type=int, default=1000, help="C5: scan pairs in the whole job")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "knn_traffic.json"),
+    ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes of the neighbour-search kernel from rocprofv3 PMC runs")
-    return ap.parse_args()
+    a = ap.parse_args()
+    for k, v in DEFAULTS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    if a.unique_scans is None:
+        a.unique_scans = {"C2": 8, "C5": 5}.get(a.config, 1)
+    if a.traffic_json is None:
+        a.traffic_json = os.path.join(REPO, "profiles", f"knn_traffic_{a.config}.json")
+    return a
 
 
-def main():
-    args = parse()
-    import numpy as np
-    import torch
-    import torch.distributed as dist
+# ----------------------------------------------------------------------------- shared plumbing
+class Dist:
+    def __init__(self):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+        else:
+            torch.cuda.set_device(0)
+        self.dev = torch.device("cuda", self.local)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local)
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
 
-    from lmsf import _lib, multi, synth
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
 
-    # ---------------- workload (C2), deterministic per rank: rank r registers its own scans
-    U = max(1, min(args.unique_scans, args.batch))
-    cfgc = synth.CONFIGS["C2"]
-    scene = synth.make_scene(1000 + cfgc["k"], road_length=80.0)
-    truth_u = synth.trajectory(U * world, 3000 + cfgc["k"], step=80.0 / max(U * world, 1))[rank * U:(rank + 1) * U]
-    scans_u = [synth.make_scan(scene, truth_u[i], 2000 + cfgc["k"] + 97 * (rank * U + i), n_cols=args.cols)
-               for i in range(U)]
-    edge_map, surf_map = synth.make_map(scene, args.map_points, 1000 + cfgc["k"] + 7, center_x=(0.0, 80.0),
-                                        radius=cfgc["radius"])
-    rng = np.random.default_rng(3000 + cfgc["k"] + rank)
-    slot_scan = [i % U for i in range(args.batch)]
-    guesses = np.stack([synth.perturb(truth_u[slot_scan[i]], rng) for i in range(args.batch)])
-    max_pts = max(len(s) for s in scans_u)
 
-    ctx = _lib.Context(device=local, max_batch=args.batch, max_scan_points=max_pts + 64,
-                       max_features=max_pts + 64, schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer)
-    ctx.set_map(_lib.EDGE, edge_map)
-    ctx.set_map(_lib.SURF, surf_map)
-    ctx.load_scans([scans_u[slot_scan[i]] for i in range(args.batch)])
-
-    gathered = torch.zeros((world, args.batch, 7), dtype=torch.float64, device=dev)
-
-    def step():
-        ctx.batch_launch(guesses)
-        poses, stats = ctx.batch_wait(args.batch)
-        if world > 1:
-            multi.gather_poses(poses, gathered, dev)     # RCCL all-gather of the 6-DoF poses
-        return poses, stats
-
-    for _ in range(args.warmup):
+def timed(d, step, warmup, steps, ctxs):
+    """W untimed steps, then K steps between barrier + synchronize; max over ranks."""
+    torch = d.torch
+    for _ in range(warmup):
         step()
-    ctx.kernel_stats_reset(True)
-    if world > 1:
-        dist.barrier()
+    for c in ctxs:
+        c.kernel_stats_reset(True)
+    d.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        poses, stats = step()
+    out = None
+    for _ in range(steps):
+        out = step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    d.barrier()
     elapsed = time.perf_counter() - t0
-    ks = ctx.kernel_stats()
-    if world > 1:
-        elapsed = multi.max_over_ranks(elapsed, dev)
+    if d.world > 1:
+        from lmsf import multi
+        elapsed = multi.max_over_ranks(elapsed, d.dev)
+    return elapsed, out
 
-    scans_total = args.batch * args.steps * world
-    value = scans_total / elapsed
-    # accuracy of the batch vs ground truth (sanity: registration converged)
-    terr = [synth.pose_delta(poses[i], truth_u[slot_scan[i]]) for i in range(args.batch)]
 
-    # ---------------- roofline of the neighbour-search kernel (SURVEY.md §8(d) algorithmic bytes)
-    # B_search = sum_q [16 (query float4) + 27*8 (cell ranges) + 16 * n27(q)]
+def shared_map(d, make):
+    """Map generated on rank 0 and replicated to every GPU by an RCCL broadcast."""
+    torch = d.torch
+    if d.world == 1:
+        e, s = make()
+        return torch.from_numpy(e).to(d.dev), torch.from_numpy(s).to(d.dev)
+    if d.rank == 0:
+        e, s = make()
+        n = torch.tensor([len(e), len(s)], dtype=torch.int64, device=d.dev)
+    else:
+        n = torch.zeros(2, dtype=torch.int64, device=d.dev)
+    d.dist.broadcast(n, 0)
+    if d.rank == 0:
+        et, st = torch.from_numpy(e).to(d.dev), torch.from_numpy(s).to(d.dev)
+    else:
+        et = torch.empty((int(n[0]), 4), dtype=torch.float32, device=d.dev)
+        st = torch.empty((int(n[1]), 4), dtype=torch.float32, device=d.dev)
+    d.dist.broadcast(et, 0)
+    d.dist.broadcast(st, 0)
+    return et, st
+
+
+def knn_roofline(ks, traffic_json, batch, map_points, note):
+    """B_search = sum_q [16 (query) + 27*8 (cell ranges) + 16 * n27(q)] per launch,
+    over the HIP-event-timed launches of the neighbour-search kernel."""
     alg_bytes = ks.queries * (16 + 27 * 8) + 16 * ks.n27_sum
     avg_launch_ms = ks.total_ms / max(ks.launches, 1)
     bytes_per_launch = alg_bytes / max(ks.launches, 1)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     traffic, l2_hit = None, None
-    if os.path.exists(args.traffic_json):
+    if os.path.exists(traffic_json):
         try:
-            tj = json.load(open(args.traffic_json))
-            if int(tj.get("batch", -1)) == args.batch and int(tj.get("map_points", -1)) == args.map_points:
+            tj = json.load(open(traffic_json))
+            if int(tj.get("batch", -1)) == batch and int(tj.get("map_points", -1)) == map_points:
                 traffic = tj.get("hbm_bytes_per_launch")
                 l2_hit = tj.get("l2_hit_rate")
-        except Exception:
+        except (ValueError, OSError):
             traffic = None
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "knn_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
-                "alg_bytes_per_launch": int(bytes_per_launch), "launches": int(ks.launches),
-                "queries_per_launch": int(ks.queries / max(ks.launches, 1)),
-                "mean_n27": round(ks.n27_sum / max(ks.queries, 1), 1),
-                "measured_hbm_gbs": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic and avg_launch_ms else None,
-                "l2_hit_rate": round(l2_hit, 3) if l2_hit is not None else None,
-                "note": "achieved = SURVEY 8(d) algorithmic bytes / launch time; the 1M-pt map + cell index "
-                        "(~27 MB) is L2/Infinity-Cache resident, so measured HBM traffic (PMC) is far lower"}
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "knn_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
+            "alg_bytes_per_launch": int(bytes_per_launch), "launches": int(ks.launches),
+            "queries_per_launch": int(ks.queries / max(ks.launches, 1)),
+            "mean_n27": round(ks.n27_sum / max(ks.queries, 1), 1),
+            "measured_hbm_gbs": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic and avg_launch_ms else None,
+            "l2_hit_rate": round(l2_hit, 3) if l2_hit is not None else None,
+            "note": note}
 
-    # ---------------- CPU baseline + pose delta vs CPU (rank 0, N = 1 only)
-    cpu = None
-    pose_dv = None
+
+def line(args, d, metric, value, unit, elapsed, scaling, workload, extra_cfg, roofline, cpu, **extra):
+    out = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": d.world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+           "config": dict({"workload": workload}, **extra_cfg), "roofline": roofline, "cpu_baseline": cpu}
+    out.update(extra)
+    print(json.dumps(out))
+
+
+def cpu_oracle():
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    oracle.set_threads(1)
+    return oracle
+
+
+# ----------------------------------------------------------------------------- C2 / C5: batch re-registration
+def run_batch(args, d):
+    import numpy as np
+    torch = d.torch
+    from lmsf import _lib, multi, synth
+    cfg = args.config
+    c = synth.CONFIGS[cfg]
+    k = c["k"]
+    world, rank = d.world, d.rank
+    U = max(1, min(args.unique_scans, args.batch))
+    if cfg == "C5" and args.batch % U:
+        args.batch -= args.batch % U          # slot j holds scan j % U in every chunk
+    scene = synth.make_scene(1000 + k, road_length=80.0)
+    truth_u = synth.trajectory(U * world, 3000 + k, step=80.0 / max(U * world, 1))[rank * U:(rank + 1) * U]
+    scans_u = [synth.make_scan(scene, truth_u[i], 2000 + k + 97 * (rank * U + i), n_cols=args.cols,
+                               elev_deg=c["elev"]) for i in range(U)]
+    em_t, sm_t = shared_map(d, lambda: synth.make_map(scene, args.map_points, 1000 + k + 7, center_x=(0.0, 80.0),
+                                                      radius=c["radius"]))
+    if cfg == "C2":
+        n_units = args.batch                                   # scans this rank registers per step
+        unit_scan = [i % U for i in range(n_units)]
+        rng = np.random.default_rng(3000 + k + rank)
+        guesses = np.stack([synth.perturb(truth_u[unit_scan[i]], rng) for i in range(n_units)])
+    else:                                                      # C5: pairs i = rank, rank + N, ...
+        mine = list(range(rank, args.pairs, world))
+        n_units = len(mine)
+        unit_scan = [j % U for j in range(n_units)]
+        guesses = np.stack([synth.perturb(truth_u[unit_scan[j]], np.random.default_rng(3000 + k + 7919 * i))
+                            for j, i in enumerate(mine)])
+    chunk = min(args.batch, n_units)
+    max_pts = max(len(s) for s in scans_u)
+    ctx = _lib.Context(device=d.local, max_batch=chunk, max_scan_points=max_pts + 64, max_features=max_pts + 64,
+                       schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer, **c["extract"])
+    ctx.set_map(_lib.EDGE, em_t)
+    ctx.set_map(_lib.SURF, sm_t)
+    map_points = int(em_t.shape[0] + sm_t.shape[0])
+    ctx.load_scans([scans_u[j % U] for j in range(chunk)])
+    per_rank = n_units if cfg == "C2" else -(-args.pairs // world)
+    gathered = torch.zeros((world, per_rank, 7), dtype=torch.float64, device=d.dev)
+    poses = np.zeros((n_units, 7))
+
+    def step():
+        for c0 in range(0, n_units, chunk):
+            nb = min(chunk, n_units - c0)
+            ctx.batch_launch(guesses[c0:c0 + nb])
+            poses[c0:c0 + nb], _ = ctx.batch_wait(nb)
+        if world > 1:                                        # RCCL all-gather of the 6-DoF poses
+            buf = np.zeros((per_rank, 7))
+            buf[:n_units] = poses
+            multi.gather_poses(buf, gathered, d.dev)
+        return poses
+
+    elapsed, _ = timed(d, step, args.warmup, args.steps, [ctx])
+    ks = ctx.kernel_stats()
+    total_units = (args.batch * world if cfg == "C2" else args.pairs) * args.steps
+    terr = [synth.pose_delta(poses[i], truth_u[unit_scan[i]]) for i in range(n_units)]
+    roof = knn_roofline(ks, args.traffic_json, chunk, map_points,
+                        "achieved = SURVEY 8(d) algorithmic bytes / HIP-event launch time; the map + cell "
+                        "index is largely L2/Infinity-Cache resident, so measured HBM traffic (PMC) is lower")
+    cpu, pose_dv = None, None
     if rank == 0 and world == 1 and not args.no_cpu:
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import oracle
-        oracle.set_threads(1)
+        oracle = cpu_oracle()
         reg = oracle.Registration()
-        reg.set_map(1, edge_map)
-        reg.set_map(2, surf_map)
+        reg.set_map(1, em_t.cpu().numpy())           # the same broadcast map
+        reg.set_map(2, sm_t.cpu().numpy())
         reg.set_fixed_schedule(True)
         reg.set_max_iterations(args.outer)
         n_done, worst_t, worst_r = 0, 0.0, 0.0
         t1 = time.perf_counter()
-        while n_done < args.batch and (n_done == 0 or time.perf_counter() - t1 < args.cpu_seconds):
-            e, s, _, _ = oracle.extract(scans_u[slot_scan[n_done]])
+        while n_done < n_units and (n_done == 0 or time.perf_counter() - t1 < args.cpu_seconds):
+            e, s, _, _ = oracle.extract(scans_u[unit_scan[n_done]], **c["extract"])
             reg.set_scan(1, e)
             reg.set_scan(2, s)
             ox, _, _ = reg.solve(guesses[n_done])
@@ -158,40 +258,225 @@ def main():
             worst_t, worst_r = max(worst_t, dt), max(worst_r, dr)
             n_done += 1
         cpu_el = time.perf_counter() - t1
-        cpu = {"value": round(n_done / cpu_el, 3), "unit": "scans/s", "cores": 1, "kind": "port",
-               "sample": f"{n_done} scans of the same C2 batch (extract + {args.outer} outer iterations, "
-                         f"kd-tree 5-NN, Ceres-LM restatement), {cpu_el:.1f} s on 1 thread of "
-                         f"{os.cpu_count()} host cores"}
+        unit = "scans/s" if cfg == "C2" else "pairs/s"
+        cpu = {"value": round(n_done / cpu_el, 3), "unit": unit, "cores": 1, "kind": "port",
+               "sample": f"{n_done} {'scans' if cfg == 'C2' else 'pairs'} of the same {cfg} workload (extract + "
+                         f"{args.outer} outer iterations, kd-tree 5-NN, Ceres-LM restatement; kd-tree build "
+                         f"excluded), {cpu_el:.1f} s on 1 thread of {os.cpu_count()} host cores"}
         pose_dv = {"scans": n_done, "max_m": worst_t, "max_rad": worst_r}
-
     if rank == 0:
-        line = {
-            "metric": "LiDAR scans/sec registered (64k-pt scan, 1M-pt map)",
-            "value": round(value, 2),
-            "unit": "scans/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic",
-            "config": {"workload": f"C2: VLP-16 16x{args.cols} scans (~{int(np.mean([len(s) for s in scans_u]))} pts) "
-                                   f"vs {args.map_points}-pt edge+surf map, {args.outer} outer iters x Ceres-LM(4), "
-                                   f"extraction included, batch {args.batch} scans/GPU ({U} distinct)",
-                       "batch_per_gpu": args.batch, "map_points": args.map_points, "outer_iterations": args.outer,
-                       "parallelism": f"scan-sharded x{world}"},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-            "pose_delta_vs_cpu": pose_dv,
-            "pose_error_vs_truth": {"max_m": max(t for t, _ in terr), "max_rad": max(r for _, r in terr)},
-        }
-        print(json.dumps(line))
-    if world > 1:
-        dist.destroy_process_group()
+        npts = int(np.mean([len(s) for s in scans_u]))
+        if cfg == "C2":
+            metric = "LiDAR scans/sec registered (64k-pt scan, 1M-pt map)"
+            wl = (f"C2: VLP-16 16x{args.cols} scans (~{npts} pts) vs {map_points}-pt edge+surf map, "
+                  f"{args.outer} outer iters x Ceres-LM(4), extraction included, batch {args.batch} scans/GPU "
+                  f"({U} distinct)")
+            extra = {"batch_per_gpu": args.batch, "map_points": map_points, "outer_iterations": args.outer,
+                     "parallelism": f"scan-sharded x{world}"}
+            unit, scaling = "scans/s", "weak"
+        else:
+            metric = "LiDAR scan pairs/sec re-registered (128-beam 254k-pt scan, 10M-pt map, 1k pairs)"
+            wl = (f"C5: 128x{args.cols} scans (~{npts} pts) vs {map_points}-pt map, {args.pairs} pairs "
+                  f"(i mod {world} per GPU, launches of {chunk}), {args.outer} outer iters x Ceres-LM(4)")
+            extra = {"pairs": args.pairs, "launch_batch": chunk, "map_points": map_points,
+                     "outer_iterations": args.outer, "parallelism": f"pair-sharded x{world}"}
+            unit, scaling = "pairs/s", "strong"
+        line(args, d, metric, total_units / elapsed, unit, elapsed, scaling, wl, extra, roof, cpu,
+             pose_delta_vs_cpu=pose_dv,
+             pose_error_vs_truth={"max_m": max(t for t, _ in terr), "max_rad": max(r for _, r in terr)})
     ctx.close()
+
+
+# ----------------------------------------------------------------------------- C4: stitched multi-stream tracking
+def run_streams(args, d):
+    import numpy as np
+    torch = d.torch
+    from lmsf import _lib, synth
+    c = synth.CONFIGS["C4"]
+    k = c["k"]
+    world, rank = d.world, d.rank
+    n = args.warmup + args.steps
+    scene = synth.make_scene(1000 + k, road_length=80.0)
+    step_m = 0.8                                                # 8 m/s at 10 Hz
+    start = 8.0 * rank if world <= 8 else 64.0 * rank / world
+    truth = synth.trajectory(n, 3000 + k + rank, step=step_m, start_x=start)
+    scans = [synth.make_scan(scene, truth[i], 2000 + k + 97 * i + 7717 * rank, n_cols=args.cols) for i in range(n)]
+    scans_dev = [torch.from_numpy(s).to(d.dev) for s in scans]
+    em_t, sm_t = shared_map(d, lambda: synth.make_map(scene, args.map_points, 1000 + k + 7, center_x=(0.0, 80.0),
+                                                      radius=c["radius"]))
+    max_pts = max(len(s) for s in scans)
+    ctx = _lib.Context(device=d.local, max_batch=1, max_scan_points=max_pts + 64, max_features=max_pts + 64,
+                       schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer)
+    tr = _lib.Tracker(ctx, manual_map_update=True)
+    T0 = np.eye(4)
+    T0[:3, :3] = synth.quat_to_mat(truth[0][:4])
+    T0[:3, 3] = truth[0][4:]
+    tr.set_initial_pose(T0)
+    tr.set_prior_map(_lib.EDGE, em_t)
+    tr.set_prior_map(_lib.SURF, sm_t)
+    map_points = int(em_t.shape[0] + sm_t.shape[0])
+    cap = max_pts + 64
+    fbuf = torch.zeros((2 * cap, 4), dtype=torch.float32, device=d.dev)       # [edges | surfs] of own scan
+    gbuf = torch.zeros((world, 2 * cap, 4), dtype=torch.float32, device=d.dev)
+    info = torch.zeros((world, 19), dtype=torch.float64, device=d.dev)
+    own = torch.zeros(19, dtype=torch.float64, device=d.dev)
+    state = {"i": 0, "kf": 0, "err": []}
+
+    def step():
+        i = state["i"]
+        ctx.extract(scans_dev[i])
+        _, r = tr.solve_extracted(0.1 * i)
+        P = tr.pose()
+        ne = ns = 0
+        if r.update_type:
+            ne = ctx.copy_features_into(_lib.EDGE, fbuf[:cap])
+            ns = ctx.copy_features_into(_lib.SURF, fbuf[cap:])
+        vec = np.concatenate([P.ravel(), [r.update_type, ne, ns]])
+        if world > 1:
+            own.copy_(torch.from_numpy(vec))
+            d.dist.all_gather_into_tensor(info, own)                        # poses + keyframe flags
+            allinfo = info.cpu().numpy()
+            if (allinfo[:, 16] > 0).any():
+                d.dist.all_gather_into_tensor(gbuf.view(-1), fbuf.view(-1))  # keyframe features
+        else:
+            allinfo = vec[None]
+            if r.update_type:
+                gbuf[0].copy_(fbuf)
+        added = False
+        for q in range(world):                                          # same order on every rank
+            if allinfo[q, 16] > 0:
+                qe, qs = int(allinfo[q, 17]), int(allinfo[q, 18])
+                tr.add_keyframe(gbuf[q, :qe], gbuf[q, cap:cap + qs], allinfo[q, :16].reshape(4, 4))
+                added = True
+                state["kf"] += 1
+        if added:
+            tr.commit_map()
+        Tt = np.eye(4)
+        Tt[:3, :3] = synth.quat_to_mat(truth[i][:4])
+        Tt[:3, 3] = truth[i][4:]
+        state["err"].append(float(np.linalg.norm(P[:3, 3] - Tt[:3, 3])))
+        state["i"] += 1
+        return P
+
+    elapsed, _ = timed(d, step, args.warmup, args.steps, [ctx])
+    ks = ctx.kernel_stats()
+    roof = knn_roofline(ks, args.traffic_json, 1, map_points,
+                        "achieved = SURVEY 8(d) algorithmic bytes / HIP-event launch time (one 63k-query scan "
+                        "per launch: latency-bound launches)")
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        oracle = cpu_oracle()
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import tracker as OT
+        ot = OT.Tracker(manual_map_update=True)
+        ot.origin = T0.copy()
+        ot.reg.set_fixed_schedule(True)
+        ot.reg.set_max_iterations(args.outer)
+        ot.set_prior_map(1, em_t.cpu().numpy())      # the same broadcast map
+        ot.set_prior_map(2, sm_t.cpu().numpy())
+        n_done = 0
+        t1 = time.perf_counter()
+        while n_done < n and (n_done == 0 or time.perf_counter() - t1 < args.cpu_seconds):
+            e, s, _, _ = oracle.extract(scans[n_done])
+            _, typ, _ = ot.solve(e, s, 0.1 * n_done)
+            if typ:
+                ot.add_keyframe(e, s, ot.curr)
+                ot.commit()
+            n_done += 1
+        cpu_el = time.perf_counter() - t1
+        cpu = {"value": round(n_done / cpu_el, 3), "unit": "scans/s", "cores": 1, "kind": "port",
+               "sample": f"first {n_done} scans of the rank-0 stream (extract + tracker Solve with "
+                         f"{args.outer} outer iterations + keyframe map rebuild incl. kd-tree over the 5M prior), "
+                         f"{cpu_el:.1f} s on 1 thread of {os.cpu_count()} host cores"}
+    if rank == 0:
+        line(args, d, "LiDAR scans/sec tracked (64k-pt scan streams, shared 5M-pt map, one stream per GPU)",
+             world * args.steps / elapsed, "scans/s", elapsed, "weak",
+             f"C4: one VLP-16 16x{args.cols} stream per GPU (8 m/s, 10 Hz) tracked against a {map_points}-pt "
+             f"shared map + stitched keyframe window (10 keyframes, voxel 0.2/0.4 m), {args.outer} outer iters",
+             {"streams": world, "map_points": map_points, "outer_iterations": args.outer,
+              "parallelism": f"stream-per-GPU x{world}"}, roof, cpu,
+             tracking_error_m={"rank0_max": max(state["err"]), "rank0_last": state["err"][-1]},
+             keyframes_appended=state["kf"])
+    tr.close()
+    ctx.close()
+
+
+# ----------------------------------------------------------------------------- C3: dual-LiDAR online refine
+def run_dual(args, d):
+    import numpy as np
+    torch = d.torch
+    from lmsf import _lib, dual, synth
+    world, rank = d.world, d.rank
+    n = args.warmup + args.steps
+    ds = synth.make_dual_sequence(n, n_cols=args.cols, step=0.5, start_x=8.0 * rank if world <= 8 else 64.0 * rank / world)
+
+    def mat(p):
+        T = np.eye(4)
+        T[:3, :3] = synth.quat_to_mat(p[:4])
+        T[:3, 3] = p[4:]
+        return T
+
+    X = mat(ds.extrinsic)
+    X0 = X @ mat(np.concatenate([synth.axis_angle_quat(np.radians([0.5, -0.5, 0.5])), [0.03, -0.02, 0.02]]))
+    prim_dev = [torch.from_numpy(s).to(d.dev) for s in ds.primary]
+    sub_dev = [torch.from_numpy(s).to(d.dev) for s in ds.sub]
+    max_pts = max(max(len(s) for s in ds.primary), max(len(s) for s in ds.sub))
+    ctx = _lib.Context(device=d.local, max_batch=1, max_scan_points=max_pts + 64, max_features=max_pts + 64)
+    system = dual.DualLidarSystem(ctx, extrinsic=X0)
+    state = {"i": 0}
+
+    def step():
+        i = state["i"]
+        out = system.process(prim_dev[i], sub_dev[i], 0.1 * i)
+        state["i"] += 1
+        return out
+
+    elapsed, _ = timed(d, step, args.warmup, args.steps, [ctx])
+    ks = ctx.kernel_stats()
+    roof = knn_roofline(ks, args.traffic_json, 1, 0,
+                        "achieved = SURVEY 8(d) algorithmic bytes / HIP-event launch time (one ~63k-query scan per "
+                        "launch against the voxelised local map: latency-bound launches)")
+    ext_err = [float(np.linalg.norm(system.extrinsic[:3, 3] - X[:3, 3])),
+               float(math.acos(max(-1.0, min(1.0, (np.trace(system.extrinsic[:3, :3].T @ X[:3, :3]) - 1) / 2))))]
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        oracle = cpu_oracle()
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import tracker as OT
+        ot = OT.Tracker()
+        ext = X0.copy()
+        n_done = 0
+        t1 = time.perf_counter()
+        while n_done < n and (n_done == 0 or time.perf_counter() - t1 < args.cpu_seconds):
+            ep, sp, _, _ = oracle.extract(ds.primary[n_done])
+            es, ss, _, _ = oracle.extract(ds.sub[n_done])
+            ot.solve(ep, sp, 0.1 * n_done)
+            prim = ot.curr.copy()
+            sub, _ = ot._register({1: es, 2: ss}, dual.iso_mul(prim, ext))
+            ext = dual.iso_mul(dual.iso_inv(prim), sub)
+            n_done += 1
+        cpu_el = time.perf_counter() - t1
+        cpu = {"value": round(n_done / cpu_el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+               "sample": f"first {n_done} frames of the same dual-LiDAR sequence (2 extractions, tracker Solve, "
+                         f"sub-LiDAR refine, keyframe map rebuild), {cpu_el:.1f} s on 1 thread of "
+                         f"{os.cpu_count()} host cores"}
+    if rank == 0:
+        npts = int(np.mean([len(s) for s in ds.primary]))
+        line(args, d, "dual-LiDAR frames/sec (2x64k-pt scans, tracking + online extrinsic refine)",
+             world * args.steps / elapsed, "frames/s", elapsed, "weak",
+             f"C3: two VLP-16 16x{args.cols} LiDARs (~{npts} pts each) at the PS-Calib extrinsic, primary "
+             f"tracking (reference decay schedule) + sub-LiDAR refine against the voxelised 10-keyframe local map",
+             {"systems": world, "parallelism": f"system-per-GPU x{world}"}, roof, cpu,
+             extrinsic_error={"m": ext_err[0], "rad": ext_err[1]})
+    system.close()
+    ctx.close()
+
+
+def main():
+    args = parse()
+    d = Dist()
+    {"C2": run_batch, "C5": run_batch, "C4": run_streams, "C3": run_dual}[args.config](args, d)
+    d.close()
 
 
 if __name__ == "__main__":
