@@ -121,20 +121,9 @@ def shared_map(d, make):
     if d.world == 1:
         e, s = make()
         return torch.from_numpy(e).to(d.dev), torch.from_numpy(s).to(d.dev)
-    if d.rank == 0:
-        e, s = make()
-        n = torch.tensor([len(e), len(s)], dtype=torch.int64, device=d.dev)
-    else:
-        n = torch.zeros(2, dtype=torch.int64, device=d.dev)
-    d.dist.broadcast(n, 0)
-    if d.rank == 0:
-        et, st = torch.from_numpy(e).to(d.dev), torch.from_numpy(s).to(d.dev)
-    else:
-        et = torch.empty((int(n[0]), 4), dtype=torch.float32, device=d.dev)
-        st = torch.empty((int(n[1]), 4), dtype=torch.float32, device=d.dev)
-    d.dist.broadcast(et, 0)
-    d.dist.broadcast(st, 0)
-    return et, st
+    from lmsf import multi
+    e, s = make() if d.rank == 0 else (None, None)
+    return multi.broadcast_map(e, s, d.dev)
 
 
 def knn_roofline(ks, traffic_json, batch, map_points, note):
@@ -204,7 +193,7 @@ def run_batch(args, d):
         rng = np.random.default_rng(3000 + k + rank)
         guesses = np.stack([synth.perturb(truth_u[unit_scan[i]], rng) for i in range(n_units)])
     else:                                                      # C5: pairs i = rank, rank + N, ...
-        mine = list(range(rank, args.pairs, world))
+        mine = multi.pair_partition(args.pairs, rank, world)
         n_units = len(mine)
         unit_scan = [j % U for j in range(n_units)]
         guesses = np.stack([synth.perturb(truth_u[unit_scan[j]], np.random.default_rng(3000 + k + 7919 * i))
@@ -217,8 +206,7 @@ def run_batch(args, d):
     ctx.set_map(_lib.SURF, sm_t)
     map_points = int(em_t.shape[0] + sm_t.shape[0])
     ctx.load_scans([scans_u[j % U] for j in range(chunk)])
-    per_rank = n_units if cfg == "C2" else -(-args.pairs // world)
-    gathered = torch.zeros((world, per_rank, 7), dtype=torch.float64, device=d.dev)
+    gathered = torch.zeros((world, n_units, 7), dtype=torch.float64, device=d.dev)
     poses = np.zeros((n_units, 7))
 
     def step():
@@ -227,9 +215,10 @@ def run_batch(args, d):
             ctx.batch_launch(guesses[c0:c0 + nb])
             poses[c0:c0 + nb], _ = ctx.batch_wait(nb)
         if world > 1:                                        # RCCL all-gather of the 6-DoF poses
-            buf = np.zeros((per_rank, 7))
-            buf[:n_units] = poses
-            multi.gather_poses(buf, gathered, d.dev)
+            if cfg == "C2":
+                multi.gather_poses(poses, gathered, d.dev)
+            else:
+                multi.gather_pair_poses(poses, args.pairs, world, d.dev)
         return poses
 
     elapsed, _ = timed(d, step, args.warmup, args.steps, [ctx])
@@ -291,7 +280,7 @@ def run_batch(args, d):
 def run_streams(args, d):
     import numpy as np
     torch = d.torch
-    from lmsf import _lib, synth
+    from lmsf import _lib, multi, synth
     c = synth.CONFIGS["C4"]
     k = c["k"]
     world, rank = d.world, d.rank
@@ -317,9 +306,7 @@ def run_streams(args, d):
     map_points = int(em_t.shape[0] + sm_t.shape[0])
     cap = max_pts + 64
     fbuf = torch.zeros((2 * cap, 4), dtype=torch.float32, device=d.dev)       # [edges | surfs] of own scan
-    gbuf = torch.zeros((world, 2 * cap, 4), dtype=torch.float32, device=d.dev)
-    info = torch.zeros((world, 19), dtype=torch.float64, device=d.dev)
-    own = torch.zeros(19, dtype=torch.float64, device=d.dev)
+    xchg = multi.KeyframeExchange(cap, world, d.dev)
     state = {"i": 0, "kf": 0, "err": []}
 
     def step():
@@ -331,26 +318,12 @@ def run_streams(args, d):
         if r.update_type:
             ne = ctx.copy_features_into(_lib.EDGE, fbuf[:cap])
             ns = ctx.copy_features_into(_lib.SURF, fbuf[cap:])
-        vec = np.concatenate([P.ravel(), [r.update_type, ne, ns]])
-        if world > 1:
-            own.copy_(torch.from_numpy(vec))
-            d.dist.all_gather_into_tensor(info, own)                        # poses + keyframe flags
-            allinfo = info.cpu().numpy()
-            if (allinfo[:, 16] > 0).any():
-                d.dist.all_gather_into_tensor(gbuf.view(-1), fbuf.view(-1))  # keyframe features
-        else:
-            allinfo = vec[None]
-            if r.update_type:
-                gbuf[0].copy_(fbuf)
-        added = False
-        for q in range(world):                                          # same order on every rank
-            if allinfo[q, 16] > 0:
-                qe, qs = int(allinfo[q, 17]), int(allinfo[q, 18])
-                tr.add_keyframe(gbuf[q, :qe], gbuf[q, cap:cap + qs], allinfo[q, :16].reshape(4, 4))
-                added = True
-                state["kf"] += 1
-        if added:
+        kfs = xchg.exchange(P, r.update_type, ne, ns, fbuf)           # same list, same order everywhere
+        for _, fe, fs, pose in kfs:
+            tr.add_keyframe(fe, fs, pose)
+        if kfs:
             tr.commit_map()
+            state["kf"] += len(kfs)
         Tt = np.eye(4)
         Tt[:3, :3] = synth.quat_to_mat(truth[i][:4])
         Tt[:3, 3] = truth[i][4:]

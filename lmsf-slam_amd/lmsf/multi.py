@@ -1,6 +1,8 @@
-"""Multi-GPU plumbing of the batch path: one process per GPU, scans sharded
-across ranks with no data-path collective, then one all-gather of the resulting 6-DoF poses
-(7 doubles per scan) over RCCL (torch.distributed "nccl") for local-map stitching.
+"""Multi-GPU plumbing: one process per GPU over RCCL (torch.distributed "nccl").
+C2 batch path: scans sharded across ranks with no data-path collective, then one all-gather of the
+6-DoF poses (7 doubles per scan).  C5: pairs partitioned i mod N, one padded pose all-gather.
+C4: shared map broadcast once from rank 0; per tracking step a pose/keyframe-flag all-gather and,
+when a stream keyframes, an all-gather of its features (KeyframeExchange).
 
 The same functions run on CPU tensors with the gloo backend (tests/test_multirank.py).
 """
@@ -34,3 +36,85 @@ def max_over_ranks(value: float, device=None) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+# ---- C5: loop-closure re-registration, pairs partitioned i mod N, one padded pose all-gather
+def pair_partition(n_pairs: int, rank: int, world: int):
+    """Global pair indices owned by `rank` (i mod world), SURVEY 8(e) C5."""
+    return list(range(rank, n_pairs, world))
+
+
+def gather_pair_poses(local_poses: np.ndarray, n_pairs: int, world: int, device=None) -> np.ndarray:
+    """All-gather every rank's (len(pair_partition), 7) poses; returns (n_pairs, 7) in global pair order."""
+    import torch
+    per = -(-n_pairs // world)
+    buf = np.zeros((per, 7))
+    buf[:len(local_poses)] = local_poses
+    out = torch.zeros((world, per, 7), dtype=torch.float64, device=device)
+    gather_poses(buf, out, device)
+    allp = out.cpu().numpy()
+    res = np.zeros((n_pairs, 7))
+    for r in range(world):
+        idx = pair_partition(n_pairs, r, world)
+        res[idx] = allp[r, :len(idx)]
+    return res
+
+
+# ---- C4: shared map replicated from rank 0, keyframe features exchanged between streams
+def broadcast_map(edge, surf, device=None):
+    """Rank 0's (n, 4) float32 edge / surf maps replicated on every rank (one broadcast each)."""
+    import torch
+    import torch.distributed as dist
+    rank = dist.get_rank()
+    if rank == 0:
+        n = torch.tensor([len(edge), len(surf)], dtype=torch.int64, device=device)
+    else:
+        n = torch.zeros(2, dtype=torch.int64, device=device)
+    dist.broadcast(n, 0)
+    out = []
+    for k, src in enumerate((edge, surf)):
+        if rank == 0:
+            t = torch.as_tensor(np.ascontiguousarray(src, dtype=np.float32)).to(device)
+        else:
+            t = torch.empty((int(n[k]), 4), dtype=torch.float32, device=device)
+        dist.broadcast(t, 0)
+        out.append(t)
+    return out[0], out[1]
+
+
+class KeyframeExchange:
+    """Per tracking step: all-gather (pose 4x4, update type, edge count, surf count) of every
+    stream, and -- only when some stream keyframed -- the padded feature buffers, so that every
+    replica appends the same keyframes in rank order (`ncclAllGather` of the pose
+    every step, of the transformed-feature payload when a stream emits a keyframe).
+
+    feat: (2 * cap, 4) float32 tensor on `device` holding this rank's [edges | surfs] (edges at 0,
+    surfs at cap).  Returns [(rank, edge_view, surf_view, pose4x4)] for the keyframed streams."""
+
+    def __init__(self, cap: int, world: int, device=None):
+        import torch
+        self.cap, self.world, self.device = cap, world, device
+        self.info = torch.zeros((world, 19), dtype=torch.float64, device=device)
+        self.own = torch.zeros(19, dtype=torch.float64, device=device)
+        self.gbuf = torch.zeros((world, 2 * cap, 4), dtype=torch.float32, device=device)
+
+    def exchange(self, pose, update_type, n_edge, n_surf, feat):
+        import torch
+        import torch.distributed as dist
+        vec = np.concatenate([np.asarray(pose, dtype=np.float64).ravel(), [update_type, n_edge, n_surf]])
+        if self.world > 1:
+            self.own.copy_(torch.from_numpy(vec))
+            dist.all_gather_into_tensor(self.info, self.own.unsqueeze(0))
+            allinfo = self.info.cpu().numpy()
+            if (allinfo[:, 16] > 0).any():
+                dist.all_gather_into_tensor(self.gbuf, feat.unsqueeze(0))
+        else:
+            allinfo = vec[None]
+            if update_type:
+                self.gbuf[0].copy_(feat)
+        out = []
+        for q in range(self.world):
+            if allinfo[q, 16] > 0:
+                ne, ns = int(allinfo[q, 17]), int(allinfo[q, 18])
+                out.append((q, self.gbuf[q, :ne], self.gbuf[q, self.cap:self.cap + ns], allinfo[q, :16].reshape(4, 4)))
+        return out

@@ -65,3 +65,70 @@ def test_gloo_world2_pose_allgather():
         for r2, lo2, hi2, _, _ in res:                    # every rank sees every rank's poses
             expect = np.stack([np.full(7, 100.0 * i + k) for i, k in enumerate(range(lo2, hi2))])
             np.testing.assert_array_equal(buf[r2], expect)
+
+
+def _worker_c45(rank, world, port, out_q):
+    """C5 pair partition + padded pose gather; C4 map broadcast + keyframe exchange."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lmsf-slam_amd"))
+    import torch
+    import torch.distributed as dist
+    from lmsf import multi
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # C5: 7 pairs, rank r owns i = r, r + 2, ...; pose of pair i = i
+    mine = multi.pair_partition(7, rank, world)
+    allp = multi.gather_pair_poses(np.stack([np.full(7, float(i)) for i in mine]), 7, world)
+    # C4: rank 0's map replicated
+    rng = np.random.default_rng(0)
+    e0 = rng.random((11, 4)).astype(np.float32)
+    s0 = rng.random((23, 4)).astype(np.float32)
+    et, st = multi.broadcast_map(e0 if rank == 0 else None, s0 if rank == 0 else None)
+    # C4 keyframe exchange over 3 steps: step 0 both keyframe, step 1 none, step 2 only rank 1
+    cap = 8
+    xchg = multi.KeyframeExchange(cap, world)
+    log = []
+    for step, kf in enumerate([(1, 1), (0, 0), (0, 2)]):
+        typ = kf[rank]
+        ne, ns = 2 + rank, 3 + step
+        feat = torch.zeros((2 * cap, 4), dtype=torch.float32)
+        feat[:ne] = 10 * rank + step
+        feat[cap:cap + ns] = -(10 * rank + step)
+        pose = np.eye(4)
+        pose[0, 3] = 100 * rank + step
+        got = xchg.exchange(pose, typ, ne if typ else 0, ns if typ else 0, feat)
+        log.append([(q, fe.numpy().copy(), fs.numpy().copy(), P.copy()) for q, fe, fs, P in got])
+    out_q.put((rank, allp, et.numpy(), st.numpy(), log))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_pairs_map_and_keyframe_exchange():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_c45, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(0)
+    e0 = rng.random((11, 4)).astype(np.float32)
+    s0 = rng.random((23, 4)).astype(np.float32)
+    for rank, allp, et, st, log in res:
+        np.testing.assert_array_equal(allp, np.stack([np.full(7, float(i)) for i in range(7)]))
+        assert et.tobytes() == e0.tobytes() and st.tobytes() == s0.tobytes()
+        assert [q for q, *_ in log[0]] == [0, 1] and log[1] == [] and [q for q, *_ in log[2]] == [1]
+        for step, entries in enumerate(log):
+            for qr, fe, fs, P in entries:
+                assert fe.shape == (2 + qr, 4) and fs.shape == (3 + step, 4)
+                assert (fe == 10 * qr + step).all() and (fs == -(10 * qr + step)).all()
+                assert P[0, 3] == 100 * qr + step
+    # both replicas append the same keyframes in the same order
+    for a, b in zip(res[0][4], res[1][4]):
+        assert len(a) == len(b)
+        for x, y in zip(a, b):
+            assert x[0] == y[0] and x[1].tobytes() == y[1].tobytes() and x[2].tobytes() == y[2].tobytes()
