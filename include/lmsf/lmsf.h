@@ -248,6 +248,17 @@ lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t);
 lmsf_status lmsf_voxel_filter(lmsf_ctx* ctx, const float* xyzi, size_t n, float leaf, float* out, size_t cap,
                               size_t* n_out);
 
+/* ---- 1-NN alignment fitness: Slam3D::PointCloudAlignmentEvaluate (REG/alignEvaluate.hpp:24-95),
+ * the loop-closure / relocalisation check (INC/LoopDetection/loopDetection.hpp:176-177, :411, :451;
+ * INC/BackEnd/backend_lifelong.hpp:318-319).
+ * SetTargetPoints (:42-46): build the target's device neighbour grid (host or device memory). */
+lmsf_status lmsf_align_set_target(lmsf_ctx* ctx, const float* xyzi, size_t n);
+/* AlignmentScore (:55-87): transform the cloud by relpose (row-major Eigen::Matrix4f, float math),
+ * 1-NN squared distance to the target, inliers d2 <= inlier_thresh; *overlap = inliers / n,
+ * *score = mean inlier d2 when *overlap > inlier_ratio_thresh, else DBL_MAX (empty cloud: DBL_MAX, 0). */
+lmsf_status lmsf_align_score(lmsf_ctx* ctx, const float* xyzi, size_t n, const float relpose[16], double inlier_thresh,
+                             double inlier_ratio_thresh, double* score, double* overlap);
+
 /* ---- dual-LiDAR extrinsic initialisation (C3): Algorithm::HandEyeCalibrationBase
  * (INC/Algorithm/calibration/handeye_calibration_base.hpp:36-244) as driven by
  * MultiLidarSystem::process phase 0 (INC/System/ML_System.hpp:268-281).  Host-only arithmetic

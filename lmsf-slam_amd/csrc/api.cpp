@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -106,6 +107,12 @@ struct lmsf_ctx {
     float4* vox_in = nullptr;
     float4* vox_out = nullptr;
     size_t vox_cap = 0;
+    // lmsf_align_score workspace (target grid = map[0])
+    float4* align_in = nullptr;
+    double* align_part_sum = nullptr;
+    unsigned int* align_part_cnt = nullptr;
+    double* align_out = nullptr;
+    size_t align_cap = 0;
 
     lmsf_status fail(lmsf_status code, const char* fmt, ...) {
         char buf[512];
@@ -350,6 +357,10 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     c->voxel.release();
     hipFree(c->vox_in);
     hipFree(c->vox_out);
+    hipFree(c->align_in);
+    hipFree(c->align_part_sum);
+    hipFree(c->align_part_cnt);
+    hipFree(c->align_out);
     if (c->h_poses) hipHostFree(c->h_poses);
     if (c->h_st) hipHostFree(c->h_st);
     if (c->h_counts) hipHostFree(c->h_counts);
@@ -558,6 +569,51 @@ lmsf_status lmsf_voxel_filter(lmsf_ctx* c, const float* xyzi, size_t n, float le
     if ((size_t)nv > cap) return c->fail(LMSF_ERR_CAPACITY, "output capacity %zu < %d voxels", cap, nv);
     HIPCHK(c, hipMemcpyAsync(out, c->vox_out, (size_t)nv * sizeof(float4), hipMemcpyDefault, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_align_set_target(lmsf_ctx* c, const float* xyzi, size_t n) {
+    if (!c || !xyzi || n == 0) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    return build_map(c, 0, xyzi, n);
+}
+
+lmsf_status lmsf_align_score(lmsf_ctx* c, const float* xyzi, size_t n, const float relpose[16], double inlier_thresh,
+                             double inlier_ratio_thresh, double* score, double* overlap) {
+    if (!c || !relpose || !score || !overlap || (n && !xyzi) || n > (size_t)INT32_MAX) return LMSF_ERR_ARG;
+    if (!c->map_set[0]) return c->fail(LMSF_ERR_STATE, "AlignmentScore before SetTargetPoints");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (n == 0) {                                                     // alignEvaluate.hpp:61
+        *score = DBL_MAX;
+        *overlap = 0.0;
+        return LMSF_OK;
+    }
+    if (n > c->align_cap) {
+        HIPCHK(c, hipFree(c->align_in));
+        HIPCHK(c, hipFree(c->align_part_sum));
+        HIPCHK(c, hipFree(c->align_part_cnt));
+        c->align_in = nullptr;
+        c->align_part_sum = nullptr;
+        c->align_part_cnt = nullptr;
+        c->align_cap = 0;
+        const size_t parts = (size_t)align_parts((int)n);
+        HIPCHK(c, hipMalloc((void**)&c->align_in, n * sizeof(float4)));
+        HIPCHK(c, hipMalloc((void**)&c->align_part_sum, parts * sizeof(double)));
+        HIPCHK(c, hipMalloc((void**)&c->align_part_cnt, parts * sizeof(unsigned int)));
+        c->align_cap = n;
+    }
+    if (!c->align_out) HIPCHK(c, hipMalloc((void**)&c->align_out, 2 * sizeof(double)));
+    Affine34f M;
+    for (int i = 0; i < 12; ++i) M.m[i] = relpose[i];
+    HIPCHK(c, hipMemcpyAsync(c->align_in, xyzi, n * sizeof(float4), hipMemcpyDefault, c->stream));
+    HIPCHK(c, launch_align(c->map[0].view(), c->align_in, (int)n, M, inlier_thresh, c->align_part_sum,
+                           c->align_part_cnt, c->align_out, c->stream));
+    double h[2];
+    HIPCHK(c, hipMemcpyAsync(h, c->align_out, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const double nr = h[1];
+    *overlap = nr / (double)n;                                        // :81
+    *score = *overlap > inlier_ratio_thresh ? h[0] / nr : DBL_MAX;    // :83-86
     return LMSF_OK;
 }
 

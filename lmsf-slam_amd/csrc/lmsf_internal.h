@@ -122,6 +122,13 @@ struct Affine34 { double m[12]; };   // row-major 3x4 of an Isometry3d matrix
 // pcl::transformPointCloud(cloud, out, Matrix4d) per point: float(m00 x + m01 y + m02 z + m03), double math
 hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hipStream_t s);
 
+// ---- 1-NN alignment fitness (k_align.hip): AlignmentScore (REG/alignEvaluate.hpp:55-87)
+struct Affine34f { float m[12]; };   // row-major 3x4 of an Eigen::Matrix4f
+int align_parts(int n);
+// out2[0] = sum of inlier d2 (double), out2[1] = inlier count; part_* hold align_parts(n) entries
+hipError_t launch_align(const GridView& g, const float4* src, int n, const Affine34f& M, double thresh,
+                        double* part_sum, unsigned int* part_cnt, double* out2, hipStream_t s);
+
 // pcl::VoxelGrid centroid downsampling on the device (k_voxel.hip); workspace grows on demand.
 // run() synchronises the stream (the output count is returned to the host).
 struct VoxelFilter {

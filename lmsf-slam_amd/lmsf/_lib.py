@@ -106,6 +106,9 @@ _SIGS = {
     "lmsf_tracker_add_keyframe": (C.c_int32, [_P, _P, C.c_size_t, _P, C.c_size_t, _P]),
     "lmsf_tracker_commit_map": (C.c_int32, [_P]),
     "lmsf_voxel_filter": (C.c_int32, [_P, _P, C.c_size_t, C.c_float, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "lmsf_align_set_target": (C.c_int32, [_P, _P, C.c_size_t]),
+    "lmsf_align_score": (C.c_int32, [_P, _P, C.c_size_t, _P, C.c_double, C.c_double, C.POINTER(C.c_double),
+                                     C.POINTER(C.c_double)]),
     "lmsf_handeye_create": (C.c_int32, [C.POINTER(_P)]),
     "lmsf_handeye_destroy": (None, [_P]),
     "lmsf_handeye_add_pose": (C.c_int32, [_P, _P, _P, C.POINTER(C.c_int32)]),
@@ -242,6 +245,20 @@ class Context:
         m = C.c_size_t()
         self._check(load().lmsf_voxel_filter(self.h, p, n, float(leaf), out.ctypes.data, out.shape[0], C.byref(m)))
         return out[:m.value].copy()
+
+    def align_set_target(self, pts):
+        """PointCloudAlignmentEvaluate::SetTargetPoints."""
+        p, n, keep = _buf(pts)
+        self._check(load().lmsf_align_set_target(self.h, p, n))
+
+    def align_score(self, pts, relpose, inlier_thresh, inlier_ratio_thresh):
+        """PointCloudAlignmentEvaluate::AlignmentScore -> (score, overlap_ratio)."""
+        p, n, keep = _buf(pts)
+        T = np.ascontiguousarray(relpose, dtype=np.float32)
+        sc, ov = C.c_double(), C.c_double()
+        self._check(load().lmsf_align_score(self.h, p, n, T.ctypes.data, float(inlier_thresh),
+                                            float(inlier_ratio_thresh), C.byref(sc), C.byref(ov)))
+        return sc.value, ov.value
 
     # ---- batch path
     def load_scans(self, scans):

@@ -374,6 +374,34 @@ def test_voxel_filter_bitexact(lib, oracle_mod, small_workload):
     assert ctx.voxel_filter(far, 0.01).tobytes() == far.tobytes()
 
 
+def test_alignment_score_parity(lib, oracle_mod, small_workload):
+    """lmsf_align_score vs oracle/align.py (AlignmentScore, REG/alignEvaluate.hpp:55-87): inlier
+    count exact, mean inlier d2 rel 1e-12 (reduction order), thresholds of the reference's callers
+    (0.1, 1.0) plus 4.0 (two-cell search radius)."""
+    import sys
+    import torch
+    import align as OA
+    from conftest import pose_matrix
+    wl = small_workload
+    ctx = _ctx(lib)
+    ctx.align_set_target(wl.surf_map)
+    tree = oracle_mod.KdMap(wl.surf_map)
+    e, s, _, _ = oracle_mod.extract(wl.scans[1])
+    for pose in (wl.truth[1], wl.guess[1]):
+        T = pose_matrix(pose).astype(np.float32)
+        for thresh, ratio in ((0.1, 0.6), (1.0, 0.6), (4.0, 0.5), (0.1, 0.99)):
+            gs, go = ctx.align_score(s, T, thresh, ratio)
+            os_, oo = OA.alignment_score(wl.surf_map, s, T, thresh, ratio, tree=tree)
+            assert go == oo
+            if os_ == sys.float_info.max:
+                assert gs == os_
+            else:
+                assert abs(gs - os_) <= 1e-12 * os_
+    gs, go = ctx.align_score(torch.from_numpy(s).to("cuda:0"), pose_matrix(wl.truth[1]), 0.1, 0.6)
+    assert go > 0.6 and gs < 0.05                      # well aligned: relocalisation accepted (:180)
+    assert ctx.align_score(s[:0], np.eye(4), 0.1, 0.6) == (sys.float_info.max, 0.0)
+
+
 def test_tracker_shared_map_streams(lib, oracle_mod, sequence_workload):
     """C4 flow on one GPU: two streams (scans 0-4 and 5-9) with a shared world-frame prior map,
     initial poses in that frame, keyframes exchanged in stream order and committed once per step

@@ -297,3 +297,25 @@ def test_oracle_voxel_filter(oracle_mod):
     # PCL refuses when the voxel index would overflow int32: input returned unchanged
     far = np.array([[0, 0, 0, 0], [1e4, 1e4, 1e4, 1]], np.float32)
     assert oracle_mod.voxel_filter(far, 0.01).tobytes() == far.tobytes()
+
+
+def test_oracle_alignment_score_vs_scipy(oracle_mod, tiny):
+    """AlignmentScore restatement (oracle/align.py) vs scipy cKDTree 1-NN on the same float inputs."""
+    import sys
+    from scipy.spatial import cKDTree
+    import align as OA
+    from conftest import pose_matrix
+    wl = tiny
+    e, s, _, _ = oracle_mod.extract(wl.scans[0])
+    T = pose_matrix(wl.truth[0]).astype(np.float32)
+    for thresh, ratio in ((0.1, 0.6), (1.0, 0.6), (0.1, 0.0)):
+        score, overlap = OA.alignment_score(wl.surf_map, s, T, thresh, ratio)
+        q = OA.transform_f32(s, T)
+        d, _ = cKDTree(wl.surf_map[:, :3].astype(np.float64)).query(q[:, :3].astype(np.float64), k=1)
+        inl = d * d <= thresh
+        assert abs(overlap - inl.mean()) < 2e-3                     # float vs double distances at the edge
+        if overlap > ratio:
+            assert abs(score - (d[inl] ** 2).mean()) < 1e-4 * max(1.0, score)
+        else:
+            assert score == sys.float_info.max
+    assert OA.alignment_score(wl.surf_map, s[:0], T, 0.1, 0.6) == (sys.float_info.max, 0.0)
