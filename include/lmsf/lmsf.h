@@ -248,6 +248,31 @@ lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t);
 lmsf_status lmsf_voxel_filter(lmsf_ctx* ctx, const float* xyzi, size_t n, float leaf, float* out, size_t cap,
                               size_t* n_out);
 
+/* ---- scan ingest: sensor_msgs/PointCloud2 -> pcl::fromROSMsg +
+ * pcl::removeNaNFromPointCloud (src/apps/src/MultiLidarSLAM_node.cpp:125-132) ->
+ * RotaryLidarPreProcess::Process (INC/Algorithm/PointClouds/processing/Preprocess/
+ * RotaryLidar_preprocessing.hpp:31-104: relative time in the intensity field) ->
+ * DistanceFilter::Filter (.../processing/Filter/distance_filter.hpp:24-43, optional). */
+typedef struct {
+    uint32_t point_step;        /* PointCloud2.point_step (bytes per point) */
+    int32_t offset_x, offset_y, offset_z;   /* byte offsets of the FLOAT32 fields */
+    int32_t offset_intensity;   /* FLOAT32 intensity offset, -1 = absent (0) */
+    int32_t is_bigendian;       /* only little-endian messages are accepted */
+    float scan_period;          /* RotaryLidarPreProcess SCAN_PERIOD (0.1 s); <= 0 keeps the intensity */
+    float distance_near;        /* DistanceFilter thresholds; both 0 = off (distance_filter.hpp:26-30) */
+    float distance_far;
+} lmsf_ingest_params;
+/* Defaults: velodyne_pointcloud layout (x 0, y 4, z 8, intensity 16, point_step 32), period 0.1, no
+ * distance filter. */
+lmsf_status lmsf_ingest_params_init(lmsf_ingest_params* p);
+/* Decode n points of message data (host or device memory) into xyzi rows at out (host or device
+ * memory, cap rows); *n_out = points kept. */
+lmsf_status lmsf_ingest_pointcloud2(lmsf_ctx* ctx, const uint8_t* data, size_t n_points, const lmsf_ingest_params* p,
+                                    float* out, size_t cap, size_t* n_out);
+/* Ingest + lmsf_extract_features in one device pass (the cloud never leaves HBM). */
+lmsf_status lmsf_extract_pointcloud2(lmsf_ctx* ctx, const uint8_t* data, size_t n_points, const lmsf_ingest_params* p,
+                                     lmsf_feature_counts* counts);
+
 /* ---- 1-NN alignment fitness: Slam3D::PointCloudAlignmentEvaluate (REG/alignEvaluate.hpp:24-95),
  * the loop-closure / relocalisation check (INC/LoopDetection/loopDetection.hpp:176-177, :411, :451;
  * INC/BackEnd/backend_lifelong.hpp:318-319).

@@ -107,6 +107,7 @@ struct lmsf_ctx {
     float4* vox_in = nullptr;
     float4* vox_out = nullptr;
     size_t vox_cap = 0;
+    Ingest ingest;                    // lmsf_ingest_pointcloud2 workspace
     // lmsf_align_score workspace (target grid = map[0])
     float4* align_in = nullptr;
     double* align_part_sum = nullptr;
@@ -357,6 +358,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     c->voxel.release();
     hipFree(c->vox_in);
     hipFree(c->vox_out);
+    c->ingest.release();
     hipFree(c->align_in);
     hipFree(c->align_part_sum);
     hipFree(c->align_part_cnt);
@@ -570,6 +572,64 @@ lmsf_status lmsf_voxel_filter(lmsf_ctx* c, const float* xyzi, size_t n, float le
     HIPCHK(c, hipMemcpyAsync(out, c->vox_out, (size_t)nv * sizeof(float4), hipMemcpyDefault, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return LMSF_OK;
+}
+
+lmsf_status lmsf_ingest_params_init(lmsf_ingest_params* p) {
+    if (!p) return LMSF_ERR_ARG;
+    std::memset(p, 0, sizeof *p);
+    p->point_step = 32;
+    p->offset_x = 0;
+    p->offset_y = 4;
+    p->offset_z = 8;
+    p->offset_intensity = 16;
+    p->is_bigendian = 0;
+    p->scan_period = 0.1f;
+    return LMSF_OK;
+}
+
+static lmsf_status ingest_device(lmsf_ctx* c, const uint8_t* data, size_t n, const lmsf_ingest_params* p, float4** res,
+                                 int* nk) {
+    if (!c || !p || (n && !data) || n > (size_t)INT32_MAX) return LMSF_ERR_ARG;
+    const int64_t step = p->point_step;
+    const int32_t offs[3] = {p->offset_x, p->offset_y, p->offset_z};
+    for (int32_t o : offs)
+        if (o < 0 || o + 4 > step) return c->fail(LMSF_ERR_ARG, "field offset %d outside point_step %lld", o, (long long)step);
+    if (p->offset_intensity >= 0 && p->offset_intensity + 4 > step) return c->fail(LMSF_ERR_ARG, "intensity offset");
+    if (p->is_bigendian) return c->fail(LMSF_ERR_ARG, "big-endian PointCloud2 is not supported");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    *nk = 0;
+    *res = nullptr;
+    if (n == 0) return LMSF_OK;
+    HIPCHK(c, c->ingest.reserve(n, n * (size_t)step));
+    HIPCHK(c, hipMemcpyAsync(c->ingest.raw, data, n * (size_t)step, hipMemcpyDefault, c->stream));
+    HIPCHK(c, c->ingest.run(c->ingest.raw, (int)n, (uint32_t)step, p->offset_x, p->offset_y, p->offset_z,
+                            p->offset_intensity, p->scan_period, p->distance_near, p->distance_far, res, nk, c->stream));
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_ingest_pointcloud2(lmsf_ctx* c, const uint8_t* data, size_t n, const lmsf_ingest_params* p, float* out,
+                                    size_t cap, size_t* n_out) {
+    float4* res = nullptr;
+    int nk = 0;
+    lmsf_status rc = ingest_device(c, data, n, p, &res, &nk);
+    if (rc) return rc;
+    if (n_out) *n_out = (size_t)nk;
+    if ((size_t)nk > cap) return c->fail(LMSF_ERR_CAPACITY, "output capacity %zu < %d points", cap, nk);
+    if (nk) {
+        if (!out) return LMSF_ERR_ARG;
+        HIPCHK(c, hipMemcpyAsync(out, res, (size_t)nk * sizeof(float4), hipMemcpyDefault, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_extract_pointcloud2(lmsf_ctx* c, const uint8_t* data, size_t n, const lmsf_ingest_params* p,
+                                     lmsf_feature_counts* counts) {
+    float4* res = nullptr;
+    int nk = 0;
+    lmsf_status rc = ingest_device(c, data, n, p, &res, &nk);
+    if (rc) return rc;
+    return lmsf_extract_features(c, reinterpret_cast<const float*>(res), (size_t)nk, counts);
 }
 
 lmsf_status lmsf_align_set_target(lmsf_ctx* c, const float* xyzi, size_t n) {

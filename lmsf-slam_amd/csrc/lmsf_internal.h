@@ -141,6 +141,22 @@ struct VoxelFilter {
     void release();
 };
 
+// PointCloud2 decode + removeNaN + rotary relative time + distance filter (k_ingest.hip).
+// run() reads the message from device memory (raw, staged by the caller) and synchronises.
+struct Ingest {
+    uint8_t* raw = nullptr;
+    size_t raw_cap = 0;
+    float4 *a = nullptr, *b = nullptr;
+    uint32_t *keep = nullptr, *pos = nullptr;
+    int* scalars = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0, cap = 0;
+    hipError_t reserve(size_t n, size_t raw_bytes);
+    hipError_t run(const uint8_t* data_dev, int n, uint32_t step, int ox, int oy, int oz, int oi, float period,
+                   double near_t, double far_t, float4** result, int* n_out, hipStream_t s);
+    void release();
+};
+
 hipStream_t ctx_stream(lmsf_ctx* c);
 int ctx_device(const lmsf_ctx* c);
 int ctx_feature_capacity(const lmsf_ctx* c);

@@ -57,6 +57,12 @@ class TrackerConfig(C.Structure):
                 ("leaf_surf", C.c_double)]
 
 
+class IngestParams(C.Structure):
+    _fields_ = [("point_step", C.c_uint32), ("offset_x", C.c_int32), ("offset_y", C.c_int32),
+                ("offset_z", C.c_int32), ("offset_intensity", C.c_int32), ("is_bigendian", C.c_int32),
+                ("scan_period", C.c_float), ("distance_near", C.c_float), ("distance_far", C.c_float)]
+
+
 class TrackerResult(C.Structure):
     _fields_ = [("initialized", C.c_int32), ("update_type", C.c_int32), ("local_map_edge", C.c_int64),
                 ("local_map_surf", C.c_int64), ("solve", SolveStats)]
@@ -106,6 +112,11 @@ _SIGS = {
     "lmsf_tracker_add_keyframe": (C.c_int32, [_P, _P, C.c_size_t, _P, C.c_size_t, _P]),
     "lmsf_tracker_commit_map": (C.c_int32, [_P]),
     "lmsf_voxel_filter": (C.c_int32, [_P, _P, C.c_size_t, C.c_float, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "lmsf_ingest_params_init": (C.c_int32, [C.POINTER(IngestParams)]),
+    "lmsf_ingest_pointcloud2": (C.c_int32, [_P, _P, C.c_size_t, C.POINTER(IngestParams), _P, C.c_size_t,
+                                            C.POINTER(C.c_size_t)]),
+    "lmsf_extract_pointcloud2": (C.c_int32, [_P, _P, C.c_size_t, C.POINTER(IngestParams),
+                                             C.POINTER(FeatureCounts)]),
     "lmsf_align_set_target": (C.c_int32, [_P, _P, C.c_size_t]),
     "lmsf_align_score": (C.c_int32, [_P, _P, C.c_size_t, _P, C.c_double, C.c_double, C.POINTER(C.c_double),
                                      C.POINTER(C.c_double)]),
@@ -245,6 +256,38 @@ class Context:
         m = C.c_size_t()
         self._check(load().lmsf_voxel_filter(self.h, p, n, float(leaf), out.ctypes.data, out.shape[0], C.byref(m)))
         return out[:m.value].copy()
+
+    @staticmethod
+    def ingest_params(**kw):
+        p = IngestParams()
+        load().lmsf_ingest_params_init(C.byref(p))
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+    def _msg(self, data):
+        if hasattr(data, "data_ptr"):
+            return data.data_ptr(), data
+        d = np.ascontiguousarray(data, dtype=np.uint8)
+        return d.ctypes.data, d
+
+    def ingest_pointcloud2(self, data, n_points, **kw):
+        """PointCloud2 bytes (numpy uint8 or a device tensor) -> (n, 4) xyzi after removeNaN, rotary
+        relative time and the optional distance filter."""
+        p = self.ingest_params(**kw)
+        ptr, keep = self._msg(data)
+        out = np.zeros((max(n_points, 1), 4), np.float32)
+        m = C.c_size_t()
+        self._check(load().lmsf_ingest_pointcloud2(self.h, ptr, n_points, C.byref(p), out.ctypes.data, out.shape[0],
+                                                   C.byref(m)))
+        return out[:m.value].copy()
+
+    def extract_pointcloud2(self, data, n_points, **kw):
+        p = self.ingest_params(**kw)
+        ptr, keep = self._msg(data)
+        fc = FeatureCounts()
+        self._check(load().lmsf_extract_pointcloud2(self.h, ptr, n_points, C.byref(p), C.byref(fc)))
+        return fc.n_edge, fc.n_surf
 
     def align_set_target(self, pts):
         """PointCloudAlignmentEvaluate::SetTargetPoints."""

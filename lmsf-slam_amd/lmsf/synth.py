@@ -201,9 +201,13 @@ def raycast(scene: Scene, origin: np.ndarray, dirs: np.ndarray, max_range: float
     return best
 
 
-def scan_directions(n_cols: int, elev_deg: np.ndarray) -> np.ndarray:
-    """Lidar-frame unit rays, azimuth-major, firing order inside each column."""
+def scan_directions(n_cols: int, elev_deg: np.ndarray, clockwise: bool = False) -> np.ndarray:
+    """Lidar-frame unit rays, azimuth-major, firing order inside each column.  clockwise=True sweeps
+    like a Velodyne seen from above (-atan2(y, x) increasing, the direction
+    RotaryLidar_preprocessing.hpp:38 assumes)."""
     az = 2 * np.pi * np.arange(n_cols) / n_cols
+    if clockwise:
+        az = -az
     el = np.radians(elev_deg)
     A, E = np.meshgrid(az, el, indexing="ij")
     d = np.stack([np.cos(E) * np.cos(A), np.cos(E) * np.sin(A), np.sin(E)], axis=-1)
@@ -211,20 +215,40 @@ def scan_directions(n_cols: int, elev_deg: np.ndarray) -> np.ndarray:
 
 
 def make_scan(scene: Scene, pose: np.ndarray, seed: int, n_cols: int = 4096,
-              elev_deg: np.ndarray = VLP16_FIRING_DEG, range_noise: float = 0.01) -> np.ndarray:
-    """One revolution seen from world<-lidar `pose`; returns (N, 4) float32 lidar-frame x y z i."""
+              elev_deg: np.ndarray = VLP16_FIRING_DEG, range_noise: float = 0.01,
+              organized: bool = False, clockwise: bool = False) -> np.ndarray:
+    """One revolution seen from world<-lidar `pose`; returns (N, 4) float32 lidar-frame x y z i.
+    organized=True keeps one row per ray (NaN x y z for no return), as a driver's organized cloud."""
     rng = np.random.default_rng(seed)
-    dl = scan_directions(n_cols, np.asarray(elev_deg, dtype=np.float64))
+    dl = scan_directions(n_cols, np.asarray(elev_deg, dtype=np.float64), clockwise)
     R = quat_to_mat(pose[:4])
     dw = dl @ R.T
     r = raycast(scene, np.asarray(pose[4:]), dw)
     keep = np.isfinite(r)
     rr = r[keep] + rng.normal(0, range_noise, int(keep.sum()))
     pts = dl[keep] * rr[:, None]
+    if organized:
+        out = np.full((dl.shape[0], 4), np.nan, dtype=np.float32)
+        out[keep, :3] = pts
+        out[:, 3] = rng.random(dl.shape[0])
+        return out
     out = np.empty((pts.shape[0], 4), dtype=np.float32)
     out[:, :3] = pts
     out[:, 3] = rng.random(pts.shape[0])
     return out
+
+
+def to_pointcloud2(points: np.ndarray, point_step: int = 32) -> np.ndarray:
+    """sensor_msgs/PointCloud2 data bytes in the velodyne_pointcloud layout (x 0, y 4, z 8,
+    intensity 16, ring uint16 20, little endian); returns a uint8 array of n * point_step bytes."""
+    n = len(points)
+    buf = np.zeros((n, point_step), np.uint8)
+    f = np.ascontiguousarray(points[:, :4], dtype="<f4")
+    buf[:, 0:12] = f[:, :3].view(np.uint8).reshape(n, 12)
+    buf[:, 16:20] = f[:, 3:4].view(np.uint8).reshape(n, 4)
+    if point_step >= 22:
+        buf[:, 20:22] = (np.arange(n) % 16).astype("<u2").view(np.uint8).reshape(n, 2)
+    return buf.reshape(-1)
 
 
 # ----------------------------------------------------------------------------- maps

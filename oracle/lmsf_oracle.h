@@ -69,6 +69,11 @@ int lmsfo_map_knn(const lmsfo_map* m, const float* q, int64_t nq, int k, int32_t
 int lmsfo_brute_knn(const float* map_xyzi, int64_t n, const float* q, int64_t nq, int k,
                     int32_t* idx, float* d2);
 
+/* PointCloud2 decode + removeNaN + rotary relative time + distance filter (oracle/ingest.cpp);
+ * out holds up to n points.  Returns the number of points written. */
+int64_t lmsfo_ingest(const uint8_t* data, int64_t n, uint32_t step, int32_t ox, int32_t oy, int32_t oz, int32_t oi,
+                     float period, float near_t, float far_t, float* out);
+
 /* pcl::VoxelGrid centroid downsampling (oracle/voxel.cpp); out holds up to n points.
  * Returns the number of voxels written. */
 int64_t lmsfo_voxel_filter(const float* xyzi, int64_t n, float leaf, float* out);

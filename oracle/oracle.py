@@ -72,6 +72,9 @@ def lib():
         L.lmsfo_pose_plus.argtypes = [dp, dp, dp]
         L.lmsfo_set_num_threads.argtypes = [C.c_int]
         L.lmsfo_voxel_filter.restype = C.c_int64
+        L.lmsfo_ingest.restype = C.c_int64
+        L.lmsfo_ingest.argtypes = [C.c_void_p, C.c_int64, C.c_uint32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                   C.c_float, C.c_float, C.c_float, fp]
         L.lmsfo_voxel_filter.argtypes = [fp, C.c_int64, C.c_float, fp]
         _lib = L
     return _lib
@@ -82,6 +85,15 @@ def voxel_filter(points, leaf):
     p = _f32(points)
     out = np.zeros((max(len(p), 1), 4), np.float32)
     m = lib().lmsfo_voxel_filter(p, len(p), float(leaf), out)
+    return out[:m].copy()
+
+
+def ingest(data: np.ndarray, n: int, point_step=32, offsets=(0, 4, 8, 16), scan_period=0.1, distance_near=0.0,
+           distance_far=0.0):
+    """PointCloud2 bytes -> xyzi rows (oracle/ingest.cpp)."""
+    buf = np.ascontiguousarray(data, dtype=np.uint8)
+    out = np.zeros((max(n, 1), 4), np.float32)
+    m = lib().lmsfo_ingest(buf.ctypes.data, n, point_step, *offsets, scan_period, distance_near, distance_far, out)
     return out[:m].copy()
 
 

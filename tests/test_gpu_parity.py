@@ -374,6 +374,35 @@ def test_voxel_filter_bitexact(lib, oracle_mod, small_workload):
     assert ctx.voxel_filter(far, 0.01).tobytes() == far.tobytes()
 
 
+def test_ingest_pointcloud2_parity(lib, oracle_mod, small_workload):
+    """lmsf_ingest_pointcloud2 / lmsf_extract_pointcloud2 vs oracle/ingest.cpp: decode + removeNaN
+    and the distance filter bit-exact; rotary relative time (double atan2 rounded to float on both
+    sides) within 1e-6 s; the extracted features equal the oracle's extraction of the oracle's
+    ingest (points and order)."""
+    import torch
+    from lmsf import synth
+    wl = small_workload
+    ctx = _ctx(lib)
+    for seed in (21, 22):
+        org = synth.make_scan(wl.scene, wl.truth[0], seed, n_cols=4096, organized=True, clockwise=True)
+        msg = synth.to_pointcloud2(org)
+        for kw in (dict(scan_period=0.0), dict(), dict(scan_period=0.0, distance_near=3.0, distance_far=50.0),
+                   dict(distance_near=3.0, distance_far=50.0)):
+            g = ctx.ingest_pointcloud2(msg, len(org), **kw)
+            o = oracle_mod.ingest(msg, len(org), **kw)
+            assert g.shape == o.shape
+            assert g[:, :3].tobytes() == o[:, :3].tobytes()
+            assert np.abs(g[:, 3] - o[:, 3]).max() <= 1e-6
+        g = ctx.ingest_pointcloud2(torch.from_numpy(msg).to("cuda:0"), len(org))        # device message
+        assert g[:, :3].tobytes() == oracle_mod.ingest(msg, len(org))[:, :3].tobytes()
+        ne, ns = ctx.extract_pointcloud2(msg, len(org))
+        e, s, _, _ = oracle_mod.extract(oracle_mod.ingest(msg, len(org)))
+        ge, _ = ctx.copy_features(lib.EDGE)
+        gs, _ = ctx.copy_features(lib.SURF)
+        assert (ne, ns) == (len(e), len(s))
+        assert ge[:, :3].tobytes() == e[:, :3].tobytes() and gs[:, :3].tobytes() == s[:, :3].tobytes()
+
+
 def test_alignment_score_parity(lib, oracle_mod, small_workload):
     """lmsf_align_score vs oracle/align.py (AlignmentScore, REG/alignEvaluate.hpp:55-87): inlier
     count exact, mean inlier d2 rel 1e-12 (reduction order), thresholds of the reference's callers

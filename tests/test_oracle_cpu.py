@@ -319,3 +319,60 @@ def test_oracle_alignment_score_vs_scipy(oracle_mod, tiny):
         else:
             assert score == sys.float_info.max
     assert OA.alignment_score(wl.surf_map, s[:0], T, 0.1, 0.6) == (sys.float_info.max, 0.0)
+
+
+def _python_rotary(pts, period=0.1):
+    """Independent line-by-line restatement of RotaryLidarPreProcess::Process
+    (RotaryLidar_preprocessing.hpp:31-91) with float32 variables and double M_PI expressions."""
+    f32 = np.float32
+
+    def neg_atan2(y, x):
+        return f32(-math.atan2(float(y), float(x)))
+
+    start = neg_atan2(pts[0, 1], pts[0, 0])
+    end = f32(float(neg_atan2(pts[-1, 1], pts[-1, 0])) + 2 * math.pi)
+    if float(f32(end - start)) > 3 * math.pi:
+        end = f32(float(end) - 2 * math.pi)
+    elif float(f32(end - start)) < math.pi:
+        end = f32(float(end) + 2 * math.pi)
+    half = False
+    out = np.empty(len(pts), np.float32)
+    for i in range(len(pts)):
+        ori = neg_atan2(pts[i, 1], pts[i, 0])
+        if not half:
+            if float(ori) < float(start) - math.pi / 2:
+                ori = f32(float(ori) + 2 * math.pi)
+            elif float(ori) > float(start) + math.pi * 3 / 2:
+                ori = f32(float(ori) - 2 * math.pi)
+            if float(f32(ori - start)) > math.pi:
+                half = True
+        else:
+            ori = f32(float(ori) + 2 * math.pi)
+            if float(ori) < float(end) - math.pi * 3 / 2:
+                ori = f32(float(ori) + 2 * math.pi)
+            elif float(ori) > float(end) + math.pi / 2:
+                ori = f32(float(ori) - 2 * math.pi)
+        out[i] = f32(f32(f32(ori - start) / f32(end - start)) * f32(period))
+    return out
+
+
+def test_oracle_ingest_pointcloud2(oracle_mod, tiny):
+    """PointCloud2 decode + removeNaN + rotary relative time + distance filter (oracle/ingest.cpp)
+    vs numpy and a line-by-line Python restatement of RotaryLidar_preprocessing.hpp."""
+    from lmsf import synth
+    org = synth.make_scan(tiny.scene, tiny.truth[0], 11, n_cols=900, organized=True, clockwise=True)
+    valid = np.isfinite(org[:, :3]).all(1)
+    assert (~valid).any() and valid.sum() > 0.8 * len(org)
+    msg = synth.to_pointcloud2(org)
+    got = oracle_mod.ingest(msg, len(org), scan_period=0.0)                    # decode + removeNaN only
+    assert got.tobytes() == org[valid].tobytes()
+    rot = oracle_mod.ingest(msg, len(org))
+    np.testing.assert_array_equal(rot[:, :3], org[valid, :3])
+    assert rot[:, 3].tobytes() == _python_rotary(org[valid]).tobytes()
+    assert rot[0, 3] == 0.0 and 0.099 < rot[:, 3].max() <= 0.1001            # one revolution = one period
+    near, far = 5.0, 40.0
+    dist = oracle_mod.ingest(msg, len(org), scan_period=0.0, distance_near=near, distance_far=far)
+    v = org[valid]
+    d = np.sqrt((v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1] + v[:, 2] * v[:, 2]).astype(np.float32)).astype(np.float64)
+    assert dist.tobytes() == v[(d > near) & (d < far)].tobytes()
+    assert len(oracle_mod.ingest(msg[:0], 0)) == 0
