@@ -10,11 +10,12 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include "bbox.h"
 #include "lmsf_internal.h"
 
 namespace lmsf {
 
-__global__ void map_bbox_kernel(const float4* pts, int n, int* bbox) {
+__global__ void __launch_bounds__(256) map_bbox_kernel(const float4* pts, int n, int* bbox) {
     int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const float4 p = pts[i];
@@ -27,21 +28,7 @@ __global__ void map_bbox_kernel(const float4* pts, int n, int* bbox) {
             hi[d] = max(hi[d], v);
         }
     }
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            lo[d] = min(lo[d], __shfl_xor(lo[d], o, 64));
-            hi[d] = max(hi[d], __shfl_xor(hi[d], o, 64));
-        }
-    }
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            atomicMin(&bbox[d], lo[d]);
-            atomicMax(&bbox[3 + d], hi[d]);
-        }
-    }
+    block_bbox_commit<256>(lo, hi, bbox);
 }
 
 __global__ void map_count_kernel(const float4* pts, int n, int ox, int oy, int oz, int nx, int ny, int nz,
@@ -93,7 +80,7 @@ hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hi
 }
 
 hipError_t launch_map_bbox(const float4* pts, int n, int* bbox, hipStream_t s) {
-    const int blocks = min((n + 255) / 256, 1024);
+    const int blocks = min((n + 255) / 256, 512);
     hipLaunchKernelGGL(map_bbox_kernel, dim3(max(blocks, 1)), dim3(256), 0, s, pts, n, bbox);
     return hipGetLastError();
 }

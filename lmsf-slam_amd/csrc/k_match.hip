@@ -420,15 +420,19 @@ __global__ __launch_bounds__(256) void eval_at_kernel(BatchView bv, const double
     block_reduce_packet(P, bv.partials + (size_t)blockIdx.x * kPacket);
 }
 
-// Team size and XCD remap are tunables (LMSF_KNN_TEAM = 8 | 16 | 32, LMSF_XCD_REMAP = 0 | 1) for
-// A/B measurement; defaults are the measured best.
-static int knn_team() {
-    static int t = [] {
+// Team size and XCD remap are tunables (LMSF_KNN_TEAM = 1 | 2 | 4 | 8 | 16 | 32, LMSF_XCD_REMAP =
+// 0 | 1) for A/B measurement.  Default (measured, r01): one lane per query when a launch carries
+// >= 2^20 query slots (C2 batch of 64: 10.8k scans/s vs 7.1k at T = 8); 8 lanes per query for
+// single-scan tracking launches (63k queries: knn 234 -> 75 us on the 5M-point C4 map, 56 -> 27
+// us on the C3 local map), where one lane per query leaves most of the chip idle.
+static int knn_team(size_t query_slots) {
+    static int forced = [] {
         const char* e = getenv("LMSF_KNN_TEAM");
-        int v = e ? atoi(e) : 1;
-        return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 1;
+        int v = e ? atoi(e) : 0;
+        return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 0;
     }();
-    return t;
+    if (forced) return forced;
+    return query_slots >= ((size_t)1 << 20) ? 1 : 8;
 }
 static int knn_remap() {
     static int r = [] {
@@ -440,7 +444,7 @@ static int knn_remap() {
 
 hipError_t launch_knn(const GridView& edge, const GridView& surf, const BatchView& bv, int skip_converged,
                       hipStream_t s) {
-    const int T = knn_team(), remap = knn_remap();
+    const int T = knn_team((size_t)bv.feat_stride * bv.B), remap = knn_remap();
     const int gx = (bv.feat_stride + (256 / T) - 1) / (256 / T);
     const dim3 grid(gx * bv.B);
     if (T == 8)

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include "bbox.h"
 #include "lmsf_internal.h"
 
 namespace lmsf {
@@ -24,7 +25,7 @@ __device__ __forceinline__ int vox_coord(float v, float inv) {
     return (int)fminf(fmaxf(floorf(v * inv), -1073741824.f), 1073741824.f);
 }
 
-__global__ void voxel_bbox_kernel(const float4* pts, int n, float inv, int* bbox) {
+__global__ void __launch_bounds__(256) voxel_bbox_kernel(const float4* pts, int n, float inv, int* bbox) {
     int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const float4 p = pts[i];
@@ -35,21 +36,7 @@ __global__ void voxel_bbox_kernel(const float4* pts, int n, float inv, int* bbox
             hi[d] = max(hi[d], c[d]);
         }
     }
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            lo[d] = min(lo[d], __shfl_xor(lo[d], o, 64));
-            hi[d] = max(hi[d], __shfl_xor(hi[d], o, 64));
-        }
-    }
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            atomicMin(&bbox[d], lo[d]);
-            atomicMax(&bbox[3 + d], hi[d]);
-        }
-    }
+    block_bbox_commit<256>(lo, hi, bbox);
 }
 
 __global__ void voxel_key_kernel(const float4* pts, int n, float inv, const int* bbox, uint32_t dx, uint32_t dy,
@@ -137,7 +124,7 @@ hipError_t VoxelFilter::run(const float4* in, int n, float leaf, float4* out, in
     const int init[6] = {INT_MAX, INT_MAX, INT_MAX, INT_MIN, INT_MIN, INT_MIN};
     int hb[6];
     if ((e = hipMemcpyAsync(bbox, init, sizeof init, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(voxel_bbox_kernel, dim3(min(max((n + 255) / 256, 1), 1024)), dim3(256), 0, s, in, n, inv, bbox);
+    hipLaunchKernelGGL(voxel_bbox_kernel, dim3(min(max((n + 255) / 256, 1), 512)), dim3(256), 0, s, in, n, inv, bbox);
     if ((e = hipMemcpyAsync(hb, bbox, sizeof hb, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     const int64_t dx = (int64_t)hb[3] - hb[0] + 1, dy = (int64_t)hb[4] - hb[1] + 1, dz = (int64_t)hb[5] - hb[2] + 1;

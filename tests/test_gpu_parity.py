@@ -173,8 +173,10 @@ def test_solve_trace_parity_gn(lib, oracle_mod, small_workload):
 
 
 def test_batch_run_matches_oracle(lib, oracle_mod, small_workload):
+    """Batch path; max_batch 16 x 70k query slots >= 2^20 selects the one-lane-per-query knn team
+    (the single-scan tests above run the 8-lane team)."""
     wl = small_workload
-    ctx = _ctx(lib, schedule=1, max_iterations=5)
+    ctx = _ctx(lib, schedule=1, max_iterations=5, max_batch=16)
     ctx.set_map(lib.EDGE, wl.edge_map)
     ctx.set_map(lib.SURF, wl.surf_map)
     ctx.load_scans(wl.scans)
