@@ -56,7 +56,8 @@ struct lmsf_ctx {
     hipStream_t stream = nullptr;
     int B = 1, R = 0, F = 0, max_parts = 0, n_tiles = 0;
     int optimization_count = 10;
-    DevMap map[3];
+    DevMap map[3];                    // map of a kind (or its keyframe window when a prior is set)
+    DevMap prior[3];                  // static prior part of a kind's map (tracker shared map)
     bool map_set[3] = {false, false, false};
     // registration buffers
     float4* feat = nullptr;
@@ -189,8 +190,8 @@ struct lmsf_ctx {
 
 namespace {
 
-lmsf_status build_map(lmsf_ctx* c, int kind, const float* xyzi, size_t n) {
-    DevMap& m = c->map[kind];
+// Cell grid of one cloud into m; sorted points carry w = base + original index.
+lmsf_status build_grid(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, int base) {
     hipStream_t s = c->stream;
     if (n > (size_t)INT32_MAX) return c->fail(LMSF_ERR_CAPACITY, "map too large (%zu points)", n);
     if (n > m.cap) {
@@ -233,9 +234,17 @@ lmsf_status build_map(lmsf_ctx* c, int kind, const float* xyzi, size_t n) {
     HIPCHK(c, launch_map_count(m.orig, (int)n, m.ox, m.oy, m.oz, nx, ny, nz, m.cell, m.counts, s));
     size_t tb = m.scan_tmp_bytes;
     HIPCHK(c, exclusive_scan_u32(m.counts, m.off, cells + 1, m.scan_tmp, tb, s));
-    HIPCHK(c, launch_map_scatter(m.orig, (int)n, m.cell, m.off, m.fill, m.pts, s));
+    HIPCHK(c, launch_map_scatter(m.orig, (int)n, m.cell, m.off, m.fill, m.pts, base, s));
     HIPCHK(c, hipStreamSynchronize(s));
     m.n = (int)n;
+    return LMSF_OK;
+}
+
+// SetInputSource: the whole map of a kind (no prior part).
+lmsf_status build_map(lmsf_ctx* c, int kind, const float* xyzi, size_t n) {
+    c->prior[kind].n = 0;
+    lmsf_status rc = build_grid(c, c->map[kind], xyzi, n, 0);
+    if (rc) return rc;
     c->map_set[kind] = true;
     return LMSF_OK;
 }
@@ -262,12 +271,14 @@ lmsf_status sync_slot0_features(lmsf_ctx* c) {
 lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
     const BatchView bv = c->bview(nb);
     const GridView ge = c->map[LMSF_EDGE].view(), gs = c->map[LMSF_SURF].view();
+    const GridView ge2 = c->prior[LMSF_EDGE].view(), gs2 = c->prior[LMSF_SURF].view();
     hipStream_t s = c->stream;
     const bool gn = c->cfg.solver == LMSF_SOLVER_GN;
     for (int o = 0; o < iters; ++o) {
         const bool t = c->timing && c->ev_used + 2 <= 2 * kEventPairs;
         if (t) HIPCHK(c, hipEventRecord(c->ev[c->ev_used], s));
-        HIPCHK(c, launch_knn(ge, gs, bv, gn ? 1 : 0, s));
+        HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{},
+                             bv, gn ? 1 : 0, s));
         if (t) {
             HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 1], s));
             c->ev_used += 2;
@@ -346,9 +357,12 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (!c) return;
     hipSetDevice(c->cfg.device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    for (auto& m : c->map) {
-        hipFree(m.orig); hipFree(m.pts); hipFree(m.cell); hipFree(m.counts); hipFree(m.off); hipFree(m.fill);
-        hipFree(m.scan_tmp);
+    for (DevMap* ms : {c->map, c->prior}) {
+        for (int k = 0; k < 3; ++k) {
+            DevMap& m = ms[k];
+            hipFree(m.orig); hipFree(m.pts); hipFree(m.cell); hipFree(m.counts); hipFree(m.off); hipFree(m.fill);
+            hipFree(m.scan_tmp);
+        }
     }
     void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->rec, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
@@ -760,7 +774,9 @@ lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int3
     const BatchView bv = c->bview(1);
     HIPCHK(c, launch_state_init(bv, c->d_poses, c->stream));
     const GridView ge = c->map[LMSF_EDGE].view(), gs = c->map[LMSF_SURF].view();
-    HIPCHK(c, launch_knn(ge, gs, bv, 0, c->stream));
+    const GridView ge2 = c->prior[LMSF_EDGE].view(), gs2 = c->prior[LMSF_SURF].view();
+    HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{}, bv, 0,
+                         c->stream));
     HIPCHK(c, launch_fit_eval(ge, gs, bv, LMSF_SOLVER_CERES_LM, c->stream));
     if (nq && out) HIPCHK(c, hipMemcpyAsync(out, c->rec, nq * sizeof(lmsf_record), hipMemcpyDeviceToHost, c->stream));
     std::vector<float4> pts(nn ? nq * 5 : 0);
@@ -842,9 +858,26 @@ bool ctx_features_on_device(const lmsf_ctx* c) { return c->features_on_device; }
 lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg) { return c->fail(code, "%s", msg); }
 
 // SetInputSource from device-resident points (local-map rebuild without a host round trip).
-lmsf_status ctx_set_map_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n) {
-    if (n == 0) return LMSF_OK;
-    return build_map(c, kind, reinterpret_cast<const float*>(d_pts), n);
+lmsf_status ctx_set_prior_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n) {
+    if (n == 0) {
+        c->prior[kind].n = 0;
+    } else {
+        lmsf_status rc = build_grid(c, c->prior[kind], reinterpret_cast<const float*>(d_pts), n, 0);
+        if (rc) return rc;
+    }
+    c->map_set[kind] = c->prior[kind].n > 0 || c->map[kind].n > 0;
+    return LMSF_OK;
+}
+
+lmsf_status ctx_set_window_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n) {
+    if (n == 0) {
+        c->map[kind].n = 0;
+    } else {
+        lmsf_status rc = build_grid(c, c->map[kind], reinterpret_cast<const float*>(d_pts), n, c->prior[kind].n);
+        if (rc) return rc;
+    }
+    c->map_set[kind] = c->prior[kind].n > 0 || c->map[kind].n > 0;
+    return LMSF_OK;
 }
 
 // Current slot-0 features on the device (after SetInputTarget / extraction): edges then surfs.

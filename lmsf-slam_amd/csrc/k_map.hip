@@ -47,13 +47,13 @@ __global__ void map_count_kernel(const float4* pts, int n, int ox, int oy, int o
 // Scatter into cell order.  Order inside a cell is arbitrary: the search ranks candidates by the
 // total order (d2, original index), so results do not depend on it.
 __global__ void map_scatter_kernel(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
-                                   float4* sorted) {
+                                   float4* sorted, int base) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int c = cell[i];
     const uint32_t pos = off[c] + atomicAdd(&fill[c], 1u);
     const float4 p = pts[i];
-    sorted[pos] = make_float4(p.x, p.y, p.z, __int_as_float(i));
+    sorted[pos] = make_float4(p.x, p.y, p.z, __int_as_float(base + i));
 }
 
 // pcl::transformPointCloud with an Eigen::Matrix4d (PCL 1.7 transforms.hpp): per point
@@ -93,8 +93,9 @@ hipError_t launch_map_count(const float4* pts, int n, int ox, int oy, int oz, in
 }
 
 hipError_t launch_map_scatter(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
-                              float4* sorted, hipStream_t s) {
-    hipLaunchKernelGGL(map_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pts, n, cell, off, fill, sorted);
+                              float4* sorted, int base, hipStream_t s) {
+    hipLaunchKernelGGL(map_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pts, n, cell, off, fill, sorted,
+                       base);
     return hipGetLastError();
 }
 

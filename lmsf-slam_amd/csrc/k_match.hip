@@ -31,21 +31,6 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// sorted insertion of (key, position) into a lane's ascending top-5
-__device__ __forceinline__ void insert5(uint64_t key, int pos, uint64_t (&k)[5], int (&p)[5]) {
-    if (key < k[4]) {
-        k[4] = key;
-        p[4] = pos;
-#pragma unroll
-        for (int i = 4; i >= 1; --i) {
-            if (k[i] < k[i - 1]) {
-                uint64_t t = k[i - 1]; k[i - 1] = k[i]; k[i] = t;
-                int u = p[i - 1]; p[i - 1] = p[i]; p[i] = u;
-            }
-        }
-    }
-}
-
 // World-frame query of a lidar-frame feature: double transform rounded to float
 // (pointAssociateToMap, ceres_...:235-244).
 __device__ __forceinline__ float3 associate(const Pose& P, float4 p) {
@@ -74,10 +59,15 @@ __device__ __forceinline__ void block_coords(int remap, int gx, int& x, int& b) 
 // x-rows (each row = 3 consecutive cells = one contiguous range of the cell-sorted points); the
 // team strides over the flattened candidate list with coalesced float4 loads, keeps a per-lane
 // sorted top-5 of (d2 bits, map index) keys with d2 < 1 (plus each key's position in the sorted
-// array), then merges the lanes' lists.  Output: sorted-array positions of the 5 neighbours.
-template <int T>
-__global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, BatchView bv, int skip_converged,
-                                                  int gx, int remap) {
+// array), then merges the lanes' lists.  Output: the 5 neighbour points (w = map index).
+// TWO: the map of a kind is split into a static grid (a shared prior map, indices [0, P)) and a
+// dynamic grid (the keyframe window, indices P + j): 18 rows, positions tagged with the grid bit.
+// Keys carry global indices, so the result equals the search of the concatenation [prior | window].
+template <int T, bool TWO>
+__global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, GridView ge2, GridView gs2, BatchView bv,
+                                                  int skip_converged, int gx, int remap) {
+    constexpr int NR = TWO ? 18 : 9;
+    constexpr uint32_t kGridBit = 0x80000000u;
     __shared__ unsigned long long blk_n27;
     __shared__ unsigned int blk_q;
     int bx, b;
@@ -91,66 +81,87 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Batc
     if (active) {
         const bool is_edge = q < ne;
         const GridView& g = is_edge ? ge : gs;
+        const GridView& g2 = is_edge ? ge2 : gs2;
         const Pose P = load_pose(bv.st[b].x);
         const float4 p = bv.feat[(size_t)b * bv.feat_stride + q];
         const float3 w = associate(P, p);
         const float fx = floorf(w.x), fy = floorf(w.y), fz = floorf(w.z);
-        const bool inside = g.n > 0 && fx >= (float)(g.ox - 2) && fx <= (float)(g.ox + g.nx + 1) &&
-                            fy >= (float)(g.oy - 2) && fy <= (float)(g.oy + g.ny + 1) &&
-                            fz >= (float)(g.oz - 2) && fz <= (float)(g.oz + g.nz + 1);
-        // rows: lane l resolves (dy, dz) rows l, l + T, ... of the 9
-        constexpr int REPS = (9 + T - 1) / T;
+        // rows: lane l resolves (grid, dy, dz) rows l, l + T, ... of the NR
+        constexpr int REPS = (NR + T - 1) / T;
         int rs_[REPS], rl_[REPS];
 #pragma unroll
         for (int rep = 0; rep < REPS; ++rep) {
             rs_[rep] = 0;
             rl_[rep] = 0;
             const int rr = lane + rep * T;
-            if (inside && rr < 9) {
-                const int cx = (int)fx - g.ox, cy = (int)fy - g.oy + (rr % 3) - 1, cz = (int)fz - g.oz + (rr / 3) - 1;
-                const int xa = max(cx - 1, 0), xb = min(cx + 1, g.nx - 1);
-                if (cy >= 0 && cy < g.ny && cz >= 0 && cz < g.nz && xa <= xb) {
-                    const size_t row = ((size_t)cz * g.ny + cy) * g.nx;
-                    rs_[rep] = (int)g.off[row + xa];
-                    rl_[rep] = (int)g.off[row + xb + 1] - rs_[rep];
+            if (rr < NR) {
+                const GridView& gg = (TWO && rr >= 9) ? g2 : g;
+                const int r9 = rr % 9;
+                const bool inside = gg.n > 0 && fx >= (float)(gg.ox - 2) && fx <= (float)(gg.ox + gg.nx + 1) &&
+                                    fy >= (float)(gg.oy - 2) && fy <= (float)(gg.oy + gg.ny + 1) &&
+                                    fz >= (float)(gg.oz - 2) && fz <= (float)(gg.oz + gg.nz + 1);
+                if (inside) {
+                    const int cx = (int)fx - gg.ox, cy = (int)fy - gg.oy + (r9 % 3) - 1, cz = (int)fz - gg.oz + (r9 / 3) - 1;
+                    const int xa = max(cx - 1, 0), xb = min(cx + 1, gg.nx - 1);
+                    if (cy >= 0 && cy < gg.ny && cz >= 0 && cz < gg.nz && xa <= xb) {
+                        const size_t row = ((size_t)cz * gg.ny + cy) * gg.nx;
+                        rs_[rep] = (int)gg.off[row + xa];
+                        rl_[rep] = (int)gg.off[row + xb + 1] - rs_[rep];
+                    }
                 }
             }
         }
-        int st[9], pre[10];
+        int st[NR], pre[NR + 1];
         pre[0] = 0;
 #pragma unroll
-        for (int r = 0; r < 9; ++r) {
+        for (int r = 0; r < NR; ++r) {
             st[r] = T == 1 ? rs_[r] : __shfl(rs_[r / T], r % T, T);
             pre[r + 1] = pre[r] + (T == 1 ? rl_[r] : __shfl(rl_[r / T], r % T, T));
         }
-        const int total = pre[9];
+        const int total = pre[NR];
         uint64_t k[5] = {kSentinel, kSentinel, kSentinel, kSentinel, kSentinel};
-        int kp[5] = {0, 0, 0, 0, 0};   // sorted-array position of each kept key
+        uint32_t kp[5] = {0, 0, 0, 0, 0};   // grid bit | sorted-array position of each kept key
         // current row r: candidates [rpre, rend) map to pts[rbase + (v - rpre)]
         int r = 0, rpre = 0, rend = pre[1], rbase = st[0];
+        const float4* rpts = g.pts;
+        uint32_t rtag = 0;
         for (int v = lane; v < total; v += T) {
             while (v >= rend) {
                 ++r;
                 rpre = rend;
-                int e = pre[9], s0 = st[8];
+                int e = pre[NR], s0 = st[NR - 1];
 #pragma unroll
-                for (int j = 8; j >= 1; --j) {   // static-index selects keep pre[]/st[] in registers
+                for (int j = NR - 1; j >= 1; --j) {   // static-index selects keep pre[]/st[] in registers
                     e = (r + 1 == j) ? pre[j] : e;
                     s0 = (r == j - 1) ? st[j - 1] : s0;
                 }
                 rend = e;
                 rbase = s0;
+                if (TWO && r == 9) {
+                    rpts = g2.pts;
+                    rtag = kGridBit;
+                }
             }
             const int pos = rbase + (v - rpre);
-            const float4 m = g.pts[pos];
+            const float4 m = rpts[pos];
             const float dx = w.x - m.x, dy = w.y - m.y, dz = w.z - m.z;
             const float d2 = dx * dx + dy * dy + dz * dz;
             const uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)__float_as_int(m.w);
-            insert5(key, pos, k, kp);
+            if (key < k[4]) {
+                k[4] = key;
+                kp[4] = (uint32_t)pos | rtag;
+#pragma unroll
+                for (int i = 4; i >= 1; --i) {
+                    if (k[i] < k[i - 1]) {
+                        uint64_t t = k[i - 1]; k[i - 1] = k[i]; k[i] = t;
+                        uint32_t u = kp[i - 1]; kp[i - 1] = kp[i]; kp[i] = u;
+                    }
+                }
+            }
         }
         // merge: five rounds of team-min; the owning lane pops its head and donates its position
         uint64_t res[5];
-        int rpos[5];
+        uint32_t rpos[5];
         const int tbase = (threadIdx.x & 63) & ~(T - 1);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
@@ -163,7 +174,7 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Batc
             const unsigned long long own = __ballot(k[0] == mn);
             const int owner = __ffsll((long long)((own >> tbase) & ((T == 64) ? ~0ull : ((1ull << T) - 1)))) - 1;
             res[i] = mn;
-            rpos[i] = __shfl(kp[0], owner < 0 ? 0 : owner, T);
+            rpos[i] = (uint32_t)__shfl((int)kp[0], owner < 0 ? 0 : owner, T);
             if (k[0] == mn) {
                 k[0] = k[1]; k[1] = k[2]; k[2] = k[3]; k[3] = k[4]; k[4] = kSentinel;
                 kp[0] = kp[1]; kp[1] = kp[2]; kp[2] = kp[3]; kp[3] = kp[4];
@@ -173,9 +184,16 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Batc
         // neighbour point itself (just touched, L1/L2 resident), so the fit reads 80 contiguous bytes
         float4* nn_out = bv.nnp + ((size_t)b * bv.feat_stride + q) * 5;
 #pragma unroll
-        for (int i = 0; i < 5; ++i)
-            if (i % T == lane)
-                nn_out[i] = res[i] < kSentinel ? g.pts[rpos[i]] : make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+        for (int i = 0; i < 5; ++i) {
+            if (i % T == lane) {
+                float4 o = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+                if (res[i] < kSentinel) {
+                    const float4* src = (TWO && (rpos[i] & kGridBit)) ? g2.pts : g.pts;
+                    o = src[rpos[i] & ~kGridBit];
+                }
+                nn_out[i] = o;
+            }
+        }
         if (lane == 0 && bv.n27) {
             atomicAdd(&blk_n27, (unsigned long long)total);
             atomicAdd(&blk_q, 1u);
@@ -442,23 +460,32 @@ static int knn_remap() {
     return r;
 }
 
-hipError_t launch_knn(const GridView& edge, const GridView& surf, const BatchView& bv, int skip_converged,
-                      hipStream_t s) {
+template <bool TWO>
+static void launch_knn_t(int T, dim3 grid, const GridView& edge, const GridView& surf, const GridView& edge2,
+                         const GridView& surf2, const BatchView& bv, int skip_converged, int gx, int remap,
+                         hipStream_t s) {
+#define LMSF_KNN(TT) hipLaunchKernelGGL((knn_kernel<TT, TWO>), grid, dim3(256), 0, s, edge, surf, edge2, surf2, bv, \
+                                        skip_converged, gx, remap)
+    switch (T) {
+        case 1: LMSF_KNN(1); break;
+        case 2: LMSF_KNN(2); break;
+        case 4: LMSF_KNN(4); break;
+        case 8: LMSF_KNN(8); break;
+        case 32: LMSF_KNN(32); break;
+        default: LMSF_KNN(16); break;
+    }
+#undef LMSF_KNN
+}
+
+hipError_t launch_knn(const GridView& edge, const GridView& surf, const GridView& edge2, const GridView& surf2,
+                      const BatchView& bv, int skip_converged, hipStream_t s) {
     const int T = knn_team((size_t)bv.feat_stride * bv.B), remap = knn_remap();
     const int gx = (bv.feat_stride + (256 / T) - 1) / (256 / T);
     const dim3 grid(gx * bv.B);
-    if (T == 8)
-        hipLaunchKernelGGL(knn_kernel<8>, grid, dim3(256), 0, s, edge, surf, bv, skip_converged, gx, remap);
-    else if (T == 1)
-        hipLaunchKernelGGL(knn_kernel<1>, grid, dim3(256), 0, s, edge, surf, bv, skip_converged, gx, remap);
-    else if (T == 2)
-        hipLaunchKernelGGL(knn_kernel<2>, grid, dim3(256), 0, s, edge, surf, bv, skip_converged, gx, remap);
-    else if (T == 4)
-        hipLaunchKernelGGL(knn_kernel<4>, grid, dim3(256), 0, s, edge, surf, bv, skip_converged, gx, remap);
-    else if (T == 32)
-        hipLaunchKernelGGL(knn_kernel<32>, grid, dim3(256), 0, s, edge, surf, bv, skip_converged, gx, remap);
+    if (edge2.n > 0 || surf2.n > 0)
+        launch_knn_t<true>(T, grid, edge, surf, edge2, surf2, bv, skip_converged, gx, remap, s);
     else
-        hipLaunchKernelGGL(knn_kernel<16>, grid, dim3(256), 0, s, edge, surf, bv, skip_converged, gx, remap);
+        launch_knn_t<false>(T, grid, edge, surf, edge2, surf2, bv, skip_converged, gx, remap, s);
     return hipGetLastError();
 }
 

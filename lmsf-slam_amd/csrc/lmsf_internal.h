@@ -68,12 +68,15 @@ struct BatchView {
 hipError_t launch_map_bbox(const float4* pts, int n, int* bbox, hipStream_t s);
 hipError_t launch_map_count(const float4* pts, int n, int ox, int oy, int oz, int nx, int ny, int nz,
                             int* cell, uint32_t* counts, hipStream_t s);
+// sorted[] w = base + original index (base > 0 for a keyframe window behind a prior map)
 hipError_t launch_map_scatter(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
-                              float4* sorted, hipStream_t s);
+                              float4* sorted, int base, hipStream_t s);
 hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, void* tmp, size_t& tmp_bytes, hipStream_t s);
 
-hipError_t launch_knn(const GridView& edge, const GridView& surf, const BatchView& bv, int skip_converged,
-                      hipStream_t s);
+// edge2 / surf2: optional second grid per kind (n = 0: none), searched as if concatenated after
+// the first (its points carry global indices).
+hipError_t launch_knn(const GridView& edge, const GridView& surf, const GridView& edge2, const GridView& surf2,
+                      const BatchView& bv, int skip_converged, hipStream_t s);
 hipError_t launch_fit_eval(const GridView& edge, const GridView& surf, const BatchView& bv, int solver,
                            hipStream_t s);
 hipError_t launch_lm_begin(const BatchView& bv, hipStream_t s);
@@ -162,7 +165,10 @@ int ctx_device(const lmsf_ctx* c);
 int ctx_feature_capacity(const lmsf_ctx* c);
 bool ctx_features_on_device(const lmsf_ctx* c);
 lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg);
-lmsf_status ctx_set_map_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n);
+// map of a kind = [prior | window]: the prior grid is built once (static), the window grid at every
+// keyframe commit with indices offset by the prior size; n == 0 clears that part.
+lmsf_status ctx_set_prior_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n);
+lmsf_status ctx_set_window_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n);
 lmsf_status ctx_slot0_features(lmsf_ctx* c, const float4** d_feat, int64_t* ne, int64_t* ns);
 
 }  // namespace lmsf

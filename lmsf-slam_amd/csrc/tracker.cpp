@@ -111,8 +111,9 @@ void R_from_quat(const double* q, double* R) {
     R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
 }
 
-// One feature kind's local map: [prior | keyframe W-ring oldest -> newest] in one device buffer
-// that the context's neighbour index is built from.
+// One feature kind's local map: [prior | keyframe W-ring oldest -> newest].  The context keeps two
+// neighbour grids per kind: the prior's (built once) and the downsampled window's (rebuilt at each
+// commit, indices offset by the prior size), searched together as one map.
 struct Window {
     std::vector<float4*> slots;
     std::vector<int> sizes;
@@ -120,9 +121,10 @@ struct Window {
     float4* prior = nullptr;
     size_t prior_n = 0;
     float4* wcat = nullptr;        // keyframes concatenated (input of the voxel filter)
-    float4* concat = nullptr;      // [prior | downsampled window] = the registration map
+    float4* concat = nullptr;      // the downsampled window (its own device grid, behind the prior's)
     size_t concat_cap = 0;
-    size_t total = 0;
+    size_t window_n = 0;
+    size_t total = 0;              // prior_n + window_n = GetLocalMap size
     double leaf = 0.0;
     bool dirty = false;
 };
@@ -188,9 +190,7 @@ lmsf_status commit(lmsf_tracker* t) {
         Window& w = t->win[kind];
         if (!w.dirty) continue;
         const int W = (int)w.slots.size();
-        if (w.prior_n)
-            TCHK(t, hipMemcpyAsync(w.concat, w.prior, w.prior_n * sizeof(float4), hipMemcpyDeviceToDevice, s));
-        float4* dst = w.leaf > 0 ? w.wcat : w.concat + w.prior_n;
+        float4* dst = w.leaf > 0 ? w.wcat : w.concat;
         size_t nw = 0;
         for (int i = 0; i < w.count; ++i) {
             const int k = (w.head + i) % W;
@@ -200,13 +200,14 @@ lmsf_status commit(lmsf_tracker* t) {
         }
         if (w.leaf > 0 && nw) {                                   // VoxelGrid of the window
             int nv = 0;
-            TCHK(t, t->voxel.run(w.wcat, (int)nw, (float)w.leaf, w.concat + w.prior_n, &nv, s));
+            TCHK(t, t->voxel.run(w.wcat, (int)nw, (float)w.leaf, w.concat, &nv, s));
             nw = (size_t)nv;
         }
-        const size_t off = w.prior_n + nw;
-        w.total = off;
+        w.window_n = nw;
+        w.total = w.prior_n + nw;
         w.dirty = false;
-        lmsf_status rc = ctx_set_map_device(t->ctx, kind, w.concat, off);
+        // only the window's grid is rebuilt; the prior's grid was built once (set_prior_map)
+        lmsf_status rc = ctx_set_window_device(t->ctx, kind, w.concat, nw);
         if (rc) return rc;
     }
     return LMSF_OK;
@@ -398,14 +399,6 @@ lmsf_status lmsf_tracker_set_prior_map(lmsf_tracker* t, int32_t kind, const floa
     Window& w = t->win[kind];
     hipStream_t s = ctx_stream(t->ctx);
     TCHK(t, hipStreamSynchronize(s));
-    const size_t need = n + (size_t)t->cap * w.slots.size();
-    if (need > w.concat_cap) {
-        TCHK(t, hipFree(w.concat));
-        w.concat = nullptr;
-        w.concat_cap = 0;
-        TCHK(t, hipMalloc((void**)&w.concat, need * sizeof(float4)));
-        w.concat_cap = need;
-    }
     TCHK(t, hipFree(w.prior));
     w.prior = nullptr;
     w.prior_n = 0;
@@ -414,7 +407,9 @@ lmsf_status lmsf_tracker_set_prior_map(lmsf_tracker* t, int32_t kind, const floa
         TCHK(t, hipMemcpyAsync(w.prior, xyzi, n * sizeof(float4), hipMemcpyDefault, s));
         w.prior_n = n;
     }
-    w.dirty = true;
+    lmsf_status rc = ctx_set_prior_device(t->ctx, kind, w.prior, n);   // static grid, built once
+    if (rc) return rc;
+    w.dirty = true;                 // window indices move behind the new prior
     return commit(t);
 }
 
@@ -484,7 +479,9 @@ lmsf_status lmsf_tracker_local_map(lmsf_tracker* t, int32_t kind, float* out, si
     if (w.total > cap) return fail(t, LMSF_ERR_CAPACITY, "output capacity smaller than the local map");
     if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
     hipStream_t s = ctx_stream(t->ctx);
-    TCHK(t, hipMemcpyAsync(out, w.concat, w.total * sizeof(float4), hipMemcpyDeviceToHost, s));
+    if (w.prior_n) TCHK(t, hipMemcpyAsync(out, w.prior, w.prior_n * sizeof(float4), hipMemcpyDefault, s));
+    if (w.window_n)
+        TCHK(t, hipMemcpyAsync(out + 4 * w.prior_n, w.concat, w.window_n * sizeof(float4), hipMemcpyDefault, s));
     TCHK(t, hipStreamSynchronize(s));
     return LMSF_OK;
 }
