@@ -173,14 +173,17 @@ def test_solve_trace_parity_gn(lib, oracle_mod, small_workload):
 
 
 def test_batch_run_matches_oracle(lib, oracle_mod, small_workload):
-    """Batch path; max_batch 16 x 70k query slots >= 2^20 selects the one-lane-per-query knn team
-    (the single-scan tests above run the 8-lane team)."""
+    """Batch path with 16 slots: 16 x 70k query slots >= 2^20 selects the one-lane-per-query knn
+    team and 16 scans x 16 rings the bitonic sector sort (the single-scan tests above run the
+    8-lane team and the rank sort)."""
     wl = small_workload
     ctx = _ctx(lib, schedule=1, max_iterations=5, max_batch=16)
     ctx.set_map(lib.EDGE, wl.edge_map)
     ctx.set_map(lib.SURF, wl.surf_map)
-    ctx.load_scans(wl.scans)
-    poses, stats = ctx.batch_run(wl.guess)
+    n = len(wl.scans)
+    ctx.load_scans([wl.scans[i % n] for i in range(16)])
+    poses, stats = ctx.batch_run(np.stack([wl.guess[i % n] for i in range(16)]))
+    np.testing.assert_array_equal(poses[n:2 * n], poses[:n])          # same scan + guess -> same pose
     for i in range(len(wl.scans)):
         e, s = _features(oracle_mod, wl.scans[i])
         ge, _ = ctx.copy_features(lib.EDGE, slot=i)
