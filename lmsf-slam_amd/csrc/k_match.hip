@@ -22,6 +22,10 @@ namespace lmsf {
 namespace {
 
 constexpr uint64_t kSentinel = (uint64_t)0x3f800000u << 32;  // key of d2 == 1.0f, idx 0
+#ifndef LMSF_KNN_UNROLL
+#define LMSF_KNN_UNROLL 4
+#endif
+constexpr int kKnnUnroll = LMSF_KNN_UNROLL;   // candidate loads in flight per lane (T = 1 path): 4 measured best (r01: 0.485 ms vs 0.522 at 1, 0.572 at 8 -- 87 VGPRs)
 
 template <int T>
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
@@ -121,35 +125,13 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
         const int total = pre[NR];
         uint64_t k[5] = {kSentinel, kSentinel, kSentinel, kSentinel, kSentinel};
         uint32_t kp[5] = {0, 0, 0, 0, 0};   // grid bit | sorted-array position of each kept key
-        // current row r: candidates [rpre, rend) map to pts[rbase + (v - rpre)]
-        int r = 0, rpre = 0, rend = pre[1], rbase = st[0];
-        const float4* rpts = g.pts;
-        uint32_t rtag = 0;
-        for (int v = lane; v < total; v += T) {
-            while (v >= rend) {
-                ++r;
-                rpre = rend;
-                int e = pre[NR], s0 = st[NR - 1];
-#pragma unroll
-                for (int j = NR - 1; j >= 1; --j) {   // static-index selects keep pre[]/st[] in registers
-                    e = (r + 1 == j) ? pre[j] : e;
-                    s0 = (r == j - 1) ? st[j - 1] : s0;
-                }
-                rend = e;
-                rbase = s0;
-                if (TWO && r == 9) {
-                    rpts = g2.pts;
-                    rtag = kGridBit;
-                }
-            }
-            const int pos = rbase + (v - rpre);
-            const float4 m = rpts[pos];
+        auto consider = [&](const float4 m, uint32_t tagged_pos) {
             const float dx = w.x - m.x, dy = w.y - m.y, dz = w.z - m.z;
             const float d2 = dx * dx + dy * dy + dz * dz;
             const uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)__float_as_int(m.w);
             if (key < k[4]) {
                 k[4] = key;
-                kp[4] = (uint32_t)pos | rtag;
+                kp[4] = tagged_pos;
 #pragma unroll
                 for (int i = 4; i >= 1; --i) {
                     if (k[i] < k[i - 1]) {
@@ -157,6 +139,51 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
                         uint32_t u = kp[i - 1]; kp[i - 1] = kp[i]; kp[i] = u;
                     }
                 }
+            }
+        };
+        if constexpr (T == 1) {
+            // one lane walks its rows; kKnnUnroll loads in flight per step (a row is contiguous: 8 points per
+            // 128-B line), so the lane waits once per kKnnUnroll candidates instead of once per candidate.
+            // Keys are unique (global index), so the kept top-5 does not depend on the visit order.
+#pragma unroll
+            for (int rr = 0; rr < NR; ++rr) {
+                const float4* rp = (TWO && rr >= 9) ? g2.pts : g.pts;
+                const uint32_t tag = (TWO && rr >= 9) ? kGridBit : 0u;
+                const int a = st[rr], len = pre[rr + 1] - pre[rr];
+                int c = 0;
+                for (; c + kKnnUnroll <= len; c += kKnnUnroll) {
+                    float4 m[kKnnUnroll];
+#pragma unroll
+                    for (int u = 0; u < kKnnUnroll; ++u) m[u] = rp[a + c + u];
+#pragma unroll
+                    for (int u = 0; u < kKnnUnroll; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
+                }
+                for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
+            }
+        } else {
+            // current row r: candidates [rpre, rend) map to pts[rbase + (v - rpre)]
+            int r = 0, rpre = 0, rend = pre[1], rbase = st[0];
+            const float4* rpts = g.pts;
+            uint32_t rtag = 0;
+            for (int v = lane; v < total; v += T) {
+                while (v >= rend) {
+                    ++r;
+                    rpre = rend;
+                    int e = pre[NR], s0 = st[NR - 1];
+#pragma unroll
+                    for (int j = NR - 1; j >= 1; --j) {   // static-index selects keep pre[]/st[] in registers
+                        e = (r + 1 == j) ? pre[j] : e;
+                        s0 = (r == j - 1) ? st[j - 1] : s0;
+                    }
+                    rend = e;
+                    rbase = s0;
+                    if (TWO && r == 9) {
+                        rpts = g2.pts;
+                        rtag = kGridBit;
+                    }
+                }
+                const int pos = rbase + (v - rpre);
+                consider(rpts[pos], (uint32_t)pos | rtag);
             }
         }
         // merge: five rounds of team-min; the owning lane pops its head and donates its position
