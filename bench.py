@@ -33,7 +33,8 @@ sys.path.insert(0, os.path.join(REPO, "lmsf-slam_amd"))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 DEFAULTS = {   # per configuration: batch (scans per launch), map points, columns, steps, warmup
-    "C2": dict(batch=64, map_points=1_000_000, cols=4096, steps=10, warmup=2),
+    # C2 defaults follow SURVEY 8(d) "Scans/s": 1,000+ scans (16 x 64) after ~50 warm-up scans (one step)
+    "C2": dict(batch=64, map_points=1_000_000, cols=4096, steps=16, warmup=1),
     "C3": dict(batch=1, map_points=0, cols=4096, steps=20, warmup=3),
     "C4": dict(batch=1, map_points=5_000_000, cols=4096, steps=20, warmup=3),
     "C5": dict(batch=125, map_points=10_000_000, cols=2048, steps=2, warmup=1),
