@@ -254,6 +254,23 @@ def run_batch(args, d):
                          f"{args.outer} outer iterations, kd-tree 5-NN, Ceres-LM restatement; kd-tree build "
                          f"excluded), {cpu_el:.1f} s on 1 thread of {os.cpu_count()} host cores"}
         pose_dv = {"scans": n_done, "max_m": worst_t, "max_rad": worst_r}
+        # the same restatement with OpenMP over queries on the host cores this job
+        # may use (the GPU box grants 16 per GPU), reported beside the single-thread baseline
+        nt = max(1, min(16, os.cpu_count() or 1))
+        oracle.set_threads(nt)
+        m_done = 0
+        t2 = time.perf_counter()
+        while m_done < n_units and (m_done == 0 or time.perf_counter() - t2 < args.cpu_seconds / 3):
+            e, s, _, _ = oracle.extract(scans_u[unit_scan[m_done]], **c["extract"])
+            reg.set_scan(1, e)
+            reg.set_scan(2, s)
+            reg.solve(guesses[m_done])
+            m_done += 1
+        mt_el = time.perf_counter() - t2
+        oracle.set_threads(1)
+        cpu["multi_thread"] = {"value": round(m_done / mt_el, 3), "cores": nt,
+                               "sample": f"{m_done} {'scans' if cfg == 'C2' else 'pairs'}, {mt_el:.1f} s, OpenMP "
+                                         f"over queries"}
     if rank == 0:
         npts = int(np.mean([len(s) for s in scans_u]))
         if cfg == "C2":
