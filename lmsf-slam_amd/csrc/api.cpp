@@ -65,7 +65,9 @@ struct lmsf_ctx {
     int* n_edge = nullptr;
     int* n_surf = nullptr;
     float4* nnp = nullptr;
-    lmsf_record* rec = nullptr;
+    float4* rec_p = nullptr;          // records: point + kind / values / edge tail (BatchView)
+    RecV* rec_v = nullptr;
+    double2* rec_e = nullptr;
     double* partials = nullptr;
     double* partials_gn = nullptr;
     double* gn_rows = nullptr;
@@ -135,7 +137,9 @@ struct lmsf_ctx {
         v.n_surf = n_surf;
         v.nnp = nnp;
         v.fit_per_thread = fit_per_thread_default();
-        v.rec = rec;
+        v.rec_p = rec_p;
+        v.rec_v = rec_v;
+        v.rec_e = rec_e;
         v.partials = partials;
         v.max_parts = max_parts;
         v.st = st;
@@ -364,7 +368,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
             hipFree(m.scan_tmp);
         }
     }
-    void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->rec, c->partials, c->partials_gn,
+    void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->edge_stage,
                     c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->d_error};
@@ -419,7 +423,9 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->n_edge, B));
     CHK(dalloc(&c->n_surf, B));
     CHK(dalloc(&c->nnp, B * F * 5));
-    CHK(dalloc(&c->rec, B * F));
+    CHK(dalloc(&c->rec_p, B * F));
+    CHK(dalloc(&c->rec_v, B * F));
+    CHK(dalloc(&c->rec_e, B * F));
     CHK(dalloc(&c->partials, B * c->max_parts * kPacket));
     CHK(dalloc(&c->st, B));
     CHK(dalloc(&c->d_poses, B * 7));
@@ -778,10 +784,27 @@ lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int3
     HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{}, bv, 0,
                          c->stream));
     HIPCHK(c, launch_fit_eval(ge, gs, bv, LMSF_SOLVER_CERES_LM, c->stream));
-    if (nq && out) HIPCHK(c, hipMemcpyAsync(out, c->rec, nq * sizeof(lmsf_record), hipMemcpyDeviceToHost, c->stream));
+    std::vector<float4> rp(out ? nq : 0);
+    std::vector<RecV> rv(out ? nq : 0);
+    std::vector<double2> re(out ? nq : 0);
+    if (nq && out) {
+        HIPCHK(c, hipMemcpyAsync(rp.data(), c->rec_p, nq * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(rv.data(), c->rec_v, nq * sizeof(RecV), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(re.data(), c->rec_e, nq * sizeof(double2), hipMemcpyDeviceToHost, c->stream));
+    }
     std::vector<float4> pts(nn ? nq * 5 : 0);
     if (nq && nn) HIPCHK(c, hipMemcpyAsync(pts.data(), c->nnp, nq * 5 * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (size_t i = 0; out && i < nq; ++i) {     // device split layout -> lmsf_record
+        lmsf_record& r = out[i];
+        std::memset(&r, 0, sizeof r);
+        r.px = rp[i].x; r.py = rp[i].y; r.pz = rp[i].z;
+        std::memcpy(&r.kind, &rp[i].w, sizeof r.kind);
+        if (r.kind != 0) {
+            r.v0[0] = rv[i].v[0]; r.v0[1] = rv[i].v[1]; r.v0[2] = rv[i].v[2]; r.v1[0] = rv[i].v[3];
+        }
+        if (r.kind == LMSF_EDGE) { r.v1[1] = re[i].x; r.v1[2] = re[i].y; }
+    }
     if (nn) {  // neighbour points carry their map index in w (-1: rank not found with d^2 < 1)
         for (size_t i = 0; i < nq * 5; ++i) {
             int32_t v;

@@ -321,6 +321,36 @@ __device__ __forceinline__ void block_reduce_packet(double* P, double* out) {
     }
 }
 
+// Split record store / load (BatchView: rec_p, rec_v, rec_e).  Readers test the kind first, so the
+// value arrays of unmatched slots are never read (lmsf_match zero-fills them on the host).
+__device__ __forceinline__ void store_record(const BatchView& bv, size_t slot, float4 p, int kind, const d3& v0, double v1x,
+                                             double v1y, double v1z) {
+    bv.rec_p[slot] = make_float4(p.x, p.y, p.z, __int_as_float(kind));
+    if (kind != 0) {
+        RecV v;
+        v.v[0] = v0.x; v.v[1] = v0.y; v.v[2] = v0.z; v.v[3] = v1x;
+        bv.rec_v[slot] = v;
+        if (kind == LMSF_EDGE) bv.rec_e[slot] = make_double2(v1y, v1z);
+    }
+}
+
+// Residual + Jacobian of one stored record at pose Ps (edge_factor.hpp:33-61, surf_factor.hpp:32-56);
+// false when the slot holds no correspondence.
+__device__ __forceinline__ bool record_residual(const BatchView& bv, size_t slot, const Pose& Ps, double& res, double* J) {
+    const float4 p = bv.rec_p[slot];
+    const int kind = __float_as_int(p.w);
+    if (kind == 0) return false;
+    const RecV v = bv.rec_v[slot];
+    const d3 pp = mk((double)p.x, (double)p.y, (double)p.z);
+    if (kind == LMSF_EDGE) {
+        const double2 e = bv.rec_e[slot];
+        res = edge_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), mk(v.v[3], e.x, e.y), J);
+    } else {
+        res = surf_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), v.v[3], J);
+    }
+    return true;
+}
+
 // Line / plane fit of one query from its 5 neighbours, record write, and its Huber-weighted
 // normal-equation contribution at the linearisation pose (Ceres' first evaluation).
 __device__ __forceinline__ void fit_one(const BatchView& bv, int solver, int b, int q, int ne, const Pose& Ps,
@@ -329,11 +359,9 @@ __device__ __forceinline__ void fit_one(const BatchView& bv, int solver, int b, 
         const bool is_edge = q < ne;
         const size_t slot = (size_t)b * bv.feat_stride + q;
         const float4 p = bv.feat[slot];
-        lmsf_record r;
-        r.px = p.x; r.py = p.y; r.pz = p.z;
-        r.kind = 0;
-        r.v0[0] = r.v0[1] = r.v0[2] = 0.0;
-        r.v1[0] = r.v1[1] = r.v1[2] = 0.0;
+        int kind = 0;
+        d3 v0 = mk(0, 0, 0);
+        double v1x = 0.0, v1y = 0.0, v1z = 0.0;
         // the 5 neighbour points, written contiguously by knn
         float4 np[5];
 #pragma unroll
@@ -344,9 +372,9 @@ __device__ __forceinline__ void fit_one(const BatchView& bv, int solver, int b, 
             if (is_edge) {
                 d3 a, bpt;
                 if (edge_fit(np, a, bpt)) {
-                    r.kind = LMSF_EDGE;
-                    r.v0[0] = a.x; r.v0[1] = a.y; r.v0[2] = a.z;
-                    r.v1[0] = bpt.x; r.v1[1] = bpt.y; r.v1[2] = bpt.z;
+                    kind = LMSF_EDGE;
+                    v0 = a;
+                    v1x = bpt.x; v1y = bpt.y; v1z = bpt.z;
                     if (solver == LMSF_SOLVER_GN) {  // EdgeCostFactorInfo residuals_ / norm_
                         const d3 cp = mk((double)w.x, (double)w.y, (double)w.z);
                         d3 nu = cross(cp - a, cp - bpt);
@@ -363,28 +391,28 @@ __device__ __forceinline__ void fit_one(const BatchView& bv, int solver, int b, 
                 d3 n;
                 double D;
                 if (surf_fit(np, w, n, D, gn_res)) {
-                    r.kind = LMSF_SURF;
-                    r.v0[0] = n.x; r.v0[1] = n.y; r.v0[2] = n.z;
-                    r.v1[0] = D;
+                    kind = LMSF_SURF;
+                    v0 = n;
+                    v1x = D;
                     gn_grad[0] = n.x; gn_grad[1] = n.y; gn_grad[2] = n.z;
                 }
             }
         }
-        bv.rec[slot] = r;
+        store_record(bv, slot, p, kind, v0, v1x, v1y, v1z);
         if (solver == LMSF_SOLVER_GN) {
             double* gr = bv.gn_rows + slot * 4;
-            gr[0] = gn_grad[0]; gr[1] = gn_grad[1]; gr[2] = gn_grad[2]; gr[3] = r.kind ? gn_res : -1.0;
-        } else if (r.kind != 0) {
+            gr[0] = gn_grad[0]; gr[1] = gn_grad[1]; gr[2] = gn_grad[2]; gr[3] = kind ? gn_res : -1.0;
+        } else if (kind != 0) {
             double J[6], res;
             const d3 pp = mk((double)p.x, (double)p.y, (double)p.z);
-            if (r.kind == LMSF_EDGE)
-                res = edge_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), mk(r.v1[0], r.v1[1], r.v1[2]), J);
+            if (kind == LMSF_EDGE)
+                res = edge_residual(Ps, pp, v0, mk(v1x, v1y, v1z), J);
             else
-                res = surf_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), r.v1[0], J);
+                res = surf_residual(Ps, pp, v0, v1x, J);
             huber_accumulate(P, res, J);
         }
-        if (r.kind == LMSF_EDGE) P[29] += 1.0;
-        if (r.kind == LMSF_SURF) P[30] += 1.0;
+        if (kind == LMSF_EDGE) P[29] += 1.0;
+        if (kind == LMSF_SURF) P[30] += 1.0;
     }
 }
 
@@ -423,16 +451,8 @@ __global__ __launch_bounds__(256) void lm_eval_kernel(BatchView bv) {
     for (int k = 0; k < kEvalPerThread; ++k) {
         const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
         if (q < nq) {
-            const lmsf_record r = bv.rec[(size_t)b * bv.feat_stride + q];
-            if (r.kind != 0) {
-                double J[6], res;
-                const d3 pp = mk((double)r.px, (double)r.py, (double)r.pz);
-                if (r.kind == LMSF_EDGE)
-                    res = edge_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), mk(r.v1[0], r.v1[1], r.v1[2]), J);
-                else
-                    res = surf_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), r.v1[0], J);
-                huber_accumulate(P, res, J);
-            }
+            double J[6], res;
+            if (record_residual(bv, (size_t)b * bv.feat_stride + q, Ps, res, J)) huber_accumulate(P, res, J);
         }
     }
     block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + blockIdx.x) * kPacket);
@@ -450,16 +470,8 @@ __global__ __launch_bounds__(256) void eval_at_kernel(BatchView bv, const double
     for (int k = 0; k < kEvalPerThread; ++k) {
         const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
         if (q < nq) {
-            const lmsf_record r = bv.rec[q];
-            if (r.kind != 0) {
-                double J[6], res;
-                const d3 pp = mk((double)r.px, (double)r.py, (double)r.pz);
-                if (r.kind == LMSF_EDGE)
-                    res = edge_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), mk(r.v1[0], r.v1[1], r.v1[2]), J);
-                else
-                    res = surf_residual(Ps, pp, mk(r.v0[0], r.v0[1], r.v0[2]), r.v1[0], J);
-                huber_accumulate(P, res, J);
-            }
+            double J[6], res;
+            if (record_residual(bv, (size_t)q, Ps, res, J)) huber_accumulate(P, res, J);
         }
     }
     block_reduce_packet(P, bv.partials + (size_t)blockIdx.x * kPacket);

@@ -47,6 +47,8 @@ struct SolveState {
     double trace[kMaxOuter][7];
 };
 
+struct alignas(32) RecV { double v[4]; };
+
 struct BatchView {
     int B;                   // slots in this launch
     int feat_stride;         // features per slot (capacity)
@@ -55,7 +57,10 @@ struct BatchView {
     const int* n_surf;       // [B]
     float4* nnp;             // [B][feat_stride][5] neighbour points (w = map index bits, -1: none)
     int fit_per_thread;      // queries per thread of fit_eval (partials per kFitThreads*fpt queries)
-    lmsf_record* rec;        // [B][feat_stride]
+    // correspondence records, split so an LM evaluation of a surf record reads 48 B (not 64):
+    float4* rec_p;           // [B][feat_stride] lidar-frame point, w = kind (int bits; 0 = none)
+    RecV* rec_v;             // [B][feat_stride] surf: n, D; edge: a, b.x
+    double2* rec_e;          // [B][feat_stride] edge only: b.y, b.z
     double* partials;        // [B][max_parts][kPacket]
     int max_parts;
     SolveState* st;          // [B]
