@@ -222,6 +222,94 @@ __device__ void ring_bad_points(const ExtractView& ev, const float4* pts, int si
     }
 }
 
+// Bitonic sort of npow (key, index) pairs ascending by (key, index), keys/indices in LDS on entry
+// and exit.  Elements live in registers: wave w owns positions [w * 64E, (w + 1) * 64E), lane l
+// holds w * 64E + e * 64 + l (e < E).  A compare-exchange at distance jj < 64 is a lane shuffle,
+// 64 <= jj < 64E a swap inside the thread, and only jj >= 64E crosses waves (LDS + barrier):
+// 2 of the 55 stages of a 1024-element sort with E = 4, instead of 55 barrier stages.
+template <int E>
+__device__ void bitonic_sort_regs(double* key, int* kidx, int npow) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int chunk = 64 * E;
+    const bool active = w * chunk < npow;
+    double k[E];
+    int id[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = w * chunk + e * 64 + lane;
+        k[e] = active ? key[i] : 0.0;
+        id[e] = active ? kidx[i] : 0;
+    }
+    for (int kk = 2; kk <= npow; kk <<= 1) {
+        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+            if (jj >= chunk) {                         // partner in another wave: through LDS
+                __syncthreads();
+                if (active) {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        const int i = w * chunk + e * 64 + lane;
+                        key[i] = k[e];
+                        kidx[i] = id[e];
+                    }
+                }
+                __syncthreads();
+                if (active) {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        const int i = w * chunk + e * 64 + lane, ixj = i ^ jj;
+                        const double ko = key[ixj];
+                        const int io = kidx[ixj];
+                        const bool lower = i < ixj;
+                        const double ka = lower ? k[e] : ko, kb = lower ? ko : k[e];
+                        const int ia = lower ? id[e] : io, ib = lower ? io : id[e];
+                        const bool a_gt_b = ka > kb || (ka == kb && ia > ib);
+                        const bool up = (i & kk) == 0;
+                        if (up == a_gt_b) { k[e] = ko; id[e] = io; }
+                    }
+                }
+            } else if (jj >= 64) {                     // same thread, another register
+                const int ej = jj >> 6;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int e2 = e ^ ej;
+                    if (e2 > e) {
+                        const int i = w * chunk + e * 64 + lane;
+                        const bool a_gt_b = k[e] > k[e2] || (k[e] == k[e2] && id[e] > id[e2]);
+                        const bool up = (i & kk) == 0;
+                        if (up == a_gt_b) {
+                            const double tk = k[e]; k[e] = k[e2]; k[e2] = tk;
+                            const int ti = id[e]; id[e] = id[e2]; id[e2] = ti;
+                        }
+                    }
+                }
+            } else {                                   // same register, another lane
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int i = w * chunk + e * 64 + lane;
+                    const double ko = __shfl_xor(k[e], jj, 64);
+                    const int io = __shfl_xor(id[e], jj, 64);
+                    const bool lower = (lane & jj) == 0;
+                    const double ka = lower ? k[e] : ko, kb = lower ? ko : k[e];
+                    const int ia = lower ? id[e] : io, ib = lower ? io : id[e];
+                    const bool a_gt_b = ka > kb || (ka == kb && ia > ib);
+                    const bool up = (i & kk) == 0;
+                    if (up == a_gt_b) { k[e] = ko; id[e] = io; }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = w * chunk + e * 64 + lane;
+            key[i] = k[e];
+            kidx[i] = id[e];
+        }
+    }
+    __syncthreads();
+}
+
 // One workgroup per (ring, scan).
 __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
     __shared__ uint8_t dis[kRingMax];
@@ -286,25 +374,11 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
             }
         }
         __syncthreads();
-        // bitonic sort ascending by (c, index)
-        for (int kk = 2; kk <= npow; kk <<= 1) {
-            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-                for (int i = tid; i < npow; i += 256) {
-                    const int ixj = i ^ jj;
-                    if (ixj > i) {
-                        const double ka = key[i], kb = key[ixj];
-                        const int ia = kidx[i], ib = kidx[ixj];
-                        const bool a_gt_b = ka > kb || (ka == kb && ia > ib);
-                        const bool up = (i & kk) == 0;
-                        if (up == a_gt_b) {
-                            key[i] = kb; key[ixj] = ka;
-                            kidx[i] = ib; kidx[ixj] = ia;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        }
+        // bitonic sort ascending by (c, index), register-resident (bitonic_sort_regs)
+        if (npow <= 256) bitonic_sort_regs<1>(key, kidx, npow);
+        else if (npow <= 512) bitonic_sort_regs<2>(key, kidx, npow);
+        else if (npow <= 1024) bitonic_sort_regs<4>(key, kidx, npow);
+        else bitonic_sort_regs<8>(key, kidx, npow);
         // greedy edge pick, largest curvature first (FX:157-195), one wave
         if (tid < 64) {
             int pos = n - 1, picked = 0, ec = sh_ec;
