@@ -13,13 +13,11 @@
 //   ring_offsets per scan: exclusive scan (ring-major) -> stable ring-ordered positions
 //   ring_scatter stable multisplit (wave ballots) into ring order
 //   ring_features one workgroup per ring: automaton (wave-ballot walk), 6 sectors of
-//                 {curvature, LDS bitonic sort, wave-ballot greedy pick, block-scan compaction}
+//                 {curvature, register-resident bitonic sort, wave-ballot greedy pick, block-scan
+//                 compaction}
 //   concat       per scan: edges (ring order) then surfs (ring order) into the feature array
 #include <hip/hip_runtime.h>
 #include <math.h>
-
-#include <cstdlib>
-#include <cstring>
 
 #include "lmsf_internal.h"
 
@@ -437,147 +435,6 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
     }
 }
 
-// Single-scan variant of ring_features_kernel (same outputs, bit for bit): 1024 threads per ring
-// and the six sector sorts replaced by one barrier-free rank pass -- every sector point counts the
-// points of its sector ordered before it by (curvature, ring index) (curvature bits compared as
-// uint64: non-negative doubles order like their bit patterns) and writes its own ring index to
-// sidx[sector offset + rank].  O(n^2) per sector but no barrier stages: a 16-ring scan runs 16
-// workgroups, where the 6 x 55-stage bitonic sorts of the batch kernel leave the chip idle.
-constexpr int kRankThreads = 1024;
-constexpr int kRankSectorMax = 1536;   // larger sectors use the bitonic kernel
-
-__global__ __launch_bounds__(kRankThreads) void ring_features_rank_kernel(ExtractView ev) {
-    __shared__ uint8_t dis[kRingMax];
-    __shared__ uint8_t flag[kRingMax];
-    __shared__ unsigned long long ukey[kRingMax];   // curvature bits of sector point j at [j - 5]
-    __shared__ int sidx[kRingMax];                  // sector-sorted ring indices, sector k from s0_k - 5
-    __shared__ int wsum[kRankThreads / 64];
-    __shared__ int sh_ec, sh_sc, sh_err;
-    const int r = blockIdx.x, b = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int* rs = ev.ring_start + (size_t)b * (kMaxRings + 1);
-    const int start = rs[r];
-    const int size = rs[r + 1] - start;
-    int* ecnt = ev.ring_edge_cnt + (size_t)b * kMaxRings;
-    int* scnt = ev.ring_surf_cnt + (size_t)b * kMaxRings;
-    if (size < 20 || size > kRingMax) {   // FX:71
-        if (tid == 0) {
-            ecnt[r] = 0;
-            scnt[r] = 0;
-            if (size > kRingMax) atomicOr(ev.error, 1);
-        }
-        return;
-    }
-    const float4* pts = ev.ring_pts + (size_t)b * ev.raw_stride + start;
-    const int* psrc = ev.ring_src + (size_t)b * ev.raw_stride + start;
-    for (int j = tid; j < size; j += kRankThreads) { dis[j] = 0; flag[j] = 0; }
-    if (tid == 0) { sh_ec = 0; sh_sc = 0; sh_err = 0; }
-    __syncthreads();
-    ring_bad_points<kRankThreads>(ev, pts, size, dis, flag);
-    const int total_points = size - 10;
-    const int L = total_points / 6;                        // (int)((total/6) + 0.5) with int division
-    const int last = size - 6;                             // sectors cover ring indices [5, size - 6]
-    if (size - 6 - (5 + 5 * L) + 1 > kSortMax || L > kSortMax) {   // same capacity rule as the batch kernel
-        if (tid == 0) { atomicOr(ev.error, 2); ecnt[r] = 0; scnt[r] = 0; }
-        return;
-    }
-    // curvature (FX:97-118): float 11-point sums, squared norm in double
-    for (int j = 5 + tid; j <= last; j += kRankThreads) {
-        const float4 m5 = pts[j - 5], m4 = pts[j - 4], m3 = pts[j - 3], m2 = pts[j - 2], m1 = pts[j - 1];
-        const float4 p0 = pts[j];
-        const float4 q1 = pts[j + 1], q2 = pts[j + 2], q3 = pts[j + 3], q4 = pts[j + 4], q5 = pts[j + 5];
-        const float fx = m5.x + m4.x + m3.x + m2.x + m1.x - 10 * p0.x + q1.x + q2.x + q3.x + q4.x + q5.x;
-        const float fy = m5.y + m4.y + m3.y + m2.y + m1.y - 10 * p0.y + q1.y + q2.y + q3.y + q4.y + q5.y;
-        const float fz = m5.z + m4.z + m3.z + m2.z + m1.z - 10 * p0.z + q1.z + q2.z + q3.z + q4.z + q5.z;
-        const double dx = fx, dy = fy, dz = fz;
-        ukey[j - 5] = (unsigned long long)__double_as_longlong(dx * dx + dy * dy + dz * dz);
-    }
-    __syncthreads();
-    // rank within the sector (total order (key, ring index))
-    for (int j = 5 + tid; j <= last; j += kRankThreads) {
-        const int k = min((j - 5) / max(L, 1), 5);
-        const int s0 = 5 + L * k, e0 = (k == 5) ? last : s0 + L - 1;
-        const unsigned long long kj = ukey[j - 5];
-        int rank = 0;
-        for (int i = s0; i <= e0; ++i) {
-            const unsigned long long ki = ukey[i - 5];
-            rank += (ki < kj || (ki == kj && i < j)) ? 1 : 0;
-        }
-        sidx[s0 - 5 + rank] = j;
-    }
-    __syncthreads();
-    const double thresh = (double)ev.edge_thresh;
-    float4* estage = ev.edge_stage + ((size_t)b * kMaxRings + r) * kEdgePerRing;
-    int* estage_src = ev.edge_stage_src + ((size_t)b * kMaxRings + r) * kEdgePerRing;
-    float4* sstage = ev.surf_stage + (size_t)b * ev.raw_stride + start;
-    int* sstage_src = ev.surf_stage_src + (size_t)b * ev.raw_stride + start;
-    for (int k = 0; k < 6; ++k) {
-        const int s0 = 5 + L * k;
-        const int e0 = (k == 5) ? last : s0 + L - 1;
-        const int n = e0 - s0 + 1;
-        const int* kidx = sidx + (s0 - 5);
-        // greedy edge pick, largest curvature first (FX:157-195), one wave
-        if (tid < 64) {
-            int pos = n - 1, picked = 0, ec = sh_ec;
-            while (pos >= 0) {
-                const int cand = pos - lane;
-                const bool elig = cand >= 0 && dis[kidx[cand]] == 0;
-                const unsigned long long m = __ballot(elig);
-                if (!m) { pos -= 64; continue; }
-                const int f = __ffsll((long long)m) - 1;
-                const int ind = kidx[pos - f];
-                const double c = __longlong_as_double((long long)ukey[ind - 5]);
-                if (c <= thresh) break;
-                ++picked;
-                if (picked > 20) break;
-                if (lane == 0) {
-                    estage[ec] = pts[ind];
-                    estage_src[ec] = psrc[ind];
-                    flag[ind] = 1;
-                }
-                if (lane >= 1 && lane <= 5) dis[min(ind + lane, size - 1)] = 1;
-                if (lane >= 6 && lane <= 10) dis[max(ind - (lane - 5), 0)] = 1;
-                ++ec;
-                pos = pos - f - 1;
-            }
-            if (lane == 0) sh_ec = ec;
-        }
-        __syncthreads();
-        // surf: every sector point not picked as edge, ascending curvature (FX:197-206);
-        // contiguous chunks per thread, block prefix via wave scans
-        const int per = (n + kRankThreads - 1) / kRankThreads;
-        const int lo = tid * per, hi = min(lo + per, n);
-        int cntv = 0;
-        for (int i = lo; i < hi; ++i) cntv += flag[kidx[i]] == 0;
-        int incl = cntv;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += t;
-        }
-        if (lane == 63) wsum[wid] = incl;
-        __syncthreads();
-        int wbase = 0;
-        for (int w2 = 0; w2 < wid; ++w2) wbase += wsum[w2];
-        int o = sh_sc + wbase + incl - cntv;
-        for (int i = lo; i < hi; ++i) {
-            const int ind = kidx[i];
-            if (flag[ind] == 0) {
-                sstage[o] = pts[ind];
-                sstage_src[o] = psrc[ind];
-                ++o;
-            }
-        }
-        __syncthreads();
-        if (tid == kRankThreads - 1) sh_sc = o;  // last thread's running offset is the sector's total
-        __syncthreads();
-    }
-    if (tid == 0) {
-        ecnt[r] = sh_err ? 0 : sh_ec;
-        scnt[r] = sh_err ? 0 : sh_sc;
-    }
-}
-
 // Concatenate per-ring stages: edges of ring 0..N-1, then surfs of ring 0..N-1 (FX:124-125 order).
 __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
     __shared__ int epre[kMaxRings + 1], spre[kMaxRings + 1];
@@ -619,28 +476,11 @@ __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
     }
 }
 
-// Sector sort: rank variant for small launches (one scan's rings cannot fill the chip) unless the
-// rings are long enough for its O(n^2) sector pass to lose; LMSF_EXTRACT_SORT = rank | bitonic
-// forces one (A/B).
-static bool use_rank_sort(const ExtractView& ev) {
-    static int forced = [] {
-        const char* e = getenv("LMSF_EXTRACT_SORT");
-        if (!e) return -1;
-        return strcmp(e, "rank") == 0 ? 1 : (strcmp(e, "bitonic") == 0 ? 0 : -1);
-    }();
-    const bool fits = ev.raw_stride / max(ev.n_scans, 1) <= 6 * kRankSectorMax;
-    if (forced >= 0) return forced == 1 && fits;
-    return fits && ev.B * ev.n_scans < 256;
-}
-
 hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
     hipLaunchKernelGGL(ring_count_kernel, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(ring_offsets_kernel, dim3(ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(ring_scatter_kernel, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
-    if (use_rank_sort(ev))
-        hipLaunchKernelGGL(ring_features_rank_kernel, dim3(ev.n_scans, ev.B), dim3(kRankThreads), 0, s, ev);
-    else
-        hipLaunchKernelGGL(ring_features_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
+    hipLaunchKernelGGL(ring_features_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
     const int cblocks = min(64, (ev.raw_stride + 255) / 256);
     hipLaunchKernelGGL(concat_kernel, dim3(max(cblocks, 1), ev.B), dim3(256), 0, s, ev);
     return hipGetLastError();

@@ -174,8 +174,7 @@ def test_solve_trace_parity_gn(lib, oracle_mod, small_workload):
 
 def test_batch_run_matches_oracle(lib, oracle_mod, small_workload):
     """Batch path with 16 slots: 16 x 70k query slots >= 2^20 selects the one-lane-per-query knn
-    team and 16 scans x 16 rings the bitonic sector sort (the single-scan tests above run the
-    8-lane team and the rank sort)."""
+    team (the single-scan tests above run the 8-lane team)."""
     wl = small_workload
     ctx = _ctx(lib, schedule=1, max_iterations=5, max_batch=16)
     ctx.set_map(lib.EDGE, wl.edge_map)
