@@ -157,25 +157,16 @@ __global__ void state_init_kernel(BatchView bv, const double* poses) {
     S.edge_matches = S.surf_matches = S.nmatch = 0;
 }
 
-// The LM / GN control logic runs on one lane; it works on an LDS copy of the registration's
-// SolveState staged by the whole wave with coalesced loads (a chain of dependent single-lane
-// global accesses to the state cost more than the arithmetic), written back the same way.
-static_assert(sizeof(SolveState) % sizeof(double) == 0, "SolveState is staged as doubles");
-__device__ __forceinline__ void state_load(const SolveState& g, SolveState& l) {
-    const double* src = reinterpret_cast<const double*>(&g);
-    double* dst = reinterpret_cast<double*>(&l);
-    for (int i = threadIdx.x; i < (int)(sizeof(SolveState) / sizeof(double)); i += blockDim.x) dst[i] = src[i];
-    __syncthreads();
-}
-__device__ __forceinline__ void state_store(const SolveState& l, SolveState& g) {
-    __syncthreads();
-    const double* src = reinterpret_cast<const double*>(&l);
-    double* dst = reinterpret_cast<double*>(&g);
-    for (int i = threadIdx.x; i < (int)(sizeof(SolveState) / sizeof(double)); i += blockDim.x) dst[i] = src[i];
-}
-
 // After fit_eval: IterationZero (evaluate at x0, jacobi scaling, gradient check) + first step.
-__device__ void lm_begin_body(SolveState& S, const double* tot) {
+__global__ __launch_bounds__(64) void lm_begin_kernel(BatchView bv) {
+    const int b = blockIdx.x;
+    const int nq = bv.n_edge[b] + bv.n_surf[b];
+    const int fb = 256 * bv.fit_per_thread;
+    const int nparts = (nq + fb - 1) / fb;
+    double tot[kPacket];
+    reduce_parts(bv, b, nparts, tot);
+    if (threadIdx.x != 0) return;
+    SolveState& S = bv.st[b];
     S.iteration = 0;
     S.need_eval = 0;
     S.done = 0;
@@ -204,22 +195,20 @@ __device__ void lm_begin_body(SolveState& S, const double* tot) {
     compute_step(S);
 }
 
-__global__ __launch_bounds__(64) void lm_begin_kernel(BatchView bv) {
-    __shared__ SolveState sS;
-    const int b = blockIdx.x;
-    state_load(bv.st[b], sS);
-    const int nq = bv.n_edge[b] + bv.n_surf[b];
-    const int fb = 256 * bv.fit_per_thread;
-    const int nparts = (nq + fb - 1) / fb;
-    double tot[kPacket];
-    reduce_parts(bv, b, nparts, tot);
-    if (threadIdx.x == 0) lm_begin_body(sS, tot);
-    state_store(sS, bv.st[b]);
-}
-
 // After lm_eval at the candidate: step acceptance (ParameterToleranceReached,
 // FunctionToleranceReached, IsStepSuccessful, HandleSuccessfulStep / StepRejected) + next step.
-__device__ void lm_step_body(SolveState& S, const double* tot, int outer, int is_last) {
+__global__ __launch_bounds__(64) void lm_step_kernel(BatchView bv, int outer, int is_last) {
+    const int b = blockIdx.x;
+    SolveState& S = bv.st[b];
+    if (!S.need_eval) {
+        if (is_last && threadIdx.x == 0) finish_outer(S, outer);
+        return;
+    }
+    const int nq = bv.n_edge[b] + bv.n_surf[b];
+    const int nparts = (nq + kEvalBlock - 1) / kEvalBlock;
+    double tot[kPacket];
+    reduce_parts(bv, b, nparts, tot);
+    if (threadIdx.x != 0) return;
     S.need_eval = 0;
     ++S.evals;
     const double cost_c = isfinite(tot[0]) ? tot[0] : 1.7976931348623157e308;
@@ -264,25 +253,6 @@ __device__ void lm_step_body(SolveState& S, const double* tot, int outer, int is
     if (is_last) finish_outer(S, outer);
 }
 
-__global__ __launch_bounds__(64) void lm_step_kernel(BatchView bv, int outer, int is_last) {
-    __shared__ SolveState sS;
-    const int b = blockIdx.x;
-    state_load(bv.st[b], sS);
-    if (!sS.need_eval) {
-        if (is_last) {
-            if (threadIdx.x == 0) finish_outer(sS, outer);
-            state_store(sS, bv.st[b]);
-        }
-        return;
-    }
-    const int nq = bv.n_edge[b] + bv.n_surf[b];
-    const int nparts = (nq + kEvalBlock - 1) / kEvalBlock;
-    double tot[kPacket];
-    reduce_parts(bv, b, nparts, tot);
-    if (threadIdx.x == 0) lm_step_body(sS, tot, outer, is_last);
-    state_store(sS, bv.st[b]);
-}
-
 // ---------------------------------------------------------------- GN (edgeSurfFeatureRegistration)
 // gn_accum writes JtJ (upper 21 at [1..21]), JtR ([22..27]) and per-block match counts
 // ([29] edge, [30] surf) into partials_gn; fit_eval's own partials carry the per-block counts
@@ -294,7 +264,18 @@ __device__ void gn_record_trace(SolveState& S, int outer) {
     S.outer_run = outer + 1;
 }
 
-__device__ void gn_solve_body(SolveState& S, const double* tot, int outer) {
+__global__ __launch_bounds__(64) void gn_solve_kernel(BatchView bv, int outer) {
+    const int b = blockIdx.x;
+    SolveState& S = bv.st[b];
+    if (S.gn_converged) return;
+    const int nq = bv.n_edge[b] + bv.n_surf[b];
+    const int fb = 256 * bv.fit_per_thread;
+    const int nparts = (nq + fb - 1) / fb;
+    double tot[kPacket];
+    BatchView g = bv;
+    g.partials = bv.partials_gn;
+    reduce_parts(g, b, nparts, tot);
+    if (threadIdx.x != 0) return;
     S.edge_matches = (int)tot[29];
     S.surf_matches = (int)tot[30];
     const int e16 = (int)(uint16_t)(int)tot[29], s16 = (int)(uint16_t)(int)tot[30];
@@ -374,22 +355,6 @@ __device__ void gn_solve_body(SolveState& S, const double* tot, int outer) {
         S.term = LMSF_TERM_MAX_ITERATIONS;
     }
     gn_record_trace(S, outer);
-}
-
-__global__ __launch_bounds__(64) void gn_solve_kernel(BatchView bv, int outer) {
-    __shared__ SolveState sS;
-    const int b = blockIdx.x;
-    state_load(bv.st[b], sS);
-    if (sS.gn_converged) return;
-    const int nq = bv.n_edge[b] + bv.n_surf[b];
-    const int fb = 256 * bv.fit_per_thread;
-    const int nparts = (nq + fb - 1) / fb;
-    double tot[kPacket];
-    BatchView g = bv;
-    g.partials = bv.partials_gn;
-    reduce_parts(g, b, nparts, tot);
-    if (threadIdx.x == 0) gn_solve_body(sS, tot, outer);
-    state_store(sS, bv.st[b]);
 }
 
 // GN accumulation: J row = grad^T [-R [p]x, I] (edgeSurf...:255-265) over the first
