@@ -404,19 +404,23 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
             if (lane == 0) sh_ec = ec;
         }
         __syncthreads();
-        // surf: every sector point not picked as edge, ascending curvature (FX:197-206)
+        // surf: every sector point not picked as edge, ascending curvature (FX:197-206);
+        // contiguous chunk per thread, block prefix from wave scans
         const int per = (n + 255) / 256;
         const int lo = tid * per, hi = min(lo + per, n);
         int cntv = 0;
         for (int i = lo; i < hi; ++i) cntv += flag[kidx[i]] == 0;
-        scan_part[tid] = cntv;
-        __syncthreads();
-        if (tid == 0) {
-            int acc = 0;
-            for (int i = 0; i < 256; ++i) { const int v = scan_part[i]; scan_part[i] = acc; acc += v; }
+        int incl = cntv;
+#pragma unroll
+        for (int o2 = 1; o2 < 64; o2 <<= 1) {
+            const int t = __shfl_up(incl, o2, 64);
+            if (lane >= o2) incl += t;
         }
+        if (lane == 63) scan_part[tid >> 6] = incl;
         __syncthreads();
-        int o = sh_sc + scan_part[tid];
+        int wbase = 0;
+        for (int w2 = 0; w2 < (tid >> 6); ++w2) wbase += scan_part[w2];
+        int o = sh_sc + wbase + incl - cntv;
         for (int i = lo; i < hi; ++i) {
             const int ind = kidx[i];
             if (flag[ind] == 0) {
