@@ -121,6 +121,22 @@ lmsf_status lmsf_set_scan(lmsf_ctx* ctx, int32_t kind, const float* xyzi, size_t
 
 /* SetMaxIteration (ceres_...:86-89). */
 lmsf_status lmsf_set_max_iterations(lmsf_ctx* ctx, int32_t n);
+/* Outer-iteration schedule: LMSF_SCHEDULE_REFERENCE_DECAY (the reference's per-object
+ * optimization_count_ decrement, ceres_...:100-101) or LMSF_SCHEDULE_FIXED (benchmarks). */
+lmsf_status lmsf_set_schedule(lmsf_ctx* ctx, int32_t schedule);
+
+/* LOAMFeatureProcessorBase constructor arguments (FX:36-50) + the build's beam model, changeable
+ * between extractions (lmsf_config holds the initial values). */
+typedef struct {
+    int32_t n_scans;           /* 1..128 */
+    float min_distance;
+    float max_distance;
+    float edge_threshold;
+    int32_t remove_bad_points;
+    double beam_lo_deg;
+    double beam_spacing_deg;
+} lmsf_extract_params;
+lmsf_status lmsf_set_extract_params(lmsf_ctx* ctx, const lmsf_extract_params* p);
 
 /* RegistrationBase::Solve (REG/registration_base.hpp:33; ceres_...:96-130).  pose: qx qy qz qw tx
  * ty tz (Eigen storage order of ceres_...:38-40); in = predicted map<-lidar pose, out = refined. */

@@ -495,6 +495,25 @@ lmsf_status lmsf_set_max_iterations(lmsf_ctx* c, int32_t n) {
     return LMSF_OK;
 }
 
+lmsf_status lmsf_set_schedule(lmsf_ctx* c, int32_t schedule) {
+    if (!c || (schedule != LMSF_SCHEDULE_REFERENCE_DECAY && schedule != LMSF_SCHEDULE_FIXED)) return LMSF_ERR_ARG;
+    c->cfg.schedule = schedule;
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_set_extract_params(lmsf_ctx* c, const lmsf_extract_params* p) {
+    if (!c || !p || p->n_scans < 1 || p->n_scans > kMaxRings || !(p->min_distance <= p->max_distance))
+        return LMSF_ERR_ARG;
+    c->cfg.n_scans = p->n_scans;
+    c->cfg.min_distance = p->min_distance;
+    c->cfg.max_distance = p->max_distance;
+    c->cfg.edge_threshold = p->edge_threshold;
+    c->cfg.remove_bad_points = p->remove_bad_points;
+    c->cfg.beam_lo_deg = p->beam_lo_deg;
+    c->cfg.beam_spacing_deg = p->beam_spacing_deg;
+    return LMSF_OK;
+}
+
 lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     if (!c || !pose) return LMSF_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->cfg.device));

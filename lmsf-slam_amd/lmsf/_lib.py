@@ -51,6 +51,12 @@ class KernelStats(C.Structure):
     _fields_ = [("launches", C.c_int64), ("total_ms", C.c_double), ("queries", C.c_int64), ("n27_sum", C.c_int64)]
 
 
+class ExtractParams(C.Structure):
+    _fields_ = [("n_scans", C.c_int32), ("min_distance", C.c_float), ("max_distance", C.c_float),
+                ("edge_threshold", C.c_float), ("remove_bad_points", C.c_int32), ("beam_lo_deg", C.c_double),
+                ("beam_spacing_deg", C.c_double)]
+
+
 class TrackerConfig(C.Structure):
     _fields_ = [("window_frames", C.c_int32), ("threshold_trans", C.c_double), ("threshold_rot", C.c_double),
                 ("time_interval", C.c_double), ("manual_map_update", C.c_int32), ("leaf_edge", C.c_double),
@@ -84,6 +90,8 @@ _SIGS = {
     "lmsf_set_map": (C.c_int32, [_P, C.c_int32, _P, C.c_size_t]),
     "lmsf_set_scan": (C.c_int32, [_P, C.c_int32, _P, C.c_size_t]),
     "lmsf_set_max_iterations": (C.c_int32, [_P, C.c_int32]),
+    "lmsf_set_schedule": (C.c_int32, [_P, C.c_int32]),
+    "lmsf_set_extract_params": (C.c_int32, [_P, C.POINTER(ExtractParams)]),
     "lmsf_solve": (C.c_int32, [_P, _P, C.POINTER(SolveStats)]),
     "lmsf_solve_trace": (C.c_int32, [_P, _P, C.c_int32, C.POINTER(C.c_int32)]),
     "lmsf_extract_features": (C.c_int32, [_P, _P, C.c_size_t, C.POINTER(FeatureCounts)]),
@@ -210,6 +218,21 @@ class Context:
 
     def set_max_iterations(self, n):
         self._check(load().lmsf_set_max_iterations(self.h, int(n)))
+
+    def set_schedule(self, schedule):
+        self._check(load().lmsf_set_schedule(self.h, int(schedule)))
+
+    def set_extract_params(self, **kw):
+        """LOAMFeatureProcessorBase(N_SCANS, min, max, edge_thresh, RemovalBadPoints) + beam model;
+        unspecified fields keep the context's current values."""
+        c = self.cfg
+        p = ExtractParams(c.n_scans, c.min_distance, c.max_distance, c.edge_threshold, c.remove_bad_points,
+                          c.beam_lo_deg, c.beam_spacing_deg)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        self._check(load().lmsf_set_extract_params(self.h, C.byref(p)))
+        for f, _ in ExtractParams._fields_:
+            setattr(self.cfg, f, getattr(p, f))
 
     def solve(self, pose):
         x = np.ascontiguousarray(pose, dtype=np.float64).copy()

@@ -78,6 +78,31 @@ def test_extract_variants_bitexact(lib, oracle_mod, small_workload, n_scans, col
     assert ge.tobytes() == e.tobytes() and gs.tobytes() == s.tobytes()
 
 
+def test_runtime_extract_params_and_schedule(lib, oracle_mod, small_workload):
+    """lmsf_set_extract_params / lmsf_set_schedule change a live context (SURVEY 8(b) surface)."""
+    from lmsf import synth
+    ctx = _ctx(lib)
+    scan = synth.make_scan(small_workload.scene, small_workload.truth[0], 91, n_cols=1024, elev_deg=synth.HDL64_DEG)
+    ctx.set_extract_params(n_scans=64, edge_threshold=0.5)
+    ctx.extract(scan)
+    e, s, _, _ = oracle_mod.extract(scan, n_scans=64, edge_threshold=0.5)
+    ge, _ = ctx.copy_features(lib.EDGE)
+    gs, _ = ctx.copy_features(lib.SURF)
+    assert ge.tobytes() == e.tobytes() and gs.tobytes() == s.tobytes()
+    with pytest.raises(lib.LmsfError):
+        ctx.set_extract_params(n_scans=0)
+    wl = small_workload
+    ctx.set_map(lib.EDGE, wl.edge_map)
+    ctx.set_map(lib.SURF, wl.surf_map)
+    ctx.set_max_iterations(3)
+    ctx.set_schedule(lib.SCHEDULE_FIXED)
+    _, st = ctx.solve(wl.guess[0])
+    assert st.outer_iterations == 3
+    ctx.set_schedule(lib.SCHEDULE_REFERENCE_DECAY)
+    _, st = ctx.solve(wl.guess[0])
+    assert st.outer_iterations == 2
+
+
 def test_match_bitexact(lib, oracle_mod, small_workload):
     wl = small_workload
     e, s = _features(oracle_mod, wl.scans[0])
