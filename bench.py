@@ -95,12 +95,24 @@ class Dist:
 
 
 def timed(d, step, warmup, steps, ctxs):
-    """W untimed steps, then K steps between barrier + synchronize; max over ranks."""
+    """W untimed steps, then K steps between barrier + synchronize; max over ranks.  The last
+    warmup step (or, with W = 0, one step after the timed region) runs with the n27 accounting on:
+    it costs the search extra loads, so the timed launches run without it.  Returns the mean n27
+    per query of that step with the elapsed time."""
     torch = d.torch
-    for _ in range(warmup):
+
+    def counted():
+        for c in ctxs:
+            c.kernel_stats_reset(timing=False, n27=True)
         step()
+        ks = [c.kernel_stats() for c in ctxs]
+        return sum(k.n27_sum for k in ks) / max(sum(k.queries for k in ks), 1)
+
+    for _ in range(warmup - 1):
+        step()
+    mean_n27 = counted() if warmup > 0 else None
     for c in ctxs:
-        c.kernel_stats_reset(True)
+        c.kernel_stats_reset(timing=True)
     d.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -113,7 +125,17 @@ def timed(d, step, warmup, steps, ctxs):
     if d.world > 1:
         from lmsf import multi
         elapsed = multi.max_over_ranks(elapsed, d.dev)
-    return elapsed, out
+    if mean_n27 is None:
+        stats = [c.kernel_stats() for c in ctxs]   # keep the timed launches' accounting
+        mean_n27 = counted()
+        for c, ks in zip(ctxs, stats):
+            c._timed_stats = ks
+    return elapsed, out, mean_n27
+
+
+def timed_stats(ctx):
+    """Neighbour-search accounting of the timed launches."""
+    return getattr(ctx, "_timed_stats", None) or ctx.kernel_stats()
 
 
 def shared_map(d, make):
@@ -127,10 +149,11 @@ def shared_map(d, make):
     return multi.broadcast_map(e, s, d.dev)
 
 
-def knn_roofline(ks, traffic_json, batch, map_points, note):
+def knn_roofline(ks, mean_n27, traffic_json, batch, map_points, note):
     """B_search = sum_q [16 (query) + 27*8 (cell ranges) + 16 * n27(q)] per launch,
-    over the HIP-event-timed launches of the neighbour-search kernel."""
-    alg_bytes = ks.queries * (16 + 27 * 8) + 16 * ks.n27_sum
+    over the HIP-event-timed launches of the neighbour-search kernel (n27 per query from the
+    counted untimed step)."""
+    alg_bytes = ks.queries * (16 + 27 * 8 + 16 * mean_n27)
     avg_launch_ms = ks.total_ms / max(ks.launches, 1)
     bytes_per_launch = alg_bytes / max(ks.launches, 1)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
@@ -148,7 +171,7 @@ def knn_roofline(ks, traffic_json, batch, map_points, note):
             "kernel": "knn_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
             "alg_bytes_per_launch": int(bytes_per_launch), "launches": int(ks.launches),
             "queries_per_launch": int(ks.queries / max(ks.launches, 1)),
-            "mean_n27": round(ks.n27_sum / max(ks.queries, 1), 1),
+            "mean_n27": round(mean_n27, 1),
             "measured_hbm_gbs": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic and avg_launch_ms else None,
             "l2_hit_rate": round(l2_hit, 3) if l2_hit is not None else None,
             "note": note}
@@ -222,11 +245,11 @@ def run_batch(args, d):
                 multi.gather_pair_poses(poses, args.pairs, world, d.dev)
         return poses
 
-    elapsed, _ = timed(d, step, args.warmup, args.steps, [ctx])
-    ks = ctx.kernel_stats()
+    elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx])
+    ks = timed_stats(ctx)
     total_units = (args.batch * world if cfg == "C2" else args.pairs) * args.steps
     terr = [synth.pose_delta(poses[i], truth_u[unit_scan[i]]) for i in range(n_units)]
-    roof = knn_roofline(ks, args.traffic_json, chunk, map_points,
+    roof = knn_roofline(ks, mean_n27, args.traffic_json, chunk, map_points,
                         "achieved = SURVEY 8(d) algorithmic bytes / HIP-event launch time; the map + cell "
                         "index is largely L2/Infinity-Cache resident, so measured HBM traffic (PMC) is lower")
     cpu, pose_dv = None, None
@@ -349,9 +372,9 @@ def run_streams(args, d):
         state["i"] += 1
         return P
 
-    elapsed, _ = timed(d, step, args.warmup, args.steps, [ctx])
-    ks = ctx.kernel_stats()
-    roof = knn_roofline(ks, args.traffic_json, 1, map_points,
+    elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx])
+    ks = timed_stats(ctx)
+    roof = knn_roofline(ks, mean_n27, args.traffic_json, 1, map_points,
                         "achieved = SURVEY 8(d) algorithmic bytes / HIP-event launch time (one 63k-query scan "
                         "per launch: latency-bound launches)")
     cpu = None
@@ -422,9 +445,9 @@ def run_dual(args, d):
         state["i"] += 1
         return out
 
-    elapsed, _ = timed(d, step, args.warmup, args.steps, [ctx])
-    ks = ctx.kernel_stats()
-    roof = knn_roofline(ks, args.traffic_json, 1, 0,
+    elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx])
+    ks = timed_stats(ctx)
+    roof = knn_roofline(ks, mean_n27, args.traffic_json, 1, 0,
                         "achieved = SURVEY 8(d) algorithmic bytes / HIP-event launch time (one ~63k-query scan per "
                         "launch against the voxelised local map: latency-bound launches)")
     ext_err = [float(np.linalg.norm(system.extrinsic[:3, 3] - X[:3, 3])),

@@ -175,7 +175,12 @@ lmsf_status lmsf_match(lmsf_ctx* ctx, const double pose[7], lmsf_record* out, in
 lmsf_status lmsf_eval(lmsf_ctx* ctx, const double pose[7], double out[29]);
 /* Neighbour-search kernel accounting since the last reset: launches, summed device time (ms,
  * HIP events on the context stream), queries, and sum over queries of n27 (map points in the
- * 3x3x3 block of 1 m cells around each query: the algorithmic-byte figure of DESIGN.md). */
+ * 3x3x3 block of 1 m cells around each query: the algorithmic-byte figure of DESIGN.md).
+ * reset mode: LMSF_STATS_TIMING (events, launches, queries) | LMSF_STATS_N27 (n27_sum and
+ * queries; costs the search extra cell-offset loads, so it is kept out of timed launches);
+ * 0 turns accounting off. */
+#define LMSF_STATS_TIMING 1
+#define LMSF_STATS_N27 2
 typedef struct {
     int64_t launches;
     double total_ms;
@@ -183,7 +188,7 @@ typedef struct {
     int64_t n27_sum;
 } lmsf_kernel_stats;
 lmsf_status lmsf_kernel_stats_get(lmsf_ctx* ctx, lmsf_kernel_stats* out);
-lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* ctx, int32_t enable_timing);
+lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* ctx, int32_t mode);
 
 /* ---- scan-to-local-map tracker: LidarTrackerLocalMap<P, RegistrationBase<P>>
  * (INC/LidarTracker/LidarTrackerLocalMap.hpp:42-263) over one context's registration.

@@ -100,7 +100,8 @@ struct lmsf_ctx {
     int last_outer = 0;
     double last_trace[kMaxOuter][7];
     // kernel accounting
-    bool timing = false;
+    bool timing = false;    // LMSF_STATS_TIMING: HIP events around each neighbour-search launch
+    bool count27 = false;   // LMSF_STATS_N27: n27 accounting inside the launch
     hipEvent_t ev[2 * kEventPairs];
     int ev_used = 0;
     double knn_ms = 0.0;
@@ -143,7 +144,8 @@ struct lmsf_ctx {
         v.partials = partials;
         v.max_parts = max_parts;
         v.st = st;
-        v.n27 = timing ? d_n27 : nullptr;
+        v.n27 = timing || count27 ? d_n27 : nullptr;
+        v.count27 = count27 ? 1 : 0;
         v.gn_rows = gn_rows;
         v.partials_gn = partials_gn;
         return v;
@@ -855,14 +857,16 @@ lmsf_status lmsf_eval(lmsf_ctx* c, const double pose[7], double out[29]) {
     return LMSF_OK;
 }
 
-lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* c, int32_t enable_timing) {
-    if (!c) return LMSF_ERR_ARG;
+lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* c, int32_t mode) {
+    if (!c || (mode & ~(LMSF_STATS_TIMING | LMSF_STATS_N27))) return LMSF_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (enable_timing && !c->ev[0]) {
+    const bool timing = (mode & LMSF_STATS_TIMING) != 0;
+    if (timing && !c->ev[0]) {
         for (int i = 0; i < 2 * kEventPairs; ++i) HIPCHK(c, hipEventCreate(&c->ev[i]));
     }
-    c->timing = enable_timing != 0;
+    c->timing = timing;
+    c->count27 = (mode & LMSF_STATS_N27) != 0;
     c->ev_used = 0;
     c->knn_ms = 0.0;
     c->knn_launches = 0;

@@ -59,6 +59,23 @@ __device__ __forceinline__ void block_coords(int remap, int gx, int& x, int& b) 
     x = logical - b * gx;
 }
 
+// Field-wise select of two grids: a runtime-selected GridView reference (or a select of whole
+// structs) makes the compiler spill the kernel arguments to scratch.
+__device__ __forceinline__ GridView pick_grid(bool c, const GridView& a, const GridView& b) {
+    GridView r;
+    r.ox = c ? a.ox : b.ox;
+    r.oy = c ? a.oy : b.oy;
+    r.oz = c ? a.oz : b.oz;
+    r.nx = c ? a.nx : b.nx;
+    r.ny = c ? a.ny : b.ny;
+    r.nz = c ? a.nz : b.nz;
+    r.off = c ? a.off : b.off;
+    r.pts = c ? a.pts : b.pts;
+    r.orig = c ? a.orig : b.orig;
+    r.n = c ? a.n : b.n;
+    return r;
+}
+
 // One team of T lanes per query.  The 27 cells around the query cell are enumerated as 9
 // x-rows (each row = 3 consecutive cells = one contiguous range of the cell-sorted points); the
 // team strides over the flattened candidate list with coalesced float4 loads, keeps a per-lane
@@ -84,45 +101,50 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
     const bool active = q < ne + ns && !(skip_converged && bv.st[b].gn_converged);
     if (active) {
         const bool is_edge = q < ne;
-        const GridView& g = is_edge ? ge : gs;
-        const GridView& g2 = is_edge ? ge2 : gs2;
+        const GridView g = pick_grid(is_edge, ge, gs);
+        const GridView g2 = pick_grid(is_edge, ge2, gs2);
         const Pose P = load_pose(bv.st[b].x);
         const float4 p = bv.feat[(size_t)b * bv.feat_stride + q];
         const float3 w = associate(P, p);
         const float fx = floorf(w.x), fy = floorf(w.y), fz = floorf(w.z);
-        // rows: lane l resolves (grid, dy, dz) rows l, l + T, ... of the NR
-        constexpr int REPS = (NR + T - 1) / T;
-        int rs_[REPS], rl_[REPS];
-#pragma unroll
-        for (int rep = 0; rep < REPS; ++rep) {
-            rs_[rep] = 0;
-            rl_[rep] = 0;
-            const int rr = lane + rep * T;
-            if (rr < NR) {
-                const GridView& gg = (TWO && rr >= 9) ? g2 : g;
-                const int r9 = rr % 9;
-                const bool inside = gg.n > 0 && fx >= (float)(gg.ox - 2) && fx <= (float)(gg.ox + gg.nx + 1) &&
-                                    fy >= (float)(gg.oy - 2) && fy <= (float)(gg.oy + gg.ny + 1) &&
-                                    fz >= (float)(gg.oz - 2) && fz <= (float)(gg.oz + gg.nz + 1);
-                if (inside) {
-                    const int cx = (int)fx - gg.ox, cy = (int)fy - gg.oy + (r9 % 3) - 1, cz = (int)fz - gg.oz + (r9 / 3) - 1;
-                    const int xa = max(cx - 1, 0), xb = min(cx + 1, gg.nx - 1);
-                    if (cy >= 0 && cy < gg.ny && cz >= 0 && cz < gg.nz && xa <= xb) {
-                        const size_t row = ((size_t)cz * gg.ny + cy) * gg.nx;
-                        rs_[rep] = (int)gg.off[row + xa];
-                        rl_[rep] = (int)gg.off[row + xb + 1] - rs_[rep];
-                    }
+        // A (grid, dy, dz) x-row of 3 cells is one contiguous range of the cell-sorted points, trimmed
+        // to the cells whose box lies within sqrt(kCullLim) m of the query: every point of a trimmed
+        // cell is farther than 1 m (the margin dwarfs float rounding of the gaps and of d2), so it can
+        // never be a d2 < 1 neighbour.  c27 counts the untrimmed 27 cells (SURVEY 8(d) accounting).
+        constexpr float kCullLim = 1.0f + 1e-5f;
+        unsigned int c27 = 0;
+        auto resolve_row = [&](int rr, int& rs, int& rl) {
+            rs = 0;
+            rl = 0;
+            const GridView gg = pick_grid(TWO && rr >= 9, g2, g);
+            const int gn = gg.n, ox = gg.ox, oy = gg.oy, oz = gg.oz, nx = gg.nx, ny = gg.ny, nz = gg.nz;
+            const uint32_t* off = gg.off;
+            const int r9 = rr % 9, dyo = (r9 % 3) - 1, dzo = (r9 / 3) - 1;
+            const bool inside = gn > 0 && fx >= (float)(ox - 2) && fx <= (float)(ox + nx + 1) &&
+                                fy >= (float)(oy - 2) && fy <= (float)(oy + ny + 1) &&
+                                fz >= (float)(oz - 2) && fz <= (float)(oz + nz + 1);
+            if (!inside) return;
+            const int cx = (int)fx - ox, cy = (int)fy - oy + dyo, cz = (int)fz - oz + dzo;
+            const int xa = max(cx - 1, 0), xb = min(cx + 1, nx - 1);
+            if (cy < 0 || cy >= ny || cz < 0 || cz >= nz || xa > xb) return;
+            const uint32_t* row = off + ((size_t)cz * ny + cy) * nx;
+            // gaps from the query to the row's y and z slabs and to the x - 1 / x + 1 cells (whole metres)
+            const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
+            const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
+            const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
+            const float rem = kCullLim - gy * gy - gz * gz;
+            const float gl = w.x - fx, gr = fx + 1.f - w.x;
+            if (rem >= 0.f) {
+                // the trimmed range's two boundaries (addresses chosen before the loads)
+                const uint32_t s0 = row[gl * gl <= rem ? xa : max(cx, xa)];
+                const uint32_t s1 = row[gr * gr <= rem ? xb + 1 : min(cx + 1, xb + 1)];
+                if (s1 > s0) {
+                    rs = (int)s0;
+                    rl = (int)(s1 - s0);
                 }
             }
-        }
-        int st[NR], pre[NR + 1];
-        pre[0] = 0;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            st[r] = T == 1 ? rs_[r] : __shfl(rs_[r / T], r % T, T);
-            pre[r + 1] = pre[r] + (T == 1 ? rl_[r] : __shfl(rl_[r / T], r % T, T));
-        }
-        const int total = pre[NR];
+            if (bv.count27) c27 += row[xb + 1] - row[xa];
+        };
         uint64_t k[5] = {kSentinel, kSentinel, kSentinel, kSentinel, kSentinel};
         uint32_t kp[5] = {0, 0, 0, 0, 0};   // grid bit | sorted-array position of each kept key
         auto consider = [&](const float4 m, uint32_t tagged_pos) {
@@ -149,7 +171,8 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
             for (int rr = 0; rr < NR; ++rr) {
                 const float4* rp = (TWO && rr >= 9) ? g2.pts : g.pts;
                 const uint32_t tag = (TWO && rr >= 9) ? kGridBit : 0u;
-                const int a = st[rr], len = pre[rr + 1] - pre[rr];
+                int a, len;
+                resolve_row(rr, a, len);
                 int c = 0;
                 for (; c + kKnnUnroll <= len; c += kKnnUnroll) {
                     float4 m[kKnnUnroll];
@@ -161,6 +184,23 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
                 for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
             }
         } else {
+            // lane l resolves rows l, l + T, ...; the team shares them by shuffles
+            constexpr int REPS = (NR + T - 1) / T;
+            int rs_[REPS], rl_[REPS];
+#pragma unroll
+            for (int rep = 0; rep < REPS; ++rep) {
+                rs_[rep] = 0;
+                rl_[rep] = 0;
+                if (lane + rep * T < NR) resolve_row(lane + rep * T, rs_[rep], rl_[rep]);
+            }
+            int st[NR], pre[NR + 1];
+            pre[0] = 0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                st[r] = __shfl(rs_[r / T], r % T, T);
+                pre[r + 1] = pre[r] + __shfl(rl_[r / T], r % T, T);
+            }
+            const int total = pre[NR];
             // current row r: candidates [rpre, rend) map to pts[rbase + (v - rpre)]
             int r = 0, rpre = 0, rend = pre[1], rbase = st[0];
             const float4* rpts = g.pts;
@@ -221,9 +261,9 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
                 nn_out[i] = o;
             }
         }
-        if (lane == 0 && bv.n27) {
-            atomicAdd(&blk_n27, (unsigned long long)total);
-            atomicAdd(&blk_q, 1u);
+        if (bv.n27) {
+            if (c27) atomicAdd(&blk_n27, (unsigned long long)c27);
+            if (lane == 0) atomicAdd(&blk_q, 1u);
         }
     }
     __syncthreads();

@@ -65,6 +65,7 @@ struct BatchView {
     int max_parts;
     SolveState* st;          // [B]
     unsigned long long* n27; // [kCounterShards][16]: [0] candidates, [1] queries (may be null)
+    int count27;             // also accumulate [0] (extra cell-offset loads: diagnostics only)
     double* gn_rows;         // [B][feat_stride][4] grad + residual (GN only)
     double* partials_gn;     // [B][max_parts][kPacket] (GN only)
 };

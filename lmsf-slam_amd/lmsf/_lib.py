@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # lmsf-slam_amd/
-LIB_PATH = os.path.join(PKG_ROOT, "liblmsf_hip.so")
+LIB_PATH = os.environ.get("LMSF_LIB") or os.path.join(PKG_ROOT, "liblmsf_hip.so")   # LMSF_LIB: A/B builds
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "lmsf", "lmsf.h")
 
 OK, ERR_ARG, ERR_HIP, ERR_NO_MAP, ERR_CAPACITY, ERR_STATE = 0, -1, -2, -3, -4, -5
@@ -363,8 +363,10 @@ class Context:
         self._check(load().lmsf_eval(self.h, x.ctypes.data, out.ctypes.data))
         return out
 
-    def kernel_stats_reset(self, timing=True):
-        self._check(load().lmsf_kernel_stats_reset(self.h, int(timing)))
+    def kernel_stats_reset(self, timing=True, n27=False):
+        """timing: HIP-event time, launches and queries of the neighbour search; n27: the n27
+        accounting (extra loads inside the launch -- use it on untimed launches)."""
+        self._check(load().lmsf_kernel_stats_reset(self.h, (1 if timing else 0) | (2 if n27 else 0)))
 
     def kernel_stats(self):
         ks = KernelStats()

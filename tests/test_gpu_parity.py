@@ -269,7 +269,11 @@ def test_n27_accounting(lib, oracle_mod, small_workload):
     ctx.set_map(lib.SURF, wl.surf_map)
     ctx.set_scan(lib.EDGE, e)
     ctx.set_scan(lib.SURF, s)
-    ctx.kernel_stats_reset(True)
+    ctx.kernel_stats_reset(timing=True)   # timed launches carry no n27 accounting
+    ctx.match(wl.guess[2], len(e) + len(s))
+    ks = ctx.kernel_stats()
+    assert ks.queries == len(e) + len(s) and ks.n27_sum == 0
+    ctx.kernel_stats_reset(timing=False, n27=True)
     ctx.match(wl.guess[2], len(e) + len(s))
     ks = ctx.kernel_stats()
     assert ks.queries == len(e) + len(s)
