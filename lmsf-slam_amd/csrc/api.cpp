@@ -203,10 +203,12 @@ lmsf_status build_grid(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, int 
     if (n > m.cap) {
         hipFree(m.orig); hipFree(m.pts); hipFree(m.cell);
         m.orig = nullptr; m.pts = nullptr; m.cell = nullptr;
-        HIPCHK(c, dalloc(&m.orig, n));
-        HIPCHK(c, dalloc(&m.pts, n));
-        HIPCHK(c, dalloc(&m.cell, n));
-        m.cap = n;
+        const size_t cap = std::min(grow_cap(n, m.cap), (size_t)INT32_MAX);
+        m.cap = 0;
+        HIPCHK(c, dalloc(&m.orig, cap));
+        HIPCHK(c, dalloc(&m.pts, cap));
+        HIPCHK(c, dalloc(&m.cell, cap));
+        m.cap = cap;
     }
     // host or device source (unified addressing): the tracker rebuilds from device-resident maps
     HIPCHK(c, hipMemcpyAsync(m.orig, xyzi, n * sizeof(float4), hipMemcpyDefault, s));
@@ -225,13 +227,15 @@ lmsf_status build_grid(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, int 
         hipFree(m.counts); hipFree(m.off); hipFree(m.fill); hipFree(m.scan_tmp);
         m.counts = m.off = m.fill = nullptr;
         m.scan_tmp = nullptr;
-        HIPCHK(c, dalloc(&m.counts, cells + 1));
-        HIPCHK(c, dalloc(&m.off, cells + 1));
-        HIPCHK(c, dalloc(&m.fill, cells + 1));
+        const size_t cap = std::min(grow_cap(cells + 1, m.cells_cap), kMaxCells + 1);
+        m.cells_cap = 0;
+        HIPCHK(c, dalloc(&m.counts, cap));
+        HIPCHK(c, dalloc(&m.off, cap));
+        HIPCHK(c, dalloc(&m.fill, cap));
         m.scan_tmp_bytes = 0;
-        HIPCHK(c, exclusive_scan_u32(m.counts, m.off, cells + 1, nullptr, m.scan_tmp_bytes, s));
+        HIPCHK(c, exclusive_scan_u32(m.counts, m.off, cap, nullptr, m.scan_tmp_bytes, s));
         HIPCHK(c, hipMalloc(&m.scan_tmp, std::max<size_t>(m.scan_tmp_bytes, 16)));
-        m.cells_cap = cells + 1;
+        m.cells_cap = cap;
     }
     m.ox = bb[0]; m.oy = bb[1]; m.oz = bb[2];
     m.nx = nx; m.ny = ny; m.nz = nz;
@@ -600,10 +604,11 @@ lmsf_status lmsf_voxel_filter(lmsf_ctx* c, const float* xyzi, size_t n, float le
         HIPCHK(c, hipFree(c->vox_in));
         HIPCHK(c, hipFree(c->vox_out));
         c->vox_in = c->vox_out = nullptr;
+        const size_t cap = grow_cap(n, c->vox_cap);
         c->vox_cap = 0;
-        HIPCHK(c, hipMalloc((void**)&c->vox_in, n * sizeof(float4)));
-        HIPCHK(c, hipMalloc((void**)&c->vox_out, n * sizeof(float4)));
-        c->vox_cap = n;
+        HIPCHK(c, hipMalloc((void**)&c->vox_in, cap * sizeof(float4)));
+        HIPCHK(c, hipMalloc((void**)&c->vox_out, cap * sizeof(float4)));
+        c->vox_cap = cap;
     }
     HIPCHK(c, hipMemcpyAsync(c->vox_in, xyzi, n * sizeof(float4), hipMemcpyDefault, c->stream));
     int nv = 0;
@@ -696,12 +701,13 @@ lmsf_status lmsf_align_score(lmsf_ctx* c, const float* xyzi, size_t n, const flo
         c->align_in = nullptr;
         c->align_part_sum = nullptr;
         c->align_part_cnt = nullptr;
+        const size_t cap = std::min(grow_cap(n, c->align_cap), (size_t)INT32_MAX);
         c->align_cap = 0;
-        const size_t parts = (size_t)align_parts((int)n);
-        HIPCHK(c, hipMalloc((void**)&c->align_in, n * sizeof(float4)));
+        const size_t parts = (size_t)align_parts((int)cap);
+        HIPCHK(c, hipMalloc((void**)&c->align_in, cap * sizeof(float4)));
         HIPCHK(c, hipMalloc((void**)&c->align_part_sum, parts * sizeof(double)));
         HIPCHK(c, hipMalloc((void**)&c->align_part_cnt, parts * sizeof(unsigned int)));
-        c->align_cap = n;
+        c->align_cap = cap;
     }
     if (!c->align_out) HIPCHK(c, hipMalloc((void**)&c->align_out, 2 * sizeof(double)));
     Affine34f M;

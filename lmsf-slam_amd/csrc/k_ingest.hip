@@ -120,11 +120,13 @@ hipError_t Ingest::reserve(size_t n, size_t raw_bytes) {
     if (raw_bytes > raw_cap) {
         hipFree(raw);
         raw = nullptr;
+        const size_t rc = grow_cap(raw_bytes, raw_cap);
         raw_cap = 0;
-        if ((e = hipMalloc((void**)&raw, raw_bytes)) != hipSuccess) return e;
-        raw_cap = raw_bytes;
+        if ((e = hipMalloc((void**)&raw, rc)) != hipSuccess) return e;
+        raw_cap = rc;
     }
     if (n <= cap) return hipSuccess;
+    n = std::min(grow_cap(n, cap), (size_t)INT32_MAX);
     void* bufs[] = {a, b, keep, pos, scalars, tmp};
     for (void* p : bufs) hipFree(p);
     a = b = nullptr;

@@ -79,6 +79,24 @@ hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hi
     return hipGetLastError();
 }
 
+// The keyframe window concatenated in window order (LidarTrackerLocalMap's local map assembly):
+// one launch over all slots instead of a device-to-device copy per keyframe.
+__global__ void gather_slots_kernel(SlotTable tab, float4* out) {
+    const int total = tab.start[tab.n];
+    int k = 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        while (i >= tab.start[k + 1]) ++k;
+        out[i] = tab.src[k][i - tab.start[k]];
+    }
+}
+
+hipError_t launch_gather_slots(const SlotTable& tab, float4* out, hipStream_t s) {
+    const int total = tab.start[tab.n];
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_slots_kernel, dim3(min((total + 255) / 256, 4096)), dim3(256), 0, s, tab, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_map_bbox(const float4* pts, int n, int* bbox, hipStream_t s) {
     const int blocks = min((n + 255) / 256, 512);
     hipLaunchKernelGGL(map_bbox_kernel, dim3(max(blocks, 1)), dim3(256), 0, s, pts, n, bbox);

@@ -39,45 +39,58 @@ __device__ void reduce_parts(const BatchView& bv, int b, int nparts, double* tot
 
 __device__ double norm7(const double* x) {
     double s = 0.0;
+#pragma unroll
     for (int i = 0; i < 7; ++i) s += x[i] * x[i];
     return sqrt(s);
 }
 
-__device__ double grad_max_norm(const double* x, const double* g) {
+__device__ __forceinline__ double grad_max_norm(const double* x, const double* g) {
     double ng[6], xp[7];
+#pragma unroll
     for (int i = 0; i < 6; ++i) ng[i] = -g[i];
     pose_plus(x, ng, xp);
     double m = 0.0;
+#pragma unroll
     for (int i = 0; i < 7; ++i) m = fmax(m, fabs(x[i] - xp[i]));
     return m;
 }
 
-__device__ bool chol_solve6(const double* A, const double* b, double* x) {
+__device__ __forceinline__ bool chol_solve6(const double* A, const double* b, double* x) {
     double L[36];
+#pragma unroll
     for (int i = 0; i < 36; ++i) L[i] = 0.0;
+#pragma unroll
     for (int j = 0; j < 6; ++j) {
         double s = A[j * 6 + j];
+#pragma unroll
         for (int k = 0; k < j; ++k) s -= L[j * 6 + k] * L[j * 6 + k];
         if (!(s > 0.0)) return false;
         double ljj = sqrt(s);
         L[j * 6 + j] = ljj;
+#pragma unroll
         for (int i = j + 1; i < 6; ++i) {
             double t = A[i * 6 + j];
+#pragma unroll
             for (int k = 0; k < j; ++k) t -= L[i * 6 + k] * L[j * 6 + k];
             L[i * 6 + j] = t / ljj;
         }
     }
     double y[6];
+#pragma unroll
     for (int i = 0; i < 6; ++i) {
         double t = b[i];
+#pragma unroll
         for (int k = 0; k < i; ++k) t -= L[i * 6 + k] * y[k];
         y[i] = t / L[i * 6 + i];
     }
+#pragma unroll
     for (int i = 5; i >= 0; --i) {
         double t = y[i];
+#pragma unroll
         for (int k = i + 1; k < 6; ++k) t -= L[k * 6 + i] * x[k];
         x[i] = t / L[i * 6 + i];
     }
+#pragma unroll
     for (int i = 0; i < 6; ++i)
         if (!isfinite(x[i])) return false;
     return true;
@@ -85,20 +98,23 @@ __device__ bool chol_solve6(const double* A, const double* b, double* x) {
 
 // ComputeTrustRegionStep + HandleInvalidStep loop: leaves a candidate awaiting evaluation, or
 // terminates (max iterations / min radius).
-__device__ void compute_step(SolveState& S) {
+__device__ __forceinline__ void compute_step(SolveState& S) {
     while (true) {
         if (S.iteration >= kMaxInner) { S.done = 1; S.term = LMSF_TERM_MAX_ITERATIONS; return; }
         if (S.radius < 1e-32) { S.done = 1; S.term = LMSF_TERM_PARAMETER_TOL; return; }
         ++S.iteration;
         double A[36], Hs[36], gs[6], nb[6], step[6];
+#pragma unroll
         for (int i = 0; i < 6; ++i) {
             gs[i] = S.g[i] * S.s[i];
+#pragma unroll
             for (int j = 0; j < 6; ++j) {
                 const int a = i <= j ? hidx(i, j) : hidx(j, i);
                 Hs[i * 6 + j] = S.H[a] * S.s[i] * S.s[j];
                 A[i * 6 + j] = Hs[i * 6 + j];
             }
         }
+#pragma unroll
         for (int i = 0; i < 6; ++i) {
             const double dg = fmin(fmax(Hs[i * 6 + i], 1e-6), 1e32);
             A[i * 6 + i] += dg / S.radius;
@@ -108,9 +124,11 @@ __device__ void compute_step(SolveState& S) {
         double mcc = 0.0;
         if (ok) {
             double sg = 0.0, sHs = 0.0;
+#pragma unroll
             for (int i = 0; i < 6; ++i) {
                 sg += step[i] * gs[i];
                 double t = 0.0;
+#pragma unroll
                 for (int j = 0; j < 6; ++j) t += Hs[i * 6 + j] * step[j];
                 sHs += step[i] * t;
             }
@@ -122,6 +140,7 @@ __device__ void compute_step(SolveState& S) {
             continue;
         }
         double delta[6];
+#pragma unroll
         for (int i = 0; i < 6; ++i) delta[i] = step[i] * S.s[i];
         pose_plus(S.x, delta, S.xc);
         S.mcc = mcc;

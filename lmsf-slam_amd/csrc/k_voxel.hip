@@ -91,8 +91,9 @@ void VoxelFilter::release() {
     *this = VoxelFilter();
 }
 
-hipError_t VoxelFilter::reserve(size_t n) {
-    if (n <= cap) return hipSuccess;
+hipError_t VoxelFilter::reserve(size_t need) {
+    if (need <= cap) return hipSuccess;
+    const size_t n = std::min(grow_cap(need, cap), (size_t)INT32_MAX);
     release();
     hipError_t e;
 #define VALLOC(p, bytes) if ((e = hipMalloc((void**)&(p), (bytes))) != hipSuccess) return e

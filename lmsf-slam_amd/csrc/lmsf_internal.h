@@ -13,6 +13,10 @@ constexpr int kFitMaxPerThread = 4;  // queries per thread in the fit / first-ev
 constexpr int kFitBlockMax = 256 * kFitMaxPerThread;
 constexpr int kEvalPerThread = 4;    // records per thread in the LM evaluation kernel
 constexpr int kEvalBlock = 256 * kEvalPerThread;
+// Workspace growth: when a request exceeds the capacity, allocate 1.5x (a growing or jittering
+// request -- the keyframe window, a varying scan size -- then reallocates rarely: hipFree
+// synchronises the device and costs ~0.5 ms on the tracking path).
+inline size_t grow_cap(size_t need, size_t cap) { return need > cap + cap / 2 ? need : cap + cap / 2; }
 constexpr int kRingMax = 8192;       // points per ring handled by the extraction kernel
 constexpr int kSortMax = 2048;       // points per sector (ring / 6 + 5, padded to a power of two)
 constexpr int kMaxRings = 128;
@@ -130,6 +134,14 @@ hipError_t launch_extract(const ExtractView& ev, hipStream_t s);
 struct Affine34 { double m[12]; };   // row-major 3x4 of an Isometry3d matrix
 // pcl::transformPointCloud(cloud, out, Matrix4d) per point: float(m00 x + m01 y + m02 z + m03), double math
 hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hipStream_t s);
+// Concatenation of up to kSlotTable device arrays (kernel-argument table, start[] exclusive prefix).
+constexpr int kSlotTable = 32;
+struct SlotTable {
+    const float4* src[kSlotTable];
+    int start[kSlotTable + 1];
+    int n;
+};
+hipError_t launch_gather_slots(const SlotTable& tab, float4* out, hipStream_t s);
 
 // ---- 1-NN alignment fitness (k_align.hip): AlignmentScore (REG/alignEvaluate.hpp:55-87)
 struct Affine34f { float m[12]; };   // row-major 3x4 of an Eigen::Matrix4f

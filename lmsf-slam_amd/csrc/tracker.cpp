@@ -13,6 +13,7 @@
 // -R^T t) and its quaternion <-> matrix conversions (the Ceres path converts at Solve, ceres_...:103, :128).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -192,11 +193,16 @@ lmsf_status commit(lmsf_tracker* t) {
         const int W = (int)w.slots.size();
         float4* dst = w.leaf > 0 ? w.wcat : w.concat;
         size_t nw = 0;
-        for (int i = 0; i < w.count; ++i) {
-            const int k = (w.head + i) % W;
-            TCHK(t, hipMemcpyAsync(dst + nw, w.slots[k], (size_t)w.sizes[k] * sizeof(float4),
-                                   hipMemcpyDeviceToDevice, s));
-            nw += (size_t)w.sizes[k];
+        for (int i0 = 0; i0 < w.count; i0 += kSlotTable) {         // keyframes in window order
+            SlotTable tab{};
+            tab.n = std::min(kSlotTable, w.count - i0);
+            for (int i = 0; i < tab.n; ++i) {
+                const int k = (w.head + i0 + i) % W;
+                tab.src[i] = w.slots[k];
+                tab.start[i + 1] = tab.start[i] + w.sizes[k];
+            }
+            TCHK(t, launch_gather_slots(tab, dst + nw, s));
+            nw += (size_t)tab.start[tab.n];
         }
         if (w.leaf > 0 && nw) {                                   // VoxelGrid of the window
             int nv = 0;
