@@ -84,6 +84,8 @@ struct lmsf_ctx {
     int* ring_src = nullptr;
     float4* surf_stage = nullptr;
     int* surf_stage_src = nullptr;
+    double* sort_key = nullptr;
+    int* sort_idx = nullptr;
     float4* edge_stage = nullptr;
     int* edge_stage_src = nullptr;
     int* ring_edge_cnt = nullptr;
@@ -165,6 +167,8 @@ struct lmsf_ctx {
         e.ring_src = ring_src;
         e.surf_stage = surf_stage;
         e.surf_stage_src = surf_stage_src;
+        e.sort_key = sort_key;
+        e.sort_idx = sort_idx;
         e.edge_stage = edge_stage;
         e.edge_stage_src = edge_stage_src;
         e.ring_edge_cnt = ring_edge_cnt;
@@ -376,8 +380,8 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     }
     void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
-                    c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->edge_stage,
-                    c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->d_error};
+                    c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->sort_key,
+                    c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->d_error};
     for (void* p : bufs) hipFree(p);
     c->voxel.release();
     hipFree(c->vox_in);
@@ -449,6 +453,8 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->ring_src, B * R));
     CHK(dalloc(&c->surf_stage, B * R));
     CHK(dalloc(&c->surf_stage_src, B * R));
+    CHK(dalloc(&c->sort_key, B * R));
+    CHK(dalloc(&c->sort_idx, B * R));
     CHK(dalloc(&c->edge_stage, B * kMaxRings * kEdgePerRing));
     CHK(dalloc(&c->edge_stage_src, B * kMaxRings * kEdgePerRing));
     CHK(dalloc(&c->ring_edge_cnt, B * kMaxRings));

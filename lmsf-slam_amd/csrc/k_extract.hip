@@ -12,9 +12,9 @@
 //   ring_count   tiles of kTile raw points: ring id per point, per-tile ring histogram
 //   ring_offsets per scan: exclusive scan (ring-major) -> stable ring-ordered positions
 //   ring_scatter stable multisplit (wave ballots) into ring order
-//   ring_features one workgroup per ring: automaton (wave-ballot walk), 6 sectors of
-//                 {curvature, register-resident bitonic sort, wave-ballot greedy pick, block-scan
-//                 compaction}
+//   sector_sort  one workgroup per (sector, ring): curvature + register-resident bitonic sort
+//   ring_features one workgroup per ring: automaton (wave-ballot walk), then per sector in order
+//                 {wave-ballot greedy pick over the sorted list, block-scan compaction}
 //   concat       per scan: edges (ring order) then surfs (ring order) into the feature array
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -308,7 +308,64 @@ __device__ void bitonic_sort_regs(double* key, int* kidx, int npow) {
     __syncthreads();
 }
 
-// One workgroup per (ring, scan).
+// Sector geometry of featureExtractionFromSector (FX:145-156): 6 sectors of a ring of `size`.
+__device__ __forceinline__ void sector_bounds(int size, int k, int& s0, int& n) {
+    const int sector_length = (size - 10) / 6;          // (int)((total/6) + 0.5) with int division
+    s0 = 5 + sector_length * k;
+    const int e0 = (k == 5) ? size - 6 : s0 + sector_length - 1;
+    n = e0 - s0 + 1;
+}
+
+// One workgroup per (sector, ring, scan): curvature (FX:84-94) of the sector's points and their
+// register-resident bitonic sort by (c, index); written to sort_key / sort_idx at the sector's
+// place in the ring.  The 6 sectors of a ring sort concurrently; only the greedy pick, which
+// carries disable marks across sectors, stays sequential (ring_features_kernel).
+__global__ __launch_bounds__(256) void sector_sort_kernel(ExtractView ev) {
+    __shared__ double key[kSortMax];
+    __shared__ int kidx[kSortMax];
+    const int r = blockIdx.x / 6, k = blockIdx.x % 6, b = blockIdx.y;
+    const int* rs = ev.ring_start + (size_t)b * (kMaxRings + 1);
+    const int start = rs[r];
+    const int size = rs[r + 1] - start;
+    if (size < 20 || size > kRingMax) return;            // ring_features_kernel reports
+    int s0, n;
+    sector_bounds(size, k, s0, n);
+    if (n > kSortMax) return;
+    const float4* pts = ev.ring_pts + (size_t)b * ev.raw_stride + start;
+    int npow = 1;
+    while (npow < n) npow <<= 1;
+    for (int i = threadIdx.x; i < npow; i += 256) {
+        if (i < n) {
+            const int j = s0 + i;
+            const float4 m5 = pts[j - 5], m4 = pts[j - 4], m3 = pts[j - 3], m2 = pts[j - 2], m1 = pts[j - 1];
+            const float4 p0 = pts[j];
+            const float4 q1 = pts[j + 1], q2 = pts[j + 2], q3 = pts[j + 3], q4 = pts[j + 4], q5 = pts[j + 5];
+            const float fx = m5.x + m4.x + m3.x + m2.x + m1.x - 10 * p0.x + q1.x + q2.x + q3.x + q4.x + q5.x;
+            const float fy = m5.y + m4.y + m3.y + m2.y + m1.y - 10 * p0.y + q1.y + q2.y + q3.y + q4.y + q5.y;
+            const float fz = m5.z + m4.z + m3.z + m2.z + m1.z - 10 * p0.z + q1.z + q2.z + q3.z + q4.z + q5.z;
+            const double dx = fx, dy = fy, dz = fz;
+            key[i] = dx * dx + dy * dy + dz * dz;
+            kidx[i] = j;
+        } else {
+            key[i] = __builtin_huge_val();
+            kidx[i] = 0x7fffffff;
+        }
+    }
+    __syncthreads();
+    if (npow <= 256) bitonic_sort_regs<1>(key, kidx, npow);
+    else if (npow <= 512) bitonic_sort_regs<2>(key, kidx, npow);
+    else if (npow <= 1024) bitonic_sort_regs<4>(key, kidx, npow);
+    else bitonic_sort_regs<8>(key, kidx, npow);
+    double* okey = ev.sort_key + (size_t)b * ev.raw_stride + start + s0;
+    int* oidx = ev.sort_idx + (size_t)b * ev.raw_stride + start + s0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        okey[i] = key[i];
+        oidx[i] = kidx[i];
+    }
+}
+
+// One workgroup per (ring, scan): bad-point automaton, then per sector in order the greedy edge
+// pick over the pre-sorted curvature list and the surf compaction.
 __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
     __shared__ uint8_t dis[kRingMax];
     __shared__ uint8_t flag[kRingMax];
@@ -337,46 +394,25 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
     if (tid == 0) { sh_ec = 0; sh_sc = 0; sh_err = 0; }
     __syncthreads();
     ring_bad_points<256>(ev, pts, size, dis, flag);
-    const int total_points = size - 10;
-    const int sector_length = total_points / 6;          // (int)((total/6) + 0.5) with int division
     const double thresh = (double)ev.edge_thresh;
     float4* estage = ev.edge_stage + ((size_t)b * kMaxRings + r) * kEdgePerRing;
     int* estage_src = ev.edge_stage_src + ((size_t)b * kMaxRings + r) * kEdgePerRing;
     float4* sstage = ev.surf_stage + (size_t)b * ev.raw_stride + start;
     int* sstage_src = ev.surf_stage_src + (size_t)b * ev.raw_stride + start;
     for (int k = 0; k < 6; ++k) {
-        const int s0 = 5 + sector_length * k;
-        const int e0 = (k == 5) ? size - 6 : s0 + sector_length - 1;
-        const int n = e0 - s0 + 1;
+        int s0, n;
+        sector_bounds(size, k, s0, n);
         if (n > kSortMax) {
             if (tid == 0) { atomicOr(ev.error, 2); sh_err = 1; }
             break;
         }
-        int npow = 1;
-        while (npow < n) npow <<= 1;
-        for (int i = tid; i < npow; i += 256) {
-            if (i < n) {
-                const int j = s0 + i;
-                const float4 m5 = pts[j - 5], m4 = pts[j - 4], m3 = pts[j - 3], m2 = pts[j - 2], m1 = pts[j - 1];
-                const float4 p0 = pts[j];
-                const float4 q1 = pts[j + 1], q2 = pts[j + 2], q3 = pts[j + 3], q4 = pts[j + 4], q5 = pts[j + 5];
-                const float fx = m5.x + m4.x + m3.x + m2.x + m1.x - 10 * p0.x + q1.x + q2.x + q3.x + q4.x + q5.x;
-                const float fy = m5.y + m4.y + m3.y + m2.y + m1.y - 10 * p0.y + q1.y + q2.y + q3.y + q4.y + q5.y;
-                const float fz = m5.z + m4.z + m3.z + m2.z + m1.z - 10 * p0.z + q1.z + q2.z + q3.z + q4.z + q5.z;
-                const double dx = fx, dy = fy, dz = fz;
-                key[i] = dx * dx + dy * dy + dz * dz;
-                kidx[i] = j;
-            } else {
-                key[i] = __builtin_huge_val();
-                kidx[i] = 0x7fffffff;
-            }
+        const double* skey = ev.sort_key + (size_t)b * ev.raw_stride + start + s0;
+        const int* sidx = ev.sort_idx + (size_t)b * ev.raw_stride + start + s0;
+        for (int i = tid; i < n; i += 256) {
+            key[i] = skey[i];
+            kidx[i] = sidx[i];
         }
         __syncthreads();
-        // bitonic sort ascending by (c, index), register-resident (bitonic_sort_regs)
-        if (npow <= 256) bitonic_sort_regs<1>(key, kidx, npow);
-        else if (npow <= 512) bitonic_sort_regs<2>(key, kidx, npow);
-        else if (npow <= 1024) bitonic_sort_regs<4>(key, kidx, npow);
-        else bitonic_sort_regs<8>(key, kidx, npow);
         // greedy edge pick, largest curvature first (FX:157-195), one wave
         if (tid < 64) {
             int pos = n - 1, picked = 0, ec = sh_ec;
@@ -484,6 +520,7 @@ hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
     hipLaunchKernelGGL(ring_count_kernel, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(ring_offsets_kernel, dim3(ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(ring_scatter_kernel, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
+    hipLaunchKernelGGL(sector_sort_kernel, dim3(ev.n_scans * 6, ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(ring_features_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
     const int cblocks = min(64, (ev.raw_stride + 255) / 256);
     hipLaunchKernelGGL(concat_kernel, dim3(max(cblocks, 1), ev.B), dim3(256), 0, s, ev);

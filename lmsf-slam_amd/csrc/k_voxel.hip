@@ -68,21 +68,30 @@ __global__ void voxel_start_kernel(const uint32_t* head, const uint32_t* seg, in
     }
 }
 
-__global__ void voxel_mean_kernel(const float4* pts, const int* idx_sorted, const int* start, const int* nseg,
-                                  float4* out) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= *nseg) return;
-    const int a = start[s], b = start[s + 1];
-    double sx = 0, sy = 0, sz = 0, sw = 0;
-    for (int k = a; k < b; ++k) {                  // input order inside the voxel
-        const float4 p = pts[idx_sorted[k]];
-        sx += p.x;
-        sy += p.y;
-        sz += p.z;
-        sw += p.w;
+// One wave per voxel (grid-stride over the voxels): the wave gathers 64 of the voxel's points at a
+// time and every lane adds them in sorted (= input) order through readlane, so the sums are the
+// sequential double sums of the thread-per-voxel form while the gathers run 64 wide.
+__global__ __launch_bounds__(256) void voxel_mean_kernel(const float4* pts, const int* idx_sorted, const int* start,
+                                                         const int* nseg, float4* out) {
+    const int lane = threadIdx.x & 63;
+    const int nw = (gridDim.x * blockDim.x) >> 6;
+    const int ns = *nseg;
+    for (int s = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; s < ns; s += nw) {
+        const int a = start[s], b = start[s + 1];
+        double sx = 0, sy = 0, sz = 0, sw = 0;
+        for (int c = a; c < b; c += 64) {
+            const int m = min(64, b - c);
+            const float4 p = lane < m ? pts[idx_sorted[c + lane]] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int j = 0; j < m; ++j) {
+                sx += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.x), j));
+                sy += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.y), j));
+                sz += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.z), j));
+                sw += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.w), j));
+            }
+        }
+        const double cnt = (double)(b - a);
+        if (lane == 0) out[s] = make_float4((float)(sx / cnt), (float)(sy / cnt), (float)(sz / cnt), (float)(sw / cnt));
     }
-    const double c = (double)(b - a);
-    out[s] = make_float4((float)(sx / c), (float)(sy / c), (float)(sz / c), (float)(sw / c));
 }
 
 void VoxelFilter::release() {
@@ -145,7 +154,7 @@ hipError_t VoxelFilter::run(const float4* in, int n, float leaf, float4* out, in
     tb = tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, head, seg, n, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(voxel_start_kernel, g, b, 0, s, head, seg, n, start, nseg);
-    hipLaunchKernelGGL(voxel_mean_kernel, g, b, 0, s, in, idx_sorted, start, nseg, out);
+    hipLaunchKernelGGL(voxel_mean_kernel, dim3(min((n + 255) / 256, 4096)), b, 0, s, in, idx_sorted, start, nseg, out);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipMemcpyAsync(n_out, nseg, sizeof(int), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     return hipStreamSynchronize(s);

@@ -112,6 +112,8 @@ struct ExtractView {
     int* ring_src;               // [B][raw_stride] raw index of each ring-ordered point
     float4* surf_stage;          // [B][raw_stride]   per ring at ring_start
     int* surf_stage_src;         // [B][raw_stride]
+    double* sort_key;            // [B][raw_stride] per sector at ring_start + sector start: curvature
+    int* sort_idx;               //                 ascending (c, index), ring-local indices
     float4* edge_stage;          // [B][kMaxRings * kEdgePerRing]
     int* edge_stage_src;         // [B][kMaxRings * kEdgePerRing]
     int* ring_edge_cnt;          // [B][kMaxRings]
