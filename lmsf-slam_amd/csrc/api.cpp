@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -28,11 +29,11 @@ struct DevMap {
     uint32_t* fill = nullptr;
     void* scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
-    int ox = 0, oy = 0, oz = 0, nx = 0, ny = 0, nz = 0;
+    int ox = 0, oy = 0, oz = 0, nx = 0, ny = 0, nz = 0, sx = 1;
 
     GridView view() const {
         GridView g;
-        g.ox = ox; g.oy = oy; g.oz = oz; g.nx = nx; g.ny = ny; g.nz = nz;
+        g.ox = ox; g.oy = oy; g.oz = oz; g.nx = nx; g.ny = ny; g.nz = nz; g.sx = sx;
         g.off = off; g.pts = pts; g.orig = orig; g.n = n;
         return g;
     }
@@ -40,6 +41,16 @@ struct DevMap {
 
 constexpr size_t kMaxCells = (size_t)1 << 30;   // 4 GiB of offsets: refuse larger map extents
 constexpr int kEventPairs = 4096;
+
+// x-slices per metre of the map grids (LMSF_GRID_SX = 1 | 2 | 4 | 8 overrides; measured in DESIGN.md)
+int grid_slices() {
+    static const int sx = [] {
+        const char* e = getenv("LMSF_GRID_SX");
+        const int v = e ? atoi(e) : 4;
+        return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 4;
+    }();
+    return sx;
+}
 
 template <typename T>
 hipError_t dalloc(T** p, size_t count) {
@@ -219,7 +230,8 @@ lmsf_status build_grid(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, int 
     int* d_bbox = c->d_error + 4;  // scratch ints after the error word
     const int init[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
     HIPCHK(c, hipMemcpyAsync(d_bbox, init, sizeof init, hipMemcpyHostToDevice, s));
-    HIPCHK(c, launch_map_bbox(m.orig, (int)n, d_bbox, s));
+    const int sx = grid_slices();
+    HIPCHK(c, launch_map_bbox(m.orig, (int)n, sx, d_bbox, s));
     int bb[6];
     HIPCHK(c, hipMemcpyAsync(bb, d_bbox, sizeof bb, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
@@ -242,10 +254,10 @@ lmsf_status build_grid(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, int 
         m.cells_cap = cap;
     }
     m.ox = bb[0]; m.oy = bb[1]; m.oz = bb[2];
-    m.nx = nx; m.ny = ny; m.nz = nz;
+    m.nx = nx; m.ny = ny; m.nz = nz; m.sx = sx;
     HIPCHK(c, hipMemsetAsync(m.counts, 0, (cells + 1) * sizeof(uint32_t), s));
     HIPCHK(c, hipMemsetAsync(m.fill, 0, (cells + 1) * sizeof(uint32_t), s));
-    HIPCHK(c, launch_map_count(m.orig, (int)n, m.ox, m.oy, m.oz, nx, ny, nz, m.cell, m.counts, s));
+    HIPCHK(c, launch_map_count(m.orig, (int)n, sx, m.ox, m.oy, m.oz, nx, ny, nz, m.cell, m.counts, s));
     size_t tb = m.scan_tmp_bytes;
     HIPCHK(c, exclusive_scan_u32(m.counts, m.off, cells + 1, m.scan_tmp, tb, s));
     HIPCHK(c, launch_map_scatter(m.orig, (int)n, m.cell, m.off, m.fill, m.pts, base, s));

@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(kAlignBlock) align_kernel(GridView g, const fl
         const float qx = M.m[0] * p.x + M.m[1] * p.y + M.m[2] * p.z + M.m[3];
         const float qy = M.m[4] * p.x + M.m[5] * p.y + M.m[6] * p.z + M.m[7];
         const float qz = M.m[8] * p.x + M.m[9] * p.y + M.m[10] * p.z + M.m[11];
-        const int cx = acell(qx, g.ox), cy = acell(qy, g.oy), cz = acell(qz, g.oz);
+        const int cy = acell(qy, g.oy), cz = acell(qz, g.oz);
         // rows / cells whose box lies farther than sqrt(lim) are skipped; lim is inflated so that
         // float rounding of d2 can never admit a skipped point
         const double lim = thresh * (1.0 + 1e-5) + 1e-7;
@@ -48,9 +48,9 @@ __global__ void __launch_bounds__(kAlignBlock) align_kernel(GridView g, const fl
                 const double ddy = fmax(0.0, fmax(by - (double)qy, (double)qy - (by + 1.0)));
                 const double rem = lim - ddz * ddz - ddy * ddy;
                 if (rem < 0.0) continue;
-                const double r = sqrt(rem);
-                const int x0 = max(max(cx - R, 0), (int)fmax(floor((double)qx - r), -1073741824.0) - g.ox);
-                const int x1 = min(min(cx + R, g.nx - 1), (int)fmin(floor((double)qx + r), 1073741824.0) - g.ox);
+                const double r = sqrt(rem);       // x-window in slices (g.sx per metre)
+                const int x0 = max(0, (int)fmax(floor(((double)qx - r) * g.sx), -1073741824.0) - g.ox);
+                const int x1 = min(g.nx - 1, (int)fmin(floor(((double)qx + r) * g.sx), 1073741824.0) - g.ox);
                 if (x0 > x1) continue;
                 const size_t row = ((size_t)z * g.ny + y) * g.nx;
                 const uint32_t a = g.off[row + x0], b = g.off[row + x1 + 1];

@@ -1,4 +1,5 @@
-// Device neighbour index of a LOAM feature map: dense 1 m cell grid with cell-sorted points.
+// Device neighbour index of a LOAM feature map: dense 1 m cell grid with cell-sorted points,
+// each cell cut into sx x-slices (the rows the search trims to the query's x-window).
 //
 // Replaces FeatureMatch::SetSearchTarget -> pcl::KdTreeFLANN::setInputCloud
 // (REG/FeatureMatch/FeatureMatchBase.hpp:40-44), rebuilt whenever the local map changes
@@ -6,7 +7,8 @@
 // (search_thresh_ = 1.0, FeatureMatchBase.hpp:29), so every map point with d^2 < 1 to a query
 // lies in the 3x3x3 cells around the query's cell; cell = floor(coord) - origin is exact in float.
 // Layout in HBM: float4 pts[n] sorted by linear cell (x fastest: the 3 x-neighbours of a cell are
-// one contiguous range), uint32 off[cells + 1]; w of each sorted point = its original index.
+// one contiguous range, and so are the slices of a row), uint32 off[slices + 1]; w of each sorted
+// point = its original index.  x-slice = floor(x * sx) (exact: sx is a power of two).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -15,11 +17,11 @@
 
 namespace lmsf {
 
-__global__ void __launch_bounds__(256) map_bbox_kernel(const float4* pts, int n, int* bbox) {
+__global__ void __launch_bounds__(256) map_bbox_kernel(const float4* pts, int n, float sx, int* bbox) {
     int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const float4 p = pts[i];
-        const float c[3] = {floorf(p.x), floorf(p.y), floorf(p.z)};
+        const float c[3] = {floorf(p.x * sx), floorf(p.y), floorf(p.z)};
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             // coordinates beyond +-2^30 m are clamped (they cannot be matched anyway)
@@ -31,12 +33,12 @@ __global__ void __launch_bounds__(256) map_bbox_kernel(const float4* pts, int n,
     block_bbox_commit<256>(lo, hi, bbox);
 }
 
-__global__ void map_count_kernel(const float4* pts, int n, int ox, int oy, int oz, int nx, int ny, int nz,
+__global__ void map_count_kernel(const float4* pts, int n, float sx, int ox, int oy, int oz, int nx, int ny, int nz,
                                  int* cell, uint32_t* counts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float4 p = pts[i];
-    const int cx = (int)fminf(fmaxf(floorf(p.x), -1073741824.f), 1073741824.f) - ox;
+    const int cx = (int)fminf(fmaxf(floorf(p.x * sx), -1073741824.f), 1073741824.f) - ox;
     const int cy = (int)fminf(fmaxf(floorf(p.y), -1073741824.f), 1073741824.f) - oy;
     const int cz = (int)fminf(fmaxf(floorf(p.z), -1073741824.f), 1073741824.f) - oz;
     const int c = (cz * ny + cy) * nx + cx;
@@ -97,16 +99,16 @@ hipError_t launch_gather_slots(const SlotTable& tab, float4* out, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_map_bbox(const float4* pts, int n, int* bbox, hipStream_t s) {
+hipError_t launch_map_bbox(const float4* pts, int n, int sx, int* bbox, hipStream_t s) {
     const int blocks = min((n + 255) / 256, 512);
-    hipLaunchKernelGGL(map_bbox_kernel, dim3(max(blocks, 1)), dim3(256), 0, s, pts, n, bbox);
+    hipLaunchKernelGGL(map_bbox_kernel, dim3(max(blocks, 1)), dim3(256), 0, s, pts, n, (float)sx, bbox);
     return hipGetLastError();
 }
 
-hipError_t launch_map_count(const float4* pts, int n, int ox, int oy, int oz, int nx, int ny, int nz, int* cell,
-                            uint32_t* counts, hipStream_t s) {
-    hipLaunchKernelGGL(map_count_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pts, n, ox, oy, oz, nx, ny, nz,
-                       cell, counts);
+hipError_t launch_map_count(const float4* pts, int n, int sx, int ox, int oy, int oz, int nx, int ny, int nz,
+                            int* cell, uint32_t* counts, hipStream_t s) {
+    hipLaunchKernelGGL(map_count_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pts, n, (float)sx, ox, oy, oz, nx,
+                       ny, nz, cell, counts);
     return hipGetLastError();
 }
 

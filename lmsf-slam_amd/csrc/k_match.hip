@@ -73,6 +73,7 @@ __device__ __forceinline__ GridView pick_grid(bool c, const GridView& a, const G
     r.pts = c ? a.pts : b.pts;
     r.orig = c ? a.orig : b.orig;
     r.n = c ? a.n : b.n;
+    r.sx = c ? a.sx : b.sx;
     return r;
 }
 
@@ -107,38 +108,40 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
         const float4 p = bv.feat[(size_t)b * bv.feat_stride + q];
         const float3 w = associate(P, p);
         const float fx = floorf(w.x), fy = floorf(w.y), fz = floorf(w.z);
-        // A (grid, dy, dz) x-row of 3 cells is one contiguous range of the cell-sorted points, trimmed
-        // to the cells whose box lies within sqrt(kCullLim) m of the query: every point of a trimmed
-        // cell is farther than 1 m (the margin dwarfs float rounding of the gaps and of d2), so it can
-        // never be a d2 < 1 neighbour.  c27 counts the untrimmed 27 cells (SURVEY 8(d) accounting).
+        // A (grid, dy, dz) x-row of 3 cells (3 sx slices) is one contiguous range of the sorted points.
+        // With rem = kCullLim - gy^2 - gz^2 (gy, gz: the query's gaps to the row's y and z slabs), only
+        // points with |x - qx| <= sqrt(rem) can have d2 < 1, so the row is trimmed to the slices
+        // meeting [qx - sqrt(rem), qx + sqrt(rem)] (window edges in double from the exact float query;
+        // the kCullLim margin dwarfs float rounding of the gaps, of sqrt and of d2).  c27 counts the
+        // untrimmed 27 cells (SURVEY 8(d) accounting).
         constexpr float kCullLim = 1.0f + 1e-5f;
         unsigned int c27 = 0;
         auto resolve_row = [&](int rr, int& rs, int& rl) {
             rs = 0;
             rl = 0;
             const GridView gg = pick_grid(TWO && rr >= 9, g2, g);
-            const int gn = gg.n, ox = gg.ox, oy = gg.oy, oz = gg.oz, nx = gg.nx, ny = gg.ny, nz = gg.nz;
+            const int gn = gg.n, ox = gg.ox, oy = gg.oy, oz = gg.oz, nx = gg.nx, ny = gg.ny, nz = gg.nz, sx = gg.sx;
             const uint32_t* off = gg.off;
             const int r9 = rr % 9, dyo = (r9 % 3) - 1, dzo = (r9 / 3) - 1;
-            const bool inside = gn > 0 && fx >= (float)(ox - 2) && fx <= (float)(ox + nx + 1) &&
+            const float fxs = fx * (float)sx;
+            const bool inside = gn > 0 && fxs >= (float)(ox - 2 * sx) && fxs <= (float)(ox + nx + sx) &&
                                 fy >= (float)(oy - 2) && fy <= (float)(oy + ny + 1) &&
                                 fz >= (float)(oz - 2) && fz <= (float)(oz + nz + 1);
             if (!inside) return;
-            const int cx = (int)fx - ox, cy = (int)fy - oy + dyo, cz = (int)fz - oz + dzo;
-            const int xa = max(cx - 1, 0), xb = min(cx + 1, nx - 1);
+            const int cxs = (int)fxs - ox, cy = (int)fy - oy + dyo, cz = (int)fz - oz + dzo;
+            const int xa = max(cxs - sx, 0), xb = min(cxs + 2 * sx - 1, nx - 1);
             if (cy < 0 || cy >= ny || cz < 0 || cz >= nz || xa > xb) return;
             const uint32_t* row = off + ((size_t)cz * ny + cy) * nx;
-            // gaps from the query to the row's y and z slabs and to the x - 1 / x + 1 cells (whole metres)
             const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
             const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
             const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
             const float rem = kCullLim - gy * gy - gz * gz;
-            const float gl = w.x - fx, gr = fx + 1.f - w.x;
             if (rem >= 0.f) {
-                // the trimmed range's two boundaries (addresses chosen before the loads)
-                const uint32_t s0 = row[gl * gl <= rem ? xa : max(cx, xa)];
-                const uint32_t s1 = row[gr * gr <= rem ? xb + 1 : min(cx + 1, xb + 1)];
-                if (s1 > s0) {
+                const double r = (double)sqrtf(rem);
+                const int sa = max(xa, (int)floor(((double)w.x - r) * sx) - ox);
+                const int sb = min(xb, (int)floor(((double)w.x + r) * sx) - ox);
+                if (sa <= sb) {
+                    const uint32_t s0 = row[sa], s1 = row[sb + 1];
                     rs = (int)s0;
                     rl = (int)(s1 - s0);
                 }

@@ -27,8 +27,9 @@ constexpr int kCounterShards = 64;   // candidate / query counters, 16 u64 (128 
 // Dense cell grid over one feature map: cell = floor(coord) - origin, 1 m cells (the match
 // radius: search_thresh_ = 1.0 squared metres, REG/FeatureMatch/FeatureMatchBase.hpp:29).
 struct GridView {
-    int ox, oy, oz;
-    int nx, ny, nz;
+    int ox, oy, oz;          // origin: x in slices, y and z in metres
+    int nx, ny, nz;          // extent: x in slices (sx per metre), y and z in 1 m cells
+    int sx;                  // x-slices per metre (power of two): a 1 m cell = sx consecutive slices
     const uint32_t* off;   // nx*ny*nz + 1 exclusive offsets into pts
     const float4* pts;     // points sorted by cell; w = original index (int bits)
     const float4* orig;    // points in the caller's order (x, y, z, intensity)
@@ -75,8 +76,8 @@ struct BatchView {
 };
 
 // ---- launchers (each enqueues on `stream`, never synchronises)
-hipError_t launch_map_bbox(const float4* pts, int n, int* bbox, hipStream_t s);
-hipError_t launch_map_count(const float4* pts, int n, int ox, int oy, int oz, int nx, int ny, int nz,
+hipError_t launch_map_bbox(const float4* pts, int n, int sx, int* bbox, hipStream_t s);
+hipError_t launch_map_count(const float4* pts, int n, int sx, int ox, int oy, int oz, int nx, int ny, int nz,
                             int* cell, uint32_t* counts, hipStream_t s);
 // sorted[] w = base + original index (base > 0 for a keyframe window behind a prior map)
 hipError_t launch_map_scatter(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
