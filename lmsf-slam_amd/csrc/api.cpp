@@ -30,11 +30,12 @@ struct DevMap {
     void* scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
     int ox = 0, oy = 0, oz = 0, nx = 0, ny = 0, nz = 0, sx = 1;
+    float lim1 = 1.f;
 
     GridView view() const {
         GridView g;
         g.ox = ox; g.oy = oy; g.oz = oz; g.nx = nx; g.ny = ny; g.nz = nz; g.sx = sx;
-        g.off = off; g.pts = pts; g.orig = orig; g.n = n;
+        g.off = off; g.pts = pts; g.orig = orig; g.n = n; g.lim1 = lim1;
         return g;
     }
 };
@@ -50,6 +51,28 @@ int grid_slices() {
         return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 4;
     }();
     return sx;
+}
+
+// First-pass radius^2 of the pruned knn walk from the map's density rho = points per occupied
+// x-slice: dense maps (rho >= 8; C5's 10M-point map: 19 surf / 38 edge) get lim1 = 1 / rho m^2,
+// between the median and the 90th percentile of the 5th-neighbour distance^2 (0.037 / 0.085 m^2 on
+// C5's surf map; per C5 knn launch: 2 / rho 7.04 ms, 0.05 for both kinds 6.52 ms); sparse
+// maps (C2's 1M-point map: 2.3 / 4.3) keep lim1 = 1, the plain walk.  LMSF_KNN_LIM1 forces a value
+// and LMSF_KNN_PRUNE_RHO the density threshold (A/B).  Speed only: results do not depend on it.
+float knn_first_radius2(size_t n, unsigned long long occupied) {
+    static const float forced = [] {
+        const char* e = getenv("LMSF_KNN_LIM1");
+        return e ? (float)atof(e) : -1.f;
+    }();
+    static const double rho_min = [] {
+        const char* e = getenv("LMSF_KNN_PRUNE_RHO");
+        return e ? atof(e) : 8.0;
+    }();
+    if (forced > 0.f) return forced;
+    if (occupied == 0) return 1.f;
+    const double rho = (double)n / (double)occupied;
+    if (rho < rho_min) return 1.f;
+    return (float)std::min(1.0, std::max(0.01, 1.0 / rho));
 }
 
 template <typename T>
@@ -261,7 +284,13 @@ lmsf_status build_grid(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, int 
     size_t tb = m.scan_tmp_bytes;
     HIPCHK(c, exclusive_scan_u32(m.counts, m.off, cells + 1, m.scan_tmp, tb, s));
     HIPCHK(c, launch_map_scatter(m.orig, (int)n, m.cell, m.off, m.fill, m.pts, base, s));
+    unsigned long long* d_occ = reinterpret_cast<unsigned long long*>(c->d_error + 16);   // scratch after the bbox
+    HIPCHK(c, hipMemsetAsync(d_occ, 0, sizeof(unsigned long long), s));
+    HIPCHK(c, launch_count_nonzero(m.counts, cells, d_occ, s));
+    unsigned long long occ = 0;
+    HIPCHK(c, hipMemcpyAsync(&occ, d_occ, sizeof occ, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
+    m.lim1 = knn_first_radius2(n, occ);
     m.n = (int)n;
     return LMSF_OK;
 }
@@ -471,8 +500,8 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->edge_stage_src, B * kMaxRings * kEdgePerRing));
     CHK(dalloc(&c->ring_edge_cnt, B * kMaxRings));
     CHK(dalloc(&c->ring_surf_cnt, B * kMaxRings));
-    CHK(dalloc(&c->d_error, 16));
-    CHK(hipMemset(c->d_error, 0, 16 * sizeof(int)));
+    CHK(dalloc(&c->d_error, 32));
+    CHK(hipMemset(c->d_error, 0, 32 * sizeof(int)));
     CHK(hipMemset(c->n_edge, 0, B * sizeof(int)));
     CHK(hipMemset(c->n_surf, 0, B * sizeof(int)));
     CHK(hipMemset(c->d_n27, 0, kCounterShards * 16 * sizeof(unsigned long long)));

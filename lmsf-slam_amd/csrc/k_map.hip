@@ -46,6 +46,25 @@ __global__ void map_count_kernel(const float4* pts, int n, float sx, int ox, int
     atomicAdd(&counts[c], 1u);
 }
 
+// Number of occupied slices (the map's density statistic that selects the pruned search).
+__global__ void __launch_bounds__(256) count_nonzero_kernel(const uint32_t* counts, size_t n, unsigned long long* out) {
+    __shared__ unsigned int part[4];
+    unsigned int c = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        c += counts[i] != 0u;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(part[0] + part[1] + part[2] + part[3]));
+}
+
+hipError_t launch_count_nonzero(const uint32_t* counts, size_t n, unsigned long long* out, hipStream_t s) {
+    const size_t blocks = std::min<size_t>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(count_nonzero_kernel, dim3((unsigned)std::max<size_t>(blocks, 1)), dim3(256), 0, s, counts, n, out);
+    return hipGetLastError();
+}
+
 // Scatter into cell order.  Order inside a cell is arbitrary: the search ranks candidates by the
 // total order (d2, original index), so results do not depend on it.
 __global__ void map_scatter_kernel(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,

@@ -74,6 +74,7 @@ __device__ __forceinline__ GridView pick_grid(bool c, const GridView& a, const G
     r.orig = c ? a.orig : b.orig;
     r.n = c ? a.n : b.n;
     r.sx = c ? a.sx : b.sx;
+    r.lim1 = c ? a.lim1 : b.lim1;
     return r;
 }
 
@@ -85,7 +86,7 @@ __device__ __forceinline__ GridView pick_grid(bool c, const GridView& a, const G
 // TWO: the map of a kind is split into a static grid (a shared prior map, indices [0, P)) and a
 // dynamic grid (the keyframe window, indices P + j): 18 rows, positions tagged with the grid bit.
 // Keys carry global indices, so the result equals the search of the concatenation [prior | window].
-template <int T, bool TWO>
+template <int T, bool TWO, bool PRUNE>
 __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, GridView ge2, GridView gs2, BatchView bv,
                                                   int skip_converged, int gx, int remap) {
     constexpr int NR = TWO ? 18 : 9;
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
                 }
             }
         };
-        if constexpr (T == 1) {
+        if constexpr (T == 1 && !PRUNE) {
             // one lane walks its rows; kKnnUnroll loads in flight per step (a row is contiguous: 8 points per
             // 128-B line), so the lane waits once per kKnnUnroll candidates instead of once per candidate.
             // Keys are unique (global index), so the kept top-5 does not depend on the visit order.
@@ -185,6 +186,116 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
                     for (int u = 0; u < kKnnUnroll; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
                 }
                 for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
+            }
+        } else if constexpr (T == 1) {
+            // Dense maps (PRUNE): the walk prunes with the current 5th-best distance d4 (1.0 until five
+            // are held), which is ~0.2 m on a 10M-point map:
+            //   pass 1: rows nearest first (own row, 4 faces, 4 corners), each trimmed to the x-window of
+            //           radius sqrt(lim1) (lim1 from the map's density, GridView::lim1); rows with yz-gap^2
+            //           lb > min(d4, lim1) skipped; scanned rows are marked;
+            //   pass 2: every row with lb <= d4, trimmed to the x-window of radius sqrt(d4) minus the
+            //           slices pass 1 scanned (recomputed from lim1).
+            // Skipping a row whose lb exceeds d4 is exact: float rounding is monotone, so every point of
+            // the row has fl(d2) >= fl(gy^2 + gz^2) > d4 (it could not enter the top-5, ties included).
+            // x-windows carry the 1e-5 relative margin of kCullLim.  Sparse maps (C2: ~6 points per
+            // occupied cell) take the plain walk above: there the extra offset loads cost more than the
+            // candidates they save (measured).
+            auto scan_range = [&](const float4* rp, uint32_t tag, int a, int len) {
+                int c = 0;
+                for (; c + kKnnUnroll <= len; c += kKnnUnroll) {
+                    float4 m[kKnnUnroll];
+#pragma unroll
+                    for (int u = 0; u < kKnnUnroll; ++u) m[u] = rp[a + c + u];
+#pragma unroll
+                    for (int u = 0; u < kKnnUnroll; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
+                }
+                for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
+            };
+            // row rr -> its (grid, dy, dz) geometry; false when the row lies outside the grid
+            auto row_geo = [&](int rr, const uint32_t*& row, int& xa, int& xb, float& lb, int& ox, int& sx) {
+                const GridView gg = pick_grid(TWO && rr >= 9, g2, g);
+                ox = gg.ox;
+                sx = gg.sx;
+                const int r9 = rr % 9, dyo = (r9 % 3) - 1, dzo = (r9 / 3) - 1;
+                const float fxs = fx * (float)gg.sx;
+                const bool inside = gg.n > 0 && fxs >= (float)(gg.ox - 2 * gg.sx) && fxs <= (float)(gg.ox + gg.nx + gg.sx) &&
+                                    fy >= (float)(gg.oy - 2) && fy <= (float)(gg.oy + gg.ny + 1) &&
+                                    fz >= (float)(gg.oz - 2) && fz <= (float)(gg.oz + gg.nz + 1);
+                if (!inside) return false;
+                const int cxs = (int)fxs - gg.ox, cy = (int)fy - gg.oy + dyo, cz = (int)fz - gg.oz + dzo;
+                xa = max(cxs - gg.sx, 0);
+                xb = min(cxs + 2 * gg.sx - 1, gg.nx - 1);
+                if (cy < 0 || cy >= gg.ny || cz < 0 || cz >= gg.nz || xa > xb) return false;
+                row = gg.off + ((size_t)cz * gg.ny + cy) * gg.nx;
+                const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
+                const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
+                const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
+                lb = gy * gy + gz * gz;
+                return true;
+            };
+            // slices of [xa, xb] meeting [w.x - r, w.x + r], r = sqrt(lim - lb) (empty when lim < lb)
+            auto window = [&](float lim, float lb, int xa, int xb, int ox, int sx, int& sa, int& sb) {
+                const float rem = lim - lb;
+                sa = 1;
+                sb = 0;
+                if (rem < 0.f) return;
+                const double r = (double)sqrtf(rem);
+                sa = max(xa, (int)floor(((double)w.x - r) * sx) - ox);
+                sb = min(xb, (int)floor(((double)w.x + r) * sx) - ox);
+            };
+            constexpr int kOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // own row, faces, corners
+            auto row_of = [&](int i) { return kOrder[TWO ? i / 2 : i] + ((TWO && (i & 1)) ? 9 : 0); };
+            const float lim1 = g.lim1 * kCullLim;   // both grids of a kind share the first-pass radius
+            uint32_t scanned = 0;
+#pragma unroll
+            for (int i = 0; i < NR; ++i) {
+                const int rr = row_of(i);
+                const uint32_t* row;
+                int xa, xb, ox, sx;
+                float lb;
+                if (!row_geo(rr, row, xa, xb, lb, ox, sx)) continue;
+                if (bv.count27) c27 += row[xb + 1] - row[xa];
+                const float d4 = __uint_as_float((uint32_t)(k[4] >> 32));
+                if (lb > d4 || lb > lim1) continue;
+                int sa, sb;
+                window(lim1, lb, xa, xb, ox, sx, sa, sb);
+                scanned |= 1u << rr;
+                if (sa <= sb) {
+                    const uint32_t s0 = row[sa];
+                    scan_range((TWO && rr >= 9) ? g2.pts : g.pts, (TWO && rr >= 9) ? kGridBit : 0u, (int)s0,
+                               (int)(row[sb + 1] - s0));
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NR; ++i) {
+                const int rr = row_of(i);
+                const float d4 = __uint_as_float((uint32_t)(k[4] >> 32));
+                const uint32_t* row;
+                int xa, xb, ox, sx;
+                float lb;
+                if (!row_geo(rr, row, xa, xb, lb, ox, sx)) continue;
+                if (lb > d4) continue;
+                int sa, sb, ta = 1, tb = 0;
+                window(d4 * kCullLim, lb, xa, xb, ox, sx, sa, sb);
+                if (scanned & (1u << rr)) window(lim1, lb, xa, xb, ox, sx, ta, tb);
+                const float4* rp = (TWO && rr >= 9) ? g2.pts : g.pts;
+                const uint32_t tag = (TWO && rr >= 9) ? kGridBit : 0u;
+                if (ta > tb) {
+                    if (sa <= sb) {
+                        const uint32_t s0 = row[sa];
+                        scan_range(rp, tag, (int)s0, (int)(row[sb + 1] - s0));
+                    }
+                } else {
+                    const int l1 = min(sb, ta - 1), r0 = max(sa, tb + 1);
+                    if (sa <= l1) {
+                        const uint32_t s0 = row[sa];
+                        scan_range(rp, tag, (int)s0, (int)(row[l1 + 1] - s0));
+                    }
+                    if (r0 <= sb) {
+                        const uint32_t s0 = row[r0];
+                        scan_range(rp, tag, (int)s0, (int)(row[sb + 1] - s0));
+                    }
+                }
             }
         } else {
             // lane l resolves rows l, l + T, ...; the team shares them by shuffles
@@ -543,18 +654,23 @@ static int knn_remap() {
 }
 
 template <bool TWO>
-static void launch_knn_t(int T, dim3 grid, const GridView& edge, const GridView& surf, const GridView& edge2,
+static void launch_knn_t(int T, bool prune, dim3 grid, const GridView& edge, const GridView& surf, const GridView& edge2,
                          const GridView& surf2, const BatchView& bv, int skip_converged, int gx, int remap,
                          hipStream_t s) {
-#define LMSF_KNN(TT) hipLaunchKernelGGL((knn_kernel<TT, TWO>), grid, dim3(256), 0, s, edge, surf, edge2, surf2, bv, \
-                                        skip_converged, gx, remap)
+#define LMSF_KNN(TT, PP) hipLaunchKernelGGL((knn_kernel<TT, TWO, PP>), grid, dim3(256), 0, s, edge, surf, edge2, surf2, bv, \
+                                            skip_converged, gx, remap)
     switch (T) {
-        case 1: LMSF_KNN(1); break;
-        case 2: LMSF_KNN(2); break;
-        case 4: LMSF_KNN(4); break;
-        case 8: LMSF_KNN(8); break;
-        case 32: LMSF_KNN(32); break;
-        default: LMSF_KNN(16); break;
+        case 1:
+            if (prune)
+                LMSF_KNN(1, true);
+            else
+                LMSF_KNN(1, false);
+            break;
+        case 2: LMSF_KNN(2, false); break;
+        case 4: LMSF_KNN(4, false); break;
+        case 8: LMSF_KNN(8, false); break;
+        case 32: LMSF_KNN(32, false); break;
+        default: LMSF_KNN(16, false); break;
     }
 #undef LMSF_KNN
 }
@@ -564,10 +680,12 @@ hipError_t launch_knn(const GridView& edge, const GridView& surf, const GridView
     const int T = knn_team((size_t)bv.feat_stride * bv.B), remap = knn_remap();
     const int gx = (bv.feat_stride + (256 / T) - 1) / (256 / T);
     const dim3 grid(gx * bv.B);
+    // the pruned walk when a searched grid is dense (first-pass radius below the match radius)
+    const bool prune = (edge.n > 0 && edge.lim1 < 1.f) || (surf.n > 0 && surf.lim1 < 1.f);
     if (edge2.n > 0 || surf2.n > 0)
-        launch_knn_t<true>(T, grid, edge, surf, edge2, surf2, bv, skip_converged, gx, remap, s);
+        launch_knn_t<true>(T, prune, grid, edge, surf, edge2, surf2, bv, skip_converged, gx, remap, s);
     else
-        launch_knn_t<false>(T, grid, edge, surf, edge2, surf2, bv, skip_converged, gx, remap, s);
+        launch_knn_t<false>(T, prune, grid, edge, surf, edge2, surf2, bv, skip_converged, gx, remap, s);
     return hipGetLastError();
 }
 

@@ -34,6 +34,7 @@ struct GridView {
     const float4* pts;     // points sorted by cell; w = original index (int bits)
     const float4* orig;    // points in the caller's order (x, y, z, intensity)
     int n;
+    float lim1;            // first-pass radius^2 of the pruned one-lane search (m^2); >= 1: sparse grid, plain walk
 };
 
 // Per-registration solver state (device resident, one per batch slot).
@@ -82,6 +83,7 @@ hipError_t launch_map_count(const float4* pts, int n, int sx, int ox, int oy, in
 // sorted[] w = base + original index (base > 0 for a keyframe window behind a prior map)
 hipError_t launch_map_scatter(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
                               float4* sorted, int base, hipStream_t s);
+hipError_t launch_count_nonzero(const uint32_t* counts, size_t n, unsigned long long* out, hipStream_t s);
 hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, void* tmp, size_t& tmp_bytes, hipStream_t s);
 
 // edge2 / surf2: optional second grid per kind (n = 0: none), searched as if concatenated after

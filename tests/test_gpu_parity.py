@@ -129,6 +129,50 @@ def test_match_bitexact(lib, oracle_mod, small_workload):
         assert (orec["kind"] > 0).sum() > 0.5 * len(orec)
 
 
+def _slice_density(m):
+    """Points per occupied 0.25 m x 1 m x 1 m slice (the statistic lmsf_set_map uses to choose the
+    pruned one-lane walk: >= 8)."""
+    p = m[:, :3].astype(np.float32)
+    c = np.stack([np.floor(p[:, 0] * 4), np.floor(p[:, 1]), np.floor(p[:, 2])], 1).astype(np.int64)
+    return len(p) / len(np.unique(c, axis=0))
+
+
+@pytest.fixture(scope="module")
+def dense_workload():
+    """C2 scans against a 1M-point map over a 30 m radius: ~25 points per occupied slice, the
+    density regime of C5's 10M-point map (pruned search)."""
+    from lmsf import synth
+    return synth.make_workload("C2", n_scans=1, map_points=1_000_000, radius=30.0, road_length=20.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dense", [False, True])
+def test_match_bitexact_one_lane(lib, oracle_mod, small_workload, dense_workload, dense):
+    """The one-lane-per-query search (query slots >= 2^20): plain walk on the sparse map, pruned
+    two-pass walk on the dense one; neighbour sets and records byte-identical to the oracle."""
+    wl = dense_workload if dense else small_workload
+    assert (_slice_density(wl.surf_map) >= 8) == dense
+    e, s = _features(oracle_mod, wl.scans[0])
+    ctx = _ctx(lib, max_batch=1, max_features=1 << 20)
+    ctx.set_map(lib.EDGE, wl.edge_map)
+    ctx.set_map(lib.SURF, wl.surf_map)
+    ctx.set_scan(lib.EDGE, e)
+    ctx.set_scan(lib.SURF, s)
+    reg = oracle_mod.Registration()
+    reg.set_map(1, wl.edge_map)
+    reg.set_map(2, wl.surf_map)
+    reg.set_scan(1, e)
+    reg.set_scan(2, s)
+    for pose in (wl.guess[0], wl.truth[0]):
+        orec, onn = reg.match(pose)
+        grec, gnn = ctx.match(pose, len(e) + len(s))
+        found = gnn >= 0
+        np.testing.assert_array_equal(gnn[found], onn[found])
+        assert (found[:, 1:] <= found[:, :-1]).all()
+        assert grec.tobytes() == orec.tobytes()
+        assert (orec["kind"] > 0).sum() > 0.2 * len(orec)
+
+
 def test_eval_packet(lib, oracle_mod, small_workload):
     wl = small_workload
     e, s = _features(oracle_mod, wl.scans[1])
