@@ -21,7 +21,15 @@ namespace lmsf {
 
 namespace {
 
-constexpr uint64_t kSentinel = (uint64_t)0x3f800000u << 32;  // key of d2 == 1.0f, idx 0
+// Candidate key = (d2 bits + kKeyBias) << 32 | map index, read as an IEEE double: a positive normal
+// double (exponent field 1 .. 0x7fe for every float d2, NaN and inf included), and positive doubles
+// order exactly as their bit patterns, so v_min_f64 / v_max_f64 rank (d2, index) lexicographically:
+// the top-5 insertion is a 5-step min/max network (10 VALU per candidate, no branches).
+constexpr uint32_t kKeyBias = 0x00100000u;
+constexpr uint64_t kSentinel = (uint64_t)(0x3f800000u + kKeyBias) << 32;  // key of d2 == 1.0f, idx 0
+__device__ __forceinline__ double key_as_double(uint64_t k) { return __longlong_as_double((long long)k); }
+__device__ __forceinline__ uint64_t key_bits(double k) { return (uint64_t)__double_as_longlong(k); }
+__device__ __forceinline__ float key_d2(double k) { return __uint_as_float((uint32_t)(key_bits(k) >> 32) - kKeyBias); }
 #ifndef LMSF_KNN_UNROLL
 #define LMSF_KNN_UNROLL 4
 #endif
@@ -149,22 +157,17 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
             }
             if (bv.count27) c27 += row[xb + 1] - row[xa];
         };
-        uint64_t k[5] = {kSentinel, kSentinel, kSentinel, kSentinel, kSentinel};
-        uint32_t kp[5] = {0, 0, 0, 0, 0};   // grid bit | sorted-array position of each kept key
-        auto consider = [&](const float4 m, uint32_t tagged_pos) {
+        const double sentinel = key_as_double(kSentinel);
+        double k[5] = {sentinel, sentinel, sentinel, sentinel, sentinel};   // ascending kept keys
+        auto consider = [&](const float4 m, uint32_t /*tagged_pos*/) {
             const float dx = w.x - m.x, dy = w.y - m.y, dz = w.z - m.z;
             const float d2 = dx * dx + dy * dy + dz * dz;
-            const uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)__float_as_int(m.w);
-            if (key < k[4]) {
-                k[4] = key;
-                kp[4] = tagged_pos;
+            double x = key_as_double(((uint64_t)(__float_as_uint(d2) + kKeyBias) << 32) | (uint32_t)__float_as_int(m.w));
 #pragma unroll
-                for (int i = 4; i >= 1; --i) {
-                    if (k[i] < k[i - 1]) {
-                        uint64_t t = k[i - 1]; k[i - 1] = k[i]; k[i] = t;
-                        uint32_t u = kp[i - 1]; kp[i - 1] = kp[i]; kp[i] = u;
-                    }
-                }
+            for (int i = 0; i < 5; ++i) {
+                const double lo = fmin(k[i], x);
+                x = fmax(k[i], x);
+                k[i] = lo;
             }
         };
         if constexpr (T == 1 && !PRUNE) {
@@ -255,7 +258,7 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
                 float lb;
                 if (!row_geo(rr, row, xa, xb, lb, ox, sx)) continue;
                 if (bv.count27) c27 += row[xb + 1] - row[xa];
-                const float d4 = __uint_as_float((uint32_t)(k[4] >> 32));
+                const float d4 = key_d2(k[4]);
                 if (lb > d4 || lb > lim1) continue;
                 int sa, sb;
                 window(lim1, lb, xa, xb, ox, sx, sa, sb);
@@ -269,7 +272,7 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
 #pragma unroll
             for (int i = 0; i < NR; ++i) {
                 const int rr = row_of(i);
-                const float d4 = __uint_as_float((uint32_t)(k[4] >> 32));
+                const float d4 = key_d2(k[4]);
                 const uint32_t* row;
                 int xa, xb, ox, sx;
                 float lb;
@@ -340,37 +343,32 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
                 consider(rpts[pos], (uint32_t)pos | rtag);
             }
         }
-        // merge: five rounds of team-min; the owning lane pops its head and donates its position
-        uint64_t res[5];
-        uint32_t rpos[5];
-        const int tbase = (threadIdx.x & 63) & ~(T - 1);
+        // merge: five rounds of team-min; the owning lane pops its head (keys are unique)
+        double res[5];
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-            uint64_t mn = k[0];
+            double mn = k[0];
 #pragma unroll
-            for (int o = T / 2; o >= 1; o >>= 1) {
-                uint64_t t = shfl_xor_u64<T>(mn, o);
-                mn = t < mn ? t : mn;
-            }
-            const unsigned long long own = __ballot(k[0] == mn);
-            const int owner = __ffsll((long long)((own >> tbase) & ((T == 64) ? ~0ull : ((1ull << T) - 1)))) - 1;
+            for (int o = T / 2; o >= 1; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o, T));
             res[i] = mn;
-            rpos[i] = (uint32_t)__shfl((int)kp[0], owner < 0 ? 0 : owner, T);
-            if (k[0] == mn) {
-                k[0] = k[1]; k[1] = k[2]; k[2] = k[3]; k[3] = k[4]; k[4] = kSentinel;
-                kp[0] = kp[1]; kp[1] = kp[2]; kp[2] = kp[3]; kp[3] = kp[4];
+            if (key_bits(k[0]) == key_bits(mn)) {
+                k[0] = k[1]; k[1] = k[2]; k[2] = k[3]; k[3] = k[4]; k[4] = sentinel;
             }
         }
         // every rank written (lane i % T writes rank i; teams smaller than 5 write several): the
-        // neighbour point itself (just touched, L1/L2 resident), so the fit reads 80 contiguous bytes
+        // neighbour point (from the caller-order copy, w = its map index), so the fit reads 80
+        // contiguous bytes.  Indices below g.n belong to g, the rest to g2 (its points carry P + j).
         float4* nn_out = bv.nnp + ((size_t)b * bv.feat_stride + q) * 5;
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
             if (i % T == lane) {
                 float4 o = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-                if (res[i] < kSentinel) {
-                    const float4* src = (TWO && (rpos[i] & kGridBit)) ? g2.pts : g.pts;
-                    o = src[rpos[i] & ~kGridBit];
+                const uint64_t kb = key_bits(res[i]);
+                if (kb < kSentinel) {
+                    const uint32_t idx = (uint32_t)kb;
+                    const bool second = TWO && idx >= (uint32_t)g.n;
+                    const float4 p = second ? g2.orig[idx - (uint32_t)g.n] : g.orig[idx];
+                    o = make_float4(p.x, p.y, p.z, __int_as_float((int)idx));
                 }
                 nn_out[i] = o;
             }
@@ -601,12 +599,32 @@ __global__ __launch_bounds__(256) void lm_eval_kernel(BatchView bv) {
     double P[kPacket];
 #pragma unroll
     for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
+    // every record's point and value loads issued before the first use (the value array is read
+    // whatever the kind: an unmatched slot's stale values are loaded but never used)
+    float4 rp[kEvalPerThread];
+    RecV rv[kEvalPerThread];
 #pragma unroll
     for (int k = 0; k < kEvalPerThread; ++k) {
         const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
-        if (q < nq) {
+        const size_t slot = (size_t)b * bv.feat_stride + (q < nq ? q : 0);
+        rp[k] = bv.rec_p[slot];
+        rv[k] = bv.rec_v[slot];
+    }
+#pragma unroll
+    for (int k = 0; k < kEvalPerThread; ++k) {
+        const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
+        const int kind = __float_as_int(rp[k].w);
+        if (q < nq && kind != 0) {
             double J[6], res;
-            if (record_residual(bv, (size_t)b * bv.feat_stride + q, Ps, res, J)) huber_accumulate(P, res, J);
+            const d3 pp = mk((double)rp[k].x, (double)rp[k].y, (double)rp[k].z);
+            const RecV& v = rv[k];
+            if (kind == LMSF_EDGE) {
+                const double2 e = bv.rec_e[(size_t)b * bv.feat_stride + q];
+                res = edge_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), mk(v.v[3], e.x, e.y), J);
+            } else {
+                res = surf_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), v.v[3], J);
+            }
+            huber_accumulate(P, res, J);
         }
     }
     block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + blockIdx.x) * kPacket);

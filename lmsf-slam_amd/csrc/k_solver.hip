@@ -23,18 +23,27 @@ namespace {
 
 constexpr int kMaxInner = 4;  // options.max_num_iterations (ceres_...:118)
 
-// Sum the first `nparts` packets of slot b in a fixed order; result valid in every lane.
+// Sum the first `nparts` packets of slot b in a fixed order; result valid in every lane.  Lane l
+// owns entry l % 32 of the packets p = l / 32 (mod 2): the loads are coalesced and all in flight
+// at once (one latency, not one per entry), then the two halves add in one shuffle.
 __device__ void reduce_parts(const BatchView& bv, int b, int nparts, double* tot) {
-    const int lane = threadIdx.x;
+    static_assert(kPacket == 32, "one packet entry per half-wave lane");
+    __shared__ double red[kPacket];
+    const int lane = threadIdx.x, e = lane & 31;
     const double* base = bv.partials + (size_t)b * bv.max_parts * kPacket;
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int p = lane >> 5;
+    for (; p + 14 < nparts; p += 16) {   // 8 independent loads in flight per lane
 #pragma unroll
-    for (int i = 0; i < kPacket; ++i) {
-        double v = 0.0;
-        for (int p = lane; p < nparts; p += 64) v += base[(size_t)p * kPacket + i];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        tot[i] = v;
+        for (int u = 0; u < 8; ++u) acc[u] += base[(size_t)(p + 2 * u) * kPacket + e];
     }
+    for (; p < nparts; p += 2) acc[0] += base[(size_t)p * kPacket + e];
+    double v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    v += __shfl_xor(v, 32, 64);
+    if (lane < 32) red[e] = v;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPacket; ++i) tot[i] = red[i];
 }
 
 __device__ double norm7(const double* x) {

@@ -3,7 +3,7 @@ import glob, json, sys
 for pat in sys.argv[1:] or ["gpurun_out/ab_*.log"]:
     for f in sorted(glob.glob(pat)):
         try:
-            d = json.loads(open(f).read().strip().splitlines()[-1])
+            d = json.loads([l for l in open(f).read().splitlines() if l.startswith('{')][-1])
         except Exception as e:  # noqa: BLE001
             print(f, "unparsed", e)
             continue
