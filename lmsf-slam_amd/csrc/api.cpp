@@ -124,6 +124,10 @@ struct lmsf_ctx {
     int* edge_stage_src = nullptr;
     int* ring_edge_cnt = nullptr;
     int* ring_surf_cnt = nullptr;
+    int* qcode = nullptr;             // ring position -> feature code / slot (knn order, k_extract.hip)
+    int* qslot = nullptr;
+    int* n_pos = nullptr;
+    bool qorder_valid = false;        // the slots' features came from the extraction kernels
     int* d_error = nullptr;
     // host side
     double* h_poses = nullptr;        // pinned [B*7]
@@ -184,6 +188,9 @@ struct lmsf_ctx {
         v.count27 = count27 ? 1 : 0;
         v.gn_rows = gn_rows;
         v.partials_gn = partials_gn;
+        v.qslot = qorder_valid ? qslot : nullptr;
+        v.n_pos = n_pos;
+        v.pos_stride = R;
         return v;
     }
 
@@ -207,6 +214,9 @@ struct lmsf_ctx {
         e.edge_stage_src = edge_stage_src;
         e.ring_edge_cnt = ring_edge_cnt;
         e.ring_surf_cnt = ring_surf_cnt;
+        e.qcode = qcode;
+        e.qslot = qslot;
+        e.n_pos = n_pos;
         e.feat = feat;
         e.feat_src = feat_src;
         e.feat_stride = F;
@@ -319,6 +329,7 @@ lmsf_status sync_slot0_features(lmsf_ctx* c) {
     c->slot0_ns = (int64_t)ns;
     c->scan_dirty = false;
     c->features_on_device = false;
+    c->qorder_valid = false;   // host features: slot order
     return LMSF_OK;
 }
 
@@ -422,7 +433,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->sort_key,
-                    c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->d_error};
+                    c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->n_pos, c->d_error};
     for (void* p : bufs) hipFree(p);
     c->voxel.release();
     hipFree(c->vox_in);
@@ -500,6 +511,9 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->edge_stage_src, B * kMaxRings * kEdgePerRing));
     CHK(dalloc(&c->ring_edge_cnt, B * kMaxRings));
     CHK(dalloc(&c->ring_surf_cnt, B * kMaxRings));
+    CHK(dalloc(&c->qcode, B * R));
+    CHK(dalloc(&c->qslot, B * R));
+    CHK(dalloc(&c->n_pos, B));
     CHK(dalloc(&c->d_error, 32));
     CHK(hipMemset(c->d_error, 0, 32 * sizeof(int)));
     CHK(hipMemset(c->n_edge, 0, B * sizeof(int)));
@@ -609,6 +623,7 @@ lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf
     if (rc) return rc;
     HIPCHK(c, hipMemsetAsync(c->d_error, 0, sizeof(int), c->stream));
     HIPCHK(c, launch_extract(c->eview(1), c->stream));
+    c->qorder_valid = true;
     int hc[3];
     HIPCHK(c, hipMemcpyAsync(&hc[0], c->n_edge, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&hc[1], c->n_surf, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -810,6 +825,7 @@ lmsf_status lmsf_batch_launch(lmsf_ctx* c, int32_t n, const double* poses) {
     std::memcpy(c->h_poses, poses, (size_t)n * 7 * sizeof(double));
     HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, (size_t)n * 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, launch_extract(c->eview(n), c->stream));
+    c->qorder_valid = true;
     HIPCHK(c, launch_state_init(c->bview(n), c->d_poses, c->stream));
     // every slot behaves as one Solve on a fresh registration object (ceres_...:100-101)
     int iters = c->optimization_count;

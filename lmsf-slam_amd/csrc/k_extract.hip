@@ -380,7 +380,9 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
     const int size = rs[r + 1] - start;
     int* ecnt = ev.ring_edge_cnt + (size_t)b * kMaxRings;
     int* scnt = ev.ring_surf_cnt + (size_t)b * kMaxRings;
+    int* qc = ev.qcode + (size_t)b * ev.raw_stride + start;   // ring position -> ring-local feature code
     if (size < 20 || size > kRingMax) {   // FX:71
+        for (int j = tid; j < size; j += 256) qc[j] = -1;
         if (tid == 0) {
             ecnt[r] = 0;
             scnt[r] = 0;
@@ -390,7 +392,7 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
     }
     const float4* pts = ev.ring_pts + (size_t)b * ev.raw_stride + start;
     const int* psrc = ev.ring_src + (size_t)b * ev.raw_stride + start;
-    for (int j = tid; j < size; j += 256) { dis[j] = 0; flag[j] = 0; }
+    for (int j = tid; j < size; j += 256) { dis[j] = 0; flag[j] = 0; qc[j] = -1; }
     if (tid == 0) { sh_ec = 0; sh_sc = 0; sh_err = 0; }
     __syncthreads();
     ring_bad_points<256>(ev, pts, size, dis, flag);
@@ -431,6 +433,7 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
                     estage[ec] = pts[ind];
                     estage_src[ec] = psrc[ind];
                     flag[ind] = 1;
+                    qc[ind] = ec;
                 }
                 if (lane >= 1 && lane <= 5) dis[min(ind + lane, size - 1)] = 1;
                 if (lane >= 6 && lane <= 10) dis[max(ind - (lane - 5), 0)] = 1;
@@ -462,6 +465,7 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
             if (flag[ind] == 0) {
                 sstage[o] = pts[ind];
                 sstage_src[o] = psrc[ind];
+                qc[ind] = kQSurf | o;
                 ++o;
             }
         }
@@ -513,6 +517,29 @@ __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
             feat[i] = ev.surf_stage[src];
             fsrc[i] = ev.surf_stage_src[src];
         }
+    }
+    // The neighbour search's order: the feature slot of every ring position, so that neighbouring
+    // lanes search neighbouring points of a ring (slot order puts a sector's surfs in curvature
+    // order, spread over ~60 degrees of the ring).  Codes of a ring whose features were dropped
+    // (capacity flags) are ignored through the ring counts.
+    const int npos = rs[nr];
+    if (blockIdx.x == 0 && threadIdx.x == 0) ev.n_pos[b] = npos;
+    const int* qc = ev.qcode + (size_t)b * ev.raw_stride;
+    int* qs = ev.qslot + (size_t)b * ev.raw_stride;
+    for (int p = blockIdx.x * 256 + threadIdx.x; p < npos; p += gridDim.x * 256) {
+        int lo = 0, hi = nr - 1;  // last ring with rs[r] <= p
+        while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (rs[mid] <= p) lo = mid; else hi = mid - 1; }
+        const int code = qc[p];
+        int slot = -1;
+        if (code >= 0) {
+            const int l = code & ~kQSurf;
+            if (code & kQSurf) {
+                if (l < spre[lo + 1] - spre[lo]) slot = ne + spre[lo] + l;
+            } else if (l < epre[lo + 1] - epre[lo]) {
+                slot = epre[lo] + l;
+            }
+        }
+        qs[p] = slot;
     }
 }
 

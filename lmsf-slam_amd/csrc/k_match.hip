@@ -107,8 +107,18 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
     __syncthreads();
     const int ne = bv.n_edge[b], ns = bv.n_surf[b];
     const int team = threadIdx.x / T, lane = threadIdx.x % T;
-    const int q = bx * (256 / T) + team;
-    const bool active = q < ne + ns && !(skip_converged && bv.st[b].gn_converged);
+    // ring order when the features came from the extraction kernels (neighbouring lanes search
+    // neighbouring ring points, whose 27-cell blocks overlap in L1), else slot order
+    int q = bx * (256 / T) + team;
+    bool active;
+    if (bv.qslot) {
+        active = q < bv.n_pos[b];
+        q = active ? bv.qslot[(size_t)b * bv.pos_stride + q] : -1;
+        active = active && q >= 0;
+    } else {
+        active = q < ne + ns;
+    }
+    active = active && !(skip_converged && bv.st[b].gn_converged);
     if (active) {
         const bool is_edge = q < ne;
         const GridView g = pick_grid(is_edge, ge, gs);
@@ -696,7 +706,8 @@ static void launch_knn_t(int T, bool prune, dim3 grid, const GridView& edge, con
 hipError_t launch_knn(const GridView& edge, const GridView& surf, const GridView& edge2, const GridView& surf2,
                       const BatchView& bv, int skip_converged, hipStream_t s) {
     const int T = knn_team((size_t)bv.feat_stride * bv.B), remap = knn_remap();
-    const int gx = (bv.feat_stride + (256 / T) - 1) / (256 / T);
+    const int span = (bv.qslot && bv.pos_stride > bv.feat_stride) ? bv.pos_stride : bv.feat_stride;
+    const int gx = (span + (256 / T) - 1) / (256 / T);
     const dim3 grid(gx * bv.B);
     // the pruned walk when a searched grid is dense (first-pass radius below the match radius)
     const bool prune = (edge.n > 0 && edge.lim1 < 1.f) || (surf.n > 0 && surf.lim1 < 1.f);

@@ -21,6 +21,7 @@ constexpr int kRingMax = 8192;       // points per ring handled by the extractio
 constexpr int kSortMax = 2048;       // points per sector (ring / 6 + 5, padded to a power of two)
 constexpr int kMaxRings = 128;
 constexpr int kEdgePerRing = 120;    // 20 per sector x 6 sectors (FX:172)
+constexpr int kQSurf = 0x40000000;  // ExtractView::qcode tag of a surf feature
 constexpr int kTile = 2048;          // raw points per ring-split tile
 constexpr int kCounterShards = 64;   // candidate / query counters, 16 u64 (128 B) apart
 
@@ -74,6 +75,9 @@ struct BatchView {
     int count27;             // also accumulate [0] (extra cell-offset loads: diagnostics only)
     double* gn_rows;         // [B][feat_stride][4] grad + residual (GN only)
     double* partials_gn;     // [B][max_parts][kPacket] (GN only)
+    const int* qslot;        // [B][pos_stride] feature slot per ring position (the knn order), null: slot order
+    const int* n_pos;        // [B] ring positions per slot (with qslot)
+    int pos_stride;
 };
 
 // ---- launchers (each enqueues on `stream`, never synchronises)
@@ -121,6 +125,9 @@ struct ExtractView {
     int* edge_stage_src;         // [B][kMaxRings * kEdgePerRing]
     int* ring_edge_cnt;          // [B][kMaxRings]
     int* ring_surf_cnt;          // [B][kMaxRings]
+    int* qcode;                  // [B][raw_stride] per ring position: ring-local edge index, kQSurf | surf index, -1
+    int* qslot;                  // [B][raw_stride] per ring position: its feature slot or -1 (the search order)
+    int* n_pos;                  // [B] ring positions of the slot (ring_start[n_scans])
     float4* feat;                // [B][feat_stride] output (edges then surfs)
     int* feat_src;               // [B][feat_stride]
     int feat_stride;

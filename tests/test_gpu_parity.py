@@ -103,14 +103,20 @@ def test_runtime_extract_params_and_schedule(lib, oracle_mod, small_workload):
     assert st.outer_iterations == 2
 
 
-def test_match_bitexact(lib, oracle_mod, small_workload):
+@pytest.mark.parametrize("extracted", [False, True])
+def test_match_bitexact(lib, oracle_mod, small_workload, extracted):
+    """8-lane teams (single-scan launch); queries in slot order (host features) or in ring order
+    (device extraction)."""
     wl = small_workload
     e, s = _features(oracle_mod, wl.scans[0])
     ctx = _ctx(lib)
     ctx.set_map(lib.EDGE, wl.edge_map)
     ctx.set_map(lib.SURF, wl.surf_map)
-    ctx.set_scan(lib.EDGE, e)
-    ctx.set_scan(lib.SURF, s)
+    if extracted:
+        assert ctx.extract(wl.scans[0]) == (len(e), len(s))
+    else:
+        ctx.set_scan(lib.EDGE, e)
+        ctx.set_scan(lib.SURF, s)
     reg = oracle_mod.Registration()
     reg.set_map(1, wl.edge_map)
     reg.set_map(2, wl.surf_map)
@@ -145,19 +151,23 @@ def dense_workload():
     return synth.make_workload("C2", n_scans=1, map_points=1_000_000, radius=30.0, road_length=20.0)
 
 
-@pytest.mark.gpu
+@pytest.mark.parametrize("extracted", [False, True])
 @pytest.mark.parametrize("dense", [False, True])
-def test_match_bitexact_one_lane(lib, oracle_mod, small_workload, dense_workload, dense):
+def test_match_bitexact_one_lane(lib, oracle_mod, small_workload, dense_workload, dense, extracted):
     """The one-lane-per-query search (query slots >= 2^20): plain walk on the sparse map, pruned
-    two-pass walk on the dense one; neighbour sets and records byte-identical to the oracle."""
+    two-pass walk on the dense one, queries in slot order (host features) or in ring order
+    (features extracted on the device); neighbour sets and records byte-identical to the oracle."""
     wl = dense_workload if dense else small_workload
     assert (_slice_density(wl.surf_map) >= 8) == dense
     e, s = _features(oracle_mod, wl.scans[0])
     ctx = _ctx(lib, max_batch=1, max_features=1 << 20)
     ctx.set_map(lib.EDGE, wl.edge_map)
     ctx.set_map(lib.SURF, wl.surf_map)
-    ctx.set_scan(lib.EDGE, e)
-    ctx.set_scan(lib.SURF, s)
+    if extracted:
+        assert ctx.extract(wl.scans[0]) == (len(e), len(s))
+    else:
+        ctx.set_scan(lib.EDGE, e)
+        ctx.set_scan(lib.SURF, s)
     reg = oracle_mod.Registration()
     reg.set_map(1, wl.edge_map)
     reg.set_map(2, wl.surf_map)
