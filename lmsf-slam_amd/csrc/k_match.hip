@@ -462,20 +462,32 @@ __device__ bool surf_fit(const float4* p, float3 q, d3& n_out, double& D_out, do
 
 // Block reduction of a kPacket-double packet: wave butterfly, then 4 wave sums in LDS.
 // Fixed order -> deterministic.
+// The wave step is a transposing butterfly: at distance 32 a lane keeps half of the entries (the
+// lower half in lanes 0-31, the upper in 32-63) and adds its partner's copy of them, at 16 half of
+// the rest, ... down to distance 2, then one plain step at distance 1: 16 + 8 + 4 + 2 + 1 + 1 = 32
+// double shuffles instead of 32 x 6.  Lanes 2e and 2e + 1 end with entry e = (lane >> 1).
+template <int H>
+__device__ __forceinline__ void butterfly_step(double* P, int lane) {
+    const bool upper = (lane & (2 * H)) != 0;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+        const double send = upper ? P[i] : P[H + i];
+        const double keep = upper ? P[H + i] : P[i];
+        P[i] = keep + __shfl_xor(send, 2 * H, 64);
+    }
+}
+
 __device__ __forceinline__ void block_reduce_packet(double* P, double* out) {
+    static_assert(kPacket == 32, "butterfly over 32 entries");
     __shared__ double red[4][kPacket];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int i = 0; i < kPacket; ++i) {
-        double v = P[i];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        P[i] = v;
-    }
-    if (lane == 0) {
-#pragma unroll
-        for (int i = 0; i < kPacket; ++i) red[wave][i] = P[i];
-    }
+    butterfly_step<16>(P, lane);
+    butterfly_step<8>(P, lane);
+    butterfly_step<4>(P, lane);
+    butterfly_step<2>(P, lane);
+    butterfly_step<1>(P, lane);
+    const double v = P[0] + __shfl_xor(P[0], 1, 64);
+    if ((lane & 1) == 0) red[wave][lane >> 1] = v;
     __syncthreads();
     if (threadIdx.x < kPacket) {
         const int i = threadIdx.x;
@@ -732,12 +744,13 @@ hipError_t launch_fit_eval(const GridView& edge, const GridView& surf, const Bat
     return hipGetLastError();
 }
 
-// Queries per thread of fit_eval (LMSF_FIT_PER_THREAD = 1 | 2 | 4, for A/B measurement).
+// Queries per thread of fit_eval (LMSF_FIT_PER_THREAD = 1 | 2 | 4, for A/B measurement).  1 (107
+// VGPRs, 4 waves/SIMD) since the butterfly packet reduction: C2 16.8k vs 16.5k scans/s at 2 (165 VGPRs).
 int fit_per_thread_default() {
     static int v = [] {
         const char* e = getenv("LMSF_FIT_PER_THREAD");
-        int x = e ? atoi(e) : 2;
-        return (x == 1 || x == 2 || x == 4) ? x : 2;
+        int x = e ? atoi(e) : 1;
+        return (x == 1 || x == 2 || x == 4) ? x : 1;
     }();
     return v;
 }
