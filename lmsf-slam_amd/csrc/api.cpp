@@ -126,6 +126,7 @@ struct lmsf_ctx {
     int* ring_surf_cnt = nullptr;
     int* qcode = nullptr;             // ring position -> feature code / slot (knn order, k_extract.hip)
     int* qslot = nullptr;
+    int* fslot = nullptr;             // [B][F] slots edges-then-surfs, each kind in ring order (fused search + fit)
     int* n_pos = nullptr;
     bool qorder_valid = false;        // the slots' features came from the extraction kernels
     int* d_error = nullptr;
@@ -189,6 +190,8 @@ struct lmsf_ctx {
         v.gn_rows = gn_rows;
         v.partials_gn = partials_gn;
         v.qslot = qorder_valid ? qslot : nullptr;
+        v.fslot = qorder_valid ? fslot : nullptr;
+        v.write_nn = 0;
         v.n_pos = n_pos;
         v.pos_stride = R;
         return v;
@@ -216,6 +219,7 @@ struct lmsf_ctx {
         e.ring_surf_cnt = ring_surf_cnt;
         e.qcode = qcode;
         e.qslot = qslot;
+        e.fslot = fslot;
         e.n_pos = n_pos;
         e.feat = feat;
         e.feat_src = feat_src;
@@ -343,14 +347,19 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
     for (int o = 0; o < iters; ++o) {
         const bool t = c->timing && c->ev_used + 2 <= 2 * kEventPairs;
         if (t) HIPCHK(c, hipEventRecord(c->ev[c->ev_used], s));
-        HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{},
-                             bv, gn ? 1 : 0, s));
+        // batch launches: one fused search + fit kernel (it is then the timed neighbour-search launch)
+        const bool fused = match_fit_applies(ge2, gs2, bv, c->cfg.solver);
+        if (fused)
+            HIPCHK(c, launch_match_fit(ge, gs, bv, s));
+        else
+            HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{},
+                                 bv, gn ? 1 : 0, s));
         if (t) {
             HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 1], s));
             c->ev_used += 2;
         }
         c->knn_launches++;
-        HIPCHK(c, launch_fit_eval(ge, gs, bv, c->cfg.solver, s));
+        if (!fused) HIPCHK(c, launch_fit_eval(ge, gs, bv, c->cfg.solver, s));
         if (gn) {
             HIPCHK(c, launch_gn_solve(bv, o, s));
         } else {
@@ -433,7 +442,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->sort_key,
-                    c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->n_pos, c->d_error};
+                    c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->n_pos, c->d_error};
     for (void* p : bufs) hipFree(p);
     c->voxel.release();
     hipFree(c->vox_in);
@@ -513,6 +522,7 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->ring_surf_cnt, B * kMaxRings));
     CHK(dalloc(&c->qcode, B * R));
     CHK(dalloc(&c->qslot, B * R));
+    CHK(dalloc(&c->fslot, B * c->F));
     CHK(dalloc(&c->n_pos, B));
     CHK(dalloc(&c->d_error, 32));
     CHK(hipMemset(c->d_error, 0, 32 * sizeof(int)));
@@ -867,13 +877,18 @@ lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int3
     if (nq > cap) return c->fail(LMSF_ERR_CAPACITY, "output capacity %zu < %zu queries", cap, nq);
     std::memcpy(c->h_poses, pose, 7 * sizeof(double));
     HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    const BatchView bv = c->bview(1);
+    BatchView bv = c->bview(1);
+    bv.write_nn = 1;
     HIPCHK(c, launch_state_init(bv, c->d_poses, c->stream));
     const GridView ge = c->map[LMSF_EDGE].view(), gs = c->map[LMSF_SURF].view();
     const GridView ge2 = c->prior[LMSF_EDGE].view(), gs2 = c->prior[LMSF_SURF].view();
-    HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{}, bv, 0,
-                         c->stream));
-    HIPCHK(c, launch_fit_eval(ge, gs, bv, LMSF_SOLVER_CERES_LM, c->stream));
+    if (match_fit_applies(ge2, gs2, bv, LMSF_SOLVER_CERES_LM)) {   // the path lmsf_solve takes
+        HIPCHK(c, launch_match_fit(ge, gs, bv, c->stream));
+    } else {
+        HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{}, bv,
+                             0, c->stream));
+        HIPCHK(c, launch_fit_eval(ge, gs, bv, LMSF_SOLVER_CERES_LM, c->stream));
+    }
     std::vector<float4> rp(out ? nq : 0);
     std::vector<RecV> rv(out ? nq : 0);
     std::vector<double2> re(out ? nq : 0);

@@ -176,14 +176,29 @@ __device__ inline void jacobi_eig(double* a, double* d, double* v) {
 
 // Eigenvalue order of a 3x3 result (ascending, stable on index) without dynamic indexing.
 __device__ __forceinline__ void order3(const double* d, int& i0, int& i1, int& i2) {
-    // insertion sort of (0,1,2) by d, stable
+    // insertion sort of (0,1,2) by d, stable; the values ride along (a0 = d[i0], a1 = d[i1]) so no
+    // runtime index touches d (a dynamically indexed array lives in scratch)
     i0 = 0; i1 = 1; i2 = 2;
-    if (d[i0] > d[i1]) { int t = i0; i0 = i1; i1 = t; }
+    double a0 = d[0], a1 = d[1];
+    const double a2 = d[2];
+    if (a0 > a1) { int t = i0; i0 = i1; i1 = t; double u = a0; a0 = a1; a1 = u; }
     // insert element 2
-    if (d[i1] > d[2]) {
+    if (a1 > a2) {
         i2 = i1;
-        if (d[i0] > d[2]) { i1 = i0; i0 = 2; } else { i1 = 2; }
+        if (a0 > a2) { i1 = i0; i0 = 2; } else { i1 = 2; }
     }
+}
+// Middle and largest value of the stable ascending order of d[0..2] and the largest's index
+// (= d[i1], d[i2] of order3), as selects: order3's reference outputs end up in scratch.
+__device__ __forceinline__ void top2_of3(const double* d, double& mid, double& big, int& ibig) {
+    double a0 = d[0], a1 = d[1];
+    int j1 = 1;
+    if (a0 > a1) { const double u = a0; a0 = a1; a1 = u; j1 = 0; }
+    const double a2 = d[2];
+    const bool hi = a1 > a2;   // element 2 inserted below a1
+    ibig = hi ? j1 : 2;
+    big = hi ? a1 : a2;
+    mid = hi ? (a0 > a2 ? a0 : a2) : a1;
 }
 __device__ __forceinline__ double pick3(const double* a, int i) { return i == 0 ? a[0] : (i == 1 ? a[1] : a[2]); }
 

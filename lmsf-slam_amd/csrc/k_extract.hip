@@ -543,6 +543,58 @@ __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
     }
 }
 
+// Stable partition of the search order by kind: fslot = the valid entries of qslot, edge slots
+// (slot < n_edge) first, each kind in ring order (the fused search + fit order: neighbouring lanes
+// search neighbouring ring points, and a wave runs one fit kind).  One 1024-thread block per slot;
+// each thread takes 8 consecutive ring positions per chunk, block-wide exclusive scan of the packed
+// (edge, surf) counts (16 bits each: a chunk holds 8192 positions).
+__global__ __launch_bounds__(1024) void order_kernel(ExtractView ev) {
+    constexpr int E = 8;
+    __shared__ uint32_t wsum[16];
+    const int b = blockIdx.x;
+    const int ne = ev.n_edge[b], npos = ev.n_pos[b];
+    const int* qs = ev.qslot + (size_t)b * ev.raw_stride;
+    int* fs = ev.fslot + (size_t)b * ev.feat_stride;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t base_e = 0, base_s = 0;
+    for (int c0 = 0; c0 < npos; c0 += 1024 * E) {
+        int v[E];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int p = c0 + threadIdx.x * E + e;
+            v[e] = p < npos ? qs[p] : -1;
+            if (v[e] >= 0) cnt += v[e] < ne ? 1u : 0x10000u;
+        }
+        uint32_t x = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        uint32_t wpre = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            const uint32_t t = wsum[w];
+            wpre += w < wave ? t : 0u;
+            tot += t;
+        }
+        const uint32_t ex = wpre + x - cnt;
+        uint32_t oe = base_e + (ex & 0xffffu), os = (uint32_t)ne + base_s + (ex >> 16);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if (v[e] < 0) continue;
+            const uint32_t o = v[e] < ne ? oe++ : os++;
+            if (o < (uint32_t)ev.feat_stride) fs[o] = v[e];
+        }
+        base_e += tot & 0xffffu;
+        base_s += tot >> 16;
+        __syncthreads();   // wsum is rewritten by the next chunk
+    }
+}
+
 hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
     hipLaunchKernelGGL(ring_count_kernel, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(ring_offsets_kernel, dim3(ev.B), dim3(256), 0, s, ev);
@@ -551,6 +603,7 @@ hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
     hipLaunchKernelGGL(ring_features_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
     const int cblocks = min(64, (ev.raw_stride + 255) / 256);
     hipLaunchKernelGGL(concat_kernel, dim3(max(cblocks, 1), ev.B), dim3(256), 0, s, ev);
+    hipLaunchKernelGGL(order_kernel, dim3(ev.B), dim3(1024), 0, s, ev);
     return hipGetLastError();
 }
 

@@ -34,6 +34,10 @@ __device__ __forceinline__ float key_d2(double k) { return __uint_as_float((uint
 #define LMSF_KNN_UNROLL 4
 #endif
 constexpr int kKnnUnroll = LMSF_KNN_UNROLL;   // candidate loads in flight per lane (T = 1 path): 4 measured best (r01: 0.485 ms vs 0.522 at 1, 0.572 at 8 -- 87 VGPRs)
+#ifndef LMSF_KNN_ROWS_FIRST
+#define LMSF_KNN_ROWS_FIRST 1
+#endif
+constexpr bool kKnnRowsFirst = LMSF_KNN_ROWS_FIRST != 0;
 
 template <int T>
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
@@ -86,6 +90,260 @@ __device__ __forceinline__ GridView pick_grid(bool c, const GridView& a, const G
     return r;
 }
 
+// The 5-NN walk of one query w (T lanes per query; lane = this lane's index in the team): the kept
+// keys of this lane in k (ascending), c27 += the untrimmed 27-cell candidate count when count27.
+template <int T, bool TWO, bool PRUNE>
+__device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, const float3 w, const int lane,
+                                         const int count27, double (&k)[5], unsigned int& c27) {
+    constexpr int NR = TWO ? 18 : 9;
+    constexpr uint32_t kGridBit = 0x80000000u;
+    const float fx = floorf(w.x), fy = floorf(w.y), fz = floorf(w.z);
+    // A (grid, dy, dz) x-row of 3 cells (3 sx slices) is one contiguous range of the sorted points.
+    // With rem = kCullLim - gy^2 - gz^2 (gy, gz: the query's gaps to the row's y and z slabs), only
+    // points with |x - qx| <= sqrt(rem) can have d2 < 1, so the row is trimmed to the slices
+    // meeting [qx - sqrt(rem), qx + sqrt(rem)] (window edges in double from the exact float query;
+    // the kCullLim margin dwarfs float rounding of the gaps, of sqrt and of d2).  c27 counts the
+    // untrimmed 27 cells (SURVEY 8(d) accounting).
+    constexpr float kCullLim = 1.0f + 1e-5f;
+    auto resolve_row = [&](int rr, int& rs, int& rl) {
+        rs = 0;
+        rl = 0;
+        const GridView gg = pick_grid(TWO && rr >= 9, g2, g);
+        const int gn = gg.n, ox = gg.ox, oy = gg.oy, oz = gg.oz, nx = gg.nx, ny = gg.ny, nz = gg.nz, sx = gg.sx;
+        const uint32_t* off = gg.off;
+        const int r9 = rr % 9, dyo = (r9 % 3) - 1, dzo = (r9 / 3) - 1;
+        const float fxs = fx * (float)sx;
+        const bool inside = gn > 0 && fxs >= (float)(ox - 2 * sx) && fxs <= (float)(ox + nx + sx) &&
+                            fy >= (float)(oy - 2) && fy <= (float)(oy + ny + 1) &&
+                            fz >= (float)(oz - 2) && fz <= (float)(oz + nz + 1);
+        if (!inside) return;
+        const int cxs = (int)fxs - ox, cy = (int)fy - oy + dyo, cz = (int)fz - oz + dzo;
+        const int xa = max(cxs - sx, 0), xb = min(cxs + 2 * sx - 1, nx - 1);
+        if (cy < 0 || cy >= ny || cz < 0 || cz >= nz || xa > xb) return;
+        const uint32_t* row = off + ((size_t)cz * ny + cy) * nx;
+        const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
+        const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
+        const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
+        const float rem = kCullLim - gy * gy - gz * gz;
+        if (rem >= 0.f) {
+            const double r = (double)sqrtf(rem);
+            const int sa = max(xa, (int)floor(((double)w.x - r) * sx) - ox);
+            const int sb = min(xb, (int)floor(((double)w.x + r) * sx) - ox);
+            if (sa <= sb) {
+                const uint32_t s0 = row[sa], s1 = row[sb + 1];
+                rs = (int)s0;
+                rl = (int)(s1 - s0);
+            }
+        }
+        if (count27) c27 += row[xb + 1] - row[xa];
+    };
+    auto consider = [&](const float4 m, uint32_t /*tagged_pos*/) {
+        const float dx = w.x - m.x, dy = w.y - m.y, dz = w.z - m.z;
+        const float d2 = dx * dx + dy * dy + dz * dz;
+        double x = key_as_double(((uint64_t)(__float_as_uint(d2) + kKeyBias) << 32) | (uint32_t)__float_as_int(m.w));
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const double lo = fmin(k[i], x);
+            x = fmax(k[i], x);
+            k[i] = lo;
+        }
+    };
+    if constexpr (T == 1 && !PRUNE && kKnnRowsFirst) {
+        // all rows resolved first (2 x NR offset loads in one batch, one latency instead of NR), then
+        // walked with kKnnUnroll candidate loads in flight
+        int rs_[NR], rl_[NR];
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) resolve_row(rr, rs_[rr], rl_[rr]);
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) {
+            const float4* rp = (TWO && rr >= 9) ? g2.pts : g.pts;
+            const uint32_t tag = (TWO && rr >= 9) ? kGridBit : 0u;
+            const int a = rs_[rr], len = rl_[rr];
+            int c = 0;
+            for (; c + kKnnUnroll <= len; c += kKnnUnroll) {
+                float4 m[kKnnUnroll];
+#pragma unroll
+                for (int u = 0; u < kKnnUnroll; ++u) m[u] = rp[a + c + u];
+#pragma unroll
+                for (int u = 0; u < kKnnUnroll; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
+            }
+            for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
+        }
+    } else if constexpr (T == 1 && !PRUNE) {
+        // one lane walks its rows; kKnnUnroll loads in flight per step (a row is contiguous: 8 points per
+        // 128-B line), so the lane waits once per kKnnUnroll candidates instead of once per candidate.
+        // Keys are unique (global index), so the kept top-5 does not depend on the visit order.
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) {
+            const float4* rp = (TWO && rr >= 9) ? g2.pts : g.pts;
+            const uint32_t tag = (TWO && rr >= 9) ? kGridBit : 0u;
+            int a, len;
+            resolve_row(rr, a, len);
+            int c = 0;
+            for (; c + kKnnUnroll <= len; c += kKnnUnroll) {
+                float4 m[kKnnUnroll];
+#pragma unroll
+                for (int u = 0; u < kKnnUnroll; ++u) m[u] = rp[a + c + u];
+#pragma unroll
+                for (int u = 0; u < kKnnUnroll; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
+            }
+            for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
+        }
+    } else if constexpr (T == 1) {
+        // Dense maps (PRUNE): the walk prunes with the current 5th-best distance d4 (1.0 until five
+        // are held), which is ~0.2 m on a 10M-point map:
+        //   pass 1: rows nearest first (own row, 4 faces, 4 corners), each trimmed to the x-window of
+        //           radius sqrt(lim1) (lim1 from the map's density, GridView::lim1); rows with yz-gap^2
+        //           lb > min(d4, lim1) skipped; scanned rows are marked;
+        //   pass 2: every row with lb <= d4, trimmed to the x-window of radius sqrt(d4) minus the
+        //           slices pass 1 scanned (recomputed from lim1).
+        // Skipping a row whose lb exceeds d4 is exact: float rounding is monotone, so every point of
+        // the row has fl(d2) >= fl(gy^2 + gz^2) > d4 (it could not enter the top-5, ties included).
+        // x-windows carry the 1e-5 relative margin of kCullLim.  Sparse maps (C2: ~6 points per
+        // occupied cell) take the plain walk above: there the extra offset loads cost more than the
+        // candidates they save (measured).
+        auto scan_range = [&](const float4* rp, uint32_t tag, int a, int len) {
+            int c = 0;
+            for (; c + kKnnUnroll <= len; c += kKnnUnroll) {
+                float4 m[kKnnUnroll];
+#pragma unroll
+                for (int u = 0; u < kKnnUnroll; ++u) m[u] = rp[a + c + u];
+#pragma unroll
+                for (int u = 0; u < kKnnUnroll; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
+            }
+            for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
+        };
+        // row rr -> its (grid, dy, dz) geometry; false when the row lies outside the grid
+        auto row_geo = [&](int rr, const uint32_t*& row, int& xa, int& xb, float& lb, int& ox, int& sx) {
+            const GridView gg = pick_grid(TWO && rr >= 9, g2, g);
+            ox = gg.ox;
+            sx = gg.sx;
+            const int r9 = rr % 9, dyo = (r9 % 3) - 1, dzo = (r9 / 3) - 1;
+            const float fxs = fx * (float)gg.sx;
+            const bool inside = gg.n > 0 && fxs >= (float)(gg.ox - 2 * gg.sx) && fxs <= (float)(gg.ox + gg.nx + gg.sx) &&
+                                fy >= (float)(gg.oy - 2) && fy <= (float)(gg.oy + gg.ny + 1) &&
+                                fz >= (float)(gg.oz - 2) && fz <= (float)(gg.oz + gg.nz + 1);
+            if (!inside) return false;
+            const int cxs = (int)fxs - gg.ox, cy = (int)fy - gg.oy + dyo, cz = (int)fz - gg.oz + dzo;
+            xa = max(cxs - gg.sx, 0);
+            xb = min(cxs + 2 * gg.sx - 1, gg.nx - 1);
+            if (cy < 0 || cy >= gg.ny || cz < 0 || cz >= gg.nz || xa > xb) return false;
+            row = gg.off + ((size_t)cz * gg.ny + cy) * gg.nx;
+            const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
+            const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
+            const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
+            lb = gy * gy + gz * gz;
+            return true;
+        };
+        // slices of [xa, xb] meeting [w.x - r, w.x + r], r = sqrt(lim - lb) (empty when lim < lb)
+        auto window = [&](float lim, float lb, int xa, int xb, int ox, int sx, int& sa, int& sb) {
+            const float rem = lim - lb;
+            sa = 1;
+            sb = 0;
+            if (rem < 0.f) return;
+            const double r = (double)sqrtf(rem);
+            sa = max(xa, (int)floor(((double)w.x - r) * sx) - ox);
+            sb = min(xb, (int)floor(((double)w.x + r) * sx) - ox);
+        };
+        constexpr int kOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // own row, faces, corners
+        auto row_of = [&](int i) { return kOrder[TWO ? i / 2 : i] + ((TWO && (i & 1)) ? 9 : 0); };
+        const float lim1 = g.lim1 * kCullLim;   // both grids of a kind share the first-pass radius
+        uint32_t scanned = 0;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const int rr = row_of(i);
+            const uint32_t* row;
+            int xa, xb, ox, sx;
+            float lb;
+            if (!row_geo(rr, row, xa, xb, lb, ox, sx)) continue;
+            if (count27) c27 += row[xb + 1] - row[xa];
+            const float d4 = key_d2(k[4]);
+            if (lb > d4 || lb > lim1) continue;
+            int sa, sb;
+            window(lim1, lb, xa, xb, ox, sx, sa, sb);
+            scanned |= 1u << rr;
+            if (sa <= sb) {
+                const uint32_t s0 = row[sa];
+                scan_range((TWO && rr >= 9) ? g2.pts : g.pts, (TWO && rr >= 9) ? kGridBit : 0u, (int)s0,
+                           (int)(row[sb + 1] - s0));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const int rr = row_of(i);
+            const float d4 = key_d2(k[4]);
+            const uint32_t* row;
+            int xa, xb, ox, sx;
+            float lb;
+            if (!row_geo(rr, row, xa, xb, lb, ox, sx)) continue;
+            if (lb > d4) continue;
+            int sa, sb, ta = 1, tb = 0;
+            window(d4 * kCullLim, lb, xa, xb, ox, sx, sa, sb);
+            if (scanned & (1u << rr)) window(lim1, lb, xa, xb, ox, sx, ta, tb);
+            const float4* rp = (TWO && rr >= 9) ? g2.pts : g.pts;
+            const uint32_t tag = (TWO && rr >= 9) ? kGridBit : 0u;
+            if (ta > tb) {
+                if (sa <= sb) {
+                    const uint32_t s0 = row[sa];
+                    scan_range(rp, tag, (int)s0, (int)(row[sb + 1] - s0));
+                }
+            } else {
+                const int l1 = min(sb, ta - 1), r0 = max(sa, tb + 1);
+                if (sa <= l1) {
+                    const uint32_t s0 = row[sa];
+                    scan_range(rp, tag, (int)s0, (int)(row[l1 + 1] - s0));
+                }
+                if (r0 <= sb) {
+                    const uint32_t s0 = row[r0];
+                    scan_range(rp, tag, (int)s0, (int)(row[sb + 1] - s0));
+                }
+            }
+        }
+    } else {
+        // lane l resolves rows l, l + T, ...; the team shares them by shuffles
+        constexpr int REPS = (NR + T - 1) / T;
+        int rs_[REPS], rl_[REPS];
+#pragma unroll
+        for (int rep = 0; rep < REPS; ++rep) {
+            rs_[rep] = 0;
+            rl_[rep] = 0;
+            if (lane + rep * T < NR) resolve_row(lane + rep * T, rs_[rep], rl_[rep]);
+        }
+        int st[NR], pre[NR + 1];
+        pre[0] = 0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            st[r] = __shfl(rs_[r / T], r % T, T);
+            pre[r + 1] = pre[r] + __shfl(rl_[r / T], r % T, T);
+        }
+        const int total = pre[NR];
+        // current row r: candidates [rpre, rend) map to pts[rbase + (v - rpre)]
+        int r = 0, rpre = 0, rend = pre[1], rbase = st[0];
+        const float4* rpts = g.pts;
+        uint32_t rtag = 0;
+        for (int v = lane; v < total; v += T) {
+            while (v >= rend) {
+                ++r;
+                rpre = rend;
+                int e = pre[NR], s0 = st[NR - 1];
+#pragma unroll
+                for (int j = NR - 1; j >= 1; --j) {   // static-index selects keep pre[]/st[] in registers
+                    e = (r + 1 == j) ? pre[j] : e;
+                    s0 = (r == j - 1) ? st[j - 1] : s0;
+                }
+                rend = e;
+                rbase = s0;
+                if (TWO && r == 9) {
+                    rpts = g2.pts;
+                    rtag = kGridBit;
+                }
+            }
+            const int pos = rbase + (v - rpre);
+            consider(rpts[pos], (uint32_t)pos | rtag);
+        }
+    }
+}
+
 // One team of T lanes per query.  The 27 cells around the query cell are enumerated as 9
 // x-rows (each row = 3 consecutive cells = one contiguous range of the cell-sorted points); the
 // team strides over the flattened candidate list with coalesced float4 loads, keeps a per-lane
@@ -97,8 +355,6 @@ __device__ __forceinline__ GridView pick_grid(bool c, const GridView& a, const G
 template <int T, bool TWO, bool PRUNE>
 __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, GridView ge2, GridView gs2, BatchView bv,
                                                   int skip_converged, int gx, int remap) {
-    constexpr int NR = TWO ? 18 : 9;
-    constexpr uint32_t kGridBit = 0x80000000u;
     __shared__ unsigned long long blk_n27;
     __shared__ unsigned int blk_q;
     int bx, b;
@@ -126,233 +382,10 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
         const Pose P = load_pose(bv.st[b].x);
         const float4 p = bv.feat[(size_t)b * bv.feat_stride + q];
         const float3 w = associate(P, p);
-        const float fx = floorf(w.x), fy = floorf(w.y), fz = floorf(w.z);
-        // A (grid, dy, dz) x-row of 3 cells (3 sx slices) is one contiguous range of the sorted points.
-        // With rem = kCullLim - gy^2 - gz^2 (gy, gz: the query's gaps to the row's y and z slabs), only
-        // points with |x - qx| <= sqrt(rem) can have d2 < 1, so the row is trimmed to the slices
-        // meeting [qx - sqrt(rem), qx + sqrt(rem)] (window edges in double from the exact float query;
-        // the kCullLim margin dwarfs float rounding of the gaps, of sqrt and of d2).  c27 counts the
-        // untrimmed 27 cells (SURVEY 8(d) accounting).
-        constexpr float kCullLim = 1.0f + 1e-5f;
-        unsigned int c27 = 0;
-        auto resolve_row = [&](int rr, int& rs, int& rl) {
-            rs = 0;
-            rl = 0;
-            const GridView gg = pick_grid(TWO && rr >= 9, g2, g);
-            const int gn = gg.n, ox = gg.ox, oy = gg.oy, oz = gg.oz, nx = gg.nx, ny = gg.ny, nz = gg.nz, sx = gg.sx;
-            const uint32_t* off = gg.off;
-            const int r9 = rr % 9, dyo = (r9 % 3) - 1, dzo = (r9 / 3) - 1;
-            const float fxs = fx * (float)sx;
-            const bool inside = gn > 0 && fxs >= (float)(ox - 2 * sx) && fxs <= (float)(ox + nx + sx) &&
-                                fy >= (float)(oy - 2) && fy <= (float)(oy + ny + 1) &&
-                                fz >= (float)(oz - 2) && fz <= (float)(oz + nz + 1);
-            if (!inside) return;
-            const int cxs = (int)fxs - ox, cy = (int)fy - oy + dyo, cz = (int)fz - oz + dzo;
-            const int xa = max(cxs - sx, 0), xb = min(cxs + 2 * sx - 1, nx - 1);
-            if (cy < 0 || cy >= ny || cz < 0 || cz >= nz || xa > xb) return;
-            const uint32_t* row = off + ((size_t)cz * ny + cy) * nx;
-            const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
-            const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
-            const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
-            const float rem = kCullLim - gy * gy - gz * gz;
-            if (rem >= 0.f) {
-                const double r = (double)sqrtf(rem);
-                const int sa = max(xa, (int)floor(((double)w.x - r) * sx) - ox);
-                const int sb = min(xb, (int)floor(((double)w.x + r) * sx) - ox);
-                if (sa <= sb) {
-                    const uint32_t s0 = row[sa], s1 = row[sb + 1];
-                    rs = (int)s0;
-                    rl = (int)(s1 - s0);
-                }
-            }
-            if (bv.count27) c27 += row[xb + 1] - row[xa];
-        };
         const double sentinel = key_as_double(kSentinel);
         double k[5] = {sentinel, sentinel, sentinel, sentinel, sentinel};   // ascending kept keys
-        auto consider = [&](const float4 m, uint32_t /*tagged_pos*/) {
-            const float dx = w.x - m.x, dy = w.y - m.y, dz = w.z - m.z;
-            const float d2 = dx * dx + dy * dy + dz * dz;
-            double x = key_as_double(((uint64_t)(__float_as_uint(d2) + kKeyBias) << 32) | (uint32_t)__float_as_int(m.w));
-#pragma unroll
-            for (int i = 0; i < 5; ++i) {
-                const double lo = fmin(k[i], x);
-                x = fmax(k[i], x);
-                k[i] = lo;
-            }
-        };
-        if constexpr (T == 1 && !PRUNE) {
-            // one lane walks its rows; kKnnUnroll loads in flight per step (a row is contiguous: 8 points per
-            // 128-B line), so the lane waits once per kKnnUnroll candidates instead of once per candidate.
-            // Keys are unique (global index), so the kept top-5 does not depend on the visit order.
-#pragma unroll
-            for (int rr = 0; rr < NR; ++rr) {
-                const float4* rp = (TWO && rr >= 9) ? g2.pts : g.pts;
-                const uint32_t tag = (TWO && rr >= 9) ? kGridBit : 0u;
-                int a, len;
-                resolve_row(rr, a, len);
-                int c = 0;
-                for (; c + kKnnUnroll <= len; c += kKnnUnroll) {
-                    float4 m[kKnnUnroll];
-#pragma unroll
-                    for (int u = 0; u < kKnnUnroll; ++u) m[u] = rp[a + c + u];
-#pragma unroll
-                    for (int u = 0; u < kKnnUnroll; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
-                }
-                for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
-            }
-        } else if constexpr (T == 1) {
-            // Dense maps (PRUNE): the walk prunes with the current 5th-best distance d4 (1.0 until five
-            // are held), which is ~0.2 m on a 10M-point map:
-            //   pass 1: rows nearest first (own row, 4 faces, 4 corners), each trimmed to the x-window of
-            //           radius sqrt(lim1) (lim1 from the map's density, GridView::lim1); rows with yz-gap^2
-            //           lb > min(d4, lim1) skipped; scanned rows are marked;
-            //   pass 2: every row with lb <= d4, trimmed to the x-window of radius sqrt(d4) minus the
-            //           slices pass 1 scanned (recomputed from lim1).
-            // Skipping a row whose lb exceeds d4 is exact: float rounding is monotone, so every point of
-            // the row has fl(d2) >= fl(gy^2 + gz^2) > d4 (it could not enter the top-5, ties included).
-            // x-windows carry the 1e-5 relative margin of kCullLim.  Sparse maps (C2: ~6 points per
-            // occupied cell) take the plain walk above: there the extra offset loads cost more than the
-            // candidates they save (measured).
-            auto scan_range = [&](const float4* rp, uint32_t tag, int a, int len) {
-                int c = 0;
-                for (; c + kKnnUnroll <= len; c += kKnnUnroll) {
-                    float4 m[kKnnUnroll];
-#pragma unroll
-                    for (int u = 0; u < kKnnUnroll; ++u) m[u] = rp[a + c + u];
-#pragma unroll
-                    for (int u = 0; u < kKnnUnroll; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
-                }
-                for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
-            };
-            // row rr -> its (grid, dy, dz) geometry; false when the row lies outside the grid
-            auto row_geo = [&](int rr, const uint32_t*& row, int& xa, int& xb, float& lb, int& ox, int& sx) {
-                const GridView gg = pick_grid(TWO && rr >= 9, g2, g);
-                ox = gg.ox;
-                sx = gg.sx;
-                const int r9 = rr % 9, dyo = (r9 % 3) - 1, dzo = (r9 / 3) - 1;
-                const float fxs = fx * (float)gg.sx;
-                const bool inside = gg.n > 0 && fxs >= (float)(gg.ox - 2 * gg.sx) && fxs <= (float)(gg.ox + gg.nx + gg.sx) &&
-                                    fy >= (float)(gg.oy - 2) && fy <= (float)(gg.oy + gg.ny + 1) &&
-                                    fz >= (float)(gg.oz - 2) && fz <= (float)(gg.oz + gg.nz + 1);
-                if (!inside) return false;
-                const int cxs = (int)fxs - gg.ox, cy = (int)fy - gg.oy + dyo, cz = (int)fz - gg.oz + dzo;
-                xa = max(cxs - gg.sx, 0);
-                xb = min(cxs + 2 * gg.sx - 1, gg.nx - 1);
-                if (cy < 0 || cy >= gg.ny || cz < 0 || cz >= gg.nz || xa > xb) return false;
-                row = gg.off + ((size_t)cz * gg.ny + cy) * gg.nx;
-                const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
-                const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
-                const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
-                lb = gy * gy + gz * gz;
-                return true;
-            };
-            // slices of [xa, xb] meeting [w.x - r, w.x + r], r = sqrt(lim - lb) (empty when lim < lb)
-            auto window = [&](float lim, float lb, int xa, int xb, int ox, int sx, int& sa, int& sb) {
-                const float rem = lim - lb;
-                sa = 1;
-                sb = 0;
-                if (rem < 0.f) return;
-                const double r = (double)sqrtf(rem);
-                sa = max(xa, (int)floor(((double)w.x - r) * sx) - ox);
-                sb = min(xb, (int)floor(((double)w.x + r) * sx) - ox);
-            };
-            constexpr int kOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // own row, faces, corners
-            auto row_of = [&](int i) { return kOrder[TWO ? i / 2 : i] + ((TWO && (i & 1)) ? 9 : 0); };
-            const float lim1 = g.lim1 * kCullLim;   // both grids of a kind share the first-pass radius
-            uint32_t scanned = 0;
-#pragma unroll
-            for (int i = 0; i < NR; ++i) {
-                const int rr = row_of(i);
-                const uint32_t* row;
-                int xa, xb, ox, sx;
-                float lb;
-                if (!row_geo(rr, row, xa, xb, lb, ox, sx)) continue;
-                if (bv.count27) c27 += row[xb + 1] - row[xa];
-                const float d4 = key_d2(k[4]);
-                if (lb > d4 || lb > lim1) continue;
-                int sa, sb;
-                window(lim1, lb, xa, xb, ox, sx, sa, sb);
-                scanned |= 1u << rr;
-                if (sa <= sb) {
-                    const uint32_t s0 = row[sa];
-                    scan_range((TWO && rr >= 9) ? g2.pts : g.pts, (TWO && rr >= 9) ? kGridBit : 0u, (int)s0,
-                               (int)(row[sb + 1] - s0));
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < NR; ++i) {
-                const int rr = row_of(i);
-                const float d4 = key_d2(k[4]);
-                const uint32_t* row;
-                int xa, xb, ox, sx;
-                float lb;
-                if (!row_geo(rr, row, xa, xb, lb, ox, sx)) continue;
-                if (lb > d4) continue;
-                int sa, sb, ta = 1, tb = 0;
-                window(d4 * kCullLim, lb, xa, xb, ox, sx, sa, sb);
-                if (scanned & (1u << rr)) window(lim1, lb, xa, xb, ox, sx, ta, tb);
-                const float4* rp = (TWO && rr >= 9) ? g2.pts : g.pts;
-                const uint32_t tag = (TWO && rr >= 9) ? kGridBit : 0u;
-                if (ta > tb) {
-                    if (sa <= sb) {
-                        const uint32_t s0 = row[sa];
-                        scan_range(rp, tag, (int)s0, (int)(row[sb + 1] - s0));
-                    }
-                } else {
-                    const int l1 = min(sb, ta - 1), r0 = max(sa, tb + 1);
-                    if (sa <= l1) {
-                        const uint32_t s0 = row[sa];
-                        scan_range(rp, tag, (int)s0, (int)(row[l1 + 1] - s0));
-                    }
-                    if (r0 <= sb) {
-                        const uint32_t s0 = row[r0];
-                        scan_range(rp, tag, (int)s0, (int)(row[sb + 1] - s0));
-                    }
-                }
-            }
-        } else {
-            // lane l resolves rows l, l + T, ...; the team shares them by shuffles
-            constexpr int REPS = (NR + T - 1) / T;
-            int rs_[REPS], rl_[REPS];
-#pragma unroll
-            for (int rep = 0; rep < REPS; ++rep) {
-                rs_[rep] = 0;
-                rl_[rep] = 0;
-                if (lane + rep * T < NR) resolve_row(lane + rep * T, rs_[rep], rl_[rep]);
-            }
-            int st[NR], pre[NR + 1];
-            pre[0] = 0;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                st[r] = __shfl(rs_[r / T], r % T, T);
-                pre[r + 1] = pre[r] + __shfl(rl_[r / T], r % T, T);
-            }
-            const int total = pre[NR];
-            // current row r: candidates [rpre, rend) map to pts[rbase + (v - rpre)]
-            int r = 0, rpre = 0, rend = pre[1], rbase = st[0];
-            const float4* rpts = g.pts;
-            uint32_t rtag = 0;
-            for (int v = lane; v < total; v += T) {
-                while (v >= rend) {
-                    ++r;
-                    rpre = rend;
-                    int e = pre[NR], s0 = st[NR - 1];
-#pragma unroll
-                    for (int j = NR - 1; j >= 1; --j) {   // static-index selects keep pre[]/st[] in registers
-                        e = (r + 1 == j) ? pre[j] : e;
-                        s0 = (r == j - 1) ? st[j - 1] : s0;
-                    }
-                    rend = e;
-                    rbase = s0;
-                    if (TWO && r == 9) {
-                        rpts = g2.pts;
-                        rtag = kGridBit;
-                    }
-                }
-                const int pos = rbase + (v - rpre);
-                consider(rpts[pos], (uint32_t)pos | rtag);
-            }
-        }
+        unsigned int c27 = 0;
+        knn_walk<T, TWO, PRUNE>(g, g2, w, lane, bv.count27, k, c27);
         // merge: five rounds of team-min; the owning lane pops its head (keys are unique)
         double res[5];
 #pragma unroll
@@ -422,9 +455,9 @@ __device__ bool edge_fit(const float4* np, d3& a, d3& b) {
     }
     double d[3], v[9];
     jacobi_eig<3>(cov, d, v);
-    int i0, i1, i2;
-    order3(d, i0, i1, i2);
-    const double l1 = pick3(d, i1), l2 = pick3(d, i2);
+    int i2;
+    double l1, l2;
+    top2_of3(d, l1, l2, i2);
     if (!(l2 > 3 * l1)) return false;
     const double c0[3] = {v[0], v[3], v[6]}, c1[3] = {v[1], v[4], v[7]}, c2[3] = {v[2], v[5], v[8]};
     d3 u = i2 == 0 ? mk(c0[0], c0[1], c0[2]) : (i2 == 1 ? mk(c1[0], c1[1], c1[2]) : mk(c2[0], c2[1], c2[2]));
@@ -527,22 +560,16 @@ __device__ __forceinline__ bool record_residual(const BatchView& bv, size_t slot
 
 // Line / plane fit of one query from its 5 neighbours, record write, and its Huber-weighted
 // normal-equation contribution at the linearisation pose (Ceres' first evaluation).
-__device__ __forceinline__ void fit_one(const BatchView& bv, int solver, int b, int q, int ne, const Pose& Ps,
-                                        double* P) {
+// np: the 5 neighbour points (w = map index bits, np[4].w < 0: fewer than 5 within the radius); w: the
+// query in the map frame (associate(Ps, p)).
+__device__ __forceinline__ void fit_query(const BatchView& bv, int solver, size_t slot, bool is_edge, const float4 p,
+                                          const float3 w, const float4* np, const Pose& Ps, double* P) {
     {
-        const bool is_edge = q < ne;
-        const size_t slot = (size_t)b * bv.feat_stride + q;
-        const float4 p = bv.feat[slot];
         int kind = 0;
         d3 v0 = mk(0, 0, 0);
         double v1x = 0.0, v1y = 0.0, v1z = 0.0;
-        // the 5 neighbour points, written contiguously by knn
-        float4 np[5];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) np[j] = bv.nnp[slot * 5 + j];
         double gn_grad[3] = {0, 0, 0}, gn_res = 0.0;
         if (__float_as_int(np[4].w) >= 0) {
-            const float3 w = associate(Ps, p);
             if (is_edge) {
                 d3 a, bpt;
                 if (edge_fit(np, a, bpt)) {
@@ -585,9 +612,21 @@ __device__ __forceinline__ void fit_one(const BatchView& bv, int solver, int b, 
                 res = surf_residual(Ps, pp, v0, v1x, J);
             huber_accumulate(P, res, J);
         }
-        if (kind == LMSF_EDGE) P[29] += 1.0;
-        if (kind == LMSF_SURF) P[30] += 1.0;
+        // branch-free: a predicated `P[kind ? 29 : 30] += 1` becomes a select of two addresses (scratch)
+        P[29] += kind == LMSF_EDGE ? 1.0 : 0.0;
+        P[30] += kind == LMSF_SURF ? 1.0 : 0.0;
     }
+}
+
+__device__ __forceinline__ void fit_one(const BatchView& bv, int solver, int b, int q, int ne, const Pose& Ps,
+                                        double* P) {
+    const size_t slot = (size_t)b * bv.feat_stride + q;
+    const float4 p = bv.feat[slot];
+    // the 5 neighbour points, written contiguously by knn
+    float4 np[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) np[j] = bv.nnp[slot * 5 + j];
+    fit_query(bv, solver, slot, q < ne, p, associate(Ps, p), np, Ps, P);
 }
 
 // FPT queries per thread (block = 256 * FPT queries): one packet reduction per block.
@@ -608,6 +647,68 @@ __global__ __launch_bounds__(256) void fit_eval_kernel(BatchView bv, int solver)
         if (q < nq) fit_one(bv, solver, b, q, ne, Ps, P);
     }
     block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + blockIdx.x) * kPacket);
+}
+
+// Fused search + fit for batch launches (one lane per query, Ceres-LM solver): the 5-NN walk of
+// knn_kernel<1, false, PRUNE>, then fit_query (line / plane fit, record write, Huber-weighted packet
+// at the linearisation pose) on the neighbours held in registers -- knn_kernel + fit_eval_kernel
+// hand the 5 neighbour points (80 B per query) through memory instead.  Queries run in fslot order:
+// edge slots then surf slots, each in ring order, so neighbouring lanes search neighbouring ring
+// points and a wave runs one fit kind.  Block x reduces fslot entries [256 x, 256 x + 256): the
+// partial count of fit_eval_kernel<1>, so lm_begin reads the same number of packets.
+template <bool PRUNE>
+__global__ __launch_bounds__(256) void match_fit_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
+    __shared__ unsigned long long blk_n27;
+    __shared__ unsigned int blk_q;
+    int bx, b;
+    block_coords(remap, gx, bx, b);
+    const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
+    if (bx * 256 >= nq) return;   // uniform per block, ahead of every barrier
+    if (threadIdx.x == 0) { blk_n27 = 0; blk_q = 0; }
+    __syncthreads();
+    const Pose Ps = load_pose(bv.st[b].x);
+    double P[kPacket];
+#pragma unroll
+    for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
+    const int i = bx * 256 + threadIdx.x;
+    const int q = i < nq ? bv.fslot[(size_t)b * bv.feat_stride + i] : -1;
+    if (q >= 0 && q < nq) {   // fslot is a permutation of [0, nq) (order_kernel); the test guards memory only
+        const bool is_edge = q < ne;
+        const GridView g = pick_grid(is_edge, ge, gs);
+        const size_t slot = (size_t)b * bv.feat_stride + q;
+        const float4 p = bv.feat[slot];
+        const float3 w = associate(Ps, p);
+        const double sentinel = key_as_double(kSentinel);
+        double k[5] = {sentinel, sentinel, sentinel, sentinel, sentinel};
+        unsigned int c27 = 0;
+        knn_walk<1, false, PRUNE>(g, g, w, 0, bv.count27, k, c27);
+        float4 np[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const uint64_t kb = key_bits(k[j]);
+            np[j] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+            if (kb < kSentinel) {
+                const uint32_t idx = (uint32_t)kb;
+                const float4 m = g.orig[idx];
+                np[j] = make_float4(m.x, m.y, m.z, __int_as_float((int)idx));
+            }
+        }
+        if (bv.write_nn) {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) bv.nnp[slot * 5 + j] = np[j];
+        }
+        fit_query(bv, LMSF_SOLVER_CERES_LM, slot, is_edge, p, w, np, Ps, P);
+        if (bv.n27) {
+            if (c27) atomicAdd(&blk_n27, (unsigned long long)c27);
+            atomicAdd(&blk_q, 1u);
+        }
+    }
+    block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + bx) * kPacket);   // barriers inside
+    if (threadIdx.x == 0 && bv.n27 && blk_q) {
+        unsigned long long* shard = bv.n27 + (size_t)(blockIdx.x & (kCounterShards - 1)) * 16;
+        atomicAdd(shard, blk_n27);
+        atomicAdd(shard + 1, (unsigned long long)blk_q);
+    }
 }
 
 // LM candidate evaluation over the fixed correspondences (Ceres re-evaluates the same residual
@@ -753,6 +854,31 @@ int fit_per_thread_default() {
         return (x == 1 || x == 2 || x == 4) ? x : 1;
     }();
     return v;
+}
+
+// LMSF_FUSED = 0 | 1 (A/B): the fused search + fit for batch launches (default 1).
+static bool fused_enabled() {
+    static bool v = [] {
+        const char* e = getenv("LMSF_FUSED");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
+bool match_fit_applies(const GridView& edge2, const GridView& surf2, const BatchView& bv, int solver) {
+    return fused_enabled() && solver == LMSF_SOLVER_CERES_LM && bv.fslot != nullptr && edge2.n == 0 && surf2.n == 0 &&
+           bv.fit_per_thread == 1 && knn_team((size_t)bv.feat_stride * bv.B) == 1;
+}
+
+hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const BatchView& bv, hipStream_t s) {
+    const int gx = (bv.feat_stride + 255) / 256;
+    const dim3 grid(gx * bv.B);
+    const bool prune = (edge.n > 0 && edge.lim1 < 1.f) || (surf.n > 0 && surf.lim1 < 1.f);
+    if (prune)
+        hipLaunchKernelGGL(match_fit_kernel<true>, grid, dim3(256), 0, s, edge, surf, bv, gx, knn_remap());
+    else
+        hipLaunchKernelGGL(match_fit_kernel<false>, grid, dim3(256), 0, s, edge, surf, bv, gx, knn_remap());
+    return hipGetLastError();
 }
 
 hipError_t launch_lm_eval(const BatchView& bv, hipStream_t s) {

@@ -78,6 +78,8 @@ struct BatchView {
     const int* qslot;        // [B][pos_stride] feature slot per ring position (the knn order), null: slot order
     const int* n_pos;        // [B] ring positions per slot (with qslot)
     int pos_stride;
+    const int* fslot;        // [B][feat_stride] edge slots then surf slots, each in ring order (with qslot)
+    int write_nn;            // fused search + fit also writes nnp (lmsf_match diagnostics)
 };
 
 // ---- launchers (each enqueues on `stream`, never synchronises)
@@ -101,6 +103,10 @@ hipError_t launch_lm_eval(const BatchView& bv, hipStream_t s);
 hipError_t launch_lm_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
 hipError_t launch_gn_solve(const BatchView& bv, int outer, hipStream_t s);
 int fit_per_thread_default();
+// Fused 5-NN search + fit + first evaluation (one lane per query, queries in fslot order); false:
+// not applicable to this launch (caller runs launch_knn + launch_fit_eval).
+bool match_fit_applies(const GridView& edge2, const GridView& surf2, const BatchView& bv, int solver);
+hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const BatchView& bv, hipStream_t s);
 hipError_t launch_state_init(const BatchView& bv, const double* poses, hipStream_t s);
 // Standalone evaluation at one pose (diagnostics): packet of slot 0 into out29 (device).
 hipError_t launch_eval_at(const BatchView& bv, const double* pose_dev, double* out_dev, hipStream_t s);
@@ -127,6 +133,7 @@ struct ExtractView {
     int* ring_surf_cnt;          // [B][kMaxRings]
     int* qcode;                  // [B][raw_stride] per ring position: ring-local edge index, kQSurf | surf index, -1
     int* qslot;                  // [B][raw_stride] per ring position: its feature slot or -1 (the search order)
+    int* fslot;                  // [B][feat_stride] qslot's valid entries, edge slots first (stable)
     int* n_pos;                  // [B] ring positions of the slot (ring_start[n_scans])
     float4* feat;                // [B][feat_stride] output (edges then surfs)
     int* feat_src;               // [B][feat_stride]
