@@ -656,8 +656,13 @@ __global__ __launch_bounds__(256) void fit_eval_kernel(BatchView bv, int solver)
 // edge slots then surf slots, each in ring order, so neighbouring lanes search neighbouring ring
 // points and a wave runs one fit kind.  Block x reduces fslot entries [256 x, 256 x + 256): the
 // partial count of fit_eval_kernel<1>, so lm_begin reads the same number of packets.
+// Waves per SIMD the fused kernel is compiled for (A/B): 4 = its natural 117 VGPRs, no scratch.
+// Forcing 5 (96 VGPRs, 100 B spill) measured 16.2k scans/s, 6 (80, 168 B) 15.2k, vs 17.0k at 4.
+#ifndef LMSF_FUSED_WAVES
+#define LMSF_FUSED_WAVES 4
+#endif
 template <bool PRUNE>
-__global__ __launch_bounds__(256) void match_fit_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void match_fit_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
     __shared__ unsigned long long blk_n27;
     __shared__ unsigned int blk_q;
     int bx, b;
