@@ -149,6 +149,13 @@ def shared_map(d, make):
     return multi.broadcast_map(e, s, d.dev)
 
 
+def kernel_name(ks):
+    """The timed neighbour-search launch: the fused search + fit kernel (batch launches) or knn_kernel."""
+    if ks.launches and ks.fused_launches == ks.launches:
+        return "match_fit_kernel (fused 5-NN search + line/plane fit + first evaluation)"
+    return "knn_kernel"
+
+
 def knn_roofline(ks, mean_n27, traffic_json, batch, map_points, note):
     """B_search = sum_q [16 (query) + 27*8 (cell ranges) + 16 * n27(q)] per launch,
     over the HIP-event-timed launches of the neighbour-search kernel (n27 per query from the
@@ -168,7 +175,7 @@ def knn_roofline(ks, mean_n27, traffic_json, batch, map_points, note):
             traffic = None
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "knn_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
+            "kernel": kernel_name(ks), "avg_launch_ms": round(avg_launch_ms, 4),
             "alg_bytes_per_launch": int(bytes_per_launch), "launches": int(ks.launches),
             "queries_per_launch": int(ks.queries / max(ks.launches, 1)),
             "mean_n27": round(mean_n27, 1),

@@ -178,7 +178,8 @@ lmsf_status lmsf_eval(lmsf_ctx* ctx, const double pose[7], double out[29]);
  * 3x3x3 block of 1 m cells around each query: the algorithmic-byte figure of DESIGN.md).
  * reset mode: LMSF_STATS_TIMING (events, launches, queries) | LMSF_STATS_N27 (n27_sum and
  * queries; costs the search extra cell-offset loads, so it is kept out of timed launches);
- * 0 turns accounting off. */
+ * 0 turns accounting off.  fused_launches: how many of the launches were the fused search + fit
+ * kernel (batch launches with the Ceres-LM solver; the fit is then inside the timed launch). */
 #define LMSF_STATS_TIMING 1
 #define LMSF_STATS_N27 2
 typedef struct {
@@ -186,6 +187,7 @@ typedef struct {
     double total_ms;
     int64_t queries;
     int64_t n27_sum;
+    int64_t fused_launches;
 } lmsf_kernel_stats;
 lmsf_status lmsf_kernel_stats_get(lmsf_ctx* ctx, lmsf_kernel_stats* out);
 lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* ctx, int32_t mode);

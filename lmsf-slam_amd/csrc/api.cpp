@@ -146,7 +146,7 @@ struct lmsf_ctx {
     hipEvent_t ev[2 * kEventPairs];
     int ev_used = 0;
     double knn_ms = 0.0;
-    int64_t knn_launches = 0, knn_queries = 0;
+    int64_t knn_launches = 0, knn_queries = 0, fused_launches = 0;
     // lmsf_voxel_filter workspace (grown on demand)
     VoxelFilter voxel;
     float4* vox_in = nullptr;
@@ -359,6 +359,7 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
             c->ev_used += 2;
         }
         c->knn_launches++;
+        if (fused) c->fused_launches++;
         if (!fused) HIPCHK(c, launch_fit_eval(ge, gs, bv, c->cfg.solver, s));
         if (gn) {
             HIPCHK(c, launch_gn_solve(bv, o, s));
@@ -954,6 +955,7 @@ lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* c, int32_t mode) {
     c->ev_used = 0;
     c->knn_ms = 0.0;
     c->knn_launches = 0;
+    c->fused_launches = 0;
     c->knn_queries = 0;
     HIPCHK(c, hipMemset(c->d_n27, 0, kCounterShards * 16 * sizeof(unsigned long long)));
     return LMSF_OK;
@@ -970,6 +972,7 @@ lmsf_status lmsf_kernel_stats_get(lmsf_ctx* c, lmsf_kernel_stats* out) {
     unsigned long long n27 = 0, q = 0;
     for (int i = 0; i < kCounterShards; ++i) { n27 += sh[(size_t)i * 16]; q += sh[(size_t)i * 16 + 1]; }
     out->launches = c->knn_launches;
+    out->fused_launches = c->fused_launches;
     out->total_ms = c->knn_ms;
     out->queries = (int64_t)q;
     out->n27_sum = (int64_t)n27;

@@ -545,25 +545,46 @@ __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
 
 // Stable partition of the search order by kind: fslot = the valid entries of qslot, edge slots
 // (slot < n_edge) first, each kind in ring order (the fused search + fit order: neighbouring lanes
-// search neighbouring ring points, and a wave runs one fit kind).  One 1024-thread block per slot;
-// each thread takes 8 consecutive ring positions per chunk, block-wide exclusive scan of the packed
-// (edge, surf) counts (16 bits each: a chunk holds 8192 positions).
-__global__ __launch_bounds__(1024) void order_kernel(ExtractView ev) {
-    constexpr int E = 8;
-    __shared__ uint32_t wsum[16];
-    const int b = blockIdx.x;
-    const int ne = ev.n_edge[b], npos = ev.n_pos[b];
+// search neighbouring ring points, and a wave runs one fit kind).  One block per (ring, slot): a
+// ring's valid positions are exactly its ring_edge_cnt edges and ring_surf_cnt surfs (concat_kernel),
+// so ring r writes edges from epre[r] and surfs from n_edge + spre[r]; inside the ring a block-wide
+// exclusive scan of the packed (edge, surf) counts (16 bits each) of 4 consecutive positions per
+// thread, 1024 positions per chunk.
+__global__ __launch_bounds__(256) void order_kernel(ExtractView ev) {
+    constexpr int E = 4;
+    __shared__ uint32_t wsum[4];
+    __shared__ int pre[2];
+    const int r = blockIdx.x, b = blockIdx.y;
+    const int nr = ev.n_scans;
+    if (threadIdx.x < 64) {   // one wave: ring-count prefixes below r
+        int e = 0, sc = 0;
+        for (int k = threadIdx.x; k < r; k += 64) {
+            e += ev.ring_edge_cnt[(size_t)b * kMaxRings + k];
+            sc += ev.ring_surf_cnt[(size_t)b * kMaxRings + k];
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            e += __shfl_xor(e, o, 64);
+            sc += __shfl_xor(sc, o, 64);
+        }
+        if (threadIdx.x == 0) { pre[0] = e; pre[1] = sc; }
+    }
+    __syncthreads();
+    if (r >= nr) return;
+    const int ne = ev.n_edge[b];
+    const int* rs = ev.ring_start + (size_t)b * (kMaxRings + 1);
+    const int p0 = rs[r], p1 = rs[r + 1];
     const int* qs = ev.qslot + (size_t)b * ev.raw_stride;
     int* fs = ev.fslot + (size_t)b * ev.feat_stride;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t base_e = 0, base_s = 0;
-    for (int c0 = 0; c0 < npos; c0 += 1024 * E) {
+    uint32_t base_e = (uint32_t)pre[0], base_s = (uint32_t)(ne + pre[1]);
+    for (int c0 = p0; c0 < p1; c0 += 256 * E) {
         int v[E];
         uint32_t cnt = 0;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const int p = c0 + threadIdx.x * E + e;
-            v[e] = p < npos ? qs[p] : -1;
+            v[e] = p < p1 ? qs[p] : -1;
             if (v[e] >= 0) cnt += v[e] < ne ? 1u : 0x10000u;
         }
         uint32_t x = cnt;
@@ -576,13 +597,13 @@ __global__ __launch_bounds__(1024) void order_kernel(ExtractView ev) {
         __syncthreads();
         uint32_t wpre = 0, tot = 0;
 #pragma unroll
-        for (int w = 0; w < 16; ++w) {
+        for (int w = 0; w < 4; ++w) {
             const uint32_t t = wsum[w];
             wpre += w < wave ? t : 0u;
             tot += t;
         }
         const uint32_t ex = wpre + x - cnt;
-        uint32_t oe = base_e + (ex & 0xffffu), os = (uint32_t)ne + base_s + (ex >> 16);
+        uint32_t oe = base_e + (ex & 0xffffu), os = base_s + (ex >> 16);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             if (v[e] < 0) continue;
@@ -603,7 +624,7 @@ hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
     hipLaunchKernelGGL(ring_features_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
     const int cblocks = min(64, (ev.raw_stride + 255) / 256);
     hipLaunchKernelGGL(concat_kernel, dim3(max(cblocks, 1), ev.B), dim3(256), 0, s, ev);
-    hipLaunchKernelGGL(order_kernel, dim3(ev.B), dim3(1024), 0, s, ev);
+    hipLaunchKernelGGL(order_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
     return hipGetLastError();
 }
 
