@@ -92,7 +92,8 @@ __device__ __forceinline__ GridView pick_grid(bool c, const GridView& a, const G
 
 // The 5-NN walk of one query w (T lanes per query; lane = this lane's index in the team): the kept
 // keys of this lane in k (ascending), c27 += the untrimmed 27-cell candidate count when count27.
-template <int T, bool TWO, bool PRUNE>
+// RU: candidate loads in flight per row step of the one-lane rows-first walk.
+template <int T, bool TWO, bool PRUNE, int RU = kKnnUnroll>
 __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, const float3 w, const int lane,
                                          const int count27, double (&k)[5], unsigned int& c27) {
     constexpr int NR = TWO ? 18 : 9;
@@ -150,7 +151,7 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
     };
     if constexpr (T == 1 && !PRUNE && kKnnRowsFirst) {
         // all rows resolved first (2 x NR offset loads in one batch, one latency instead of NR), then
-        // walked with kKnnUnroll candidate loads in flight
+        // walked with RU candidate loads in flight
         int rs_[NR], rl_[NR];
 #pragma unroll
         for (int rr = 0; rr < NR; ++rr) resolve_row(rr, rs_[rr], rl_[rr]);
@@ -160,12 +161,12 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
             const uint32_t tag = (TWO && rr >= 9) ? kGridBit : 0u;
             const int a = rs_[rr], len = rl_[rr];
             int c = 0;
-            for (; c + kKnnUnroll <= len; c += kKnnUnroll) {
-                float4 m[kKnnUnroll];
+            for (; c + RU <= len; c += RU) {
+                float4 m[RU];
 #pragma unroll
-                for (int u = 0; u < kKnnUnroll; ++u) m[u] = rp[a + c + u];
+                for (int u = 0; u < RU; ++u) m[u] = rp[a + c + u];
 #pragma unroll
-                for (int u = 0; u < kKnnUnroll; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
+                for (int u = 0; u < RU; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
             }
             for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
         }
@@ -658,6 +659,11 @@ __global__ __launch_bounds__(256) void fit_eval_kernel(BatchView bv, int solver)
 // partial count of fit_eval_kernel<1>, so lm_begin reads the same number of packets.
 // Waves per SIMD the fused kernel is compiled for (A/B): 4 = its natural 117 VGPRs, no scratch.
 // Forcing 5 (96 VGPRs, 100 B spill) measured 16.2k scans/s, 6 (80, 168 B) 15.2k, vs 17.0k at 4.
+// Candidate loads in flight per row step of the fused kernel's walk (A/B): 4 (0.472-0.477 ms) beat 2
+// (0.49), 6 (0.485), 8 (0.51) and a walk flattened across rows with 4-16 in flight (0.52-0.54).
+#ifndef LMSF_FUSED_UNROLL
+#define LMSF_FUSED_UNROLL 4
+#endif
 #ifndef LMSF_FUSED_WAVES
 #define LMSF_FUSED_WAVES 4
 #endif
@@ -686,7 +692,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         const double sentinel = key_as_double(kSentinel);
         double k[5] = {sentinel, sentinel, sentinel, sentinel, sentinel};
         unsigned int c27 = 0;
-        knn_walk<1, false, PRUNE>(g, g, w, 0, bv.count27, k, c27);
+        knn_walk<1, false, PRUNE, LMSF_FUSED_UNROLL>(g, g, w, 0, bv.count27, k, c27);
         float4 np[5];
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
