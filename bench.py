@@ -33,8 +33,10 @@ sys.path.insert(0, os.path.join(REPO, "lmsf-slam_amd"))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 DEFAULTS = {   # per configuration: batch (scans per launch), map points, columns, steps, warmup
-    # C2 defaults follow SURVEY 8(d) "Scans/s": 1,000+ scans (16 x 64) after ~50 warm-up scans (one step)
-    "C2": dict(batch=64, map_points=1_000_000, cols=4096, steps=16, warmup=1),
+    # C2 defaults follow SURVEY 8(d) "Scans/s": 1,000+ scans (8 x 128) after one warm-up step.  Batch 128
+    # over 2 context streams (measured, r01: 64 x 1 stream 17.3k scans/s, 64 x 2 17.8k, 128 x 1 18.7k,
+    # 128 x 2 19.3k, 256 x 2 20.0k; 4 streams lose): one launch per context is ~6.6 ms of latency
+    "C2": dict(batch=128, map_points=1_000_000, cols=4096, steps=8, warmup=1, streams=2),
     "C3": dict(batch=1, map_points=0, cols=4096, steps=20, warmup=3),
     "C4": dict(batch=1, map_points=5_000_000, cols=4096, steps=20, warmup=3),
     "C5": dict(batch=125, map_points=10_000_000, cols=2048, steps=2, warmup=1),
@@ -49,6 +51,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None, help="scans per GPU per launch")
     ap.add_argument("--unique-scans", type=int, default=None, help="distinct synthetic scans per rank")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="C2/C5: contexts per GPU (one HIP stream each) sharing a launch batch; their kernels "
+                         "run concurrently, so the small solver / extraction launches of one fill the chip "
+                         "beside the other's")
     ap.add_argument("--map-points", type=int, default=None)
     ap.add_argument("--cols", type=int, default=None)
     ap.add_argument("--outer", type=int, default=5)
@@ -61,6 +67,8 @@ def parse():
     for k, v in DEFAULTS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
+    if a.streams is None:
+        a.streams = 1
     if a.unique_scans is None:
         a.unique_scans = {"C2": 8, "C5": 5}.get(a.config, 1)
     if a.traffic_json is None:
@@ -136,6 +144,13 @@ def timed(d, step, warmup, steps, ctxs):
 def timed_stats(ctx):
     """Neighbour-search accounting of the timed launches."""
     return getattr(ctx, "_timed_stats", None) or ctx.kernel_stats()
+
+
+def sum_stats(stats):
+    """Kernel accounting summed over contexts (launch time: each launch's own HIP-event span)."""
+    import types
+    return types.SimpleNamespace(**{f: sum(getattr(k, f) for k in stats)
+                                    for f in ("launches", "total_ms", "queries", "n27_sum", "fused_launches")})
 
 
 def shared_map(d, make):
@@ -230,21 +245,28 @@ def run_batch(args, d):
         guesses = np.stack([synth.perturb(truth_u[unit_scan[j]], np.random.default_rng(3000 + k + 7919 * i))
                             for j, i in enumerate(mine)])
     chunk = min(args.batch, n_units)
+    S = max(1, min(args.streams, chunk))
+    sub_b = -(-chunk // S)                                   # slots per context
     max_pts = max(len(s) for s in scans_u)
-    ctx = _lib.Context(device=d.local, max_batch=chunk, max_scan_points=max_pts + 64, max_features=max_pts + 64,
-                       schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer, **c["extract"])
-    ctx.set_map(_lib.EDGE, em_t)
-    ctx.set_map(_lib.SURF, sm_t)
+    ctxs = [_lib.Context(device=d.local, max_batch=sub_b, max_scan_points=max_pts + 64, max_features=max_pts + 64,
+                         schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer, **c["extract"]) for _ in range(S)]
+    for i, cx in enumerate(ctxs):
+        cx.set_map(_lib.EDGE, em_t)
+        cx.set_map(_lib.SURF, sm_t)
+        cx.load_scans([scans_u[j % U] for j in range(i * sub_b, min((i + 1) * sub_b, chunk))])
+    ctx = ctxs[0]
     map_points = int(em_t.shape[0] + sm_t.shape[0])
-    ctx.load_scans([scans_u[j % U] for j in range(chunk)])
     gathered = torch.zeros((world, n_units, 7), dtype=torch.float64, device=d.dev)
     poses = np.zeros((n_units, 7))
 
     def step():
         for c0 in range(0, n_units, chunk):
             nb = min(chunk, n_units - c0)
-            ctx.batch_launch(guesses[c0:c0 + nb])
-            poses[c0:c0 + nb], _ = ctx.batch_wait(nb)
+            parts = [(cx, c0 + i * sub_b, min(sub_b, nb - i * sub_b)) for i, cx in enumerate(ctxs) if nb > i * sub_b]
+            for cx, a, m in parts:                           # every context's batch enqueued before any wait
+                cx.batch_launch(guesses[a:a + m])
+            for cx, a, m in parts:
+                poses[a:a + m], _ = cx.batch_wait(m)
         if world > 1:                                        # RCCL all-gather of the 6-DoF poses
             if cfg == "C2":
                 multi.gather_poses(poses, gathered, d.dev)
@@ -252,13 +274,15 @@ def run_batch(args, d):
                 multi.gather_pair_poses(poses, args.pairs, world, d.dev)
         return poses
 
-    elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx])
-    ks = timed_stats(ctx)
+    elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, ctxs)
+    ks = sum_stats([timed_stats(cx) for cx in ctxs])
     total_units = (args.batch * world if cfg == "C2" else args.pairs) * args.steps
     terr = [synth.pose_delta(poses[i], truth_u[unit_scan[i]]) for i in range(n_units)]
-    roof = knn_roofline(ks, mean_n27, args.traffic_json, chunk, map_points,
-                        "achieved = SURVEY 8(d) algorithmic bytes / HIP-event launch time; the map + cell "
-                        "index is largely L2/Infinity-Cache resident, so measured HBM traffic (PMC) is lower")
+    roof = knn_roofline(ks, mean_n27, args.traffic_json, sub_b, map_points,
+                        "achieved = SURVEY 8(d) algorithmic bytes / HIP-event launch time (with several context "
+                        "streams a launch's span includes the time it shares the chip with the other stream's "
+                        "kernels); the map + cell index is largely L2/Infinity-Cache resident, so measured HBM "
+                        "traffic (PMC, from a one-stream run: device-wide counters) is lower")
     cpu, pose_dv = None, None
     if rank == 0 and world == 1 and not args.no_cpu:
         oracle = cpu_oracle()
@@ -307,7 +331,7 @@ def run_batch(args, d):
             metric = "LiDAR scans/sec registered (64k-pt scan, 1M-pt map)"
             wl = (f"C2: VLP-16 16x{args.cols} scans (~{npts} pts) vs {map_points}-pt edge+surf map, "
                   f"{args.outer} outer iters x Ceres-LM(4), extraction included, batch {args.batch} scans/GPU "
-                  f"({U} distinct)")
+                  f"({U} distinct) over {S} context stream(s)")
             extra = {"batch_per_gpu": args.batch, "map_points": map_points, "outer_iterations": args.outer,
                      "parallelism": f"scan-sharded x{world}"}
             unit, scaling = "scans/s", "weak"
@@ -321,7 +345,8 @@ def run_batch(args, d):
         line(args, d, metric, total_units / elapsed, unit, elapsed, scaling, wl, extra, roof, cpu,
              pose_delta_vs_cpu=pose_dv,
              pose_error_vs_truth={"max_m": max(t for t, _ in terr), "max_rad": max(r for _, r in terr)})
-    ctx.close()
+    for cx in ctxs:
+        cx.close()
 
 
 # ----------------------------------------------------------------------------- C4: stitched multi-stream tracking
