@@ -261,6 +261,8 @@ def test_batch_run_matches_oracle(lib, oracle_mod, small_workload):
     n = len(wl.scans)
     ctx.load_scans([wl.scans[i % n] for i in range(16)])
     poses, stats = ctx.batch_run(np.stack([wl.guess[i % n] for i in range(16)]))
+    ks = ctx.kernel_stats()
+    assert ks.launches == 5 and ks.fused_launches == 5               # the fused search + fit path ran
     np.testing.assert_array_equal(poses[n:2 * n], poses[:n])          # same scan + guess -> same pose
     for i in range(len(wl.scans)):
         e, s = _features(oracle_mod, wl.scans[i])
@@ -313,16 +315,22 @@ def test_edge_cases(lib, oracle_mod, small_workload):
     assert ne == 0 and ns == 0
 
 
-def test_n27_accounting(lib, oracle_mod, small_workload):
-    """The per-launch candidate count equals the map points in the 3x3x3 cells around each query."""
+@pytest.mark.parametrize("fused", [False, True])
+def test_n27_accounting(lib, oracle_mod, small_workload, fused):
+    """The per-launch candidate count equals the map points in the 3x3x3 cells around each query;
+    8-lane knn_kernel (host features) or the fused one-lane search + fit (extracted features,
+    >= 2^20 query slots)."""
     from lmsf import synth
     wl = small_workload
     e, s = _features(oracle_mod, wl.scans[2])
-    ctx = _ctx(lib)
+    ctx = _ctx(lib, max_batch=1, max_features=1 << 20) if fused else _ctx(lib)
     ctx.set_map(lib.EDGE, wl.edge_map)
     ctx.set_map(lib.SURF, wl.surf_map)
-    ctx.set_scan(lib.EDGE, e)
-    ctx.set_scan(lib.SURF, s)
+    if fused:
+        assert ctx.extract(wl.scans[2]) == (len(e), len(s))
+    else:
+        ctx.set_scan(lib.EDGE, e)
+        ctx.set_scan(lib.SURF, s)
     ctx.kernel_stats_reset(timing=True)   # timed launches carry no n27 accounting
     ctx.match(wl.guess[2], len(e) + len(s))
     ks = ctx.kernel_stats()
