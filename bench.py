@@ -150,7 +150,8 @@ def sum_stats(stats):
     """Kernel accounting summed over contexts (launch time: each launch's own HIP-event span)."""
     import types
     return types.SimpleNamespace(**{f: sum(getattr(k, f) for k in stats)
-                                    for f in ("launches", "total_ms", "queries", "n27_sum", "fused_launches")})
+                                    for f in ("launches", "total_ms", "queries", "n27_sum", "fused_launches",
+                                              "reused_queries")})
 
 
 def shared_map(d, make):
@@ -194,6 +195,7 @@ def knn_roofline(ks, mean_n27, traffic_json, batch, map_points, note):
             "alg_bytes_per_launch": int(bytes_per_launch), "launches": int(ks.launches),
             "queries_per_launch": int(ks.queries / max(ks.launches, 1)),
             "mean_n27": round(mean_n27, 1),
+            "reused_query_frac": round(getattr(ks, "reused_queries", 0) / max(ks.queries, 1), 4),
             "measured_hbm_gbs": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic and avg_launch_ms else None,
             "l2_hit_rate": round(l2_hit, 3) if l2_hit is not None else None,
             "note": note}

@@ -179,7 +179,10 @@ lmsf_status lmsf_eval(lmsf_ctx* ctx, const double pose[7], double out[29]);
  * reset mode: LMSF_STATS_TIMING (events, launches, queries) | LMSF_STATS_N27 (n27_sum and
  * queries; costs the search extra cell-offset loads, so it is kept out of timed launches);
  * 0 turns accounting off.  fused_launches: how many of the launches were the fused search + fit
- * kernel (batch launches with the Ceres-LM solver; the fit is then inside the timed launch). */
+ * kernel (batch launches with the Ceres-LM solver; the fit is then inside the timed launch).
+ * reused_queries: queries of those launches (outer iterations > 0) whose float map-frame query was
+ * bit-identical to the previous iteration's, so their 5-NN set and fit were reused (counted with
+ * the queries). */
 #define LMSF_STATS_TIMING 1
 #define LMSF_STATS_N27 2
 typedef struct {
@@ -188,6 +191,7 @@ typedef struct {
     int64_t queries;
     int64_t n27_sum;
     int64_t fused_launches;
+    int64_t reused_queries;
 } lmsf_kernel_stats;
 lmsf_status lmsf_kernel_stats_get(lmsf_ctx* ctx, lmsf_kernel_stats* out);
 lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* ctx, int32_t mode);

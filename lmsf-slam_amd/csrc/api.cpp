@@ -99,6 +99,7 @@ struct lmsf_ctx {
     int* n_edge = nullptr;
     int* n_surf = nullptr;
     float4* nnp = nullptr;
+    float4* prevw = nullptr;          // [B][F] last searched float query per slot (fused path memo)
     float4* rec_p = nullptr;          // records: point + kind / values / edge tail (BatchView)
     RecV* rec_v = nullptr;
     double2* rec_e = nullptr;
@@ -178,7 +179,10 @@ struct lmsf_ctx {
         v.n_edge = n_edge;
         v.n_surf = n_surf;
         v.nnp = nnp;
+        v.prevw = prevw;
+        v.memo = 0;
         v.fit_per_thread = fit_per_thread_default();
+        v.part_q = 256 * v.fit_per_thread;
         v.rec_p = rec_p;
         v.rec_v = rec_v;
         v.rec_e = rec_e;
@@ -349,8 +353,11 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
         if (t) HIPCHK(c, hipEventRecord(c->ev[c->ev_used], s));
         // batch launches: one fused search + fit kernel (it is then the timed neighbour-search launch)
         const bool fused = match_fit_applies(ge2, gs2, bv, c->cfg.solver);
-        if (fused)
-            HIPCHK(c, launch_match_fit(ge, gs, bv, s));
+        if (fused) {
+            BatchView bvo = bv;
+            bvo.memo = o > 0 && !c->count27 && match_memo_enabled() ? 1 : 0;   // within one solve only
+            HIPCHK(c, launch_match_fit(ge, gs, bvo, s));
+        }
         else
             HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{},
                                  bv, gn ? 1 : 0, s));
@@ -364,7 +371,9 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
         if (gn) {
             HIPCHK(c, launch_gn_solve(bv, o, s));
         } else {
-            HIPCHK(c, launch_lm_begin(bv, s));
+            BatchView bvb = bv;
+            if (fused) bvb.part_q = 64;
+            HIPCHK(c, launch_lm_begin(bvb, s));
             for (int i = 0; i < 4; ++i) {
                 HIPCHK(c, launch_lm_eval(bv, s));
                 HIPCHK(c, launch_lm_step(bv, o, i == 3 ? 1 : 0, s));
@@ -440,7 +449,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
             hipFree(m.scan_tmp);
         }
     }
-    void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
+    void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->prevw, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->sort_key,
                     c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->n_pos, c->d_error};
@@ -477,7 +486,7 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     c->B = cfg->max_batch;
     c->R = cfg->max_scan_points;
     c->F = std::max(cfg->max_features, cfg->max_scan_points);
-    c->max_parts = (c->F + 255) / 256;   // worst case: one query per fit thread
+    c->max_parts = (c->F + 63) / 64;   // worst case: one packet per wave of the fused search + fit
     c->n_tiles = (c->R + kTile - 1) / kTile;
     auto bail = [&](lmsf_status code) {
         lmsf_ctx_destroy(c);
@@ -495,6 +504,7 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->n_edge, B));
     CHK(dalloc(&c->n_surf, B));
     CHK(dalloc(&c->nnp, B * F * 5));
+    CHK(dalloc(&c->prevw, B * F));
     CHK(dalloc(&c->rec_p, B * F));
     CHK(dalloc(&c->rec_v, B * F));
     CHK(dalloc(&c->rec_e, B * F));
@@ -969,13 +979,18 @@ lmsf_status lmsf_kernel_stats_get(lmsf_ctx* c, lmsf_kernel_stats* out) {
     if (rc) return rc;
     std::vector<unsigned long long> sh((size_t)kCounterShards * 16, 0);
     HIPCHK(c, hipMemcpy(sh.data(), c->d_n27, sh.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    unsigned long long n27 = 0, q = 0;
-    for (int i = 0; i < kCounterShards; ++i) { n27 += sh[(size_t)i * 16]; q += sh[(size_t)i * 16 + 1]; }
+    unsigned long long n27 = 0, q = 0, r = 0;
+    for (int i = 0; i < kCounterShards; ++i) {
+        n27 += sh[(size_t)i * 16];
+        q += sh[(size_t)i * 16 + 1];
+        r += sh[(size_t)i * 16 + 2];
+    }
     out->launches = c->knn_launches;
     out->fused_launches = c->fused_launches;
     out->total_ms = c->knn_ms;
     out->queries = (int64_t)q;
     out->n27_sum = (int64_t)n27;
+    out->reused_queries = (int64_t)r;
     return LMSF_OK;
 }
 

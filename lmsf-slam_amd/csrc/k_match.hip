@@ -92,10 +92,12 @@ __device__ __forceinline__ GridView pick_grid(bool c, const GridView& a, const G
 
 // The 5-NN walk of one query w (T lanes per query; lane = this lane's index in the team): the kept
 // keys of this lane in k (ascending), c27 += the untrimmed 27-cell candidate count when count27.
-// RU: candidate loads in flight per row step of the one-lane rows-first walk.
-template <int T, bool TWO, bool PRUNE, int RU = kKnnUnroll>
+// RU: candidate loads in flight per row step of the one-lane rows-first walk.  NK: keys kept (5, or 6
+// for the fused kernel, whose query memo needs the 6th-nearest distance; the pruned walk prunes with
+// the NK-th key, so all NK are exact).
+template <int T, bool TWO, bool PRUNE, int RU = kKnnUnroll, int NK = 5>
 __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, const float3 w, const int lane,
-                                         const int count27, double (&k)[5], unsigned int& c27) {
+                                         const int count27, double (&k)[NK], unsigned int& c27) {
     constexpr int NR = TWO ? 18 : 9;
     constexpr uint32_t kGridBit = 0x80000000u;
     const float fx = floorf(w.x), fy = floorf(w.y), fz = floorf(w.z);
@@ -143,7 +145,7 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
         const float d2 = dx * dx + dy * dy + dz * dz;
         double x = key_as_double(((uint64_t)(__float_as_uint(d2) + kKeyBias) << 32) | (uint32_t)__float_as_int(m.w));
 #pragma unroll
-        for (int i = 0; i < 5; ++i) {
+        for (int i = 0; i < NK; ++i) {
             const double lo = fmin(k[i], x);
             x = fmax(k[i], x);
             k[i] = lo;
@@ -258,7 +260,7 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
             float lb;
             if (!row_geo(rr, row, xa, xb, lb, ox, sx)) continue;
             if (count27) c27 += row[xb + 1] - row[xa];
-            const float d4 = key_d2(k[4]);
+            const float d4 = key_d2(k[NK - 1]);
             if (lb > d4 || lb > lim1) continue;
             int sa, sb;
             window(lim1, lb, xa, xb, ox, sx, sa, sb);
@@ -272,7 +274,7 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
             const int rr = row_of(i);
-            const float d4 = key_d2(k[4]);
+            const float d4 = key_d2(k[NK - 1]);
             const uint32_t* row;
             int xa, xb, ox, sx;
             float lb;
@@ -559,6 +561,22 @@ __device__ __forceinline__ bool record_residual(const BatchView& bv, size_t slot
     return true;
 }
 
+__device__ __forceinline__ bool record_residual_kind(const BatchView& bv, size_t slot, const Pose& Ps, double& res,
+                                                    double* J, int& kind) {
+    const float4 p = bv.rec_p[slot];
+    kind = __float_as_int(p.w);
+    if (kind == 0) return false;
+    const RecV v = bv.rec_v[slot];
+    const d3 pp = mk((double)p.x, (double)p.y, (double)p.z);
+    if (kind == LMSF_EDGE) {
+        const double2 e = bv.rec_e[slot];
+        res = edge_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), mk(v.v[3], e.x, e.y), J);
+    } else {
+        res = surf_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), v.v[3], J);
+    }
+    return true;
+}
+
 // Line / plane fit of one query from its 5 neighbours, record write, and its Huber-weighted
 // normal-equation contribution at the linearisation pose (Ceres' first evaluation).
 // np: the 5 neighbour points (w = map index bits, np[4].w < 0: fewer than 5 within the radius); w: the
@@ -667,32 +685,141 @@ __global__ __launch_bounds__(256) void fit_eval_kernel(BatchView bv, int solver)
 #ifndef LMSF_FUSED_WAVES
 #define LMSF_FUSED_WAVES 4
 #endif
+// Wave-level packet reduction (the transposing butterfly of block_reduce_packet without the LDS
+// step): entry e lands in lane 2e; out[e] written by that lane.
+__device__ __forceinline__ void wave_reduce_packet(double* P, double* out) {
+    const int lane = threadIdx.x & 63;
+    butterfly_step<16>(P, lane);
+    butterfly_step<8>(P, lane);
+    butterfly_step<4>(P, lane);
+    butterfly_step<2>(P, lane);
+    butterfly_step<1>(P, lane);
+    const double v = P[0] + __shfl_xor(P[0], 1, 64);
+    if ((lane & 1) == 0) out[lane >> 1] = v;
+}
+
+// The slot's record values (kind, v0 = a | n, v1 = b | (D, -, -)) -> its residual and Huber-weighted
+// packet at the linearisation pose, plus the match counts (fit_query's LM tail).
+__device__ __forceinline__ void record_packet(int kind, const float4 p, const d3& v0, double v1x, double v1y, double v1z,
+                                              const Pose& Ps, double* P) {
+    if (kind != 0) {
+        double J[6], res;
+        const d3 pp = mk((double)p.x, (double)p.y, (double)p.z);
+        if (kind == LMSF_EDGE)
+            res = edge_residual(Ps, pp, v0, mk(v1x, v1y, v1z), J);
+        else
+            res = surf_residual(Ps, pp, v0, v1x, J);
+        huber_accumulate(P, res, J);
+    }
+    P[29] += kind == LMSF_EDGE ? 1.0 : 0.0;
+    P[30] += kind == LMSF_SURF ? 1.0 : 0.0;
+}
+
 template <bool PRUNE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void match_fit_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
-    __shared__ unsigned long long blk_n27;
-    __shared__ unsigned int blk_q;
+    __shared__ int wcnt[4];
+    __shared__ int work[256];
+    __shared__ double rj[7][256];   // phase-1 residual + Jacobian of a reused query (kept out of registers
+    __shared__ int rk[256];         // across the search), rk = its kind (0: none)
     int bx, b;
     block_coords(remap, gx, bx, b);
     const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
     if (bx * 256 >= nq) return;   // uniform per block, ahead of every barrier
-    if (threadIdx.x == 0) { blk_n27 = 0; blk_q = 0; }
-    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const Pose Ps = load_pose(bv.st[b].x);
-    double P[kPacket];
-#pragma unroll
-    for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
+    unsigned int n_reused = 0;
+    rk[threadIdx.x] = 0;
+    // Phase 1 (every query of the block, fslot order): the query memo of outer iterations > 0.
+    // prevw = (anchor query w0 of the slot's last full search, gap = min over i < 5 of s[i+1] - s[i],
+    // s = sqrt of the kept d2s and s[5] = sqrt(min(6th d2, 1)); -1 when fewer than 5 were found).
+    // Every map point moves by at most |w - w0| relative to the query, and float d2 / sqrt are within
+    // 1e-6 m of exact below 1 m, so with 2 |w - w0| + 1e-5 < gap the 5-NN set, its order and the
+    // d2 < 1 test are unchanged: the line fit and the plane fit (up to its orientation, which follows
+    // the sign of n . w + D) are what a new search would give; only the packet at the new pose is new.
     const int i = bx * 256 + threadIdx.x;
     const int q = i < nq ? bv.fslot[(size_t)b * bv.feat_stride + i] : -1;
-    if (q >= 0 && q < nq) {   // fslot is a permutation of [0, nq) (order_kernel); the test guards memory only
-        const bool is_edge = q < ne;
-        const GridView g = pick_grid(is_edge, ge, gs);
+    bool full = q >= 0 && q < nq;   // fslot is a permutation of [0, nq) (order_kernel); the test guards memory
+    if (full && bv.memo && !bv.count27) {
         const size_t slot = (size_t)b * bv.feat_stride + q;
+        const float4 pw = bv.prevw[slot];
+        if (pw.w > 0.f) {
+            const float4 p = bv.feat[slot];
+            const float3 w = associate(Ps, p);
+            const double dx = (double)w.x - pw.x, dy = (double)w.y - pw.y, dz = (double)w.z - pw.z;
+            if (2.0 * sqrt(dx * dx + dy * dy + dz * dz) + 1e-5 < (double)pw.w) {
+                const int kind = __float_as_int(bv.rec_p[slot].w);
+                d3 v0 = mk(0, 0, 0);
+                double v1x = 0.0, v1y = 0.0, v1z = 0.0;
+                bool reuse = true;
+                if (kind != 0) {
+                    const RecV v = bv.rec_v[slot];
+                    v0 = mk(v.v[0], v.v[1], v.v[2]);
+                    v1x = v.v[3];
+                    if (kind == LMSF_SURF) {   // surf_fit's orientation test at the new query (the stored
+                        const d3 cp = mk((double)w.x, (double)w.y, (double)w.z);   // n, D were flipped to
+                        reuse = (float)(dot(v0, cp) + v1x) > 0.f;                   // make it >= 0 at w0)
+                    } else {
+                        const double2 e = bv.rec_e[slot];
+                        v1y = e.x;
+                        v1z = e.y;
+                    }
+                }
+                if (reuse) {
+                    if (kind != 0) {
+                        double J[6];
+                        const d3 pp = mk((double)p.x, (double)p.y, (double)p.z);
+                        rj[6][threadIdx.x] = kind == LMSF_EDGE ? edge_residual(Ps, pp, v0, mk(v1x, v1y, v1z), J)
+                                                               : surf_residual(Ps, pp, v0, v1x, J);
+#pragma unroll
+                        for (int j = 0; j < 6; ++j) rj[j][threadIdx.x] = J[j];
+                        rk[threadIdx.x] = kind;
+                    }
+                    full = false;
+                    n_reused = 1;
+                }
+            }
+        }
+    }
+    // Phase 2: the queries needing a search are packed to the front of the block (deterministic: fslot
+    // order), so they fill whole waves and the waves left without one finish early.
+    const unsigned long long m = __ballot(full);
+    if (lane == 0) wcnt[wave] = __popcll(m);
+    __syncthreads();
+    int before = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        before += k < wave ? wcnt[k] : 0;
+        total += wcnt[k];
+    }
+    if (full) work[before + __popcll(m & ((1ull << lane) - 1ull))] = q;
+    __syncthreads();
+    unsigned int c27 = 0;
+    double P[kPacket];
+#pragma unroll
+    for (int e = 0; e < kPacket; ++e) P[e] = 0.0;
+    if ((int)threadIdx.x < total) {
+        const int qq = work[threadIdx.x];
+        const bool is_edge = qq < ne;
+        const GridView g = pick_grid(is_edge, ge, gs);
+        const size_t slot = (size_t)b * bv.feat_stride + qq;
         const float4 p = bv.feat[slot];
         const float3 w = associate(Ps, p);
         const double sentinel = key_as_double(kSentinel);
-        double k[5] = {sentinel, sentinel, sentinel, sentinel, sentinel};
-        unsigned int c27 = 0;
-        knn_walk<1, false, PRUNE, LMSF_FUSED_UNROLL>(g, g, w, 0, bv.count27, k, c27);
+        double k[6] = {sentinel, sentinel, sentinel, sentinel, sentinel, sentinel};
+        knn_walk<1, false, PRUNE, LMSF_FUSED_UNROLL, 6>(g, g, w, 0, bv.count27, k, c27);
+        float gap = -1.f;
+        if (key_bits(k[4]) < kSentinel) {
+            double sp = sqrt((double)key_d2(k[0]));
+            double mg = 1e30;
+#pragma unroll
+            for (int j = 1; j < 6; ++j) {
+                const double sj = sqrt((double)fminf(key_d2(k[j]), 1.0f));
+                mg = fmin(mg, sj - sp);
+                sp = sj;
+            }
+            gap = (float)mg;
+        }
+        bv.prevw[slot] = make_float4(w.x, w.y, w.z, gap);
         float4 np[5];
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
@@ -700,25 +827,68 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
             np[j] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
             if (kb < kSentinel) {
                 const uint32_t idx = (uint32_t)kb;
-                const float4 m = g.orig[idx];
-                np[j] = make_float4(m.x, m.y, m.z, __int_as_float((int)idx));
+                const float4 mp = g.orig[idx];
+                np[j] = make_float4(mp.x, mp.y, mp.z, __int_as_float((int)idx));
             }
         }
         if (bv.write_nn) {
 #pragma unroll
             for (int j = 0; j < 5; ++j) bv.nnp[slot * 5 + j] = np[j];
         }
-        fit_query(bv, LMSF_SOLVER_CERES_LM, slot, is_edge, p, w, np, Ps, P);
-        if (bv.n27) {
-            if (c27) atomicAdd(&blk_n27, (unsigned long long)c27);
-            atomicAdd(&blk_q, 1u);
+        int kind = 0;
+        d3 v0 = mk(0, 0, 0);
+        double v1x = 0.0, v1y = 0.0, v1z = 0.0;
+        if (__float_as_int(np[4].w) >= 0) {   // fit_query's LM branch
+            if (is_edge) {
+                d3 a, bpt;
+                if (edge_fit(np, a, bpt)) {
+                    kind = LMSF_EDGE;
+                    v0 = a;
+                    v1x = bpt.x; v1y = bpt.y; v1z = bpt.z;
+                }
+            } else {
+                d3 n;
+                double D, gn_res;
+                if (surf_fit(np, w, n, D, gn_res)) {
+                    kind = LMSF_SURF;
+                    v0 = n;
+                    v1x = D;
+                }
+            }
+        }
+        store_record(bv, slot, p, kind, v0, v1x, v1y, v1z);
+        record_packet(kind, p, v0, v1x, v1y, v1z, Ps, P);
+    }
+    {   // this lane's reused query (phase 1), if any
+        const int kind = rk[threadIdx.x];
+        if (kind != 0) {
+            double J[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) J[j] = rj[j][threadIdx.x];
+            huber_accumulate(P, rj[6][threadIdx.x], J);
+            P[29] += kind == LMSF_EDGE ? 1.0 : 0.0;
+            P[30] += kind == LMSF_SURF ? 1.0 : 0.0;
         }
     }
-    block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + bx) * kPacket);   // barriers inside
-    if (threadIdx.x == 0 && bv.n27 && blk_q) {
-        unsigned long long* shard = bv.n27 + (size_t)(blockIdx.x & (kCounterShards - 1)) * 16;
-        atomicAdd(shard, blk_n27);
-        atomicAdd(shard + 1, (unsigned long long)blk_q);
+    // one packet per wave (no block barrier: a wave without a search ends as soon as it is reduced);
+    // partial index 4 bx + wave, the waves of a block holding any query of [0, nq) write
+    if (bx * 256 + wave * 64 < nq)
+        wave_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + (size_t)bx * 4 + wave) * kPacket);
+    if (bv.n27) {   // accounting runs: queries (phase 1 lanes), reused, n27 of the searches
+        unsigned int qn = (q >= 0 && q < nq) ? 1u : 0u;
+        unsigned long long c = c27;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            qn += __shfl_xor(qn, o, 64);
+            n_reused += __shfl_xor(n_reused, o, 64);
+            c += __shfl_xor(c, o, 64);
+        }
+        if (lane == 0) {
+            unsigned long long* shard = bv.n27 + (size_t)((blockIdx.x * 4 + wave) & (kCounterShards - 1)) * 16;
+            if (c) atomicAdd(shard, c);
+            if (qn) atomicAdd(shard + 1, (unsigned long long)qn);
+            if (n_reused) atomicAdd(shard + 2, (unsigned long long)n_reused);
+        }
     }
 }
 
@@ -874,6 +1044,12 @@ static bool fused_enabled() {
         return e ? atoi(e) != 0 : true;
     }();
     return v;
+}
+
+// LMSF_MEMO = 0 | 1 (default 1), read at every launch so a test can compare both in one process.
+bool match_memo_enabled() {
+    const char* e = getenv("LMSF_MEMO");
+    return e ? atoi(e) != 0 : true;
 }
 
 bool match_fit_applies(const GridView& edge2, const GridView& surf2, const BatchView& bv, int solver) {

@@ -189,7 +189,7 @@ __global__ void state_init_kernel(BatchView bv, const double* poses) {
 __global__ __launch_bounds__(64) void lm_begin_kernel(BatchView bv) {
     const int b = blockIdx.x;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
-    const int fb = 256 * bv.fit_per_thread;
+    const int fb = bv.part_q;
     const int nparts = (nq + fb - 1) / fb;
     double tot[kPacket];
     reduce_parts(bv, b, nparts, tot);

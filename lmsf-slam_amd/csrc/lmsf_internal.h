@@ -64,6 +64,8 @@ struct BatchView {
     const int* n_surf;       // [B]
     float4* nnp;             // [B][feat_stride][5] neighbour points (w = map index bits, -1: none)
     int fit_per_thread;      // queries per thread of fit_eval (partials per kFitThreads*fpt queries)
+    int part_q;              // queries per partial packet of the first evaluation (lm_begin): 256 * fit_per_thread,
+                             // 64 after the fused search + fit (one packet per wave)
     // correspondence records, split so an LM evaluation of a surf record reads 48 B (not 64):
     float4* rec_p;           // [B][feat_stride] lidar-frame point, w = kind (int bits; 0 = none)
     RecV* rec_v;             // [B][feat_stride] surf: n, D; edge: a, b.x
@@ -80,6 +82,9 @@ struct BatchView {
     int pos_stride;
     const int* fslot;        // [B][feat_stride] edge slots then surf slots, each in ring order (with qslot)
     int write_nn;            // fused search + fit also writes nnp (lmsf_match diagnostics)
+    float4* prevw;           // [B][feat_stride] map-frame query of the slot's last full search (fused path)
+    int memo;                // 1: a query whose float query equals prevw reuses its record (same 5-NN
+                             //    set and fit: both depend only on the float query); outer iterations > 0
 };
 
 // ---- launchers (each enqueues on `stream`, never synchronises)
@@ -107,6 +112,7 @@ int fit_per_thread_default();
 // not applicable to this launch (caller runs launch_knn + launch_fit_eval).
 bool match_fit_applies(const GridView& edge2, const GridView& surf2, const BatchView& bv, int solver);
 hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const BatchView& bv, hipStream_t s);
+bool match_memo_enabled();   // LMSF_MEMO (default 1)
 hipError_t launch_state_init(const BatchView& bv, const double* poses, hipStream_t s);
 // Standalone evaluation at one pose (diagnostics): packet of slot 0 into out29 (device).
 hipError_t launch_eval_at(const BatchView& bv, const double* pose_dev, double* out_dev, hipStream_t s);

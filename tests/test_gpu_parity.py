@@ -6,6 +6,8 @@ Bars (DESIGN.md "Parity"):
 * the 29-double normal-equation packet differs only by summation order -> rel 1e-9;
 * poses per outer iteration <= 1e-4 m / 1e-4 rad (north_star tolerance).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -263,6 +265,15 @@ def test_batch_run_matches_oracle(lib, oracle_mod, small_workload):
     poses, stats = ctx.batch_run(np.stack([wl.guess[i % n] for i in range(16)]))
     ks = ctx.kernel_stats()
     assert ks.launches == 5 and ks.fused_launches == 5               # the fused search + fit path ran
+    # outer iterations > 0 reuse the 5-NN set and fit of queries that moved less than half their
+    # neighbour-distance gap: same records, packets summed in another grouping (the searching lanes
+    # are packed), so the poses agree with re-searching every query to rounding
+    os.environ["LMSF_MEMO"] = "0"
+    try:
+        poses0, _ = ctx.batch_run(np.stack([wl.guess[i % n] for i in range(16)]))
+    finally:
+        del os.environ["LMSF_MEMO"]
+    assert np.abs(poses0 - poses).max() <= 1e-12
     np.testing.assert_array_equal(poses[n:2 * n], poses[:n])          # same scan + guess -> same pose
     for i in range(len(wl.scans)):
         e, s = _features(oracle_mod, wl.scans[i])
@@ -280,6 +291,41 @@ def test_batch_run_matches_oracle(lib, oracle_mod, small_workload):
         dt, dr = pose_err(poses[i], ox)
         assert dt <= POSE_TOL and dr <= POSE_TOL
         assert stats[i].outer_iterations == 5
+
+
+def test_batch_memo_dense(lib, oracle_mod, dense_workload):
+    """Query memo on the pruned (dense-map) fused walk: outer iterations > 0 reuse the 5-NN set and fit
+    of every query that moved by less than half its neighbour-distance gap; poses equal to
+    re-searching every query up to summation order, and the reuse actually happens."""
+    wl = dense_workload
+    ctx = _ctx(lib, schedule=1, max_iterations=5, max_batch=16)
+    ctx.set_map(lib.EDGE, wl.edge_map)
+    ctx.set_map(lib.SURF, wl.surf_map)
+    ctx.load_scans([wl.scans[0]] * 16)
+    rng = np.random.default_rng(5)
+    from lmsf import synth
+    guesses = np.stack([synth.perturb(wl.truth[0], rng) for _ in range(16)])
+    ctx.kernel_stats_reset(timing=True)
+    poses, _ = ctx.batch_run(guesses)
+    ks = ctx.kernel_stats()
+    assert ks.fused_launches == 5 and ks.reused_queries > 0.2 * ks.queries
+    os.environ["LMSF_MEMO"] = "0"
+    try:
+        poses0, _ = ctx.batch_run(guesses)
+    finally:
+        del os.environ["LMSF_MEMO"]
+    assert np.abs(poses0 - poses).max() <= 1e-12
+    e, s = _features(oracle_mod, wl.scans[0])
+    reg = oracle_mod.Registration()
+    reg.set_map(1, wl.edge_map)
+    reg.set_map(2, wl.surf_map)
+    reg.set_scan(1, e)
+    reg.set_scan(2, s)
+    reg.set_fixed_schedule(True)
+    reg.set_max_iterations(5)
+    ox, _, _ = reg.solve(guesses[3])
+    dt, dr = pose_err(poses[3], ox)
+    assert dt <= POSE_TOL and dr <= POSE_TOL
 
 
 def test_edge_cases(lib, oracle_mod, small_workload):
