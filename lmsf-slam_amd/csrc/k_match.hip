@@ -717,6 +717,11 @@ __device__ __forceinline__ void record_packet(int kind, const float4 p, const d3
 
 template <bool PRUNE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void match_fit_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
+    // The memo needs the 6th-nearest distance; on dense maps (PRUNE) keeping 6 keys weakens the pruning
+    // (the walk prunes with the last kept key) more than the reuse saves (C5: 2568 / 2660 pairs/s with
+    // the memo off / on vs 2830 without it), so the pruned walk keeps 5 and searches every query.
+    constexpr bool kMemo = !PRUNE;
+    constexpr int kNK = kMemo ? 6 : 5;
     __shared__ int wcnt[4];
     __shared__ int work[256];
     __shared__ double rj[7][256];   // phase-1 residual + Jacobian of a reused query (kept out of registers
@@ -739,7 +744,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     const int i = bx * 256 + threadIdx.x;
     const int q = i < nq ? bv.fslot[(size_t)b * bv.feat_stride + i] : -1;
     bool full = q >= 0 && q < nq;   // fslot is a permutation of [0, nq) (order_kernel); the test guards memory
-    if (full && bv.memo && !bv.count27) {
+    if (kMemo && full && bv.memo && !bv.count27) {
         const size_t slot = (size_t)b * bv.feat_stride + q;
         const float4 pw = bv.prevw[slot];
         if (pw.w > 0.f) {
@@ -805,14 +810,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         const float4 p = bv.feat[slot];
         const float3 w = associate(Ps, p);
         const double sentinel = key_as_double(kSentinel);
-        double k[6] = {sentinel, sentinel, sentinel, sentinel, sentinel, sentinel};
-        knn_walk<1, false, PRUNE, LMSF_FUSED_UNROLL, 6>(g, g, w, 0, bv.count27, k, c27);
+        double k[kNK];
+#pragma unroll
+        for (int j = 0; j < kNK; ++j) k[j] = sentinel;
+        knn_walk<1, false, PRUNE, LMSF_FUSED_UNROLL, kNK>(g, g, w, 0, bv.count27, k, c27);
         float gap = -1.f;
-        if (key_bits(k[4]) < kSentinel) {
+        if (kMemo && key_bits(k[4]) < kSentinel) {
             double sp = sqrt((double)key_d2(k[0]));
             double mg = 1e30;
 #pragma unroll
-            for (int j = 1; j < 6; ++j) {
+            for (int j = 1; j < kNK; ++j) {
                 const double sj = sqrt((double)fminf(key_d2(k[j]), 1.0f));
                 mg = fmin(mg, sj - sp);
                 sp = sj;
