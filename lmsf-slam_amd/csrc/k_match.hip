@@ -826,7 +826,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
             }
             gap = (float)mg;
         }
-        bv.prevw[slot] = make_float4(w.x, w.y, w.z, gap);
+        if (kMemo) bv.prevw[slot] = make_float4(w.x, w.y, w.z, gap);
         float4 np[5];
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
