@@ -33,10 +33,11 @@ sys.path.insert(0, os.path.join(REPO, "lmsf-slam_amd"))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 DEFAULTS = {   # per configuration: batch (scans per launch), map points, columns, steps, warmup
-    # C2 defaults follow SURVEY 8(d) "Scans/s": 1,000+ scans (8 x 128) after one warm-up step.  Batch 128
-    # over 2 context streams (measured, r01: 64 x 1 stream 17.3k scans/s, 64 x 2 17.8k, 128 x 1 18.7k,
-    # 128 x 2 19.3k, 256 x 2 20.0k; 4 streams lose): one launch per context is ~6.6 ms of latency
-    "C2": dict(batch=128, map_points=1_000_000, cols=4096, steps=8, warmup=1, streams=2),
+    # C2 defaults follow SURVEY 8(d) "Scans/s": 1,024 scans (4 x 256) after one warm-up step.  Batch 256
+    # over 2 context streams of 128 (measured, r01, with the query memo: 128 x 1 stream 19.0k scans/s,
+    # 128 x 2 19.8k, 256 x 2 20.9k; before it 64 x 1 17.3k, 64 x 2 17.8k; 4 streams lose): one launch
+    # per context is ~12 ms of latency, well inside a 10 Hz LiDAR's 100 ms
+    "C2": dict(batch=256, map_points=1_000_000, cols=4096, steps=4, warmup=1, streams=2),
     "C3": dict(batch=1, map_points=0, cols=4096, steps=20, warmup=3),
     "C4": dict(batch=1, map_points=5_000_000, cols=4096, steps=20, warmup=3),
     "C5": dict(batch=125, map_points=10_000_000, cols=2048, steps=2, warmup=1),
