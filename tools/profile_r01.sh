@@ -7,6 +7,6 @@ timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_r01" -
 rc=$?; echo "trace_rc=$rc"; case $rc in 0) ;; *) exit $rc;; esac
 for ctr in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
   tag=$(echo $ctr | tr ' ' '_')
-  timeout -s KILL 300 rocprofv3 --pmc $ctr --kernel-trace -d "$R/gpurun_out/pmc_$tag" -o pmc --output-format csv -- python "$R/bench.py" --steps 2 --warmup 1 --no-cpu --streams 1 --batch 64 > "$R/gpurun_out/pmc_$tag.log" 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc $ctr --kernel-trace -d "$R/gpurun_out/pmc_$tag" -o pmc --output-format csv -- python "$R/bench.py" --steps 2 --warmup 1 --no-cpu --streams 1 --batch 128 > "$R/gpurun_out/pmc_$tag.log" 2>&1
   rc=$?; echo "pmc $tag rc=$rc"; case $rc in 0) ;; *) exit $rc;; esac
 done
