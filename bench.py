@@ -18,12 +18,21 @@ Other configurations (`--config`), each its own JSON line:
       10M-point map, pairs partitioned i mod N, one all-gather of the poses (strong scaling).
 
 Usage: python bench.py [--config C2|C3|C4|C5] [--gpus N --steps K --warmup W ...]
-       (N > 1 is launched by torch.distributed.run, one rank per GPU).
+       With --gpus N > 1 outside torch.distributed.run, the bench starts
+       `python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child process (one rank
+       per GPU) and exits with its return code; inside the ranks WORLD_SIZE must equal N.
+
+Roofline (`roofline`): the dominant kernel's PMC-measured HBM bytes per launch (rocprofv3 FETCH_SIZE /
+WRITE_SIZE passes committed under profiles/, `traffic`) over its live HIP-event launch time; the
+SURVEY 8(d) byte model (counted over the queries that actually searched) is reported beside it as
+`roofline.model`, flagged when it would exceed the HBM peak.
 """
 import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,14 +46,15 @@ DEFAULTS = {   # per configuration: batch (scans per launch), map points, column
     # over 2 context streams of 128 (measured, r01, with the query memo: 128 x 1 stream 19.0k scans/s,
     # 128 x 2 19.8k, 256 x 2 20.9k; before it 64 x 1 17.3k, 64 x 2 17.8k; 4 streams lose): one launch
     # per context is ~12 ms of latency, well inside a 10 Hz LiDAR's 100 ms
-    "C2": dict(batch=256, map_points=1_000_000, cols=4096, steps=4, warmup=1, streams=2),
+    # 40 steps = ~0.5 s timed (a 4-step window is dominated by clock ramp / host jitter)
+    "C2": dict(batch=256, map_points=1_000_000, cols=4096, steps=40, warmup=2, streams=2),
     "C3": dict(batch=1, map_points=0, cols=4096, steps=20, warmup=3),
     "C4": dict(batch=1, map_points=5_000_000, cols=4096, steps=20, warmup=3),
     "C5": dict(batch=125, map_points=10_000_000, cols=2048, steps=2, warmup=1),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C2", choices=sorted(DEFAULTS))
     ap.add_argument("--gpus", type=int, default=1)
@@ -64,28 +74,63 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes of the neighbour-search kernel from rocprofv3 PMC runs")
-    a = ap.parse_args()
+    ap.add_argument("--h2d", choices=("auto", "on", "off"), default="auto",
+                    help="C2: also time K steps that stream every step's scans from pinned host memory "
+                         "(lmsf_batch_load_scans_async, overlapped with the previous launch) -- reported as "
+                         "`h2d_inclusive` beside the HBM-resident headline")
+    ap.add_argument("--workers", type=int, default=None, help="processes generating the synthetic scans")
+    ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend of the ranks (nccl = RCCL)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="no GPU work: ranks join the process group, run the C2 pose all-gather on CPU tensors and "
+                         "print the line skeleton (CPU test of the --gpus launcher)")
+    a = ap.parse_args(argv)
     for k, v in DEFAULTS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
     if a.streams is None:
         a.streams = 1
     if a.unique_scans is None:
-        a.unique_scans = {"C2": 8, "C5": 5}.get(a.config, 1)
+        a.unique_scans = {"C2": a.batch, "C5": 5}.get(a.config, 1)   # C2: one distinct scan per slot
     if a.traffic_json is None:
-        a.traffic_json = os.path.join(REPO, "profiles", f"knn_traffic_{a.config}.json")
+        a.traffic_json = os.path.join(REPO, "profiles", f"traffic_{a.config}.json")   # latest PMC summary (tools/traffic.py)
     return a
 
 
 # ----------------------------------------------------------------------------- shared plumbing
+def launch_ranks(argv, n):
+    """--gpus N outside torch.distributed.run: one child process running the standard launcher with N
+    ranks over this script (never exec: the parent must not have touched the GPU, and it waits for and
+    forwards the child's return code)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this pool (RCCL)
+    return subprocess.run(cmd, env=env).returncode
+
+
 class Dist:
-    def __init__(self):
-        import torch
-        import torch.distributed as dist
-        self.torch, self.dist = torch, dist
+    def __init__(self, backend="nccl"):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.backend = backend
+        self.torch = self.dist = self.dev = None
+
+    def init(self):
+        """Bind the GPU and join the process group (after the host-side input generation)."""
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        if self.backend != "nccl":                        # CPU rehearsal (gloo)
+            self.dev = torch.device("cpu")
+            if self.world > 1:
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                dist.init_process_group(self.backend)
+            return self
         if self.world > 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             torch.cuda.set_device(self.local)
@@ -93,13 +138,18 @@ class Dist:
         else:
             torch.cuda.set_device(0)
         self.dev = torch.device("cuda", self.local)
+        return self
+
+    def sync(self):
+        if self.dev is not None and self.dev.type == "cuda":
+            self.torch.cuda.synchronize()
 
     def barrier(self):
         if self.world > 1:
             self.dist.barrier()
 
     def close(self):
-        if self.world > 1:
+        if self.world > 1 and self.dist is not None and self.dist.is_initialized():
             self.dist.destroy_process_group()
 
 
@@ -123,12 +173,12 @@ def timed(d, step, warmup, steps, ctxs):
     for c in ctxs:
         c.kernel_stats_reset(timing=True)
     d.barrier()
-    torch.cuda.synchronize()
+    d.sync()
     t0 = time.perf_counter()
     out = None
     for _ in range(steps):
         out = step()
-    torch.cuda.synchronize()
+    d.sync()
     d.barrier()
     elapsed = time.perf_counter() - t0
     if d.world > 1:
@@ -173,33 +223,60 @@ def kernel_name(ks):
     return "knn_kernel"
 
 
-def knn_roofline(ks, mean_n27, traffic_json, batch, map_points, note):
-    """B_search = sum_q [16 (query) + 27*8 (cell ranges) + 16 * n27(q)] per launch,
-    over the HIP-event-timed launches of the neighbour-search kernel (n27 per query from the
-    counted untimed step)."""
-    alg_bytes = ks.queries * (16 + 27 * 8 + 16 * mean_n27)
-    avg_launch_ms = ks.total_ms / max(ks.launches, 1)
-    bytes_per_launch = alg_bytes / max(ks.launches, 1)
-    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
-    traffic, l2_hit = None, None
-    if os.path.exists(traffic_json):
-        try:
-            tj = json.load(open(traffic_json))
-            if int(tj.get("batch", -1)) == batch and int(tj.get("map_points", -1)) == map_points:
-                traffic = tj.get("hbm_bytes_per_launch")
-                l2_hit = tj.get("l2_hit_rate")
-        except (ValueError, OSError):
-            traffic = None
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": kernel_name(ks), "avg_launch_ms": round(avg_launch_ms, 4),
-            "alg_bytes_per_launch": int(bytes_per_launch), "launches": int(ks.launches),
-            "queries_per_launch": int(ks.queries / max(ks.launches, 1)),
-            "mean_n27": round(mean_n27, 1),
-            "reused_query_frac": round(getattr(ks, "reused_queries", 0) / max(ks.queries, 1), 4),
-            "measured_hbm_gbs": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic and avg_launch_ms else None,
-            "l2_hit_rate": round(l2_hit, 3) if l2_hit is not None else None,
-            "note": note}
+def load_traffic(traffic_json, **match):
+    """PMC summary of the dominant kernel (tools/traffic.py) when it was measured on this workload."""
+    if not traffic_json or not os.path.exists(traffic_json):
+        return None
+    try:
+        tj = json.load(open(traffic_json))
+    except (ValueError, OSError):
+        return None
+    for k, v in match.items():
+        if tj.get(k) != v:
+            return None
+    return tj
+
+
+def knn_roofline(ks, mean_n27, tj, elapsed_s, note):
+    """Roofline of the dominant (neighbour-search) kernel over the HIP-event-timed launches.
+
+    achieved = PMC-measured HBM bytes per launch (`traffic`: (2 FETCH_SIZE + WRITE_SIZE) KiB per
+    dispatch, MI355X_MICROARCH.md's gfx950 correction, from the committed rocprofv3 passes `tj`) /
+    average HIP-event launch time.  `rocprof` recomputes the same from the profiler's own mean duration
+    of that kernel in the PMC run.  `model` is SURVEY 8(d)'s algorithmic figure, sum over the queries
+    that searched of [16 (query) + 27*8 (cell ranges) + 16 n27(q)] + 16 B per memo-reused query (n27 per
+    searched query from the counted untimed step); it counts every candidate read as an HBM read while
+    the 16 MB map + index stay in L2 / Infinity Cache, hence `exceeds_peak` when it would imply more
+    than the HBM peak (per launch or over the whole timed window)."""
+    launches = max(int(ks.launches), 1)
+    avg_launch_ms = ks.total_ms / launches
+    reused = int(getattr(ks, "reused_queries", 0))
+    searched = int(ks.queries) - reused
+    model_bytes = (searched * (16 + 27 * 8 + 16 * mean_n27) + reused * 16) / launches
+    model_gbs = model_bytes / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+    model_wall_gbs = model_bytes * launches / elapsed_s / 1e9 if elapsed_s > 0 else 0.0
+    traffic = int(tj["hbm_bytes_per_launch"]) if tj else None
+    if traffic:
+        achieved, basis = traffic / (avg_launch_ms * 1e-3) / 1e9, "pmc"
+    else:
+        achieved, basis = model_gbs, "model (no PMC profile of this workload under profiles/)"
+    out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "basis": basis,
+           "kernel": kernel_name(ks), "avg_launch_ms": round(avg_launch_ms, 4), "launches": int(ks.launches),
+           "queries_per_launch": int(ks.queries / launches),
+           "reused_query_frac": round(reused / max(int(ks.queries), 1), 4),
+           "l2_hit_rate": round(tj["l2_hit_rate"], 3) if tj and tj.get("l2_hit_rate") is not None else None,
+           "model": {"bytes_per_launch": int(model_bytes), "searched_queries_per_launch": int(searched / launches),
+                     "mean_n27": round(mean_n27, 1), "gbs": round(model_gbs, 1),
+                     "frac": round(model_gbs / HBM_PEAK_GBS, 4), "gbs_over_timed_window": round(model_wall_gbs, 1),
+                     "exceeds_peak": bool(model_gbs > HBM_PEAK_GBS or model_wall_gbs > HBM_PEAK_GBS)},
+           "note": note}
+    if tj:
+        mean_us = tj.get("rocprof_mean_us")
+        out["rocprof"] = {"profile": tj.get("profile"), "mean_us": mean_us,
+                          "frac": round(traffic / (mean_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if mean_us else None,
+                          "dispatches": tj.get("dispatches")}
+    return out
 
 
 def line(args, d, metric, value, unit, elapsed, scaling, workload, extra_cfg, roofline, cpu, **extra):
@@ -218,11 +295,72 @@ def cpu_oracle():
     return oracle
 
 
+def host_cpu():
+    """Host CPU model (report the CPU the baseline ran on) and the cores this process may use."""
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return model, usable
+
+
+def _scan_job(job):
+    from lmsf import synth
+    seed_scene, pose, seed, cols, elev = job
+    return synth.make_scan(synth.make_scene(seed_scene, road_length=80.0), pose, seed, n_cols=cols, elev_deg=elev)
+
+
+def make_scans(jobs, workers):
+    """Synthetic scans generated in a process pool (before the rank touches the GPU: fork is safe)."""
+    if workers <= 1 or len(jobs) < 4:
+        return [_scan_job(j) for j in jobs]
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(min(workers, len(jobs))) as pool:
+        return pool.map(_scan_job, jobs, chunksize=max(1, len(jobs) // (4 * workers)))
+
+
+def exchange_poses(cfg, poses, gathered, pairs, world, dev):
+    """The C2 / C5 collective section: the RCCL all-gather of every rank's 6-DoF poses."""
+    from lmsf import multi
+    if world <= 1:
+        return poses
+    if cfg == "C2":
+        return multi.gather_poses(poses, gathered, dev)
+    return multi.gather_pair_poses(poses, pairs, world, dev)
+
+
+def run_launch_check(args, d):
+    """--launch-check: the ranks of a `--gpus N` launch join the process group (gloo on CPU) and run the
+    C2 pose all-gather; rank 0 prints the line skeleton (n_gpus = world size)."""
+    import numpy as np
+    import torch
+    n = 4
+    poses = np.stack([np.full(7, 1000.0 * d.rank + i) for i in range(n)])
+    gathered = torch.zeros((d.world, n, 7), dtype=torch.float64)
+    g = exchange_poses("C2", poses, gathered, 0, d.world, d.dev)
+    g = g.numpy() if hasattr(g, "numpy") else np.asarray(g)[None]
+    ok = all(np.array_equal(g[r], np.stack([np.full(7, 1000.0 * r + i) for i in range(n)])) for r in range(d.world))
+    if d.world > 1:
+        from lmsf import multi
+        ok = multi.max_over_ranks(0.0 if ok else 1.0, d.dev) == 0.0
+    if d.rank == 0:
+        print(json.dumps({"metric": "launch-check", "value": 0.0, "unit": "scans/s", "n_gpus": d.world,
+                          "steps": args.steps, "warmup": args.warmup, "backend": d.backend, "gather_ok": bool(ok)}))
+    return 0 if ok else 4
+
+
 # ----------------------------------------------------------------------------- C2 / C5: batch re-registration
 def run_batch(args, d):
     import numpy as np
-    torch = d.torch
-    from lmsf import _lib, multi, synth
+    from lmsf import multi, synth
     cfg = args.config
     c = synth.CONFIGS[cfg]
     k = c["k"]
@@ -230,10 +368,13 @@ def run_batch(args, d):
     U = max(1, min(args.unique_scans, args.batch))
     if cfg == "C5" and args.batch % U:
         args.batch -= args.batch % U          # slot j holds scan j % U in every chunk
-    scene = synth.make_scene(1000 + k, road_length=80.0)
     truth_u = synth.trajectory(U * world, 3000 + k, step=80.0 / max(U * world, 1))[rank * U:(rank + 1) * U]
-    scans_u = [synth.make_scan(scene, truth_u[i], 2000 + k + 97 * (rank * U + i), n_cols=args.cols,
-                               elev_deg=c["elev"]) for i in range(U)]
+    scans_u = make_scans([(1000 + k, truth_u[i], 2000 + k + 97 * (rank * U + i), args.cols, c["elev"])
+                          for i in range(U)], args.workers)
+    d.init()
+    torch = d.torch
+    from lmsf import _lib
+    scene = synth.make_scene(1000 + k, road_length=80.0)
     em_t, sm_t = shared_map(d, lambda: synth.make_map(scene, args.map_points, 1000 + k + 7, center_x=(0.0, 80.0),
                                                       radius=c["radius"]))
     if cfg == "C2":
@@ -253,42 +394,74 @@ def run_batch(args, d):
     max_pts = max(len(s) for s in scans_u)
     ctxs = [_lib.Context(device=d.local, max_batch=sub_b, max_scan_points=max_pts + 64, max_features=max_pts + 64,
                          schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer, **c["extract"]) for _ in range(S)]
-    for i, cx in enumerate(ctxs):
+    ctx_scans = [[scans_u[j % U] for j in range(i * sub_b, min((i + 1) * sub_b, chunk))] for i in range(S)]
+    for cx, sc in zip(ctxs, ctx_scans):
         cx.set_map(_lib.EDGE, em_t)
         cx.set_map(_lib.SURF, sm_t)
-        cx.load_scans([scans_u[j % U] for j in range(i * sub_b, min((i + 1) * sub_b, chunk))])
-    ctx = ctxs[0]
+        cx.load_scans(sc)
     map_points = int(em_t.shape[0] + sm_t.shape[0])
     gathered = torch.zeros((world, n_units, 7), dtype=torch.float64, device=d.dev)
     poses = np.zeros((n_units, 7))
+    stream_in = {"on": False}
+    host_bufs = []
 
     def step():
         for c0 in range(0, n_units, chunk):
             nb = min(chunk, n_units - c0)
-            parts = [(cx, c0 + i * sub_b, min(sub_b, nb - i * sub_b)) for i, cx in enumerate(ctxs) if nb > i * sub_b]
-            for cx, a, m in parts:                           # every context's batch enqueued before any wait
+            parts = [(i, cx, c0 + i * sub_b, min(sub_b, nb - i * sub_b)) for i, cx in enumerate(ctxs) if nb > i * sub_b]
+            for i, cx, a, m in parts:                        # every context's batch enqueued before any wait
                 cx.batch_launch(guesses[a:a + m])
-            for cx, a, m in parts:
+                if stream_in["on"]:                          # next step's scans, overlapped with this launch
+                    cx.load_scans_async(*host_bufs[i])
+            for i, cx, a, m in parts:
                 poses[a:a + m], _ = cx.batch_wait(m)
-        if world > 1:                                        # RCCL all-gather of the 6-DoF poses
-            if cfg == "C2":
-                multi.gather_poses(poses, gathered, d.dev)
-            else:
-                multi.gather_pair_poses(poses, args.pairs, world, d.dev)
+        exchange_poses(cfg, poses, gathered, args.pairs, world, d.dev)
         return poses
 
     elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, ctxs)
     ks = sum_stats([timed_stats(cx) for cx in ctxs])
     total_units = (args.batch * world if cfg == "C2" else args.pairs) * args.steps
     terr = [synth.pose_delta(poses[i], truth_u[unit_scan[i]]) for i in range(n_units)]
-    roof = knn_roofline(ks, mean_n27, args.traffic_json, sub_b, map_points,
-                        "achieved = SURVEY 8(d) algorithmic bytes / HIP-event launch time (with several context "
-                        "streams a launch's span includes the time it shares the chip with the other stream's "
-                        "kernels); the map + cell index is largely L2/Infinity-Cache resident, so measured HBM "
-                        "traffic (PMC, from a one-stream run: device-wide counters) is lower")
+    tj = load_traffic(args.traffic_json, config=cfg, batch=sub_b, streams=1, map_points=map_points,
+                      unique_scans=min(U, sub_b))
+    roof = knn_roofline(ks, mean_n27, tj, elapsed,
+                        "traffic: PMC bytes per dispatch from a one-stream run of the same per-context batch "
+                        "(device-wide counters); avg_launch_ms: HIP events on the context streams (with two "
+                        "streams a launch's span includes time it shares the chip with the other stream's kernels)")
+    h2d = None
+    if cfg == "C2" and (args.h2d == "on" or (args.h2d == "auto" and U == n_units)):
+        # SURVEY 8(d) "including ... H2D of the scan": the same K steps with every step's scans streamed
+        # from page-locked host memory (one DMA per context, issued right after that context's launch so
+        # it overlaps the registration; the copy waits for the launch's extraction to have read the slots)
+        for sc in ctx_scans:
+            counts = np.array([len(x) for x in sc], np.int64)
+            buf = torch.from_numpy(np.concatenate(sc, 0)).pin_memory()
+            host_bufs.append((buf, counts))
+        for cx, (buf, counts) in zip(ctxs, host_bufs):
+            cx.load_scans_async(buf, counts)
+        stream_in["on"] = True
+        step()
+        d.barrier()
+        d.sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        d.sync()
+        d.barrier()
+        el2 = time.perf_counter() - t0
+        if world > 1:
+            el2 = multi.max_over_ranks(el2, d.dev)
+        stream_in["on"] = False
+        up = sum(int(b.numel()) * 4 for b, _ in host_bufs)
+        h2d = {"value": round(args.batch * world * args.steps / el2, 2), "unit": "scans/s",
+               "ms_per_step": round(el2 / args.steps * 1e3, 3), "upload_bytes_per_step_per_gpu": up,
+               "note": "every step's raw scans uploaded from pinned host memory inside the timed window "
+                       "(lmsf_batch_load_scans_async on each context's copy stream, overlapped with the previous "
+                       "launch); the headline `value` keeps the scans HBM-resident"}
     cpu, pose_dv = None, None
     if rank == 0 and world == 1 and not args.no_cpu:
         oracle = cpu_oracle()
+        model, usable = host_cpu()
         reg = oracle.Registration()
         reg.set_map(1, em_t.cpu().numpy())           # the same broadcast map
         reg.set_map(2, sm_t.cpu().numpy())
@@ -306,14 +479,15 @@ def run_batch(args, d):
             n_done += 1
         cpu_el = time.perf_counter() - t1
         unit = "scans/s" if cfg == "C2" else "pairs/s"
-        cpu = {"value": round(n_done / cpu_el, 3), "unit": unit, "cores": 1, "kind": "port",
+        cpu = {"value": round(n_done / cpu_el, 3), "unit": unit, "cores": 1, "kind": "port", "cpu_model": model,
                "sample": f"{n_done} {'scans' if cfg == 'C2' else 'pairs'} of the same {cfg} workload (extract + "
                          f"{args.outer} outer iterations, kd-tree 5-NN, Ceres-LM restatement; kd-tree build "
-                         f"excluded), {cpu_el:.1f} s on 1 thread of {os.cpu_count()} host cores"}
+                         f"excluded), {cpu_el:.1f} s on 1 thread of a {model} ({os.cpu_count()} host CPUs, "
+                         f"{usable} usable)"}
         pose_dv = {"scans": n_done, "max_m": worst_t, "max_rad": worst_r}
         # the same restatement with OpenMP over queries on the host cores this job
         # may use (the GPU box grants 16 per GPU), reported beside the single-thread baseline
-        nt = max(1, min(16, os.cpu_count() or 1))
+        nt = max(1, min(16, usable))
         oracle.set_threads(nt)
         m_done = 0
         t2 = time.perf_counter()
@@ -334,9 +508,9 @@ def run_batch(args, d):
             metric = "LiDAR scans/sec registered (64k-pt scan, 1M-pt map)"
             wl = (f"C2: VLP-16 16x{args.cols} scans (~{npts} pts) vs {map_points}-pt edge+surf map, "
                   f"{args.outer} outer iters x Ceres-LM(4), extraction included, batch {args.batch} scans/GPU "
-                  f"({U} distinct) over {S} context stream(s)")
-            extra = {"batch_per_gpu": args.batch, "map_points": map_points, "outer_iterations": args.outer,
-                     "parallelism": f"scan-sharded x{world}"}
+                  f"({U} distinct) over {S} context stream(s), scans HBM-resident")
+            extra = {"batch_per_gpu": args.batch, "distinct_scans_per_gpu": U, "map_points": map_points,
+                     "outer_iterations": args.outer, "parallelism": f"scan-sharded x{world}"}
             unit, scaling = "scans/s", "weak"
         else:
             metric = "LiDAR scan pairs/sec re-registered (128-beam 254k-pt scan, 10M-pt map, 1k pairs)"
@@ -346,7 +520,7 @@ def run_batch(args, d):
                      "outer_iterations": args.outer, "parallelism": f"pair-sharded x{world}"}
             unit, scaling = "pairs/s", "strong"
         line(args, d, metric, total_units / elapsed, unit, elapsed, scaling, wl, extra, roof, cpu,
-             pose_delta_vs_cpu=pose_dv,
+             h2d_inclusive=h2d, pose_delta_vs_cpu=pose_dv,
              pose_error_vs_truth={"max_m": max(t for t, _ in terr), "max_rad": max(r for _, r in terr)})
     for cx in ctxs:
         cx.close()
@@ -355,8 +529,7 @@ def run_batch(args, d):
 # ----------------------------------------------------------------------------- C4: stitched multi-stream tracking
 def run_streams(args, d):
     import numpy as np
-    torch = d.torch
-    from lmsf import _lib, multi, synth
+    from lmsf import multi, synth
     c = synth.CONFIGS["C4"]
     k = c["k"]
     world, rank = d.world, d.rank
@@ -365,7 +538,11 @@ def run_streams(args, d):
     step_m = 0.8                                                # 8 m/s at 10 Hz
     start = 8.0 * rank if world <= 8 else 64.0 * rank / world
     truth = synth.trajectory(n, 3000 + k + rank, step=step_m, start_x=start)
-    scans = [synth.make_scan(scene, truth[i], 2000 + k + 97 * i + 7717 * rank, n_cols=args.cols) for i in range(n)]
+    scans = make_scans([(1000 + k, truth[i], 2000 + k + 97 * i + 7717 * rank, args.cols, c["elev"]) for i in range(n)],
+                       args.workers)
+    d.init()
+    torch = d.torch
+    from lmsf import _lib
     scans_dev = [torch.from_numpy(s).to(d.dev) for s in scans]
     em_t, sm_t = shared_map(d, lambda: synth.make_map(scene, args.map_points, 1000 + k + 7, center_x=(0.0, 80.0),
                                                       radius=c["radius"]))
@@ -409,9 +586,8 @@ def run_streams(args, d):
 
     elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx])
     ks = timed_stats(ctx)
-    roof = knn_roofline(ks, mean_n27, args.traffic_json, 1, map_points,
-                        "achieved = SURVEY 8(d) algorithmic bytes / HIP-event launch time (one 63k-query scan "
-                        "per launch: latency-bound launches)")
+    roof = knn_roofline(ks, mean_n27, load_traffic(args.traffic_json, config="C4", batch=1, map_points=map_points),
+                        elapsed, "one 63k-query scan per launch (8 lanes per query): latency-bound launches")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         oracle = cpu_oracle()
@@ -434,6 +610,7 @@ def run_streams(args, d):
             n_done += 1
         cpu_el = time.perf_counter() - t1
         cpu = {"value": round(n_done / cpu_el, 3), "unit": "scans/s", "cores": 1, "kind": "port",
+               "cpu_model": host_cpu()[0],
                "sample": f"first {n_done} scans of the rank-0 stream (extract + tracker Solve with "
                          f"{args.outer} outer iterations + keyframe map rebuild incl. kd-tree over the 5M prior), "
                          f"{cpu_el:.1f} s on 1 thread of {os.cpu_count()} host cores"}
@@ -453,6 +630,7 @@ def run_streams(args, d):
 # ----------------------------------------------------------------------------- C3: dual-LiDAR online refine
 def run_dual(args, d):
     import numpy as np
+    d.init()
     torch = d.torch
     from lmsf import _lib, dual, synth
     world, rank = d.world, d.rank
@@ -482,9 +660,9 @@ def run_dual(args, d):
 
     elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx])
     ks = timed_stats(ctx)
-    roof = knn_roofline(ks, mean_n27, args.traffic_json, 1, 0,
-                        "achieved = SURVEY 8(d) algorithmic bytes / HIP-event launch time (one ~63k-query scan per "
-                        "launch against the voxelised local map: latency-bound launches)")
+    roof = knn_roofline(ks, mean_n27, load_traffic(args.traffic_json, config="C3", batch=1), elapsed,
+                        "one ~63k-query scan per launch (8 lanes per query) against the voxelised local map: "
+                        "latency-bound launches")
     ext_err = [float(np.linalg.norm(system.extrinsic[:3, 3] - X[:3, 3])),
                float(math.acos(max(-1.0, min(1.0, (np.trace(system.extrinsic[:3, :3].T @ X[:3, :3]) - 1) / 2))))]
     cpu = None
@@ -506,6 +684,7 @@ def run_dual(args, d):
             n_done += 1
         cpu_el = time.perf_counter() - t1
         cpu = {"value": round(n_done / cpu_el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+               "cpu_model": host_cpu()[0],
                "sample": f"first {n_done} frames of the same dual-LiDAR sequence (2 extractions, tracker Solve, "
                          f"sub-LiDAR refine, keyframe map rebuild), {cpu_el:.1f} s on 1 thread of "
                          f"{os.cpu_count()} host cores"}
@@ -521,12 +700,26 @@ def run_dual(args, d):
     ctx.close()
 
 
-def main():
-    args = parse()
-    d = Dist()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if args.workers is None:
+        args.workers = max(1, min(16, (host_cpu()[1] or 1)))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(argv, args.gpus)          # before anything touches the GPU
+    d = Dist(args.dist_backend)
+    if d.world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={d.world}", file=sys.stderr)
+        return 3
+    if args.launch_check:
+        d.init()
+        rc = run_launch_check(args, d)
+        d.close()
+        return rc
     {"C2": run_batch, "C5": run_batch, "C4": run_streams, "C3": run_dual}[args.config](args, d)
     d.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

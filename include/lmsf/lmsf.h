@@ -12,7 +12,7 @@
  * device; distinct contexts may run concurrently (same rule as the reference, where each
  * tracker owns its registration object: INC/System/ML_System.hpp:248-264).
  * Ownership: the library copies every input into device buffers it owns; no caller pointer is
- * retained after a call returns.
+ * retained after a call returns, except by lmsf_batch_load_scans_async (documented there).
  */
 #ifndef LMSF_LMSF_H_
 #define LMSF_LMSF_H_
@@ -159,10 +159,20 @@ lmsf_status lmsf_copy_features(lmsf_ctx* ctx, int32_t kind, float* out, int32_t*
  * into device slots;
  * run extracts features for every slot and registers slot i from poses[i] (in/out). */
 lmsf_status lmsf_batch_load_scans(lmsf_ctx* ctx, const float* xyzi, const int64_t* counts, int32_t n);
+/* Streaming ingest (the driver callback feeding MultiLidarSystem, APPS/MultiLidarSLAM_node.cpp:126-180):
+ * the copy of lmsf_batch_load_scans enqueued on the context's copy stream without blocking, into
+ * the raw slots the NEXT lmsf_batch_launch extracts from.  It starts once the previous launch's
+ * extraction has read those slots, so it overlaps that launch's registration.  The caller keeps
+ * xyzi (page-locked host memory for a truly asynchronous copy) and counts' values unchanged until
+ * the lmsf_batch_wait of that next launch returns. */
+lmsf_status lmsf_batch_load_scans_async(lmsf_ctx* ctx, const float* xyzi, const int64_t* counts, int32_t n);
 lmsf_status lmsf_batch_run(lmsf_ctx* ctx, int32_t n, double* poses, lmsf_solve_stats* stats);
 /* Same, but without blocking: poses are read back by lmsf_batch_wait. */
 lmsf_status lmsf_batch_launch(lmsf_ctx* ctx, int32_t n, const double* poses);
 lmsf_status lmsf_batch_wait(lmsf_ctx* ctx, int32_t n, double* poses, lmsf_solve_stats* stats);
+/* Pose after every outer iteration of batch slot `slot` in the last lmsf_batch_wait / lmsf_batch_run
+ * (rows of 7 doubles, as lmsf_solve_trace); *n_out = rows. */
+lmsf_status lmsf_batch_trace(lmsf_ctx* ctx, int32_t slot, double* trace, int32_t cap, int32_t* n_out);
 /* Features of one batch slot after lmsf_batch_run. */
 lmsf_status lmsf_batch_copy_features(lmsf_ctx* ctx, int32_t slot, int32_t kind, float* out, int32_t* src,
                                      size_t cap, size_t* n_out);
@@ -180,9 +190,9 @@ lmsf_status lmsf_eval(lmsf_ctx* ctx, const double pose[7], double out[29]);
  * queries; costs the search extra cell-offset loads, so it is kept out of timed launches);
  * 0 turns accounting off.  fused_launches: how many of the launches were the fused search + fit
  * kernel (batch launches with the Ceres-LM solver; the fit is then inside the timed launch).
- * reused_queries: queries of those launches (outer iterations > 0) whose float map-frame query was
- * bit-identical to the previous iteration's, so their 5-NN set and fit were reused (counted with
- * the queries). */
+ * reused_queries: queries of those launches (outer iterations > 0) that moved less than half the
+ * neighbour-distance gap of their last full search, so their 5-NN set and fit were reused without a
+ * search (counted with the queries; DESIGN.md "Query memo"). */
 #define LMSF_STATS_TIMING 1
 #define LMSF_STATS_N27 2
 typedef struct {

@@ -131,6 +131,12 @@ struct lmsf_ctx {
     int* n_pos = nullptr;
     bool qorder_valid = false;        // the slots' features came from the extraction kernels
     int* d_error = nullptr;
+    // streaming ingest (lmsf_batch_load_scans_async): copies on their own stream into the raw slots,
+    // ordered after the extraction that last read them (ev_raw_free) and before the next (ev_raw_ready)
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t ev_raw_free = nullptr, ev_raw_ready = nullptr;
+    bool raw_pending = false;
+    int* h_raw_counts = nullptr;      // pinned [B]
     // host side
     double* h_poses = nullptr;        // pinned [B*7]
     SolveState* h_st = nullptr;       // pinned [B]
@@ -140,6 +146,7 @@ struct lmsf_ctx {
     bool features_on_device = false;  // slot 0 features came from lmsf_extract_features
     int64_t slot0_ne = 0, slot0_ns = 0;
     int last_outer = 0;
+    int batch_done = 0;               // slots whose SolveState the last lmsf_batch_wait read back into h_st
     double last_trace[kMaxOuter][7];
     // kernel accounting
     bool timing = false;    // LMSF_STATS_TIMING: HIP events around each neighbour-search launch
@@ -465,6 +472,11 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (c->h_poses) hipHostFree(c->h_poses);
     if (c->h_st) hipHostFree(c->h_st);
     if (c->h_counts) hipHostFree(c->h_counts);
+    if (c->h_raw_counts) hipHostFree(c->h_raw_counts);
+    if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
+    if (c->ev_raw_free) hipEventDestroy(c->ev_raw_free);
+    if (c->ev_raw_ready) hipEventDestroy(c->ev_raw_ready);
+    if (c->copy_stream) hipStreamDestroy(c->copy_stream);
     for (int i = 0; i < 2 * kEventPairs; ++i)
         if (c->ev[i]) hipEventDestroy(c->ev[i]);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -543,6 +555,11 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(hipHostMalloc((void**)&c->h_poses, B * 7 * sizeof(double), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_st, B * sizeof(SolveState), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_counts, 2 * B * sizeof(int), hipHostMallocDefault));
+    CHK(hipHostMalloc((void**)&c->h_raw_counts, B * sizeof(int), hipHostMallocDefault));
+    CHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    CHK(hipEventCreateWithFlags(&c->ev_raw_free, hipEventDisableTiming));
+    CHK(hipEventCreateWithFlags(&c->ev_raw_ready, hipEventDisableTiming));
+    CHK(hipEventRecord(c->ev_raw_free, c->stream));
 #undef CHK
     *out = c;
     return LMSF_OK;
@@ -644,6 +661,7 @@ lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf
     if (rc) return rc;
     HIPCHK(c, hipMemsetAsync(c->d_error, 0, sizeof(int), c->stream));
     HIPCHK(c, launch_extract(c->eview(1), c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_raw_free, c->stream));
     c->qorder_valid = true;
     int hc[3];
     HIPCHK(c, hipMemcpyAsync(&hc[0], c->n_edge, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -824,6 +842,10 @@ lmsf_status lmsf_batch_copy_features(lmsf_ctx* c, int32_t slot, int32_t kind, fl
 lmsf_status lmsf_batch_load_scans(lmsf_ctx* c, const float* xyzi, const int64_t* counts, int32_t n) {
     if (!c || !counts || n < 1 || n > c->B) return LMSF_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (c->raw_pending) {   // a streamed upload not yet consumed: this copy replaces it, after it
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_raw_ready, 0));
+        c->raw_pending = false;
+    }
     size_t off = 0;
     for (int i = 0; i < n; ++i) {
         if (counts[i] < 0 || counts[i] > c->R)
@@ -839,13 +861,41 @@ lmsf_status lmsf_batch_load_scans(lmsf_ctx* c, const float* xyzi, const int64_t*
     return LMSF_OK;
 }
 
+lmsf_status lmsf_batch_load_scans_async(lmsf_ctx* c, const float* xyzi, const int64_t* counts, int32_t n) {
+    if (!c || !counts || n < 1 || n > c->B) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    for (int i = 0; i < n; ++i)
+        if (counts[i] < 0 || counts[i] > c->R)
+            return c->fail(LMSF_ERR_CAPACITY, "scan %d has %lld points (max_scan_points %d)", i, (long long)counts[i], c->R);
+    HIPCHK(c, hipStreamSynchronize(c->copy_stream));   // the previous upload (normally long done) owns h_raw_counts
+    HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->ev_raw_free, 0));     // the last extraction has read raw
+    size_t off = 0;
+    for (int i = 0; i < n; ++i) {
+        if (counts[i])
+            HIPCHK(c, hipMemcpyAsync(c->raw + (size_t)i * c->R, xyzi + 4 * off, counts[i] * sizeof(float4),
+                                     hipMemcpyDefault, c->copy_stream));
+        c->h_raw_counts[i] = (int)counts[i];
+        off += (size_t)counts[i];
+    }
+    HIPCHK(c, hipMemcpyAsync(c->raw_count, c->h_raw_counts, n * sizeof(int), hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(c, hipEventRecord(c->ev_raw_ready, c->copy_stream));
+    c->raw_pending = true;
+    return LMSF_OK;
+}
+
 lmsf_status lmsf_batch_launch(lmsf_ctx* c, int32_t n, const double* poses) {
     if (!c || !poses || n < 1 || n > c->B) return LMSF_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->cfg.device));
     if (!c->map_set[LMSF_EDGE] && !c->map_set[LMSF_SURF]) return c->fail(LMSF_ERR_NO_MAP, "no map set");
     std::memcpy(c->h_poses, poses, (size_t)n * 7 * sizeof(double));
     HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, (size_t)n * 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_error, 0, sizeof(int), c->stream));   // capacity flags of this batch only
+    if (c->raw_pending) {   // streamed scans: extract once their copy has landed
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_raw_ready, 0));
+        c->raw_pending = false;
+    }
     HIPCHK(c, launch_extract(c->eview(n), c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_raw_free, c->stream));
     c->qorder_valid = true;
     HIPCHK(c, launch_state_init(c->bview(n), c->d_poses, c->stream));
     // every slot behaves as one Solve on a fresh registration object (ceres_...:100-101)
@@ -869,7 +919,18 @@ lmsf_status lmsf_batch_wait(lmsf_ctx* c, int32_t n, double* poses, lmsf_solve_st
         std::memcpy(poses + 7 * i, c->h_st[i].x, 7 * sizeof(double));
         if (stats) fill_stats(c->h_st[i], &stats[i]);
     }
+    c->batch_done = n;
     if (herr) return c->fail(LMSF_ERR_CAPACITY, "ring or sector larger than the extraction kernel supports (flags %d)", herr);
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_batch_trace(lmsf_ctx* c, int32_t slot, double* trace, int32_t cap, int32_t* n_out) {
+    if (!c || (!trace && cap > 0)) return LMSF_ERR_ARG;
+    if (slot < 0 || slot >= c->batch_done) return c->fail(LMSF_ERR_STATE, "slot %d not in the last batch_wait", slot);
+    const SolveState& S = c->h_st[slot];
+    const int rows = std::min(S.outer_run, kMaxOuter);
+    for (int i = 0; i < std::min(cap, rows); ++i) std::memcpy(trace + 7 * i, S.trace[i], 7 * sizeof(double));
+    if (n_out) *n_out = rows;
     return LMSF_OK;
 }
 

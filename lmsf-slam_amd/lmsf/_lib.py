@@ -98,9 +98,11 @@ _SIGS = {
     "lmsf_extract_features": (C.c_int32, [_P, _P, C.c_size_t, C.POINTER(FeatureCounts)]),
     "lmsf_copy_features": (C.c_int32, [_P, C.c_int32, _P, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "lmsf_batch_load_scans": (C.c_int32, [_P, _P, _P, C.c_int32]),
+    "lmsf_batch_load_scans_async": (C.c_int32, [_P, _P, _P, C.c_int32]),
     "lmsf_batch_run": (C.c_int32, [_P, C.c_int32, _P, _P]),
     "lmsf_batch_launch": (C.c_int32, [_P, C.c_int32, _P]),
     "lmsf_batch_wait": (C.c_int32, [_P, C.c_int32, _P, _P]),
+    "lmsf_batch_trace": (C.c_int32, [_P, C.c_int32, _P, C.c_int32, C.POINTER(C.c_int32)]),
     "lmsf_batch_copy_features": (C.c_int32, [_P, C.c_int32, C.c_int32, _P, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "lmsf_match": (C.c_int32, [_P, _P, _P, _P, C.c_size_t]),
     "lmsf_eval": (C.c_int32, [_P, _P, _P]),
@@ -333,6 +335,17 @@ class Context:
         cat = np.ascontiguousarray(np.concatenate([_f4(s) for s in scans], 0)) if counts.sum() else np.zeros((0, 4), np.float32)
         self._check(load().lmsf_batch_load_scans(self.h, cat.ctypes.data, counts.ctypes.data, len(scans)))
 
+    def load_scans_async(self, buf, counts):
+        """lmsf_batch_load_scans_async: buf is a contiguous (sum(counts), 4) float32 torch tensor
+        (pinned host memory for an asynchronous copy) holding the next launch's scans back to back.
+        The buffer and counts are kept alive here until the following batch_wait."""
+        counts = np.ascontiguousarray(counts, dtype=np.int64)
+        p, n, keep = _buf(buf)
+        if n != int(counts.sum()):
+            raise ValueError("buffer rows != sum(counts)")
+        self._check(load().lmsf_batch_load_scans_async(self.h, p, counts.ctypes.data, len(counts)))
+        self._uploads = (getattr(self, "_uploads", ()) + ((keep, counts),))[-2:]   # this one and the one in flight
+
     def batch_run(self, poses):
         x = np.ascontiguousarray(poses, dtype=np.float64).copy()
         n = x.shape[0]
@@ -349,6 +362,13 @@ class Context:
         st = (SolveStats * n)()
         self._check(load().lmsf_batch_wait(self.h, n, x.ctypes.data, C.cast(st, C.c_void_p)))
         return x, list(st)
+
+    def batch_trace(self, slot, cap=32):
+        """Per-outer-iteration poses of one slot of the last batch_wait / batch_run."""
+        out = np.zeros((cap, 7), np.float64)
+        n = C.c_int32()
+        self._check(load().lmsf_batch_trace(self.h, int(slot), out.ctypes.data, cap, C.byref(n)))
+        return out[:min(n.value, cap)].copy()
 
     # ---- diagnostics
     def match(self, pose, n_queries):

@@ -172,7 +172,11 @@ def raycast(scene: Scene, origin: np.ndarray, dirs: np.ndarray, max_range: float
         ok = (d[:, 2] < 0) & (t > 0)
         best = np.where(ok & (t < best), t, best)
         inv = 1.0 / d
-        for b in scene.boxes:
+        # boxes / poles farther than max_range from the origin can only give hits that are dropped
+        # below (culling them leaves the result bit-identical and halves the cost of a scan)
+        gap = np.maximum(np.maximum(scene.boxes[:, :3] - o, o - scene.boxes[:, 3:]), 0.0)
+        near_boxes = scene.boxes[np.sqrt((gap ** 2).sum(1)) <= max_range]
+        for b in near_boxes:
             t1 = (b[:3] - o) * inv
             t2 = (b[3:] - o) * inv
             tn = np.max(np.minimum(t1, t2), axis=1)
@@ -180,7 +184,8 @@ def raycast(scene: Scene, origin: np.ndarray, dirs: np.ndarray, max_range: float
             hit = (tn <= tf) & (tn > 1e-6)
             best = np.where(hit & (tn < best), tn, best)
         dxy2 = d[:, 0] ** 2 + d[:, 1] ** 2
-        for p in scene.poles:
+        pole_d = np.hypot(scene.poles[:, 0] - o[0], scene.poles[:, 1] - o[1]) - POLE_R if len(scene.poles) else np.zeros(0)
+        for p in scene.poles[pole_d <= max_range] if len(scene.poles) else scene.poles:
             ox, oy = o[0] - p[0], o[1] - p[1]
             bq = 2 * (ox * d[:, 0] + oy * d[:, 1])
             cq = ox * ox + oy * oy - POLE_R * POLE_R

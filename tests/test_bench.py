@@ -1,0 +1,69 @@
+"""bench.py host logic on CPU: the --gpus N launcher (torch.distributed.run as a child process, the
+ranks' world-size check, the C2 pose all-gather over gloo) and the roofline arithmetic."""
+import json
+import os
+import subprocess
+import sys
+import types
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _run(args, env=None, timeout=180):
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, timeout=timeout, env=e)
+
+
+def test_gpus2_launches_two_ranks_and_gathers():
+    r = _run(["--gpus", "2", "--launch-check", "--dist-backend", "gloo"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1                       # rank 0 only
+    assert lines[0]["n_gpus"] == 2 and lines[0]["gather_ok"] is True
+
+
+def test_world_size_mismatch_fails():
+    r = _run(["--gpus", "2", "--launch-check", "--dist-backend", "gloo"], env={"WORLD_SIZE": "1"})
+    assert r.returncode == 3 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_child_return_code_propagates():
+    r = _run(["--gpus", "2", "--launch-check", "--dist-backend", "no-such-backend"])
+    assert r.returncode != 0
+
+
+def _bench_module():
+    sys.path.insert(0, REPO)
+    import bench
+    return bench
+
+
+def test_roofline_measured_and_model():
+    bench = _bench_module()
+    ks = types.SimpleNamespace(launches=10, total_ms=10.0, queries=1_000_000, reused_queries=400_000,
+                               fused_launches=10, n27_sum=0)
+    tj = {"hbm_bytes_per_launch": 1_000_000_000, "l2_hit_rate": 0.75, "rocprof_mean_us": 800.0,
+          "profile": "profiles/x", "dispatches": 3}
+    r = bench.knn_roofline(ks, 50.0, tj, 0.02, "n")
+    # 1 GB per 1 ms launch = 1000 GB/s; rocprof: 1 GB / 0.8 ms
+    assert r["basis"] == "pmc" and r["achieved"] == 1000.0 and r["frac"] == 0.125
+    assert abs(r["rocprof"]["frac"] - 1e9 / 0.8e-3 / 1e9 / 8000) < 1e-4
+    # model over the 600k searched queries per 10 launches + 16 B per reused query
+    mb = (600_000 * (16 + 216 + 16 * 50) + 400_000 * 16) / 10
+    assert r["model"]["bytes_per_launch"] == int(mb) and r["model"]["searched_queries_per_launch"] == 60_000
+    assert r["model"]["exceeds_peak"] is False
+    # a model figure above the HBM peak is flagged
+    r2 = bench.knn_roofline(types.SimpleNamespace(**dict(vars(ks), total_ms=0.01)), 50.0, None, 0.02, "n")
+    assert r2["basis"].startswith("model") and r2["model"]["exceeds_peak"] is True and r2["traffic"] is None
+
+
+def test_load_traffic_matches_workload(tmp_path):
+    bench = _bench_module()
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps({"config": "C2", "batch": 128, "map_points": 10, "hbm_bytes_per_launch": 5}))
+    assert bench.load_traffic(str(p), config="C2", batch=128, map_points=10)["hbm_bytes_per_launch"] == 5
+    assert bench.load_traffic(str(p), config="C2", batch=64, map_points=10) is None
+    assert bench.load_traffic(str(tmp_path / "missing.json"), config="C2") is None

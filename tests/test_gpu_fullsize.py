@@ -1,0 +1,216 @@
+"""GPU parity at the BASELINE.json configurations' full sizes (configs[1..4]), through the C ABI,
+against the CPU restatement in oracle/ (test infrastructure; OpenMP over queries here so each test
+stays within its time limit).
+
+* C2: 64k-point VLP-16 scans vs the 1M-point map (conftest.c2_workload), 16 slots of the batch path
+  with the query memo on (the kernel bench.py times): every slot's pose per outer iteration
+  <= 1e-4 m / rad; records byte-identical on one scan.
+* C3: the 4096-column dual-LiDAR refine is tests/test_gpu_parity.py::test_dual_lidar_refine_parity[4096].
+* C4: two tracked VLP-16 streams against a 5M-point shared prior map + the stitched keyframe window
+  (keyframes exchanged in stream order), 5 tracked scans each, against two oracle trackers.
+* C5: 128 x 2048 (~254k-point) scans vs a 10M-point map through batch_run (one-lane pruned fused
+  walk), 2 pairs, pose per outer iteration; records byte-identical on one scan.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import mat_err, pose_err, pose_matrix
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from lmsf import _lib
+    _lib.load()
+    return _lib
+
+
+@pytest.fixture
+def oracle_mt(oracle_mod):
+    """The oracle with OpenMP over queries on the cores this job may use (restored afterwards)."""
+    oracle_mod.set_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    yield oracle_mod
+    oracle_mod.set_threads(1)
+
+
+def _oracle_reg(oracle_mod, wl, iters, **extract):
+    reg = oracle_mod.Registration()
+    reg.set_map(1, wl.edge_map)
+    reg.set_map(2, wl.surf_map)
+    reg.set_fixed_schedule(True)
+    reg.set_max_iterations(iters)
+    return reg
+
+
+def _check_trace(gtr, otr, what):
+    assert gtr.shape == otr.shape, (what, gtr.shape, otr.shape)
+    for it, (a, b) in enumerate(zip(gtr, otr)):
+        dt, dr = pose_err(a, b)
+        assert dt <= POSE_TOL and dr <= POSE_TOL, (what, it, dt, dr)
+
+
+def _records_bitexact(lib, oracle_mod, wl, scan, pose, ctx_kw, extract_kw):
+    e, s, _, _ = oracle_mod.extract(scan, **extract_kw)
+    ctx = lib.Context(max_batch=1, max_features=1 << 20, **ctx_kw)    # >= 2^20 slots: the fused one-lane path
+    ctx.set_map(lib.EDGE, wl.edge_map)
+    ctx.set_map(lib.SURF, wl.surf_map)
+    assert ctx.extract(scan) == (len(e), len(s))
+    reg = _oracle_reg(oracle_mod, wl, 1)
+    reg.set_scan(1, e)
+    reg.set_scan(2, s)
+    orec, onn = reg.match(pose)
+    grec, gnn = ctx.match(pose, len(e) + len(s))
+    found = gnn >= 0
+    np.testing.assert_array_equal(gnn[found], onn[found])
+    assert grec.tobytes() == orec.tobytes()
+    assert (orec["kind"] > 0).sum() > 0.2 * len(orec)
+    ctx.close()
+
+
+def test_c2_fullsize_memo_batch(lib, oracle_mt, c2_workload):
+    """C2 (BASELINE configs[1]): 16 slots of 64k-point scans vs the 1M-point map at radius 100 m, the
+    memo path bench.py times (match_fit_kernel<false>, memo on in outer iterations > 0)."""
+    from lmsf import synth
+    wl = c2_workload
+    n = 16
+    rng = np.random.default_rng(77)
+    unit = [i % len(wl.scans) for i in range(n)]
+    guesses = np.stack([synth.perturb(wl.truth[u], rng) for u in unit])
+    ctx = lib.Context(max_batch=n, max_scan_points=70000, max_features=70000, schedule=lib.SCHEDULE_FIXED,
+                      max_iterations=5)
+    ctx.set_map(lib.EDGE, wl.edge_map)
+    ctx.set_map(lib.SURF, wl.surf_map)
+    ctx.load_scans([wl.scans[u] for u in unit])
+    ctx.kernel_stats_reset(timing=True)
+    poses, stats = ctx.batch_run(guesses)
+    ks = ctx.kernel_stats()
+    assert ks.fused_launches == 5 and ks.reused_queries > 0.1 * ks.queries
+    feats = [oracle_mt.extract(s) for s in wl.scans]
+    reg = _oracle_reg(oracle_mt, wl, 5)
+    for i in range(n):
+        e, s, _, _ = feats[unit[i]]
+        reg.set_scan(1, e)
+        reg.set_scan(2, s)
+        ox, otr, ost = reg.solve(guesses[i])
+        _check_trace(ctx.batch_trace(i), otr, ("C2 slot", i))
+        assert (stats[i].edge_matches, stats[i].surf_matches) == (ost.edge_matches, ost.surf_matches)
+        dt, dr = pose_err(poses[i], wl.truth[unit[i]])
+        assert dt < 0.05 and dr < 0.01
+    ctx.close()
+    _records_bitexact(lib, oracle_mt, wl, wl.scans[1], guesses[1], dict(max_scan_points=70000), {})
+
+
+@pytest.fixture(scope="module")
+def c5_workload():
+    """C5 (BASELINE configs[4]): 128-beam 2048-column scans (~254k points) vs a 10M-point map."""
+    from lmsf import synth
+    return synth.make_workload("C5", n_scans=2, map_points=10_000_000)
+
+
+def test_c5_fullsize_pruned_batch(lib, oracle_mt, c5_workload):
+    from lmsf import synth
+    wl = c5_workload
+    c = synth.CONFIGS["C5"]
+    n = 2
+    R = 1 << 19                                                      # 2 x 2^19 slots: one lane per query
+    ctx = lib.Context(max_batch=n, max_scan_points=R, max_features=R, schedule=lib.SCHEDULE_FIXED, max_iterations=5,
+                      **c["extract"])
+    ctx.set_map(lib.EDGE, wl.edge_map)
+    ctx.set_map(lib.SURF, wl.surf_map)
+    ctx.load_scans(wl.scans[:n])
+    ctx.kernel_stats_reset(timing=True)
+    poses, stats = ctx.batch_run(wl.guess[:n])
+    ks = ctx.kernel_stats()
+    assert ks.fused_launches == 5 and ks.reused_queries == 0          # pruned dense-map walk: no memo
+    reg = _oracle_reg(oracle_mt, wl, 5)
+    for i in range(n):
+        e, s, _, _ = oracle_mt.extract(wl.scans[i], **c["extract"])
+        ge, _ = ctx.copy_features(lib.EDGE, slot=i)
+        gs, _ = ctx.copy_features(lib.SURF, slot=i)
+        assert ge.tobytes() == e.tobytes() and gs.tobytes() == s.tobytes()
+        reg.set_scan(1, e)
+        reg.set_scan(2, s)
+        ox, otr, ost = reg.solve(wl.guess[i])
+        _check_trace(ctx.batch_trace(i), otr, ("C5 pair", i))
+        assert (stats[i].edge_matches, stats[i].surf_matches) == (ost.edge_matches, ost.surf_matches)
+    ctx.close()
+    _records_bitexact(lib, oracle_mt, wl, wl.scans[0], wl.guess[0], dict(max_scan_points=R, **c["extract"]),
+                      c["extract"])
+
+
+def test_c4_fullsize_shared_map_streams(lib, oracle_mt):
+    """C4 (BASELINE configs[3]) on one GPU: two VLP-16 4096-column streams tracked against a 5M-point
+    shared prior map plus the stitched window of both streams' keyframes (exchanged in stream order,
+    committed once per step), 5 outer iterations, against two oracle trackers doing the same."""
+    import torch
+    import tracker as OT
+    from lmsf import synth
+    c = synth.CONFIGS["C4"]
+    k = c["k"]
+    scene = synth.make_scene(1000 + k, road_length=80.0)
+    n_steps = 6                                                      # first scan seeds, 5 tracked
+    streams = []
+    for r in range(2):
+        truth = synth.trajectory(n_steps, 3000 + k + r, step=0.8, start_x=8.0 * r)
+        scans = [synth.make_scan(scene, truth[i], 2000 + k + 97 * i + 7717 * r, n_cols=4096) for i in range(n_steps)]
+        streams.append((truth, scans))
+    em, sm = synth.make_map(scene, 5_000_000, 1000 + k + 7, center_x=(0.0, 80.0), radius=c["radius"])
+    dev = torch.device("cuda", 0)
+    em_t, sm_t = torch.from_numpy(em).to(dev), torch.from_numpy(sm).to(dev)
+    ctxs, gts, ots = [], [], []
+    for truth, _ in streams:
+        cx = lib.Context(max_batch=1, max_scan_points=70000, max_features=70000, schedule=lib.SCHEDULE_FIXED,
+                         max_iterations=5)
+        gt = lib.Tracker(cx, manual_map_update=True)
+        T0 = pose_matrix(truth[0])
+        gt.set_initial_pose(T0)
+        gt.set_prior_map(lib.EDGE, em_t)
+        gt.set_prior_map(lib.SURF, sm_t)
+        ot = OT.Tracker(manual_map_update=True)
+        ot.origin = T0.copy()
+        ot.reg.set_fixed_schedule(True)
+        ot.reg.set_max_iterations(5)
+        ot.set_prior_map(1, em)
+        ot.set_prior_map(2, sm)
+        ctxs.append(cx)
+        gts.append(gt)
+        ots.append(ot)
+    buf = {kk: torch.zeros((70000, 4), dtype=torch.float32, device=dev) for kk in (lib.EDGE, lib.SURF)}
+    tracked = 0
+    for step in range(n_steps):
+        kfs_g, kfs_o = [], []
+        for r, (truth, scans) in enumerate(streams):
+            e, su, _, _ = oracle_mt.extract(scans[step])
+            assert ctxs[r].extract(torch.from_numpy(scans[step]).to(dev)) == (len(e), len(su))
+            _, res = gts[r].solve_extracted(0.1 * step)
+            _, otyp, _ = ots[r].solve(e, su, 0.1 * step)
+            assert res.update_type == otyp, (step, r)
+            dt, dr = mat_err(gts[r].pose(), ots[r].curr)
+            assert dt <= POSE_TOL and dr <= POSE_TOL, (step, r, dt, dr)
+            dt, dr = mat_err(gts[r].pose(), pose_matrix(truth[step]))
+            assert dt < 0.05 and dr < 0.01, (step, r, dt, dr)
+            tracked += step > 0
+            if otyp:
+                ne = ctxs[r].copy_features_into(lib.EDGE, buf[lib.EDGE])
+                ns = ctxs[r].copy_features_into(lib.SURF, buf[lib.SURF])
+                assert (ne, ns) == (len(e), len(su))
+                kfs_g.append((buf[lib.EDGE][:ne].clone(), buf[lib.SURF][:ns].clone(), gts[r].pose()))
+                kfs_o.append((e, su, ots[r].curr.copy()))
+        for g, o in zip(kfs_g, kfs_o):
+            for r in range(len(streams)):
+                gts[r].add_keyframe(*g)
+                ots[r].add_keyframe(*o)
+        for r in range(len(streams)):
+            gts[r].commit_map()
+            ots[r].commit()
+            assert len(gts[r].local_map(lib.SURF)) == len(ots[r].local_map(2))
+    assert tracked == 2 * (n_steps - 1)
+    for t in gts:
+        t.close()
+    for cx in ctxs:
+        cx.close()

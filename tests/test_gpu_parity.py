@@ -262,9 +262,11 @@ def test_batch_run_matches_oracle(lib, oracle_mod, small_workload):
     ctx.set_map(lib.SURF, wl.surf_map)
     n = len(wl.scans)
     ctx.load_scans([wl.scans[i % n] for i in range(16)])
+    ctx.kernel_stats_reset(timing=True)
     poses, stats = ctx.batch_run(np.stack([wl.guess[i % n] for i in range(16)]))
     ks = ctx.kernel_stats()
     assert ks.launches == 5 and ks.fused_launches == 5               # the fused search + fit path ran
+    assert ks.reused_queries > 0.1 * ks.queries                      # ... and the query memo fired
     # outer iterations > 0 reuse the 5-NN set and fit of queries that moved less than half their
     # neighbour-distance gap: same records, packets summed in another grouping (the searching lanes
     # are packed), so the poses agree with re-searching every query to rounding
@@ -291,6 +293,65 @@ def test_batch_run_matches_oracle(lib, oracle_mod, small_workload):
         dt, dr = pose_err(poses[i], ox)
         assert dt <= POSE_TOL and dr <= POSE_TOL
         assert stats[i].outer_iterations == 5
+
+
+def test_batch_capacity_flag_is_per_batch(lib, small_workload):
+    """A batch whose scan overflows the extraction kernel's ring capacity fails with ERR_CAPACITY; the
+    next valid batch on the same context succeeds (the flag is cleared per launch)."""
+    wl = small_workload
+    ctx = _ctx(lib, schedule=1, max_iterations=2, max_batch=2)
+    ctx.set_map(lib.EDGE, wl.edge_map)
+    ctx.set_map(lib.SURF, wl.surf_map)
+    az = np.linspace(0, 2 * np.pi, 10000, endpoint=False)        # 10,000 points in ring 0 (> 8,192)
+    r = 10.0
+    bad = np.stack([r * np.cos(az), r * np.sin(az), np.full_like(az, -r * np.tan(np.radians(15.0))),
+                    np.zeros_like(az)], 1).astype(np.float32)
+    ctx.load_scans([bad, wl.scans[0]])
+    with pytest.raises(lib.LmsfError) as ei:
+        ctx.batch_run(np.stack([wl.guess[0], wl.guess[0]]))
+    assert ei.value.code == lib.ERR_CAPACITY
+    ctx.load_scans([wl.scans[0], wl.scans[1]])
+    poses, st = ctx.batch_run(np.stack([wl.guess[0], wl.guess[1]]))
+    assert st[0].outer_iterations == 2 and st[0].surf_matches > 0
+
+
+def test_batch_streamed_upload(lib, small_workload):
+    """lmsf_batch_load_scans_async: the next batch's scans upload (pinned host memory, copy stream)
+    while the current batch registers; results equal the synchronous loads, batch by batch."""
+    import torch
+    wl = small_workload
+    A = [wl.scans[i] for i in (0, 1, 2, 0)]
+    B = [wl.scans[i] for i in (2, 1, 0, 1)]
+    gA = np.stack([wl.guess[i] for i in (0, 1, 2, 0)])
+    gB = np.stack([wl.guess[i] for i in (2, 1, 0, 1)])
+
+    def mk():
+        c = _ctx(lib, schedule=1, max_iterations=3, max_batch=4)
+        c.set_map(lib.EDGE, wl.edge_map)
+        c.set_map(lib.SURF, wl.surf_map)
+        return c
+
+    ref = mk()
+    ref.load_scans(A)
+    pA, _ = ref.batch_run(gA)
+    ref.load_scans(B)
+    pB, _ = ref.batch_run(gB)
+
+    def pinned(scans):
+        return torch.from_numpy(np.concatenate(scans, 0)).pin_memory(), np.array([len(x) for x in scans])
+
+    ctx = mk()
+    ctx.load_scans_async(*pinned(A))
+    ctx.batch_launch(gA)
+    ctx.load_scans_async(*pinned(B))          # overlaps batch A's registration
+    qA, _ = ctx.batch_wait(4)
+    ctx.batch_launch(gB)
+    qB, _ = ctx.batch_wait(4)
+    np.testing.assert_array_equal(qA, pA)
+    np.testing.assert_array_equal(qB, pB)
+    for i in range(4):                         # per-slot outer-iteration trace of the last batch
+        tr = ctx.batch_trace(i)
+        assert tr.shape == (3, 7) and np.array_equal(tr[-1], qB[i])
 
 
 def test_batch_memo_dense(lib, oracle_mod, dense_workload):
@@ -628,14 +689,16 @@ def test_tracker_shared_map_streams(lib, oracle_mod, sequence_workload):
         t.close()
 
 
-def test_dual_lidar_refine_parity(lib, oracle_mod):
+@pytest.mark.parametrize("cols", [1800, 4096])
+def test_dual_lidar_refine_parity(lib, oracle_mod, cols):
     """C3 phase 1 (ML_System.hpp:284-322): primary tracker Solve, sub-LiDAR features extracted on
     the same context and registered against the primary local map from primary * extrinsic,
-    extrinsic = primary^-1 * sub -- against the oracle tracker doing the same."""
+    extrinsic = primary^-1 * sub -- against the oracle tracker doing the same.  4096 columns is the
+    C3 configuration (2 x ~63k points per frame)."""
     import tracker as OT
     from conftest import mat_err, pose_matrix, relative_truth
     from lmsf import dual, synth
-    ds = synth.make_dual_sequence(6, n_cols=1800, step=0.5)
+    ds = synth.make_dual_sequence(6, n_cols=cols, step=0.5)
     X = pose_matrix(ds.extrinsic)
     X0 = X @ pose_matrix(np.concatenate([synth.axis_angle_quat(np.radians([0.5, -0.5, 0.5])), [0.03, -0.02, 0.02]]))
     rel = relative_truth(ds.truth)
