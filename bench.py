@@ -318,13 +318,25 @@ def _scan_job(job):
     return synth.make_scan(synth.make_scene(seed_scene, road_length=80.0), pose, seed, n_cols=cols, elev_deg=elev)
 
 
+def under_profiler():
+    """rocprofv3 preloads its tool library (and with --pmc initialises the GPU) before the program starts."""
+    return "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ)
+
+
 def make_scans(jobs, workers):
-    """Synthetic scans generated in a process pool (before the rank touches the GPU: fork is safe)."""
-    if workers <= 1 or len(jobs) < 4:
+    """Synthetic scans generated in a process pool (before the rank touches the GPU: fork is safe), workers
+    closed and joined (never signalled).  Serial under rocprofv3: a forked child would carry the profiler's
+    tool state and signal handlers."""
+    if workers <= 1 or len(jobs) < 4 or under_profiler():
         return [_scan_job(j) for j in jobs]
     import multiprocessing as mp
-    with mp.get_context("fork").Pool(min(workers, len(jobs))) as pool:
-        return pool.map(_scan_job, jobs, chunksize=max(1, len(jobs) // (4 * workers)))
+    pool = mp.get_context("fork").Pool(min(workers, len(jobs)))
+    try:
+        out = pool.map(_scan_job, jobs, chunksize=max(1, len(jobs) // (4 * workers)))
+    finally:
+        pool.close()
+        pool.join()
+    return out
 
 
 def exchange_poses(cfg, poses, gathered, pairs, world, dev):

@@ -149,6 +149,25 @@ lmsf_status lmsf_solve_trace(lmsf_ctx* ctx, double* trace, int32_t cap, int32_t*
  * stay device-resident and become the current scan target (as SetInputTarget with the
  * processor's output container) without a host round trip.  xyzi: host or device memory. */
 lmsf_status lmsf_extract_features(lmsf_ctx* ctx, const float* xyzi, size_t n, lmsf_feature_counts* counts);
+/* PointCloudCommonProcess<P>(output_name = "filtered")::Process (INC/Algorithm/PointClouds/processing/
+ * common_processing.hpp:87-112), the preprocessor of the "sparse_point_plane_icp" scan-to-map mode
+ * (INC/factory/System/ML_SystemFactory.hpp:141-178): optional removeNaNFromPointCloud, VoxelGrid
+ * (centroids, as lmsf_voxel_filter), then DistanceFilter (float |p| promoted to double, keep
+ * near < d < far; distance_filter.hpp:24-43); the outlier filter is not configured on that path.  The
+ * "filtered" cloud becomes the current surf target on the device (no edge cloud: the registration is
+ * CeresEdgeSurfFeatureRegistration("", "filtered")), as lmsf_extract_features does for the LOAM
+ * clouds; lmsf_copy_features(LMSF_SURF) returns it.  Defaults (lmsf_common_params_init) are
+ * config/MultiSensorSystem/point_plane_icp_test.yaml:16-24: VoxelGrid 0.5 m, distance 2 .. 100 m,
+ * no NaN removal (the constructor's removal_nan = false). */
+typedef struct {
+    int32_t removal_nan;
+    float voxel_leaf;          /* m; 0: no downsampling */
+    float distance_near;       /* both 0: no distance filter (DistanceFilter's pass-through) */
+    float distance_far;
+} lmsf_common_params;
+lmsf_status lmsf_common_params_init(lmsf_common_params* p);
+lmsf_status lmsf_common_process(lmsf_ctx* ctx, const float* xyzi, size_t n, const lmsf_common_params* p,
+                                lmsf_feature_counts* counts);
 /* Copy the current features of one kind (xyzi rows, reference emission order) to host or device
  * memory; src (nullable) receives each feature's index in the raw scan. */
 lmsf_status lmsf_copy_features(lmsf_ctx* ctx, int32_t kind, float* out, int32_t* src, size_t cap, size_t* n_out);

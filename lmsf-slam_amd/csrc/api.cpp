@@ -679,6 +679,66 @@ lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf
     return LMSF_OK;
 }
 
+lmsf_status lmsf_common_params_init(lmsf_common_params* p) {
+    if (!p) return LMSF_ERR_ARG;
+    p->removal_nan = 0;        // PointCloudCommonProcess(output_name, removal_nan = false)
+    p->voxel_leaf = 0.5f;      // point_plane_icp_test.yaml:22-23
+    p->distance_near = 2.f;    // :19-20
+    p->distance_far = 100.f;
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_common_process(lmsf_ctx* c, const float* xyzi, size_t n, const lmsf_common_params* p,
+                                lmsf_feature_counts* counts) {
+    if (!c || !p || (n && !xyzi) || n > (size_t)INT32_MAX || p->voxel_leaf < 0.f) return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    hipStream_t s = c->stream;
+    if (n > c->vox_cap) {
+        HIPCHK(c, hipFree(c->vox_in));
+        HIPCHK(c, hipFree(c->vox_out));
+        c->vox_in = c->vox_out = nullptr;
+        const size_t cap = grow_cap(n, c->vox_cap);
+        c->vox_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->vox_in, cap * sizeof(float4)));
+        HIPCHK(c, hipMalloc((void**)&c->vox_out, cap * sizeof(float4)));
+        c->vox_cap = cap;
+    }
+    float4* cur = c->vox_in;
+    float4* other = c->vox_out;
+    int m = (int)n;
+    if (n) HIPCHK(c, hipMemcpyAsync(cur, xyzi, n * sizeof(float4), hipMemcpyDefault, s));
+    if (p->removal_nan && m > 0) {                                   // :93-97
+        HIPCHK(c, c->ingest.finite(cur, m, other, &m, s));
+        std::swap(cur, other);
+    }
+    if (p->voxel_leaf > 0.f && m > 0) {                              // :104
+        int nv = 0;
+        HIPCHK(c, c->voxel.run(cur, m, p->voxel_leaf, other, &nv, s));
+        m = nv;
+        std::swap(cur, other);
+    }
+    if (!(p->distance_near == 0.f && p->distance_far == 0.f) && m > 0) {   // :108
+        HIPCHK(c, c->ingest.distance(cur, m, (double)p->distance_near, (double)p->distance_far, other, &m, s));
+        std::swap(cur, other);
+    }
+    if (m > c->F) return c->fail(LMSF_ERR_CAPACITY, "%d filtered points exceed max_features %d", m, c->F);
+    if (m) HIPCHK(c, hipMemcpyAsync(c->feat, cur, (size_t)m * sizeof(float4), hipMemcpyDeviceToDevice, s));
+    c->h_counts[0] = 0;
+    c->h_counts[1] = m;
+    HIPCHK(c, hipMemcpyAsync(c->n_edge, &c->h_counts[0], sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->n_surf, &c->h_counts[1], sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->slot0_ne = 0;
+    c->slot0_ns = m;
+    c->features_on_device = true;
+    c->qorder_valid = false;          // slot order (no ring order for a filtered cloud)
+    c->scan_dirty = false;
+    c->host_scan[LMSF_EDGE].clear();
+    c->host_scan[LMSF_SURF].clear();
+    if (counts) { counts->n_edge = 0; counts->n_surf = m; }
+    return LMSF_OK;
+}
+
 static lmsf_status copy_slot_features(lmsf_ctx* c, int slot, int32_t kind, float* out, int32_t* src, size_t cap,
                                       size_t* n_out) {
     int hc[2];

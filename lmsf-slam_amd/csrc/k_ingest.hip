@@ -115,6 +115,53 @@ __global__ void distance_flag_kernel(const float4* pts, const int* count, double
     keep[i] = (d > near_t && d < far_t) ? 1u : 0u;
 }
 
+// Flags over a host-known count (PointCloudCommonProcess stages, common_processing.hpp:87-112)
+__global__ void finite_flag_kernel(const float4* pts, int n, uint32_t* keep) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = pts[i];
+    keep[i] = (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) ? 1u : 0u;   // removeNaNFromPointCloud
+}
+
+__global__ void distance_flag_n_kernel(const float4* pts, int n, double near_t, double far_t, uint32_t* keep) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = pts[i];
+    const double d = (double)sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
+    keep[i] = (d > near_t && d < far_t) ? 1u : 0u;
+}
+
+hipError_t Ingest::compact_flagged(const float4* in, int n, float4* out, int* n_out, hipStream_t s) {
+    int* count = scalars;
+    hipError_t e;
+    size_t tb = tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, keep, pos, n, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(compact_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, keep, pos, n, out, count);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(n_out, count, sizeof(int), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    return hipStreamSynchronize(s);
+}
+
+hipError_t Ingest::finite(const float4* in, int n, float4* out, int* n_out, hipStream_t s) {
+    *n_out = 0;
+    if (n <= 0) return hipSuccess;
+    hipError_t e = reserve((size_t)n, 0);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(finite_flag_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, keep);
+    return compact_flagged(in, n, out, n_out, s);
+}
+
+hipError_t Ingest::distance(const float4* in, int n, double near_t, double far_t, float4* out, int* n_out,
+                            hipStream_t s) {
+    *n_out = 0;
+    if (n <= 0) return hipSuccess;
+    hipError_t e = reserve((size_t)n, 0);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(distance_flag_n_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, near_t, far_t, keep);
+    return compact_flagged(in, n, out, n_out, s);
+}
+
 hipError_t Ingest::reserve(size_t n, size_t raw_bytes) {
     hipError_t e;
     if (raw_bytes > raw_cap) {

@@ -200,6 +200,10 @@ struct Ingest {
     hipError_t reserve(size_t n, size_t raw_bytes);
     hipError_t run(const uint8_t* data_dev, int n, uint32_t step, int ox, int oy, int oz, int oi, float period,
                    double near_t, double far_t, float4** result, int* n_out, hipStream_t s);
+    // stable compactions of device points (in != out), synchronising: removeNaN / DistanceFilter
+    hipError_t finite(const float4* in, int n, float4* out, int* n_out, hipStream_t s);
+    hipError_t distance(const float4* in, int n, double near_t, double far_t, float4* out, int* n_out, hipStream_t s);
+    hipError_t compact_flagged(const float4* in, int n, float4* out, int* n_out, hipStream_t s);
     void release();
 };
 

@@ -58,6 +58,11 @@ class ExtractParams(C.Structure):
                 ("beam_spacing_deg", C.c_double)]
 
 
+class CommonParams(C.Structure):
+    _fields_ = [("removal_nan", C.c_int32), ("voxel_leaf", C.c_float), ("distance_near", C.c_float),
+                ("distance_far", C.c_float)]
+
+
 class TrackerConfig(C.Structure):
     _fields_ = [("window_frames", C.c_int32), ("threshold_trans", C.c_double), ("threshold_rot", C.c_double),
                 ("time_interval", C.c_double), ("manual_map_update", C.c_int32), ("leaf_edge", C.c_double),
@@ -96,6 +101,8 @@ _SIGS = {
     "lmsf_solve": (C.c_int32, [_P, _P, C.POINTER(SolveStats)]),
     "lmsf_solve_trace": (C.c_int32, [_P, _P, C.c_int32, C.POINTER(C.c_int32)]),
     "lmsf_extract_features": (C.c_int32, [_P, _P, C.c_size_t, C.POINTER(FeatureCounts)]),
+    "lmsf_common_params_init": (C.c_int32, [C.POINTER(CommonParams)]),
+    "lmsf_common_process": (C.c_int32, [_P, _P, C.c_size_t, C.POINTER(CommonParams), C.POINTER(FeatureCounts)]),
     "lmsf_copy_features": (C.c_int32, [_P, C.c_int32, _P, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "lmsf_batch_load_scans": (C.c_int32, [_P, _P, _P, C.c_int32]),
     "lmsf_batch_load_scans_async": (C.c_int32, [_P, _P, _P, C.c_int32]),
@@ -254,6 +261,23 @@ class Context:
         fc = FeatureCounts()
         self._check(load().lmsf_extract_features(self.h, p, n, C.byref(fc)))
         return fc.n_edge, fc.n_surf
+
+    @staticmethod
+    def common_params(**kw):
+        p = CommonParams()
+        load().lmsf_common_params_init(C.byref(p))
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+    def common_process(self, pts, **kw):
+        """lmsf_common_process (PointCloudCommonProcess "filtered": NaN removal?, VoxelGrid, distance
+        filter); the result is the current surf target.  Returns its point count."""
+        prm = self.common_params(**kw)
+        p, n, keep = _buf(pts)
+        fc = FeatureCounts()
+        self._check(load().lmsf_common_process(self.h, p, n, C.byref(prm), C.byref(fc)))
+        return fc.n_surf
 
     def copy_features(self, kind, slot=None):
         n = C.c_size_t()

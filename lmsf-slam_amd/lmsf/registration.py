@@ -9,7 +9,12 @@ that a caller (or a test) reads like the reference's own code:
 * PointCloudProcessBase<In, Out>::Process(LidarData, CloudContainer)
   (INC/Algorithm/PointClouds/processing/process_base.hpp:26-39)
   implemented by LOAMFeatureProcessorHIP (FX/LOAMFeatureProcessor_base.hpp);
-* the factory selection string (INC/factory/System/ML_SystemFactory.hpp:179-198): "feature_based_hip".
+* PointCloudCommonProcess<P> (INC/Algorithm/PointClouds/processing/common_processing.hpp:39-122)
+  implemented by PointCloudCommonProcessHIP (removeNaN? -> VoxelGrid -> DistanceFilter);
+* the factory selection strings (INC/factory/System/ML_SystemFactory.hpp:141-198):
+  "feature_based_hip" (LOAM processor + CeresEdgeSurfFeatureRegistration("loam_edge", "loam_surf")) and
+  "sparse_point_plane_icp_hip" (PointCloudCommonProcess("filtered") + CeresEdgeSurfFeatureRegistration("",
+  "filtered")), each with a LidarTrackerLocalMap sliding window (ScanMapSystem).
 
 Clouds are (N, 4) float32 arrays of x, y, z, intensity (PointXYZI payload).  Poses are either
 (q, t) 7-vectors (qx qy qz qw tx ty tz) or 4x4 isometries; Solve accepts and returns the same
@@ -170,11 +175,95 @@ class LOAMFeatureProcessorHIP:
         return out
 
 
+FILTERED_NAME = "filtered"
+
+
+class PointCloudCommonProcessHIP:
+    """PointCloudCommonProcess<P>(output_name, removal_nan=false) (common_processing.hpp:39-122): the
+    "sparse_point_plane_icp" preprocessor.  SetVoxelGrid / SetDistanceFilter as the factory calls them
+    (ML_SystemFactory.hpp:158-171); Process runs lmsf_common_process on the device."""
+
+    def __init__(self, output_name=FILTERED_NAME, removal_nan=False, device=0, max_points=1 << 17, ctx=None):
+        self.output_name = output_name
+        self.ctx = ctx or _lib.Context(device=device, max_scan_points=max_points, max_features=max_points)
+        self.params = dict(removal_nan=int(bool(removal_nan)), voxel_leaf=0.0, distance_near=0.0, distance_far=0.0)
+
+    def SetVoxelGrid(self, name, cell_size):
+        if name != "VoxelGrid":       # ApproximateVoxelGrid (voxel_grid.hpp) is not on the MI355X path
+            raise ValueError(f"downsample filter {name!r} is not provided (VoxelGrid only)")
+        self.params["voxel_leaf"] = float(cell_size)
+
+    def SetDistanceFilter(self, distance_near_thresh, distance_far_thresh):
+        self.params["distance_near"] = float(distance_near_thresh)
+        self.params["distance_far"] = float(distance_far_thresh)
+
+    def run(self, cloud):
+        """Filter on the device; the result stays there as the context's current surf target."""
+        return self.ctx.common_process(cloud, **self.params)
+
+    def Process(self, data_in, data_out=None):
+        """LidarData (or an (N, 4) cloud) -> CloudContainer {output_name: filtered cloud} (:87-112)."""
+        self.run(getattr(data_in, "point_cloud", data_in))
+        out = {self.output_name: self.ctx.copy_features(_lib.SURF)[0]}
+        if data_out is not None:
+            data_out.update(out)
+        return out
+
+
 def make_registration(method: str, **kw):
-    """tracker.scan_map.registration_method (ML_SystemFactory.hpp:82-83, 179-198)."""
+    """tracker.scan_map.registration_method (ML_SystemFactory.hpp:82-83, 141-198)."""
     if method == "feature_based_hip":
         return CeresEdgeSurfFeatureRegistrationHIP("loam_edge", "loam_surf", **kw)
     if method == "feature_based_hip_gn":
         return EdgeSurfFeatureRegistrationHIP("loam_edge", "loam_surf", **kw)
+    if method == "sparse_point_plane_icp_hip":
+        return CeresEdgeSurfFeatureRegistrationHIP("", FILTERED_NAME, **kw)
     raise ValueError(f"registration method {method!r} is not provided by the MI355X path "
-                     "(scope: feature_based registration only; see DESIGN.md)")
+                     "(scope: the Ceres edge/surf registration; see DESIGN.md)")
+
+
+# point_plane_icp_test.yaml:16-24, 36-37 (the only shipped config reaching this registration)
+SPARSE_ICP_DEFAULTS = dict(voxel_size=0.5, distance_min=2.0, distance_max=100.0, window=10)
+
+
+class ScanMapSystem:
+    """One LiDAR's scan-to-map tracking as MultiLidarSystem builds it from
+    tracker.scan_map.registration_method (ML_SystemFactory.hpp:141-198): processor -> LidarTrackerLocalMap
+    (sliding window) -> CeresEdgeSurfFeatureRegistration, all on one device context, the processed
+    clouds staying in HBM between the processor and the tracker.
+
+      "feature_based_hip":          LOAMFeatureProcessorBase(16, 2, 80); window on {loam_edge, loam_surf}
+                                    (the build's sliding_Localmap, VoxelGrid 0.2 / 0.4 m)
+      "sparse_point_plane_icp_hip": PointCloudCommonProcess("filtered") = VoxelGrid(voxel_size) ->
+                                    DistanceFilter(distance_min, distance_max); registration ("", "filtered");
+                                    window on {filtered} of `window` keyframes, downsampled with the same
+                                    voxel_size (build-defined)
+    process(scan, timestamp) -> (pose 4x4 in the tracker frame, update type)."""
+
+    def __init__(self, method, ctx=None, device=0, max_points=1 << 17, **cfg):
+        self.method = method
+        self.ctx = ctx or _lib.Context(device=device, max_scan_points=max_points, max_features=max_points)
+        if method == "feature_based_hip":
+            self.processor = None
+            self.tracker = _lib.Tracker(self.ctx, window_frames=cfg.get("window", 10))
+        elif method == "sparse_point_plane_icp_hip":
+            c = dict(SPARSE_ICP_DEFAULTS, **cfg)
+            self.processor = PointCloudCommonProcessHIP(FILTERED_NAME, ctx=self.ctx)
+            self.processor.SetVoxelGrid("VoxelGrid", c["voxel_size"])
+            self.processor.SetDistanceFilter(c["distance_min"], c["distance_max"])
+            self.tracker = _lib.Tracker(self.ctx, window_frames=c["window"], leaf_edge=0.0, leaf_surf=c["voxel_size"])
+        else:
+            raise ValueError(f"scan-map method {method!r} is not provided by the MI355X path")
+        self.last = None
+
+    def process(self, scan, timestamp, deltaT=None):
+        if self.processor is None:
+            self.ctx.extract(scan)
+        else:
+            self.processor.run(scan)
+        _, r = self.tracker.solve_extracted(timestamp, deltaT)
+        self.last = r
+        return self.tracker.pose(), r.update_type
+
+    def close(self):
+        self.tracker.close()

@@ -88,6 +88,22 @@ def voxel_filter(points, leaf):
     return out[:m].copy()
 
 
+def common_process(points, removal_nan=False, voxel_leaf=0.5, distance_near=2.0, distance_far=100.0):
+    """PointCloudCommonProcess("filtered")::Process (INC/Algorithm/PointClouds/processing/
+    common_processing.hpp:87-112): removeNaN (optional) -> VoxelGrid (voxel.cpp) -> DistanceFilter
+    (distance_filter.hpp:24-43: float |p| promoted to double, near < d < far; both 0: pass-through)."""
+    p = _f32(points)
+    if removal_nan:
+        p = p[np.isfinite(p[:, :3]).all(1)]
+    if voxel_leaf > 0 and len(p):
+        p = voxel_filter(p, voxel_leaf)
+    if not (distance_near == 0 and distance_far == 0) and len(p):
+        x, y, z = p[:, 0], p[:, 1], p[:, 2]
+        d = np.sqrt(x * x + y * y + z * z).astype(np.float64)       # float32 arithmetic, as getVector3fMap().norm()
+        p = p[(d > float(np.float32(distance_near))) & (d < float(np.float32(distance_far)))]
+    return np.ascontiguousarray(p)
+
+
 def ingest(data: np.ndarray, n: int, point_step=32, offsets=(0, 4, 8, 16), scan_period=0.1, distance_near=0.0,
            distance_far=0.0):
     """PointCloud2 bytes -> xyzi rows (oracle/ingest.cpp)."""

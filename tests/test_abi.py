@@ -57,7 +57,8 @@ def test_struct_layouts(lib, tmp_path):
     structs = {"lmsf_config": lib.Config, "lmsf_solve_stats": lib.SolveStats,
                "lmsf_feature_counts": lib.FeatureCounts, "lmsf_kernel_stats": lib.KernelStats,
                "lmsf_tracker_config": lib.TrackerConfig, "lmsf_tracker_result": lib.TrackerResult,
-               "lmsf_extract_params": lib.ExtractParams, "lmsf_ingest_params": lib.IngestParams}
+               "lmsf_extract_params": lib.ExtractParams, "lmsf_ingest_params": lib.IngestParams,
+               "lmsf_common_params": lib.CommonParams}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "lmsf/lmsf.h"', 'int main(void) {']
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')

@@ -11,7 +11,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import pose_err
+from conftest import mat_err, pose_err
 
 pytestmark = pytest.mark.gpu
 
@@ -741,3 +741,54 @@ def test_reference_interface(lib, oracle_mod, small_workload):
     dt, dr = pose_err(R.to_pose7(out), wl.truth[0])
     assert dt < 0.05 and dr < 0.01
     assert reg.last_stats.outer_iterations == 9
+
+
+def test_common_process_parity(lib, oracle_mod, small_workload):
+    """lmsf_common_process (PointCloudCommonProcess "filtered": removeNaN? -> VoxelGrid -> DistanceFilter)
+    == oracle.common_process, points and order, for the shipped parameters and variants."""
+    from lmsf import synth
+    wl = small_workload
+    ctx = _ctx(lib)
+    org = synth.make_scan(wl.scene, wl.truth[0], 31, n_cols=4096, organized=True)      # NaN rows kept
+    for scan, kw in ((wl.scans[0], {}), (wl.scans[1], dict(voxel_leaf=0.2, distance_near=5.0, distance_far=40.0)),
+                     (wl.scans[2], dict(voxel_leaf=0.0)), (wl.scans[0], dict(distance_near=0.0, distance_far=0.0)),
+                     (org, dict(removal_nan=1))):
+        n = ctx.common_process(scan, **kw)
+        want = oracle_mod.common_process(scan, **{k: bool(v) if k == "removal_nan" else v for k, v in kw.items()})
+        got, _ = ctx.copy_features(lib.SURF)
+        assert n == len(want) and got.tobytes() == want.tobytes(), kw
+        assert ctx.copy_features(lib.EDGE)[0].shape[0] == 0
+
+
+def test_sparse_point_plane_icp_tracking(lib, oracle_mod, sequence_workload):
+    """"sparse_point_plane_icp_hip" (ML_SystemFactory.hpp:141-178, point_plane_icp_test.yaml:16-24, 36-37):
+    VoxelGrid 0.5 m -> distance 2..100 m -> CeresEdgeSurfFeatureRegistration("", "filtered") against a
+    10-keyframe sliding window on {filtered}, 10 scans, against the oracle tracker doing the same."""
+    import tracker as OT
+    from conftest import relative_truth
+    from lmsf import registration as R
+    wl = sequence_workload
+    rel = relative_truth(wl.truth)
+    system = R.ScanMapSystem("sparse_point_plane_icp_hip", ctx=_ctx(lib))
+    ot = OT.Tracker(window_frames=10, leaf_edge=0.0, leaf_surf=0.5)
+    empty = np.zeros((0, 4), np.float32)
+    types = []
+    for i, scan in enumerate(wl.scans):
+        f = oracle_mod.common_process(scan, voxel_leaf=0.5, distance_near=2.0, distance_far=100.0)
+        pose, typ = system.process(scan, wl.dt * i)
+        got, _ = system.ctx.copy_features(lib.SURF)
+        assert got.tobytes() == f.tobytes()
+        _, otyp, _ = ot.solve(empty, f, wl.dt * i)
+        assert typ == otyp, i
+        assert system.last.local_map_surf == len(ot.local_map(2)) and system.last.local_map_edge == 0
+        dt, dr = mat_err(pose, ot.curr)
+        assert dt <= POSE_TOL and dr <= POSE_TOL, (i, dt, dr)
+        dt, dr = mat_err(pose, rel[i])
+        assert dt < 0.1 and dr < 0.02, (i, dt, dr)
+        types.append(typ)
+    assert 1 in types[1:]
+    system.close()
+    with pytest.raises(ValueError):
+        R.PointCloudCommonProcessHIP().SetVoxelGrid("ApproximateVoxelGrid", 0.5)
+    reg = R.make_registration("sparse_point_plane_icp_hip", max_features=70000)
+    assert (reg.edge_name, reg.surf_name) == ("", "filtered")
