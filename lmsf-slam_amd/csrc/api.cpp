@@ -75,6 +75,15 @@ float knn_first_radius2(size_t n, unsigned long long occupied) {
     return (float)std::min(1.0, std::max(0.01, 1.0 / rho));
 }
 
+// LMSF_MEMO_BOUND = 0 | 1 (A/B, default 1): memo misses search a bounded radius (k_match.hip).
+bool memo_bound_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("LMSF_MEMO_BOUND");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 template <typename T>
 hipError_t dalloc(T** p, size_t count) {
     *p = nullptr;
@@ -99,7 +108,13 @@ struct lmsf_ctx {
     int* n_edge = nullptr;
     int* n_surf = nullptr;
     float4* nnp = nullptr;
-    float4* prevw = nullptr;          // [B][F] last searched float query per slot (fused path memo)
+    float4* prevw = nullptr;          // [B][F] fused-path memo anchors, by search position
+    int* memo_nbr = nullptr;          // [B][5][F] their neighbour indices
+    int* wl = nullptr;                // [B][F] memo pass work lists
+    float* wlim = nullptr;            // [B][F] their search radii^2
+    int* wcount = nullptr;            // [B][F / 256 + 1] their counts
+    int* n_search = nullptr;          // [B] positions searched by the last fused launch
+    int* ticket = nullptr;            // [B] LM evaluation arrival counters
     float4* rec_p = nullptr;          // records: point + kind / values / edge tail (BatchView)
     RecV* rec_v = nullptr;
     double2* rec_e = nullptr;
@@ -187,6 +202,15 @@ struct lmsf_ctx {
         v.n_surf = n_surf;
         v.nnp = nnp;
         v.prevw = prevw;
+        v.memo_nbr = memo_nbr;
+        v.wl = wl;
+        v.wlim = wlim;
+        v.ticket = ticket;
+        v.memo_bound = memo_bound_enabled() ? 1 : 0;
+        v.wcount = wcount;
+        v.n_search = n_search;
+        v.fused_parts = 0;            // set for the fused path's lm_begin (enqueue_register)
+        v.part2_base = (F + 63) / 64;
         v.memo = 0;
         v.fit_per_thread = fit_per_thread_default();
         v.part_q = 256 * v.fit_per_thread;
@@ -379,12 +403,12 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
             HIPCHK(c, launch_gn_solve(bv, o, s));
         } else {
             BatchView bvb = bv;
-            if (fused) bvb.part_q = 64;
-            HIPCHK(c, launch_lm_begin(bvb, s));
-            for (int i = 0; i < 4; ++i) {
-                HIPCHK(c, launch_lm_eval(bv, s));
-                HIPCHK(c, launch_lm_step(bv, o, i == 3 ? 1 : 0, s));
+            if (fused) {   // packets: memo pass [0, ceil(nq / 64)) when it ran, search [part2_base, + ceil(n_search / 64))
+                bvb.fused_parts = 1;
+                bvb.memo = o > 0 && !c->count27 && match_memo_enabled() && !match_fit_prune(ge, gs) ? 1 : 0;
             }
+            HIPCHK(c, launch_lm_begin(bvb, s));
+            for (int i = 0; i < 4; ++i) HIPCHK(c, launch_lm_eval_step(bv, o, i == 3 ? 1 : 0, s));
         }
     }
     return LMSF_OK;
@@ -456,7 +480,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
             hipFree(m.scan_tmp);
         }
     }
-    void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->prevw, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
+    void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->prevw, c->memo_nbr, c->wl, c->wlim, c->wcount, c->n_search, c->ticket, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->sort_key,
                     c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->n_pos, c->d_error};
@@ -498,7 +522,7 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     c->B = cfg->max_batch;
     c->R = cfg->max_scan_points;
     c->F = std::max(cfg->max_features, cfg->max_scan_points);
-    c->max_parts = (c->F + 63) / 64;   // worst case: one packet per wave of the fused search + fit
+    c->max_parts = 2 * ((c->F + 63) / 64);   // fused path: one packet per wave of the memo pass + of the search
     c->n_tiles = (c->R + kTile - 1) / kTile;
     auto bail = [&](lmsf_status code) {
         lmsf_ctx_destroy(c);
@@ -517,6 +541,13 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->n_surf, B));
     CHK(dalloc(&c->nnp, B * F * 5));
     CHK(dalloc(&c->prevw, B * F));
+    CHK(dalloc(&c->memo_nbr, B * kMemoWords * F));
+    CHK(dalloc(&c->wl, B * F));
+    CHK(dalloc(&c->wlim, B * F));
+    CHK(dalloc(&c->wcount, B * (F / 256 + 1)));
+    CHK(dalloc(&c->n_search, B));
+    CHK(dalloc(&c->ticket, B));
+    CHK(hipMemset(c->ticket, 0, B * sizeof(int)));
     CHK(dalloc(&c->rec_p, B * F));
     CHK(dalloc(&c->rec_v, B * F));
     CHK(dalloc(&c->rec_e, B * F));

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include "devmath.h"
+#include "lm_control.h"
 #include "lmsf_internal.h"
 
 #pragma clang fp contract(off)
@@ -95,9 +96,12 @@ __device__ __forceinline__ GridView pick_grid(bool c, const GridView& a, const G
 // RU: candidate loads in flight per row step of the one-lane rows-first walk.  NK: keys kept (5, or 6
 // for the fused kernel, whose query memo needs the 6th-nearest distance; the pruned walk prunes with
 // the NK-th key, so all NK are exact).
+// lim (plain walks): the squared search radius with its rounding margin -- kCullLim for the 1 m match
+// radius, smaller when a bound on the NK-th neighbour distance is known (memo misses, match_fit_kernel).
 template <int T, bool TWO, bool PRUNE, int RU = kKnnUnroll, int NK = 5>
 __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, const float3 w, const int lane,
-                                         const int count27, double (&k)[NK], unsigned int& c27) {
+                                         const int count27, double (&k)[NK], unsigned int& c27,
+                                         const float lim = 1.0f + 1e-5f) {
     constexpr int NR = TWO ? 18 : 9;
     constexpr uint32_t kGridBit = 0x80000000u;
     const float fx = floorf(w.x), fy = floorf(w.y), fz = floorf(w.z);
@@ -127,7 +131,7 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
         const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
         const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
         const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
-        const float rem = kCullLim - gy * gy - gz * gz;
+        const float rem = lim - gy * gy - gz * gz;
         if (rem >= 0.f) {
             const double r = (double)sqrtf(rem);
             const int sa = max(xa, (int)floor(((double)w.x - r) * sx) - ox);
@@ -513,7 +517,11 @@ __device__ __forceinline__ void butterfly_step(double* P, int lane) {
     }
 }
 
-__device__ __forceinline__ void block_reduce_packet(double* P, double* out) {
+typedef __attribute__((address_space(1))) unsigned int gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+// sc1: the packet is stored write-through (8-B agent-scope atomic stores) for a hand-off inside the launch.
+__device__ __forceinline__ void block_reduce_packet(double* P, double* out, bool sc1 = false) {
     static_assert(kPacket == 32, "butterfly over 32 entries");
     __shared__ double red[4][kPacket];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -527,7 +535,12 @@ __device__ __forceinline__ void block_reduce_packet(double* P, double* out) {
     __syncthreads();
     if (threadIdx.x < kPacket) {
         const int i = threadIdx.x;
-        out[i] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+        const double v = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+        if (sc1)
+            __hip_atomic_store((gu64*)(out + i), (unsigned long long)__double_as_longlong(v),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            out[i] = v;
     }
 }
 
@@ -675,16 +688,6 @@ __global__ __launch_bounds__(256) void fit_eval_kernel(BatchView bv, int solver)
 // edge slots then surf slots, each in ring order, so neighbouring lanes search neighbouring ring
 // points and a wave runs one fit kind.  Block x reduces fslot entries [256 x, 256 x + 256): the
 // partial count of fit_eval_kernel<1>, so lm_begin reads the same number of packets.
-// Waves per SIMD the fused kernel is compiled for (A/B): 4 = its natural 117 VGPRs, no scratch.
-// Forcing 5 (96 VGPRs, 100 B spill) measured 16.2k scans/s, 6 (80, 168 B) 15.2k, vs 17.0k at 4.
-// Candidate loads in flight per row step of the fused kernel's walk (A/B): 4 (0.472-0.477 ms) beat 2
-// (0.49), 6 (0.485), 8 (0.51) and a walk flattened across rows with 4-16 in flight (0.52-0.54).
-#ifndef LMSF_FUSED_UNROLL
-#define LMSF_FUSED_UNROLL 4
-#endif
-#ifndef LMSF_FUSED_WAVES
-#define LMSF_FUSED_WAVES 4
-#endif
 // Wave-level packet reduction (the transposing butterfly of block_reduce_packet without the LDS
 // step): entry e lands in lane 2e; out[e] written by that lane.
 __device__ __forceinline__ void wave_reduce_packet(double* P, double* out) {
@@ -715,118 +718,249 @@ __device__ __forceinline__ void record_packet(int kind, const float4 p, const d3
     P[30] += kind == LMSF_SURF ? 1.0 : 0.0;
 }
 
-template <bool PRUNE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void match_fit_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
-    // The memo needs the 6th-nearest distance; on dense maps (PRUNE) keeping 6 keys weakens the pruning
-    // (the walk prunes with the last kept key) more than the reuse saves (C5: 2568 / 2660 pairs/s with
-    // the memo off / on vs 2830 without it), so the pruned walk keeps 5 and searches every query.
-    constexpr bool kMemo = !PRUNE;
-    constexpr int kNK = kMemo ? 6 : 5;
+constexpr float kFullLim = 1.0f + 1e-5f;   // knn_walk's squared radius for the 1 m match radius (+ margin)
+
+// Key of map point m (caller-order index idx) for the query w: the expression of knn_walk's consider().
+__device__ __forceinline__ double nn_key(const float3 w, const float4 m, uint32_t idx) {
+    const float dx = w.x - m.x, dy = w.y - m.y, dz = w.z - m.z;
+    const float d2 = dx * dx + dy * dy + dz * dz;
+    return key_as_double(((uint64_t)(__float_as_uint(d2) + kKeyBias) << 32) | idx);
+}
+
+__device__ __forceinline__ void key_cswap(double& a, double& b) {
+    const double lo = fmin(a, b);
+    b = fmax(a, b);
+    a = lo;
+}
+
+// Entries of one memo block's work list per scan: wcount stride.
+__host__ __device__ __forceinline__ size_t memo_blocks(size_t feat_stride) { return feat_stride / 256 + 1; }
+
+// Query memo pass (outer iterations > 0 of a batch solve, sparse maps): one lane per search position
+// i (fslot order).  Position i's last full search left its anchor w0, gap = s6 - s5 and the 5
+// neighbour indices.  Every map point's distance to the query changes by at most d = |w - w0|, and
+// float d2 / sqrt are within 1e-6 m of exact below 1 m, so with 2 d + 1e-5 < gap the 5 nearest points
+// (all within the 1 m radius, the 6th capped there) are still the same 5: a new search returns these
+// 5 keys recomputed at w, in key order.  They are recomputed (the consider() expression) and sorted;
+// when the order equals the stored one, the new search's result is the stored one and so is the fit
+// (line / plane fits depend only on the ordered neighbours; the plane's orientation, which follows the
+// sign of n . w + D, is re-tested): only the residual, Jacobian and Huber-weighted packet at the
+// linearisation pose are new.  Otherwise the position goes to this block's work list for
+// match_fit_kernel<., true>, with a search radius: the 6 nearest points at w0 lie within s6 + d of w,
+// so the new 6 nearest do too, and a walk over the rows / x-slices within min(1 m, s6 + d) (+ margin)
+// returns the same 6 keys as the full 1 m walk.  One packet per wave at partial index 4 bx + wave.
+__global__ __launch_bounds__(256) void match_memo_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
     __shared__ int wcnt[4];
-    __shared__ int work[256];
-    __shared__ double rj[7][256];   // phase-1 residual + Jacobian of a reused query (kept out of registers
-    __shared__ int rk[256];         // across the search), rk = its kind (0: none)
     int bx, b;
     block_coords(remap, gx, bx, b);
     const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
-    if (bx * 256 >= nq) return;   // uniform per block, ahead of every barrier
+    if (bx * 256 >= nq) return;   // uniform per block, ahead of the barrier
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t F = bv.feat_stride;
     const Pose Ps = load_pose(bv.st[b].x);
-    unsigned int n_reused = 0;
-    rk[threadIdx.x] = 0;
-    // Phase 1 (every query of the block, fslot order): the query memo of outer iterations > 0.
-    // prevw = (anchor query w0 of the slot's last full search, gap = min over i < 5 of s[i+1] - s[i],
-    // s = sqrt of the kept d2s and s[5] = sqrt(min(6th d2, 1)); -1 when fewer than 5 were found).
-    // Every map point moves by at most |w - w0| relative to the query, and float d2 / sqrt are within
-    // 1e-6 m of exact below 1 m, so with 2 |w - w0| + 1e-5 < gap the 5-NN set, its order and the
-    // d2 < 1 test are unchanged: the line fit and the plane fit (up to its orientation, which follows
-    // the sign of n . w + D) are what a new search would give; only the packet at the new pose is new.
     const int i = bx * 256 + threadIdx.x;
-    const int q = i < nq ? bv.fslot[(size_t)b * bv.feat_stride + i] : -1;
-    bool full = q >= 0 && q < nq;   // fslot is a permutation of [0, nq) (order_kernel); the test guards memory
-    if (kMemo && full && bv.memo && !bv.count27) {
-        const size_t slot = (size_t)b * bv.feat_stride + q;
-        const float4 pw = bv.prevw[slot];
-        if (pw.w > 0.f) {
+    bool need = i < nq;
+    unsigned int n_reused = 0;
+    float lim = kFullLim;   // a miss's search radius^2: the 6 nearest at w0 are within s6 + d of w
+    double P[kPacket];
+#pragma unroll
+    for (int e = 0; e < kPacket; ++e) P[e] = 0.0;
+    if (need) {
+        const size_t pos = (size_t)b * F + i;
+        const int q = bv.fslot[pos];
+        const float4 pw = bv.prevw[pos];
+        if (q >= 0 && q < nq && pw.w > 0.f) {
+            const size_t slot = (size_t)b * F + q;
             const float4 p = bv.feat[slot];
             const float3 w = associate(Ps, p);
             const double dx = (double)w.x - pw.x, dy = (double)w.y - pw.y, dz = (double)w.z - pw.z;
-            if (2.0 * sqrt(dx * dx + dy * dy + dz * dz) + 1e-5 < (double)pw.w) {
-                const int kind = __float_as_int(bv.rec_p[slot].w);
-                d3 v0 = mk(0, 0, 0);
-                double v1x = 0.0, v1y = 0.0, v1z = 0.0;
-                bool reuse = true;
-                if (kind != 0) {
-                    const RecV v = bv.rec_v[slot];
-                    v0 = mk(v.v[0], v.v[1], v.v[2]);
-                    v1x = v.v[3];
-                    if (kind == LMSF_SURF) {   // surf_fit's orientation test at the new query (the stored
-                        const d3 cp = mk((double)w.x, (double)w.y, (double)w.z);   // n, D were flipped to
-                        reuse = (float)(dot(v0, cp) + v1x) > 0.f;                   // make it >= 0 at w0)
-                    } else {
-                        const double2 e = bv.rec_e[slot];
-                        v1y = e.x;
-                        v1z = e.y;
-                    }
-                }
-                if (reuse) {
-                    if (kind != 0) {
-                        double J[6];
-                        const d3 pp = mk((double)p.x, (double)p.y, (double)p.z);
-                        rj[6][threadIdx.x] = kind == LMSF_EDGE ? edge_residual(Ps, pp, v0, mk(v1x, v1y, v1z), J)
-                                                               : surf_residual(Ps, pp, v0, v1x, J);
+            const double dd = sqrt(dx * dx + dy * dy + dz * dz);
+            const double r6 = (double)__int_as_float(bv.memo_nbr[((size_t)b * kMemoWords + 5) * F + i]) + dd + 1e-5;
+            if (r6 < 1.0 && bv.memo_bound) lim = fminf(kFullLim, (float)(r6 * r6) + 1e-5f);
+            if (2.0 * dd + 1e-5 < (double)pw.w) {
+                const float4* orig = q < ne ? ge.orig : gs.orig;
+                uint32_t idx[5];
+                double k[5];
 #pragma unroll
-                        for (int j = 0; j < 6; ++j) rj[j][threadIdx.x] = J[j];
-                        rk[threadIdx.x] = kind;
+                for (int j = 0; j < 5; ++j) idx[j] = (uint32_t)bv.memo_nbr[((size_t)b * kMemoWords + j) * F + i];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) k[j] = nn_key(w, orig[idx[j]], idx[j]);
+                // 5-key sorting network (9 compare-exchanges)
+                key_cswap(k[0], k[1]); key_cswap(k[3], k[4]); key_cswap(k[2], k[4]);
+                key_cswap(k[2], k[3]); key_cswap(k[0], k[3]); key_cswap(k[0], k[2]);
+                key_cswap(k[1], k[4]); key_cswap(k[1], k[3]); key_cswap(k[1], k[2]);
+                bool same = key_bits(k[4]) < kSentinel;   // all five still inside the radius
+#pragma unroll
+                for (int j = 0; j < 5; ++j) same = same && (uint32_t)key_bits(k[j]) == idx[j];
+                if (same) {
+                    const int kind = __float_as_int(bv.rec_p[slot].w);
+                    d3 v0 = mk(0, 0, 0);
+                    double v1x = 0.0, v1y = 0.0, v1z = 0.0;
+                    bool reuse = true;
+                    if (kind != 0) {
+                        const RecV v = bv.rec_v[slot];
+                        v0 = mk(v.v[0], v.v[1], v.v[2]);
+                        v1x = v.v[3];
+                        if (kind == LMSF_SURF) {   // surf_fit's orientation test at the new query (the stored
+                            const d3 cp = mk((double)w.x, (double)w.y, (double)w.z);   // n, D were flipped to
+                            reuse = (float)(dot(v0, cp) + v1x) > 0.f;                   // make it >= 0 at w0)
+                        } else {
+                            const double2 e = bv.rec_e[slot];
+                            v1y = e.x;
+                            v1z = e.y;
+                        }
                     }
-                    full = false;
-                    n_reused = 1;
+                    if (reuse) {
+                        record_packet(kind, p, v0, v1x, v1y, v1z, Ps, P);
+                        need = false;
+                        n_reused = 1;
+                    }
                 }
             }
         }
     }
-    // Phase 2: the queries needing a search are packed to the front of the block (deterministic: fslot
-    // order), so they fill whole waves and the waves left without one finish early.
-    const unsigned long long m = __ballot(full);
+    if (bx * 256 + wave * 64 < nq)
+        wave_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + (size_t)bx * 4 + wave) * kPacket);
+    // this block's positions still needing a search, in position order (deterministic)
+    const unsigned long long m = __ballot(need);
     if (lane == 0) wcnt[wave] = __popcll(m);
     __syncthreads();
     int before = 0, total = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        before += k < wave ? wcnt[k] : 0;
-        total += wcnt[k];
+    for (int w4 = 0; w4 < 4; ++w4) {
+        before += w4 < wave ? wcnt[w4] : 0;
+        total += wcnt[w4];
     }
-    if (full) work[before + __popcll(m & ((1ull << lane) - 1ull))] = q;
-    __syncthreads();
+    if (need) {
+        const size_t at = (size_t)b * F + (size_t)bx * 256 + before + __popcll(m & ((1ull << lane) - 1ull));
+        bv.wl[at] = i;
+        bv.wlim[at] = lim;
+    }
+    if (threadIdx.x == 0) bv.wcount[(size_t)b * memo_blocks(F) + bx] = total;
+    if (bv.n27) {   // accounting runs: queries and reused ones
+        unsigned int qn = i < nq ? 1u : 0u;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            qn += __shfl_xor(qn, o, 64);
+            n_reused += __shfl_xor(n_reused, o, 64);
+        }
+        if (lane == 0) {
+            unsigned long long* shard = bv.n27 + (size_t)((blockIdx.x * 4 + wave) & (kCounterShards - 1)) * 16;
+            if (qn) atomicAdd(shard + 1, (unsigned long long)qn);
+            if (n_reused) atomicAdd(shard + 2, (unsigned long long)n_reused);
+        }
+    }
+}
+
+// Fused 5-NN search + fit for batch launches (one lane per query, Ceres-LM solver): the walk of
+// knn_walk<1, false, PRUNE>, then the line / plane fit, record write and Huber-weighted packet at the
+// linearisation pose on the neighbours held in registers (knn_kernel + fit_eval_kernel hand the 5
+// neighbour points through memory instead).  LIST = false: every search position i < nq (edge slots
+// then surf slots, each in ring order, so neighbouring lanes search neighbouring ring points and a
+// wave runs one fit kind).  LIST = true: only the positions the memo pass listed -- entry e of the
+// concatenation of its blocks' lists (each block scans the block counts into LDS and finds its
+// entries' blocks by binary search), so the searches fill whole waves.  Sparse maps (!PRUNE) keep
+// the 6th-nearest key and leave position i's anchor (w, s6 - s5) and neighbour indices for the memo
+// pass; on dense maps (PRUNE) the walk prunes with the last kept key, so it keeps 5 and has no memo
+// (C5: keeping a 6th weakens the pruning more than reuse saves, 2568 / 2660 vs 2830 pairs/s, r01).
+// One packet per wave at partial index part2_base + 4 bx + wave.
+// Waves per SIMD the kernel is compiled for (A/B): 4 = its natural ~120 VGPRs, no scratch.  Forcing 5
+// (96 VGPRs, 100 B spill) measured 16.2k scans/s, 6 (80, 168 B) 15.2k, vs 17.0k at 4 (r01).
+// Candidate loads in flight per row step of the walk (A/B): 4 (0.472-0.477 ms) beat 2 (0.49), 6
+// (0.485), 8 (0.51) and a walk flattened across rows with 4-16 in flight (0.52-0.54) (r01).
+#ifndef LMSF_FUSED_UNROLL
+#define LMSF_FUSED_UNROLL 4
+#endif
+#ifndef LMSF_FUSED_WAVES
+#define LMSF_FUSED_WAVES 4
+#endif
+template <bool PRUNE, bool LIST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void match_fit_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
+    extern __shared__ int soff[];   // LIST: exclusive prefix of the memo blocks' counts, [nblk + 1]
+    constexpr bool kMemo = !PRUNE;
+    constexpr int kNK = kMemo ? 6 : 5;
+    int bx, b;
+    block_coords(remap, gx, bx, b);
+    const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
+    const size_t F = bv.feat_stride;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int total = nq, nblk = 0;
+    if constexpr (LIST) {
+        __shared__ int wsum[4];
+        nblk = (nq + 255) / 256;
+        const int* wc = bv.wcount + (size_t)b * memo_blocks(F);
+        const int per = (nblk + 255) / 256;
+        const int j0 = threadIdx.x * per;
+        int mine = 0;
+        for (int j = 0; j < per; ++j) mine += j0 + j < nblk ? wc[j0 + j] : 0;
+        int incl = mine;   // wave inclusive scan
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o, 64);
+            incl += lane >= o ? t : 0;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        int run = incl - mine;
+#pragma unroll
+        for (int w4 = 0; w4 < 4; ++w4) run += w4 < wave ? wsum[w4] : 0;
+        for (int j = 0; j < per; ++j) {
+            if (j0 + j < nblk) {
+                soff[j0 + j] = run;
+                run += wc[j0 + j];
+            }
+        }
+        total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (threadIdx.x == 0) soff[nblk] = total;
+        __syncthreads();
+    }
+    if (bx == 0 && threadIdx.x == 0) bv.n_search[b] = total;
+    if (bx * 256 >= total) return;   // uniform per block, after the last barrier
+    const Pose Ps = load_pose(bv.st[b].x);
+    const int e = bx * 256 + threadIdx.x;
     unsigned int c27 = 0;
     double P[kPacket];
 #pragma unroll
-    for (int e = 0; e < kPacket; ++e) P[e] = 0.0;
-    if ((int)threadIdx.x < total) {
-        const int qq = work[threadIdx.x];
+    for (int j = 0; j < kPacket; ++j) P[j] = 0.0;
+    if (e < total) {
+        int pos = e;
+        float lim = kFullLim;
+        if constexpr (LIST) {   // largest block whose list starts at or before e (empty blocks share offsets)
+            int lo = 0, hi = nblk - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (soff[mid] <= e) lo = mid;
+                else hi = mid - 1;
+            }
+            const size_t at = (size_t)b * F + (size_t)lo * 256 + (e - soff[lo]);
+            pos = bv.wl[at];
+            lim = bv.wlim[at];
+        }
+        const size_t ppos = (size_t)b * F + pos;
+        const int qq = bv.fslot[ppos];
         const bool is_edge = qq < ne;
         const GridView g = pick_grid(is_edge, ge, gs);
-        const size_t slot = (size_t)b * bv.feat_stride + qq;
+        const size_t slot = (size_t)b * F + qq;
         const float4 p = bv.feat[slot];
         const float3 w = associate(Ps, p);
         const double sentinel = key_as_double(kSentinel);
         double k[kNK];
 #pragma unroll
         for (int j = 0; j < kNK; ++j) k[j] = sentinel;
-        knn_walk<1, false, PRUNE, LMSF_FUSED_UNROLL, kNK>(g, g, w, 0, bv.count27, k, c27);
-        float gap = -1.f;
-        if (kMemo && key_bits(k[4]) < kSentinel) {
-            double sp = sqrt((double)key_d2(k[0]));
-            double mg = 1e30;
+#ifndef LMSF_AB_NOWALK   // A/B ablation builds only (tools/build_variant.sh): no search
+        knn_walk<1, false, PRUNE, LMSF_FUSED_UNROLL, kNK>(g, g, w, 0, bv.count27, k, c27, lim);
+#endif
+        if (kMemo) {   // anchor for the memo pass: gap between the 5th and the 6th neighbour (capped at 1 m)
+            float gap = -1.f;
+            if (key_bits(k[4]) < kSentinel) {
+                const double s6 = sqrt((double)fminf(key_d2(k[5]), 1.0f));
+                gap = (float)(s6 - sqrt((double)key_d2(k[4])));
 #pragma unroll
-            for (int j = 1; j < kNK; ++j) {
-                const double sj = sqrt((double)fminf(key_d2(k[j]), 1.0f));
-                mg = fmin(mg, sj - sp);
-                sp = sj;
+                for (int j = 0; j < 5; ++j) bv.memo_nbr[((size_t)b * kMemoWords + j) * F + pos] = (int)(uint32_t)key_bits(k[j]);
+                bv.memo_nbr[((size_t)b * kMemoWords + 5) * F + pos] = __float_as_int((float)s6);
             }
-            gap = (float)mg;
+            bv.prevw[ppos] = make_float4(w.x, w.y, w.z, gap);
         }
-        if (kMemo) bv.prevw[slot] = make_float4(w.x, w.y, w.z, gap);
         float4 np[5];
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
@@ -845,6 +979,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         int kind = 0;
         d3 v0 = mk(0, 0, 0);
         double v1x = 0.0, v1y = 0.0, v1z = 0.0;
+#ifndef LMSF_AB_NOFIT      // A/B ablation builds only: search without the fit
         if (__float_as_int(np[4].w) >= 0) {   // fit_query's LM branch
             if (is_edge) {
                 d3 a, bpt;
@@ -863,44 +998,106 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
                 }
             }
         }
+#endif
         store_record(bv, slot, p, kind, v0, v1x, v1y, v1z);
         record_packet(kind, p, v0, v1x, v1y, v1z, Ps, P);
     }
-    {   // this lane's reused query (phase 1), if any
-        const int kind = rk[threadIdx.x];
-        if (kind != 0) {
-            double J[6];
-#pragma unroll
-            for (int j = 0; j < 6; ++j) J[j] = rj[j][threadIdx.x];
-            huber_accumulate(P, rj[6][threadIdx.x], J);
-            P[29] += kind == LMSF_EDGE ? 1.0 : 0.0;
-            P[30] += kind == LMSF_SURF ? 1.0 : 0.0;
-        }
-    }
-    // one packet per wave (no block barrier: a wave without a search ends as soon as it is reduced);
-    // partial index 4 bx + wave, the waves of a block holding any query of [0, nq) write
-    if (bx * 256 + wave * 64 < nq)
-        wave_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + (size_t)bx * 4 + wave) * kPacket);
-    if (bv.n27) {   // accounting runs: queries (phase 1 lanes), reused, n27 of the searches
-        unsigned int qn = (q >= 0 && q < nq) ? 1u : 0u;
+    if (bx * 256 + wave * 64 < total)
+        wave_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + bv.part2_base + (size_t)bx * 4 + wave) * kPacket);
+    if (bv.n27) {   // accounting runs: n27 of the searches (+ the queries when there was no memo pass)
+        unsigned int qn = (!LIST && e < total) ? 1u : 0u;
         unsigned long long c = c27;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
             qn += __shfl_xor(qn, o, 64);
-            n_reused += __shfl_xor(n_reused, o, 64);
             c += __shfl_xor(c, o, 64);
         }
         if (lane == 0) {
             unsigned long long* shard = bv.n27 + (size_t)((blockIdx.x * 4 + wave) & (kCounterShards - 1)) * 16;
             if (c) atomicAdd(shard, c);
             if (qn) atomicAdd(shard + 1, (unsigned long long)qn);
-            if (n_reused) atomicAdd(shard + 2, (unsigned long long)n_reused);
         }
     }
 }
 
-// LM candidate evaluation over the fixed correspondences (Ceres re-evaluates the same residual
-// blocks at every trial point).  kEvalPerThread records per thread.
+#ifndef LMSF_EVAL_WAVES
+#define LMSF_EVAL_WAVES 4
+#endif
+// One Ceres LM inner iteration per launch: every record's residual + Jacobian at the candidate pose
+// (Ceres re-evaluates the same residual blocks at every trial point), a packet per block, and -- in
+// the last block of the slot to finish (an agent-scope ticket per slot, the blocks' packet stores
+// released before it and acquired after it) -- the fixed-order packet reduction and the step
+// acceptance / next step (lm_step_apply): one launch where an evaluation kernel and a 64-lane step
+// kernel ran before.  kEvalPerThread records per thread.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_EVAL_WAVES))) void lm_eval_step_kernel(BatchView bv, int outer, int is_last) {
+    const int b = blockIdx.y;
+    SolveState& S = bv.st[b];
+    if (!S.need_eval) {   // solver finished: only the outer iteration's trace row, once per slot
+        if (is_last && blockIdx.x == 0 && threadIdx.x == 0) finish_outer(S, outer);
+        return;
+    }
+    const int nq = bv.n_edge[b] + bv.n_surf[b];
+    if (blockIdx.x * kEvalBlock >= nq) return;
+    const Pose Ps = load_pose(S.xc);
+    double P[kPacket];
+#pragma unroll
+    for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
+    // every record's point and value loads issued before the first use (the value array is read
+    // whatever the kind: an unmatched slot's stale values are loaded but never used)
+    float4 rp[kEvalPerThread];
+    RecV rv[kEvalPerThread];
+#pragma unroll
+    for (int k = 0; k < kEvalPerThread; ++k) {
+        const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
+        const size_t slot = (size_t)b * bv.feat_stride + (q < nq ? q : 0);
+        rp[k] = bv.rec_p[slot];
+        rv[k] = bv.rec_v[slot];
+    }
+#pragma unroll
+    for (int k = 0; k < kEvalPerThread; ++k) {
+        const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
+        const int kind = __float_as_int(rp[k].w);
+        if (q < nq && kind != 0) {
+            double J[6], res;
+            const d3 pp = mk((double)rp[k].x, (double)rp[k].y, (double)rp[k].z);
+            const RecV& v = rv[k];
+            if (kind == LMSF_EDGE) {
+                const double2 e = bv.rec_e[(size_t)b * bv.feat_stride + q];
+                res = edge_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), mk(v.v[3], e.x, e.y), J);
+            } else {
+                res = surf_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), v.v[3], J);
+            }
+            huber_accumulate(P, res, J);
+        }
+    }
+    // Hand-off to the slot's last block (cdna_hip_programming.md Guideline 16, R1): the packet is stored
+    // write-through (sc1: 8-B agent-scope atomic stores, no L2 write-back fence), the storing wave drains
+    // it, then after the barrier ONE lane adds to the slot's ticket; the block whose add returns the last
+    // count acquires once (this CU's L1) and reads every packet with plain loads.
+    block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + blockIdx.x) * kPacket, true);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int last;
+    const int nblk = (nq + kEvalBlock - 1) / kEvalBlock;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        gu32* tk = (gu32*)(bv.ticket + b);
+        const unsigned t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = t == (unsigned)(nblk - 1);
+        if (last) {
+            __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every block's packet, fresh
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!last) return;
+    double tot[kPacket];
+    reduce_parts(bv, b, nblk, tot);
+    if (threadIdx.x == 0) lm_step_apply(S, tot, outer, is_last);
+}
+
+// The same evaluation without the hand-off (LMSF_LM_FUSED=0, A/B): one packet per block; the step
+// runs in lm_step_kernel (k_solver.hip).
 __global__ __launch_bounds__(256) void lm_eval_kernel(BatchView bv) {
     const int b = blockIdx.y;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
@@ -910,8 +1107,6 @@ __global__ __launch_bounds__(256) void lm_eval_kernel(BatchView bv) {
     double P[kPacket];
 #pragma unroll
     for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
-    // every record's point and value loads issued before the first use (the value array is read
-    // whatever the kind: an unmatched slot's stale values are loaded but never used)
     float4 rp[kEvalPerThread];
     RecV rv[kEvalPerThread];
 #pragma unroll
@@ -1064,21 +1259,49 @@ bool match_fit_applies(const GridView& edge2, const GridView& surf2, const Batch
            bv.fit_per_thread == 1 && knn_team((size_t)bv.feat_stride * bv.B) == 1;
 }
 
+bool match_fit_prune(const GridView& edge, const GridView& surf) {
+    return (edge.n > 0 && edge.lim1 < 1.f) || (surf.n > 0 && surf.lim1 < 1.f);
+}
+
+// bv.memo: run the memo pass first, then search only its work lists (sparse maps only).
 hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const BatchView& bv, hipStream_t s) {
     const int gx = (bv.feat_stride + 255) / 256;
     const dim3 grid(gx * bv.B);
-    const bool prune = (edge.n > 0 && edge.lim1 < 1.f) || (surf.n > 0 && surf.lim1 < 1.f);
-    if (prune)
-        hipLaunchKernelGGL(match_fit_kernel<true>, grid, dim3(256), 0, s, edge, surf, bv, gx, knn_remap());
-    else
-        hipLaunchKernelGGL(match_fit_kernel<false>, grid, dim3(256), 0, s, edge, surf, bv, gx, knn_remap());
+    const int remap = knn_remap();
+    if (match_fit_prune(edge, surf)) {
+        hipLaunchKernelGGL((match_fit_kernel<true, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
+    } else if (bv.memo) {
+        hipLaunchKernelGGL(match_memo_kernel, grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
+        const size_t lds = (memo_blocks(bv.feat_stride) + 1) * sizeof(int);
+        hipLaunchKernelGGL((match_fit_kernel<false, true>), grid, dim3(256), lds, s, edge, surf, bv, gx, remap);
+    } else {
+        hipLaunchKernelGGL((match_fit_kernel<false, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_lm_eval(const BatchView& bv, hipStream_t s) {
+// LMSF_LM_FUSED = 0 | 1 (A/B, default 0): the evaluation and the step in one launch (ticket hand-off)
+// or two.  Measured (r02, C2 default bench, one process): fused 20.9k / 20.8k scans/s, two launches
+// 22.1k -- the step code caps the fused kernel at 128 VGPRs (spilling only on the last-block path),
+// and its serial step lands on the launch's tail instead of a 64-lane kernel of its own.
+static bool lm_fused() {
+    static bool v = [] {
+        const char* e = getenv("LMSF_LM_FUSED");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return v;
+}
+
+hipError_t launch_lm_eval_step(const BatchView& bv, int outer, int is_last, hipStream_t s) {
     dim3 grid((bv.feat_stride + kEvalBlock - 1) / kEvalBlock, bv.B);
+    if (lm_fused()) {
+        hipLaunchKernelGGL(lm_eval_step_kernel, grid, dim3(256), 0, s, bv, outer, is_last);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(lm_eval_kernel, grid, dim3(256), 0, s, bv);
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_lm_step(bv, outer, is_last, s);
 }
 
 hipError_t launch_eval_at(const BatchView& bv, const double* pose_dev, double* out_dev, hipStream_t s) {

@@ -1,0 +1,213 @@
+// Device-side Ceres LM control shared by the solver kernels (k_solver.hip) and the fused LM
+// evaluation + step kernel (k_match.hip): fixed-order packet reduction, 6x6 Cholesky, the trust-region
+// step and the step acceptance, restating ceres::Solve as configured in
+// CeresEdgeSurfFeatureRegistration::Solve (REG/ceres_edgeSurfFeatureRegistration.hpp:107-123); see
+// k_solver.hip for the Ceres semantics restated.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "devmath.h"
+#include "lmsf_internal.h"
+
+namespace lmsf {
+namespace {
+
+constexpr int kMaxInner = 4;  // options.max_num_iterations (ceres_...:118)
+
+// Sum the packets [0, nparts) and [base2, base2 + n2) of slot b in a fixed order; result valid in
+// every lane.  Lane l owns entry l % 32 of the packets p = l / 32 (mod 2): the loads are coalesced
+// and all in flight at once (one latency, not one per entry), then the two halves add in one shuffle.
+__device__ void reduce_parts(const BatchView& bv, int b, int nparts, double* tot, int base2 = 0, int n2 = 0) {
+    static_assert(kPacket == 32, "one packet entry per half-wave lane");
+    __shared__ double red[kPacket];
+    const int lane = threadIdx.x, e = lane & 31;
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int range = 0; range < 2 && lane < 64; ++range) {   // wave 0 loads; every thread reaches the barrier
+        const int np = range ? n2 : nparts;
+        const double* base = bv.partials + ((size_t)b * bv.max_parts + (range ? base2 : 0)) * kPacket;
+        int p = lane >> 5;
+        for (; p + 14 < np; p += 16) {   // 8 independent loads in flight per lane
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u] += base[(size_t)(p + 2 * u) * kPacket + e];
+        }
+        for (; p < np; p += 2) acc[0] += base[(size_t)p * kPacket + e];
+    }
+    double v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    v += __shfl_xor(v, 32, 64);
+    if (lane < 32) red[e] = v;   // wave 0's first half
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPacket; ++i) tot[i] = red[i];
+}
+
+__device__ double norm7(const double* x) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) s += x[i] * x[i];
+    return sqrt(s);
+}
+
+__device__ __forceinline__ double grad_max_norm(const double* x, const double* g) {
+    double ng[6], xp[7];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) ng[i] = -g[i];
+    pose_plus(x, ng, xp);
+    double m = 0.0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) m = fmax(m, fabs(x[i] - xp[i]));
+    return m;
+}
+
+__device__ __forceinline__ bool chol_solve6(const double* A, const double* b, double* x) {
+    double L[36];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) L[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        double s = A[j * 6 + j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s -= L[j * 6 + k] * L[j * 6 + k];
+        if (!(s > 0.0)) return false;
+        double ljj = sqrt(s);
+        L[j * 6 + j] = ljj;
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) {
+            double t = A[i * 6 + j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) t -= L[i * 6 + k] * L[j * 6 + k];
+            L[i * 6 + j] = t / ljj;
+        }
+    }
+    double y[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        double t = b[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) t -= L[i * 6 + k] * y[k];
+        y[i] = t / L[i * 6 + i];
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+        double t = y[i];
+#pragma unroll
+        for (int k = i + 1; k < 6; ++k) t -= L[k * 6 + i] * x[k];
+        x[i] = t / L[i * 6 + i];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+        if (!isfinite(x[i])) return false;
+    return true;
+}
+
+// ComputeTrustRegionStep + HandleInvalidStep loop: leaves a candidate awaiting evaluation, or
+// terminates (max iterations / min radius).
+__device__ __forceinline__ void compute_step(SolveState& S) {
+    while (true) {
+        if (S.iteration >= kMaxInner) { S.done = 1; S.term = LMSF_TERM_MAX_ITERATIONS; return; }
+        if (S.radius < 1e-32) { S.done = 1; S.term = LMSF_TERM_PARAMETER_TOL; return; }
+        ++S.iteration;
+        double A[36], Hs[36], gs[6], nb[6], step[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            gs[i] = S.g[i] * S.s[i];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int a = i <= j ? hidx(i, j) : hidx(j, i);
+                Hs[i * 6 + j] = S.H[a] * S.s[i] * S.s[j];
+                A[i * 6 + j] = Hs[i * 6 + j];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double dg = fmin(fmax(Hs[i * 6 + i], 1e-6), 1e32);
+            A[i * 6 + i] += dg / S.radius;
+            nb[i] = -gs[i];
+        }
+        const bool ok = chol_solve6(A, nb, step);
+        double mcc = 0.0;
+        if (ok) {
+            double sg = 0.0, sHs = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                sg += step[i] * gs[i];
+                double t = 0.0;
+#pragma unroll
+                for (int j = 0; j < 6; ++j) t += Hs[i * 6 + j] * step[j];
+                sHs += step[i] * t;
+            }
+            mcc = -(sg + 0.5 * sHs);
+        }
+        if (!ok || !(mcc > 0.0)) {  // StepIsInvalid == StepRejected(0)
+            S.radius = S.radius / S.decrease;
+            S.decrease *= 2.0;
+            continue;
+        }
+        double delta[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) delta[i] = step[i] * S.s[i];
+        pose_plus(S.x, delta, S.xc);
+        S.mcc = mcc;
+        S.need_eval = 1;
+        return;
+    }
+}
+
+__device__ void finish_outer(SolveState& S, int outer) {
+    if (outer < kMaxOuter)
+        for (int i = 0; i < 7; ++i) S.trace[outer][i] = S.x[i];
+    S.inner_total += S.iteration;
+    S.evals_total += S.evals;
+    S.outer_run = outer + 1;
+}
+
+
+// lm_step after the evaluation at the candidate (tot = its reduced packet): step acceptance
+// (ParameterToleranceReached, FunctionToleranceReached, IsStepSuccessful, HandleSuccessfulStep /
+// StepRejected) + next step; one thread.
+__device__ __forceinline__ void lm_step_apply(SolveState& S, const double* tot, int outer, int is_last) {
+    S.need_eval = 0;
+    ++S.evals;
+    const double cost_c = isfinite(tot[0]) ? tot[0] : 1.7976931348623157e308;
+    double dx[7];
+    for (int i = 0; i < 7; ++i) dx[i] = S.x[i] - S.xc[i];
+    if (norm7(dx) <= 1e-8 * (S.x_norm + 1e-8)) {
+        S.done = 1;
+        S.term = LMSF_TERM_PARAMETER_TOL;
+    } else {
+        const double cost_change = S.cost - cost_c;
+        if (fabs(cost_change) <= 1e-6 * S.cost) {
+            S.done = 1;
+            S.term = LMSF_TERM_FUNCTION_TOL;
+        } else {
+            const double rel = cost_change / S.mcc;
+            if (rel > 1e-3) {
+                const double f = 1.0 - pow(2.0 * rel - 1.0, 3.0);
+                S.radius = S.radius / fmax(1.0 / 3.0, f);
+                S.radius = fmin(1e16, S.radius);
+                S.decrease = 2.0;
+                for (int i = 0; i < 7; ++i) S.x[i] = S.xc[i];
+                S.x_norm = norm7(S.x);
+                S.cost = cost_c;
+                for (int i = 0; i < 21; ++i) S.H[i] = tot[1 + i];
+                for (int i = 0; i < 6; ++i) S.g[i] = tot[22 + i];
+                if (S.iteration >= kMaxInner) {
+                    S.done = 1;
+                    S.term = LMSF_TERM_MAX_ITERATIONS;
+                } else if (grad_max_norm(S.x, S.g) <= 1e-10) {
+                    S.done = 1;
+                    S.term = LMSF_TERM_GRADIENT_TOL;
+                } else {
+                    compute_step(S);
+                }
+            } else {
+                S.radius = S.radius / S.decrease;
+                S.decrease *= 2.0;
+                compute_step(S);
+            }
+        }
+    }
+    if (is_last) finish_outer(S, outer);
+}
+
+}  // namespace
+}  // namespace lmsf

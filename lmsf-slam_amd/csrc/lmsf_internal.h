@@ -24,6 +24,7 @@ constexpr int kEdgePerRing = 120;    // 20 per sector x 6 sectors (FX:172)
 constexpr int kQSurf = 0x40000000;  // ExtractView::qcode tag of a surf feature
 constexpr int kTile = 2048;          // raw points per ring-split tile
 constexpr int kCounterShards = 64;   // candidate / query counters, 16 u64 (128 B) apart
+constexpr int kMemoWords = 6;        // memo words per search position: 5 neighbour indices + s6
 
 // Dense cell grid over one feature map: cell = floor(coord) - origin, 1 m cells (the match
 // radius: search_thresh_ = 1.0 squared metres, REG/FeatureMatch/FeatureMatchBase.hpp:29).
@@ -82,9 +83,22 @@ struct BatchView {
     int pos_stride;
     const int* fslot;        // [B][feat_stride] edge slots then surf slots, each in ring order (with qslot)
     int write_nn;            // fused search + fit also writes nnp (lmsf_match diagnostics)
-    float4* prevw;           // [B][feat_stride] map-frame query of the slot's last full search (fused path)
-    int memo;                // 1: a query whose float query equals prevw reuses its record (same 5-NN
-                             //    set and fit: both depend only on the float query); outer iterations > 0
+    // Query memo of the fused path (outer iterations > 0 of one solve), indexed by search position i
+    // (fslot order, so one lane per position reads them coalesced):
+    float4* prevw;           // [B][feat_stride] anchor of position i's last full search: map-frame query w0
+                             //   and gap = s6 - s5 (s = distance of the k-th neighbour, the 6th capped at
+                             //   the 1 m radius); w = -1 when fewer than 5 neighbours were found
+    int* memo_nbr;           // [B][kMemoWords][feat_stride] that search's 5 neighbour map indices, nearest
+                             //   first, then s6 (float bits)
+    float* wlim;             // [B][feat_stride] the listed positions' search radius^2 (knn_walk lim)
+    int memo;                // 1: match_memo_kernel ran before match_fit_kernel in this outer iteration
+    int* wl;                 // [B][feat_stride] per block of the memo pass: the positions still needing a search
+    int* wcount;             // [B][feat_stride / 256 + 1] their count per memo block
+    int* n_search;           // [B] positions searched by the last match_fit_kernel (lm_begin's second range)
+    int part2_base;          // packet index of match_fit_kernel's first wave packet (memo pass: [0, ceil(nq/64)))
+    int fused_parts;         // lm_begin: packets laid out by the fused path (memo pass + search ranges)
+    int* ticket;             // [B] lm_eval_step_kernel's per-slot arrival counters (zero between launches)
+    int memo_bound;          // memo misses search within min(1 m, s6 + d) (LMSF_MEMO_BOUND, default 1)
 };
 
 // ---- launchers (each enqueues on `stream`, never synchronises)
@@ -104,7 +118,8 @@ hipError_t launch_knn(const GridView& edge, const GridView& surf, const GridView
 hipError_t launch_fit_eval(const GridView& edge, const GridView& surf, const BatchView& bv, int solver,
                            hipStream_t s);
 hipError_t launch_lm_begin(const BatchView& bv, hipStream_t s);
-hipError_t launch_lm_eval(const BatchView& bv, hipStream_t s);
+// One LM inner iteration: evaluation at the candidate + (last block per slot) step control.
+hipError_t launch_lm_eval_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
 hipError_t launch_lm_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
 hipError_t launch_gn_solve(const BatchView& bv, int outer, hipStream_t s);
 int fit_per_thread_default();
@@ -112,6 +127,7 @@ int fit_per_thread_default();
 // not applicable to this launch (caller runs launch_knn + launch_fit_eval).
 bool match_fit_applies(const GridView& edge2, const GridView& surf2, const BatchView& bv, int solver);
 hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const BatchView& bv, hipStream_t s);
+bool match_fit_prune(const GridView& edge, const GridView& surf);   // dense map: pruned walk, no memo
 bool match_memo_enabled();   // LMSF_MEMO (default 1)
 hipError_t launch_state_init(const BatchView& bv, const double* poses, hipStream_t s);
 // Standalone evaluation at one pose (diagnostics): packet of slot 0 into out29 (device).
