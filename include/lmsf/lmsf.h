@@ -70,6 +70,13 @@ typedef struct {
        behaviour, every point in ring 0, FX:337-341) */
     double beam_lo_deg;
     double beam_spacing_deg;
+    /* Which libm overloads the reference's unqualified sqrt / atan2 calls on float arguments bind to
+       (FX:223-224 atan2(x, y), FX:247-252 sqrt, FX:300-301 sqrt): 0 = the double versions, as on the
+       reference's documented toolchain (README.md:35, ROS kinetic: GCC 5, whose global-scope <math.h>
+       declares only double sqrt / atan2); 1 = the float overloads, as with GCC >= 6 once libstdc++'s
+       <math.h> wrapper is included (it exports std::sqrt(float) / std::atan2(float, float) to the
+       global namespace) -- float atan2 taken as (float)atan2 in double, within glibc atan2f's 1 ulp. */
+    int32_t libm_float;
 } lmsf_config;
 
 /* One correspondence (64 bytes).  kind 0: none, 1: edge (v0 = a, v1 = b: the two line points of
@@ -135,6 +142,7 @@ typedef struct {
     int32_t remove_bad_points;
     double beam_lo_deg;
     double beam_spacing_deg;
+    int32_t libm_float;        /* lmsf_config::libm_float */
 } lmsf_extract_params;
 lmsf_status lmsf_set_extract_params(lmsf_ctx* ctx, const lmsf_extract_params* p);
 

@@ -269,6 +269,7 @@ struct lmsf_ctx {
         e.remove_bad = cfg.remove_bad_points;
         e.beam_lo = cfg.beam_lo_deg;
         e.beam_spacing = cfg.beam_spacing_deg;
+        e.libm_float = cfg.libm_float;
         return e;
     }
 };
@@ -466,6 +467,7 @@ lmsf_status lmsf_config_init(lmsf_config* cfg) {
     cfg->remove_bad_points = 1;
     cfg->beam_lo_deg = 0.0;
     cfg->beam_spacing_deg = 0.0;
+    cfg->libm_float = 0;
     return LMSF_OK;
 }
 
@@ -647,6 +649,7 @@ lmsf_status lmsf_set_extract_params(lmsf_ctx* c, const lmsf_extract_params* p) {
     c->cfg.remove_bad_points = p->remove_bad_points;
     c->cfg.beam_lo_deg = p->beam_lo_deg;
     c->cfg.beam_spacing_deg = p->beam_spacing_deg;
+    c->cfg.libm_float = p->libm_float;
     return LMSF_OK;
 }
 

@@ -27,9 +27,19 @@ namespace lmsf {
 
 namespace {
 
+// The reference's unqualified sqrt / atan2 on float arguments (lmsf_config::libm_float): the double
+// versions, or the float overloads (sqrtf; atan2 in double rounded to float).
+__device__ __forceinline__ double ref_sqrt(float s, int libm_float) {
+    return libm_float ? (double)sqrtf(s) : sqrt((double)s);
+}
+__device__ __forceinline__ double ref_atan2(float y, float x, int libm_float) {
+    const double a = atan2((double)y, (double)x);
+    return libm_float ? (double)(float)a : a;
+}
+
 __device__ __forceinline__ int ring_of(const ExtractView& ev, float4 p) {
     const float s = p.x * p.x + p.y * p.y;                       // float expression (FX:300-301)
-    const double distance = sqrt((double)s);
+    const double distance = ref_sqrt(s, ev.libm_float);
     if (distance > (double)ev.max_d || distance < (double)ev.min_d) return -1;   // FX:302
     const double angle = atan((double)p.z / distance) * 180 / M_PI;              // FX:307
     const bool bad = isnan(angle);   // int(NaN) is INT_MIN on the reference's x86 host
@@ -173,8 +183,8 @@ __device__ void ring_bad_points(const ExtractView& ev, const float4* pts, int si
     if (ev.remove_bad) {
         for (int j = 5 + tid; j <= jmax; j += NT) {
             const float4 a = pts[j], c = pts[j + 1];
-            const double angle_curr = atan2((double)a.x, (double)a.y);
-            const double angle_after = atan2((double)c.x, (double)c.y);
+            const double angle_curr = ref_atan2(a.x, a.y, ev.libm_float);   // atan2(x, y) order (FX:223-224)
+            const double angle_after = ref_atan2(c.x, c.y, ev.libm_float);
             double delta_angle = fabs(angle_curr - angle_after);
             if (delta_angle > M_PI) delta_angle = M_PI * 2 - delta_angle;
             uint8_t e = 0;
@@ -183,7 +193,7 @@ __device__ void ring_bad_points(const ExtractView& ev, const float4* pts, int si
             } else {
                 const float sc = a.x * a.x + a.y * a.y + a.z * a.z;
                 const float sa = c.x * c.x + c.y * c.y + c.z * c.z;
-                const double dc = sqrt((double)sc), da = sqrt((double)sa);
+                const double dc = ref_sqrt(sc, ev.libm_float), da = ref_sqrt(sa, ev.libm_float);
                 const double ang = dc < da ? atan2(dc * delta_angle, da - dc) : atan2(da * delta_angle, dc - da);
                 if (ang <= 0.17) e = dc < da ? 2 : 3;
             }

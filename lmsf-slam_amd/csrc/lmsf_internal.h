@@ -168,6 +168,7 @@ struct ExtractView {
     float min_d, max_d, edge_thresh;
     int remove_bad;
     double beam_lo, beam_spacing;
+    int libm_float;              // lmsf_config::libm_float
 };
 hipError_t launch_extract(const ExtractView& ev, hipStream_t s);
 

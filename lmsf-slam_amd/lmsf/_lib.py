@@ -31,7 +31,7 @@ class Config(C.Structure):
                 ("max_iterations", C.c_int32), ("max_batch", C.c_int32), ("max_scan_points", C.c_int32),
                 ("max_features", C.c_int32), ("n_scans", C.c_int32), ("min_distance", C.c_float),
                 ("max_distance", C.c_float), ("edge_threshold", C.c_float), ("remove_bad_points", C.c_int32),
-                ("beam_lo_deg", C.c_double), ("beam_spacing_deg", C.c_double)]
+                ("beam_lo_deg", C.c_double), ("beam_spacing_deg", C.c_double), ("libm_float", C.c_int32)]
 
 
 class SolveStats(C.Structure):
@@ -55,7 +55,7 @@ class KernelStats(C.Structure):
 class ExtractParams(C.Structure):
     _fields_ = [("n_scans", C.c_int32), ("min_distance", C.c_float), ("max_distance", C.c_float),
                 ("edge_threshold", C.c_float), ("remove_bad_points", C.c_int32), ("beam_lo_deg", C.c_double),
-                ("beam_spacing_deg", C.c_double)]
+                ("beam_spacing_deg", C.c_double), ("libm_float", C.c_int32)]
 
 
 class CommonParams(C.Structure):
@@ -237,7 +237,7 @@ class Context:
         unspecified fields keep the context's current values."""
         c = self.cfg
         p = ExtractParams(c.n_scans, c.min_distance, c.max_distance, c.edge_threshold, c.remove_bad_points,
-                          c.beam_lo_deg, c.beam_spacing_deg)
+                          c.beam_lo_deg, c.beam_spacing_deg, c.libm_float)
         for k, v in kw.items():
             setattr(p, k, v)
         self._check(load().lmsf_set_extract_params(self.h, C.byref(p)))

@@ -3,8 +3,10 @@
 // Algorithm/PointClouds/processing/FeatureExtract/).  Parity vs the reference: unpinned
 // (see lmsf_oracle.h).  Arithmetic follows the reference's C++ evaluation rules literally:
 // PointXYZI members are float, so `x*x + y*y` and the 11-point curvature sums are float
-// expressions that are only widened to double on assignment; math.h sqrt/atan/atan2 are the
-// double versions.
+// expressions that are only widened to double on assignment.  Unqualified sqrt / atan2 on float
+// arguments bind to the double versions on the reference's toolchain (ROS kinetic, GCC 5) and to the
+// float overloads with GCC >= 6 when libstdc++'s <math.h> wrapper is in scope: prm.libm_float picks
+// (float atan2 as the double atan2 rounded to float, within glibc atan2f's 1 ulp).
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -18,10 +20,16 @@ namespace {
 
 struct P4 { float x, y, z, i; };
 
+double ref_sqrt(float s, int libm_float) { return libm_float ? (double)std::sqrt(s) : std::sqrt((double)s); }
+double ref_atan2(float y, float x, int libm_float) {
+    const double a = std::atan2((double)y, (double)x);
+    return libm_float ? (double)(float)a : a;
+}
+
 // splitScan ring assignment (FX:290-343).  Returns -1 for rejected points.
 int ring_of(const lmsfo_extract_params& prm, const P4& p) {
     float s = p.x * p.x + p.y * p.y;                 // float expression (FX:300-301)
-    double distance = std::sqrt((double)s);
+    double distance = ref_sqrt(s, prm.libm_float);
     if (distance > (double)prm.max_distance || distance < (double)prm.min_distance) return -1;  // FX:302
     double angle = std::atan((double)p.z / distance) * 180 / M_PI;                               // FX:307
     int n = prm.n_scans;
@@ -49,11 +57,11 @@ int ring_of(const lmsfo_extract_params& prm, const P4& p) {
 }
 
 // checkBadEdgePoint (FX:216-282).
-void check_bad(const std::vector<P4>& pc, std::vector<int>& dis) {
+void check_bad(const std::vector<P4>& pc, std::vector<int>& dis, int libm_float) {
     int scan_num = (int)pc.size();
     for (int j = 5; j < scan_num - 6; j++) {
-        double angle_curr = std::atan2((double)pc[j].x, (double)pc[j].y);        // atan2(x, y) order
-        double angle_after = std::atan2((double)pc[j + 1].x, (double)pc[j + 1].y);
+        double angle_curr = ref_atan2(pc[j].x, pc[j].y, libm_float);        // atan2(x, y) order
+        double angle_after = ref_atan2(pc[j + 1].x, pc[j + 1].y, libm_float);
         double delta_angle = std::fabs(angle_curr - angle_after);
         if (delta_angle > M_PI) delta_angle = M_PI * 2 - delta_angle;
         if (delta_angle > 0.0175) {
@@ -63,8 +71,8 @@ void check_bad(const std::vector<P4>& pc, std::vector<int>& dis) {
         }
         float sc = pc[j].x * pc[j].x + pc[j].y * pc[j].y + pc[j].z * pc[j].z;
         float sa = pc[j + 1].x * pc[j + 1].x + pc[j + 1].y * pc[j + 1].y + pc[j + 1].z * pc[j + 1].z;
-        double distance_curr = std::sqrt((double)sc);
-        double distance_after = std::sqrt((double)sa);
+        double distance_curr = ref_sqrt(sc, libm_float);
+        double distance_after = ref_sqrt(sa, libm_float);
         double angle;
         if (distance_curr < distance_after)
             angle = std::atan2(distance_curr * delta_angle, distance_after - distance_curr);
@@ -93,7 +101,7 @@ void process_ring(const lmsfo_extract_params& prm, const std::vector<P4>& pc, co
     if (total_points < 6) return;
     int sector_length = (int)((total_points / 6) + 0.5);     // integer division first (FX:74)
     std::vector<int> dis(size, 0), is_edge(size, 0);
-    if (prm.remove_bad_points) check_bad(pc, dis);
+    if (prm.remove_bad_points) check_bad(pc, dis, prm.libm_float);
     const double thresh = (double)prm.edge_threshold;
     std::vector<Curv> cc;
     cc.reserve(total_points);

@@ -48,6 +48,7 @@ typedef struct {
      * LOAMFeatureProcessor_base.hpp:337-341). */
     double beam_lo_deg;
     double beam_spacing_deg;
+    int32_t libm_float;      /* 0: double sqrt / atan2 (GCC 5, kinetic), 1: float overloads (see lmsf.h) */
 } lmsfo_extract_params;
 
 /* LOAMFeatureProcessorBase::Process (FX/LOAMFeatureProcessor_base.hpp:59-126).

@@ -24,7 +24,7 @@ assert RECORD_DTYPE.itemsize == 64
 class ExtractParams(C.Structure):
     _fields_ = [("n_scans", C.c_int32), ("min_distance", C.c_float), ("max_distance", C.c_float),
                 ("edge_threshold", C.c_float), ("remove_bad_points", C.c_int32),
-                ("beam_lo_deg", C.c_double), ("beam_spacing_deg", C.c_double)]
+                ("beam_lo_deg", C.c_double), ("beam_spacing_deg", C.c_double), ("libm_float", C.c_int32)]
 
 
 class SolveStats(C.Structure):
@@ -122,12 +122,12 @@ def _f32(a):
 
 
 def extract(points, n_scans=16, min_distance=2.0, max_distance=80.0, edge_threshold=1.0,
-            remove_bad_points=True, beam_lo_deg=0.0, beam_spacing_deg=0.0):
+            remove_bad_points=True, beam_lo_deg=0.0, beam_spacing_deg=0.0, libm_float=False):
     """LOAMFeatureProcessorBase::Process -> (edge xyzi, surf xyzi, edge src idx, surf src idx)."""
     pts = _f32(points)
     n = pts.shape[0]
     prm = ExtractParams(n_scans, min_distance, max_distance, edge_threshold, int(remove_bad_points),
-                        beam_lo_deg, beam_spacing_deg)
+                        beam_lo_deg, beam_spacing_deg, int(libm_float))
     cap = max(n, 1)
     e = np.empty((cap, 4), np.float32)
     s = np.empty((cap, 4), np.float32)

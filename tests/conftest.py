@@ -87,3 +87,19 @@ def mat_err(A, B):
 def pose_err(a, b):
     from lmsf import synth
     return synth.pose_delta(a, b)
+
+
+def libm_probe_scan():
+    """A 16-ring VLP-16 cylinder (r = 20 m, 1800 columns) with one extra point at index 900 whose
+    x*x + y*y is 6400 + 2^-11 in float: inside max_distance 80 with the float sqrt overload, outside
+    with the double one (lmsf_config::libm_float)."""
+    from lmsf import synth
+    rng = np.random.default_rng(3)
+    az = np.linspace(0, 2 * np.pi, 1800, endpoint=False)
+    rows = []
+    for el in synth.VLP16_FIRING_DEG:
+        r = 20.0 + rng.normal(0, 0.05, az.size)
+        rows.append(np.stack([r * np.cos(az), r * np.sin(az), r * np.tan(np.radians(el)), rng.random(az.size)], 1))
+    scan = np.concatenate(rows, 0).astype(np.float32)
+    odd = np.array([[80.0, 0.0221, 80.0 * np.tan(np.radians(-15.0)), 0.5]], np.float32)
+    return np.concatenate([scan[:900], odd, scan[900:]], 0)

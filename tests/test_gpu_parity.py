@@ -56,6 +56,8 @@ def test_extract_bitexact(lib, oracle_mod, small_workload):
     (128, 512, dict(beam_lo_deg=-25.0, beam_spacing_deg=40.0 / 127)),
     (16, 1800, dict(remove_bad_points=0)),
     (16, 1800, dict(edge_threshold=0.1, min_distance=1.0, max_distance=50.0)),
+    (16, 4096, dict(libm_float=1)),
+    (64, 1024, dict(libm_float=1)),
 ])
 def test_extract_variants_bitexact(lib, oracle_mod, small_workload, n_scans, cols, kw):
     from lmsf import synth
@@ -72,6 +74,23 @@ def test_extract_variants_bitexact(lib, oracle_mod, small_workload, n_scans, col
     okw.update(kw)
     e, s, ei, si = oracle_mod.extract(scan, **okw)
     ctx = _ctx(lib, n_scans=n_scans, **kw)
+    ctx.extract(scan)
+    ge, gei = ctx.copy_features(lib.EDGE)
+    gs, gsi = ctx.copy_features(lib.SURF)
+    np.testing.assert_array_equal(gei, ei)
+    np.testing.assert_array_equal(gsi, si)
+    assert ge.tobytes() == e.tobytes() and gs.tobytes() == s.tobytes()
+
+
+@pytest.mark.parametrize("libm_float", [0, 1])
+def test_extract_libm_overload_bitexact(lib, oracle_mod, libm_float):
+    """The device takes the reference's sqrt / atan2 overload decision exactly as the oracle does on a
+    point that the two choices keep / reject (conftest.libm_probe_scan)."""
+    from conftest import libm_probe_scan
+    scan = libm_probe_scan()
+    e, s, ei, si = oracle_mod.extract(scan, libm_float=bool(libm_float))
+    assert (900 in set(ei) | set(si)) == bool(libm_float)
+    ctx = _ctx(lib, libm_float=libm_float)
     ctx.extract(scan)
     ge, gei = ctx.copy_features(lib.EDGE)
     gs, gsi = ctx.copy_features(lib.SURF)

@@ -376,3 +376,20 @@ def test_oracle_ingest_pointcloud2(oracle_mod, tiny):
     d = np.sqrt((v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1] + v[:, 2] * v[:, 2]).astype(np.float32)).astype(np.float64)
     assert dist.tobytes() == v[(d > near) & (d < far)].tobytes()
     assert len(oracle_mod.ingest(msg[:0], 0)) == 0
+
+
+def test_oracle_libm_overload_choice(oracle_mod):
+    """libm_float selects which overloads the reference's unqualified sqrt / atan2 on float arguments bind
+    to (FX:223-224, :247-252, :300-301; lmsf_config::libm_float).  A point with x*x + y*y = 6400 + 2^-11 in
+    float: sqrt in double is 80.000003 > max_distance 80 (rejected, GCC 5 / kinetic), sqrtf rounds to
+    80.0f (kept, GCC >= 6 with <math.h>) -- the two toolchains extract different features."""
+    from conftest import libm_probe_scan
+    scan = libm_probe_scan()
+    x, y = np.float32(80.0), np.float32(0.0221)
+    s = np.float32(x * x) + np.float32(y * y)
+    assert s == np.float32(6400.0 + 2.0 ** -11)
+    assert np.sqrt(np.float64(s)) > 80.0 and np.sqrt(s) == np.float32(80.0)
+    e0, s0, ei0, si0 = oracle_mod.extract(scan)
+    e1, s1, ei1, si1 = oracle_mod.extract(scan, libm_float=True)
+    assert 900 not in set(ei0) | set(si0)                    # double sqrt: out of range
+    assert 900 in set(ei1) | set(si1)                        # float sqrt: kept, becomes a feature
