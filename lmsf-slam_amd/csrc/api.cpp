@@ -114,7 +114,6 @@ struct lmsf_ctx {
     float* wlim = nullptr;            // [B][F] their search radii^2
     int* wcount = nullptr;            // [B][F / 256 + 1] their counts
     int* n_search = nullptr;          // [B] positions searched by the last fused launch
-    int* ticket = nullptr;            // [B] LM evaluation arrival counters
     float4* rec_p = nullptr;          // records: point + kind / values / edge tail (BatchView)
     RecV* rec_v = nullptr;
     double2* rec_e = nullptr;
@@ -205,7 +204,6 @@ struct lmsf_ctx {
         v.memo_nbr = memo_nbr;
         v.wl = wl;
         v.wlim = wlim;
-        v.ticket = ticket;
         v.memo_bound = memo_bound_enabled() ? 1 : 0;
         v.wcount = wcount;
         v.n_search = n_search;
@@ -390,9 +388,12 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
             bvo.memo = o > 0 && !c->count27 && match_memo_enabled() ? 1 : 0;   // within one solve only
             HIPCHK(c, launch_match_fit(ge, gs, bvo, s));
         }
-        else
+        else {   // single-scan launches: the 8-lane search, with the slot memo under the Ceres-LM solver
+            BatchView bvk = bv;
+            bvk.memo = !gn && o > 0 && !c->count27 && match_memo_enabled() ? 1 : 0;
             HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{},
-                                 bv, gn ? 1 : 0, s));
+                                 bvk, gn ? 1 : 0, s, !gn && match_memo_enabled()));
+        }
         if (t) {
             HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 1], s));
             c->ev_used += 2;
@@ -482,7 +483,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
             hipFree(m.scan_tmp);
         }
     }
-    void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->prevw, c->memo_nbr, c->wl, c->wlim, c->wcount, c->n_search, c->ticket, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
+    void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->prevw, c->memo_nbr, c->wl, c->wlim, c->wcount, c->n_search, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->sort_key,
                     c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->n_pos, c->d_error};
@@ -548,8 +549,6 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->wlim, B * F));
     CHK(dalloc(&c->wcount, B * (F / 256 + 1)));
     CHK(dalloc(&c->n_search, B));
-    CHK(dalloc(&c->ticket, B));
-    CHK(hipMemset(c->ticket, 0, B * sizeof(int)));
     CHK(dalloc(&c->rec_p, B * F));
     CHK(dalloc(&c->rec_v, B * F));
     CHK(dalloc(&c->rec_e, B * F));

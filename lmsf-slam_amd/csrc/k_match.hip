@@ -359,14 +359,36 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
 // TWO: the map of a kind is split into a static grid (a shared prior map, indices [0, P)) and a
 // dynamic grid (the keyframe window, indices P + j): 18 rows, positions tagged with the grid bit.
 // Keys carry global indices, so the result equals the search of the concatenation [prior | window].
-template <int T, bool TWO, bool PRUNE>
+constexpr float kFullLim = 1.0f + 1e-5f;   // knn_walk's squared radius for the 1 m match radius (+ margin)
+
+// Key of map point m (caller-order index idx) for the query w: the expression of knn_walk's consider().
+__device__ __forceinline__ double nn_key(const float3 w, const float4 m, uint32_t idx) {
+    const float dx = w.x - m.x, dy = w.y - m.y, dz = w.z - m.z;
+    const float d2 = dx * dx + dy * dy + dz * dz;
+    return key_as_double(((uint64_t)(__float_as_uint(d2) + kKeyBias) << 32) | idx);
+}
+
+__device__ __forceinline__ void key_cswap(double& a, double& b) {
+    const double lo = fmin(a, b);
+    b = fmax(a, b);
+    a = lo;
+}
+
+// MEMO (single-scan Ceres-LM launches on sparse maps, T > 1): the team keeps the 6th-nearest key and
+// leaves the slot's anchor (w, s6 - s5, s6) beside its 5 neighbour points in nnp; in outer iterations
+// > 0 (bv.memo) a query that moved d < (s6 - s5) / 2 still has the same 5 nearest, whose keys are
+// recomputed from nnp (points + indices) and sorted: when the order is unchanged nnp already holds this
+// search's answer and the walk is skipped (fit_eval refits from it); otherwise the walk covers only
+// min(1 m, s6 + d) (match_memo_kernel's argument, DESIGN.md "Query memo").
+template <int T, bool TWO, bool PRUNE, bool MEMO = false>
 __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, GridView ge2, GridView gs2, BatchView bv,
                                                   int skip_converged, int gx, int remap) {
+    constexpr int NK = MEMO ? 6 : 5;
     __shared__ unsigned long long blk_n27;
-    __shared__ unsigned int blk_q;
+    __shared__ unsigned int blk_q, blk_r;
     int bx, b;
     block_coords(remap, gx, bx, b);
-    if (threadIdx.x == 0) { blk_n27 = 0; blk_q = 0; }
+    if (threadIdx.x == 0) { blk_n27 = 0; blk_q = 0; blk_r = 0; }
     __syncthreads();
     const int ne = bv.n_edge[b], ns = bv.n_surf[b];
     const int team = threadIdx.x / T, lane = threadIdx.x % T;
@@ -387,45 +409,90 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
         const GridView g = pick_grid(is_edge, ge, gs);
         const GridView g2 = pick_grid(is_edge, ge2, gs2);
         const Pose P = load_pose(bv.st[b].x);
-        const float4 p = bv.feat[(size_t)b * bv.feat_stride + q];
+        const size_t slot = (size_t)b * bv.feat_stride + q;
+        const float4 p = bv.feat[slot];
         const float3 w = associate(P, p);
-        const double sentinel = key_as_double(kSentinel);
-        double k[5] = {sentinel, sentinel, sentinel, sentinel, sentinel};   // ascending kept keys
-        unsigned int c27 = 0;
-        knn_walk<T, TWO, PRUNE>(g, g2, w, lane, bv.count27, k, c27);
-        // merge: five rounds of team-min; the owning lane pops its head (keys are unique)
-        double res[5];
+        float4* nn_out = bv.nnp + slot * 5;
+        bool reuse = false;
+        float lim = kFullLim;
+        if (MEMO && bv.memo) {   // every lane of the team decides alike (same loads, same arithmetic)
+            const float4 pw = bv.prevw[slot];
+            if (pw.w > 0.f) {
+                const double dx = (double)w.x - pw.x, dy = (double)w.y - pw.y, dz = (double)w.z - pw.z;
+                const double dd = sqrt(dx * dx + dy * dy + dz * dz);
+                const double r6 = (double)__int_as_float(bv.memo_nbr[((size_t)b * kMemoWords + 5) * bv.feat_stride + q]) +
+                                  dd + 1e-5;
+                if (r6 < 1.0 && bv.memo_bound) lim = fminf(kFullLim, (float)(r6 * r6) + 1e-5f);
+                if (2.0 * dd + 1e-5 < (double)pw.w) {
+                    double k5[5];
+                    uint32_t idx[5];
 #pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            double mn = k[0];
+                    for (int j = 0; j < 5; ++j) {
+                        const float4 m = nn_out[j];
+                        idx[j] = (uint32_t)__float_as_int(m.w);
+                        k5[j] = nn_key(w, m, idx[j]);
+                    }
+                    key_cswap(k5[0], k5[1]); key_cswap(k5[3], k5[4]); key_cswap(k5[2], k5[4]);
+                    key_cswap(k5[2], k5[3]); key_cswap(k5[0], k5[3]); key_cswap(k5[0], k5[2]);
+                    key_cswap(k5[1], k5[4]); key_cswap(k5[1], k5[3]); key_cswap(k5[1], k5[2]);
+                    reuse = key_bits(k5[4]) < kSentinel;
 #pragma unroll
-            for (int o = T / 2; o >= 1; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o, T));
-            res[i] = mn;
-            if (key_bits(k[0]) == key_bits(mn)) {
-                k[0] = k[1]; k[1] = k[2]; k[2] = k[3]; k[3] = k[4]; k[4] = sentinel;
+                    for (int j = 0; j < 5; ++j) reuse = reuse && (uint32_t)key_bits(k5[j]) == idx[j];
+                }
             }
         }
-        // every rank written (lane i % T writes rank i; teams smaller than 5 write several): the
-        // neighbour point (from the caller-order copy, w = its map index), so the fit reads 80
-        // contiguous bytes.  Indices below g.n belong to g, the rest to g2 (its points carry P + j).
-        float4* nn_out = bv.nnp + ((size_t)b * bv.feat_stride + q) * 5;
+        unsigned int c27 = 0;
+        if (!reuse) {
+            const double sentinel = key_as_double(kSentinel);
+            double k[NK];   // ascending kept keys
 #pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            if (i % T == lane) {
-                float4 o = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-                const uint64_t kb = key_bits(res[i]);
-                if (kb < kSentinel) {
-                    const uint32_t idx = (uint32_t)kb;
-                    const bool second = TWO && idx >= (uint32_t)g.n;
-                    const float4 p = second ? g2.orig[idx - (uint32_t)g.n] : g.orig[idx];
-                    o = make_float4(p.x, p.y, p.z, __int_as_float((int)idx));
+            for (int j = 0; j < NK; ++j) k[j] = sentinel;
+            knn_walk<T, TWO, PRUNE, kKnnUnroll, NK>(g, g2, w, lane, bv.count27, k, c27, lim);
+            // merge: NK rounds of team-min; the owning lane pops its head (keys are unique)
+            double res[NK];
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                double mn = k[0];
+#pragma unroll
+                for (int o = T / 2; o >= 1; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o, T));
+                res[i] = mn;
+                if (key_bits(k[0]) == key_bits(mn)) {
+#pragma unroll
+                    for (int j = 0; j + 1 < NK; ++j) k[j] = k[j + 1];
+                    k[NK - 1] = sentinel;
                 }
-                nn_out[i] = o;
+            }
+            // every rank written (lane i % T writes rank i; teams smaller than 5 write several): the
+            // neighbour point (from the caller-order copy, w = its map index), so the fit reads 80
+            // contiguous bytes.  Indices below g.n belong to g, the rest to g2 (its points carry P + j).
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                if (i % T == lane) {
+                    float4 o = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+                    const uint64_t kb = key_bits(res[i]);
+                    if (kb < kSentinel) {
+                        const uint32_t idx = (uint32_t)kb;
+                        const bool second = TWO && idx >= (uint32_t)g.n;
+                        const float4 m = second ? g2.orig[idx - (uint32_t)g.n] : g.orig[idx];
+                        o = make_float4(m.x, m.y, m.z, __int_as_float((int)idx));
+                    }
+                    nn_out[i] = o;
+                }
+            }
+            if (MEMO && lane == 0) {   // the anchor of this full search
+                float gap = -1.f;
+                if (key_bits(res[4]) < kSentinel) {
+                    const double s6 = sqrt((double)fminf(key_d2(res[NK - 1]), 1.0f));
+                    gap = (float)(s6 - sqrt((double)key_d2(res[4])));
+                    bv.memo_nbr[((size_t)b * kMemoWords + 5) * bv.feat_stride + q] = __float_as_int((float)s6);
+                }
+                bv.prevw[slot] = make_float4(w.x, w.y, w.z, gap);
             }
         }
         if (bv.n27) {
             if (c27) atomicAdd(&blk_n27, (unsigned long long)c27);
             if (lane == 0) atomicAdd(&blk_q, 1u);
+            if (lane == 0 && reuse) atomicAdd(&blk_r, 1u);
         }
     }
     __syncthreads();
@@ -434,6 +501,7 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
         unsigned long long* shard = bv.n27 + (size_t)(blockIdx.x & (kCounterShards - 1)) * 16;
         atomicAdd(shard, blk_n27);
         atomicAdd(shard + 1, (unsigned long long)blk_q);
+        if (blk_r) atomicAdd(shard + 2, (unsigned long long)blk_r);
     }
 }
 
@@ -517,11 +585,7 @@ __device__ __forceinline__ void butterfly_step(double* P, int lane) {
     }
 }
 
-typedef __attribute__((address_space(1))) unsigned int gu32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-
-// sc1: the packet is stored write-through (8-B agent-scope atomic stores) for a hand-off inside the launch.
-__device__ __forceinline__ void block_reduce_packet(double* P, double* out, bool sc1 = false) {
+__device__ __forceinline__ void block_reduce_packet(double* P, double* out) {
     static_assert(kPacket == 32, "butterfly over 32 entries");
     __shared__ double red[4][kPacket];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -535,12 +599,7 @@ __device__ __forceinline__ void block_reduce_packet(double* P, double* out, bool
     __syncthreads();
     if (threadIdx.x < kPacket) {
         const int i = threadIdx.x;
-        const double v = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
-        if (sc1)
-            __hip_atomic_store((gu64*)(out + i), (unsigned long long)__double_as_longlong(v),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-            out[i] = v;
+        out[i] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
     }
 }
 
@@ -716,21 +775,6 @@ __device__ __forceinline__ void record_packet(int kind, const float4 p, const d3
     }
     P[29] += kind == LMSF_EDGE ? 1.0 : 0.0;
     P[30] += kind == LMSF_SURF ? 1.0 : 0.0;
-}
-
-constexpr float kFullLim = 1.0f + 1e-5f;   // knn_walk's squared radius for the 1 m match radius (+ margin)
-
-// Key of map point m (caller-order index idx) for the query w: the expression of knn_walk's consider().
-__device__ __forceinline__ double nn_key(const float3 w, const float4 m, uint32_t idx) {
-    const float dx = w.x - m.x, dy = w.y - m.y, dz = w.z - m.z;
-    const float d2 = dx * dx + dy * dy + dz * dz;
-    return key_as_double(((uint64_t)(__float_as_uint(d2) + kKeyBias) << 32) | idx);
-}
-
-__device__ __forceinline__ void key_cswap(double& a, double& b) {
-    const double lo = fmin(a, b);
-    b = fmax(a, b);
-    a = lo;
 }
 
 // Entries of one memo block's work list per scan: wcount stride.
@@ -1020,84 +1064,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     }
 }
 
-#ifndef LMSF_EVAL_WAVES
-#define LMSF_EVAL_WAVES 4
-#endif
-// One Ceres LM inner iteration per launch: every record's residual + Jacobian at the candidate pose
-// (Ceres re-evaluates the same residual blocks at every trial point), a packet per block, and -- in
-// the last block of the slot to finish (an agent-scope ticket per slot, the blocks' packet stores
-// released before it and acquired after it) -- the fixed-order packet reduction and the step
-// acceptance / next step (lm_step_apply): one launch where an evaluation kernel and a 64-lane step
-// kernel ran before.  kEvalPerThread records per thread.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_EVAL_WAVES))) void lm_eval_step_kernel(BatchView bv, int outer, int is_last) {
-    const int b = blockIdx.y;
-    SolveState& S = bv.st[b];
-    if (!S.need_eval) {   // solver finished: only the outer iteration's trace row, once per slot
-        if (is_last && blockIdx.x == 0 && threadIdx.x == 0) finish_outer(S, outer);
-        return;
-    }
-    const int nq = bv.n_edge[b] + bv.n_surf[b];
-    if (blockIdx.x * kEvalBlock >= nq) return;
-    const Pose Ps = load_pose(S.xc);
-    double P[kPacket];
-#pragma unroll
-    for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
-    // every record's point and value loads issued before the first use (the value array is read
-    // whatever the kind: an unmatched slot's stale values are loaded but never used)
-    float4 rp[kEvalPerThread];
-    RecV rv[kEvalPerThread];
-#pragma unroll
-    for (int k = 0; k < kEvalPerThread; ++k) {
-        const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
-        const size_t slot = (size_t)b * bv.feat_stride + (q < nq ? q : 0);
-        rp[k] = bv.rec_p[slot];
-        rv[k] = bv.rec_v[slot];
-    }
-#pragma unroll
-    for (int k = 0; k < kEvalPerThread; ++k) {
-        const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
-        const int kind = __float_as_int(rp[k].w);
-        if (q < nq && kind != 0) {
-            double J[6], res;
-            const d3 pp = mk((double)rp[k].x, (double)rp[k].y, (double)rp[k].z);
-            const RecV& v = rv[k];
-            if (kind == LMSF_EDGE) {
-                const double2 e = bv.rec_e[(size_t)b * bv.feat_stride + q];
-                res = edge_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), mk(v.v[3], e.x, e.y), J);
-            } else {
-                res = surf_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), v.v[3], J);
-            }
-            huber_accumulate(P, res, J);
-        }
-    }
-    // Hand-off to the slot's last block (cdna_hip_programming.md Guideline 16, R1): the packet is stored
-    // write-through (sc1: 8-B agent-scope atomic stores, no L2 write-back fence), the storing wave drains
-    // it, then after the barrier ONE lane adds to the slot's ticket; the block whose add returns the last
-    // count acquires once (this CU's L1) and reads every packet with plain loads.
-    block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + blockIdx.x) * kPacket, true);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __shared__ int last;
-    const int nblk = (nq + kEvalBlock - 1) / kEvalBlock;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        gu32* tk = (gu32*)(bv.ticket + b);
-        const unsigned t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = t == (unsigned)(nblk - 1);
-        if (last) {
-            __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every block's packet, fresh
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-    __syncthreads();
-    if (!last) return;
-    double tot[kPacket];
-    reduce_parts(bv, b, nblk, tot);
-    if (threadIdx.x == 0) lm_step_apply(S, tot, outer, is_last);
-}
-
-// The same evaluation without the hand-off (LMSF_LM_FUSED=0, A/B): one packet per block; the step
-// runs in lm_step_kernel (k_solver.hip).
+// LM candidate evaluation over the fixed correspondences (Ceres re-evaluates the same residual blocks
+// at every trial point): one packet per block; the step runs in lm_step_kernel (k_solver.hip).
+// kEvalPerThread records per thread.  (Fusing the step into the last block to finish, behind an
+// agent-scope ticket with sc1 packet stores, measured slower in r02 on C2 / C3 / C4 -- 20.9k vs 22.1k
+// scans/s, 1.95 vs 1.73 ms per C3 frame, 2.12 vs 2.05 ms per C4 scan: the step code capped the
+// kernel at 128 VGPRs and its serial step lands on the launch's tail -- and was removed.)
 __global__ __launch_bounds__(256) void lm_eval_kernel(BatchView bv) {
     const int b = blockIdx.y;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
@@ -1178,11 +1150,16 @@ static int knn_remap() {
 }
 
 template <bool TWO>
-static void launch_knn_t(int T, bool prune, dim3 grid, const GridView& edge, const GridView& surf, const GridView& edge2,
-                         const GridView& surf2, const BatchView& bv, int skip_converged, int gx, int remap,
-                         hipStream_t s) {
+static void launch_knn_t(int T, bool prune, bool memo, dim3 grid, const GridView& edge, const GridView& surf,
+                         const GridView& edge2, const GridView& surf2, const BatchView& bv, int skip_converged, int gx,
+                         int remap, hipStream_t s) {
 #define LMSF_KNN(TT, PP) hipLaunchKernelGGL((knn_kernel<TT, TWO, PP>), grid, dim3(256), 0, s, edge, surf, edge2, surf2, bv, \
                                             skip_converged, gx, remap)
+    if (memo && T == 8) {   // the team walk never prunes
+        hipLaunchKernelGGL((knn_kernel<8, TWO, false, true>), grid, dim3(256), 0, s, edge, surf, edge2, surf2, bv,
+                           skip_converged, gx, remap);
+        return;
+    }
     switch (T) {
         case 1:
             if (prune)
@@ -1200,7 +1177,7 @@ static void launch_knn_t(int T, bool prune, dim3 grid, const GridView& edge, con
 }
 
 hipError_t launch_knn(const GridView& edge, const GridView& surf, const GridView& edge2, const GridView& surf2,
-                      const BatchView& bv, int skip_converged, hipStream_t s) {
+                      const BatchView& bv, int skip_converged, hipStream_t s, bool memo) {
     const int T = knn_team((size_t)bv.feat_stride * bv.B), remap = knn_remap();
     const int span = (bv.qslot && bv.pos_stride > bv.feat_stride) ? bv.pos_stride : bv.feat_stride;
     const int gx = (span + (256 / T) - 1) / (256 / T);
@@ -1208,9 +1185,9 @@ hipError_t launch_knn(const GridView& edge, const GridView& surf, const GridView
     // the pruned walk when a searched grid is dense (first-pass radius below the match radius)
     const bool prune = (edge.n > 0 && edge.lim1 < 1.f) || (surf.n > 0 && surf.lim1 < 1.f);
     if (edge2.n > 0 || surf2.n > 0)
-        launch_knn_t<true>(T, prune, grid, edge, surf, edge2, surf2, bv, skip_converged, gx, remap, s);
+        launch_knn_t<true>(T, prune, memo, grid, edge, surf, edge2, surf2, bv, skip_converged, gx, remap, s);
     else
-        launch_knn_t<false>(T, prune, grid, edge, surf, edge2, surf2, bv, skip_converged, gx, remap, s);
+        launch_knn_t<false>(T, prune, memo, grid, edge, surf, edge2, surf2, bv, skip_converged, gx, remap, s);
     return hipGetLastError();
 }
 
@@ -1280,24 +1257,8 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
     return hipGetLastError();
 }
 
-// LMSF_LM_FUSED = 0 | 1 (A/B, default 0): the evaluation and the step in one launch (ticket hand-off)
-// or two.  Measured (r02, C2 default bench, one process): fused 20.9k / 20.8k scans/s, two launches
-// 22.1k -- the step code caps the fused kernel at 128 VGPRs (spilling only on the last-block path),
-// and its serial step lands on the launch's tail instead of a 64-lane kernel of its own.
-static bool lm_fused() {
-    static bool v = [] {
-        const char* e = getenv("LMSF_LM_FUSED");
-        return e ? atoi(e) != 0 : false;
-    }();
-    return v;
-}
-
 hipError_t launch_lm_eval_step(const BatchView& bv, int outer, int is_last, hipStream_t s) {
     dim3 grid((bv.feat_stride + kEvalBlock - 1) / kEvalBlock, bv.B);
-    if (lm_fused()) {
-        hipLaunchKernelGGL(lm_eval_step_kernel, grid, dim3(256), 0, s, bv, outer, is_last);
-        return hipGetLastError();
-    }
     hipLaunchKernelGGL(lm_eval_kernel, grid, dim3(256), 0, s, bv);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -97,7 +97,6 @@ struct BatchView {
     int* n_search;           // [B] positions searched by the last match_fit_kernel (lm_begin's second range)
     int part2_base;          // packet index of match_fit_kernel's first wave packet (memo pass: [0, ceil(nq/64)))
     int fused_parts;         // lm_begin: packets laid out by the fused path (memo pass + search ranges)
-    int* ticket;             // [B] lm_eval_step_kernel's per-slot arrival counters (zero between launches)
     int memo_bound;          // memo misses search within min(1 m, s6 + d) (LMSF_MEMO_BOUND, default 1)
 };
 
@@ -113,12 +112,13 @@ hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, void*
 
 // edge2 / surf2: optional second grid per kind (n = 0: none), searched as if concatenated after
 // the first (its points carry global indices).
+// memo: keep the per-slot anchors (and, with bv.memo, reuse unchanged 5-NN sets) -- 8-lane sparse launches.
 hipError_t launch_knn(const GridView& edge, const GridView& surf, const GridView& edge2, const GridView& surf2,
-                      const BatchView& bv, int skip_converged, hipStream_t s);
+                      const BatchView& bv, int skip_converged, hipStream_t s, bool memo = false);
 hipError_t launch_fit_eval(const GridView& edge, const GridView& surf, const BatchView& bv, int solver,
                            hipStream_t s);
 hipError_t launch_lm_begin(const BatchView& bv, hipStream_t s);
-// One LM inner iteration: evaluation at the candidate + (last block per slot) step control.
+// One LM inner iteration: evaluation at the candidate, then the step control.
 hipError_t launch_lm_eval_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
 hipError_t launch_lm_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
 hipError_t launch_gn_solve(const BatchView& bv, int outer, hipStream_t s);
