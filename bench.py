@@ -72,6 +72,8 @@ def parse(argv=None):
     ap.add_argument("--pairs", type=int, default=1000, help="C5: scan pairs in the whole job")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-n27", action="store_true",
+                    help="skip the untimed n27-counting step (PMC passes: every dispatch then runs as timed)")
     ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes of the neighbour-search kernel from rocprofv3 PMC runs")
     ap.add_argument("--h2d", choices=("auto", "on", "off"), default="auto",
@@ -153,7 +155,7 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def timed(d, step, warmup, steps, ctxs):
+def timed(d, step, warmup, steps, ctxs, count_n27=True):
     """W untimed steps, then K steps between barrier + synchronize; max over ranks.  The last
     warmup step (or, with W = 0, one step after the timed region) runs with the n27 accounting on:
     it costs the search extra loads, so the timed launches run without it.  Returns the mean n27
@@ -167,9 +169,13 @@ def timed(d, step, warmup, steps, ctxs):
         ks = [c.kernel_stats() for c in ctxs]
         return sum(k.n27_sum for k in ks) / max(sum(k.queries for k in ks), 1)
 
-    for _ in range(warmup - 1):
-        step()
-    mean_n27 = counted() if warmup > 0 else None
+    if not count_n27:
+        for _ in range(warmup):
+            step()
+    else:
+        for _ in range(warmup - 1):
+            step()
+    mean_n27 = (counted() if warmup > 0 else None) if count_n27 else 0.0
     for c in ctxs:
         c.kernel_stats_reset(timing=True)
     d.barrier()
@@ -430,7 +436,7 @@ def run_batch(args, d):
         exchange_poses(cfg, poses, gathered, args.pairs, world, d.dev)
         return poses
 
-    elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, ctxs)
+    elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, ctxs, not args.no_n27)
     ks = sum_stats([timed_stats(cx) for cx in ctxs])
     total_units = (args.batch * world if cfg == "C2" else args.pairs) * args.steps
     terr = [synth.pose_delta(poses[i], truth_u[unit_scan[i]]) for i in range(n_units)]
@@ -596,7 +602,7 @@ def run_streams(args, d):
         state["i"] += 1
         return P
 
-    elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx])
+    elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx], not args.no_n27)
     ks = timed_stats(ctx)
     roof = knn_roofline(ks, mean_n27, load_traffic(args.traffic_json, config="C4", batch=1, map_points=map_points),
                         elapsed, "one 63k-query scan per launch (8 lanes per query): latency-bound launches")
@@ -670,7 +676,7 @@ def run_dual(args, d):
         state["i"] += 1
         return out
 
-    elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx])
+    elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx], not args.no_n27)
     ks = timed_stats(ctx)
     roof = knn_roofline(ks, mean_n27, load_traffic(args.traffic_json, config="C3", batch=1), elapsed,
                         "one ~63k-query scan per launch (8 lanes per query) against the voxelised local map: "

@@ -142,6 +142,7 @@ struct lmsf_ctx {
     int* qcode = nullptr;             // ring position -> feature code / slot (knn order, k_extract.hip)
     int* qslot = nullptr;
     int* fslot = nullptr;             // [B][F] slots edges-then-surfs, each kind in ring order (fused search + fit)
+    float4* featp = nullptr;          // [B][F] the features in that order (w = slot)
     int* n_pos = nullptr;
     bool qorder_valid = false;        // the slots' features came from the extraction kernels
     int* d_error = nullptr;
@@ -224,6 +225,7 @@ struct lmsf_ctx {
         v.partials_gn = partials_gn;
         v.qslot = qorder_valid ? qslot : nullptr;
         v.fslot = qorder_valid ? fslot : nullptr;
+        v.featp = featp;
         v.write_nn = 0;
         v.n_pos = n_pos;
         v.pos_stride = R;
@@ -253,6 +255,7 @@ struct lmsf_ctx {
         e.qcode = qcode;
         e.qslot = qslot;
         e.fslot = fslot;
+        e.featp = featp;
         e.n_pos = n_pos;
         e.feat = feat;
         e.feat_src = feat_src;
@@ -486,7 +489,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->prevw, c->memo_nbr, c->wl, c->wlim, c->wcount, c->n_search, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->sort_key,
-                    c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->n_pos, c->d_error};
+                    c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->featp, c->n_pos, c->d_error};
     for (void* p : bufs) hipFree(p);
     c->voxel.release();
     hipFree(c->vox_in);
@@ -578,6 +581,7 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->qcode, B * R));
     CHK(dalloc(&c->qslot, B * R));
     CHK(dalloc(&c->fslot, B * c->F));
+    CHK(dalloc(&c->featp, B * c->F));
     CHK(dalloc(&c->n_pos, B));
     CHK(dalloc(&c->d_error, 32));
     CHK(hipMemset(c->d_error, 0, 32 * sizeof(int)));
@@ -1047,7 +1051,8 @@ lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int3
     HIPCHK(c, launch_state_init(bv, c->d_poses, c->stream));
     const GridView ge = c->map[LMSF_EDGE].view(), gs = c->map[LMSF_SURF].view();
     const GridView ge2 = c->prior[LMSF_EDGE].view(), gs2 = c->prior[LMSF_SURF].view();
-    if (match_fit_applies(ge2, gs2, bv, LMSF_SOLVER_CERES_LM)) {   // the path lmsf_solve takes
+    const bool by_position = match_fit_applies(ge2, gs2, bv, LMSF_SOLVER_CERES_LM);   // the path lmsf_solve takes
+    if (by_position) {
         HIPCHK(c, launch_match_fit(ge, gs, bv, c->stream));
     } else {
         HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{}, bv,
@@ -1064,16 +1069,20 @@ lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int3
     }
     std::vector<float4> pts(nn ? nq * 5 : 0);
     if (nq && nn) HIPCHK(c, hipMemcpyAsync(pts.data(), c->nnp, nq * 5 * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    std::vector<int> order(by_position ? nq : 0);   // fused path: record i belongs to slot fslot[i]
+    if (nq && by_position) HIPCHK(c, hipMemcpyAsync(order.data(), c->fslot, nq * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    for (size_t i = 0; out && i < nq; ++i) {     // device split layout -> lmsf_record
+    for (size_t j = 0; out && j < nq; ++j) {     // device split layout -> lmsf_record (slot order)
+        const size_t i = by_position ? (size_t)order[j] : j;
+        if (i >= nq) return c->fail(LMSF_ERR_HIP, "search order out of range");
         lmsf_record& r = out[i];
         std::memset(&r, 0, sizeof r);
-        r.px = rp[i].x; r.py = rp[i].y; r.pz = rp[i].z;
-        std::memcpy(&r.kind, &rp[i].w, sizeof r.kind);
+        r.px = rp[j].x; r.py = rp[j].y; r.pz = rp[j].z;
+        std::memcpy(&r.kind, &rp[j].w, sizeof r.kind);
         if (r.kind != 0) {
-            r.v0[0] = rv[i].v[0]; r.v0[1] = rv[i].v[1]; r.v0[2] = rv[i].v[2]; r.v1[0] = rv[i].v[3];
+            r.v0[0] = rv[j].v[0]; r.v0[1] = rv[j].v[1]; r.v0[2] = rv[j].v[2]; r.v1[0] = rv[j].v[3];
         }
-        if (r.kind == LMSF_EDGE) { r.v1[1] = re[i].x; r.v1[2] = re[i].y; }
+        if (r.kind == LMSF_EDGE) { r.v1[1] = re[j].x; r.v1[2] = re[j].y; }
     }
     if (nn) {  // neighbour points carry their map index in w (-1: rank not found with d^2 < 1)
         for (size_t i = 0; i < nq * 5; ++i) {

@@ -618,7 +618,11 @@ __global__ __launch_bounds__(256) void order_kernel(ExtractView ev) {
         for (int e = 0; e < E; ++e) {
             if (v[e] < 0) continue;
             const uint32_t o = v[e] < ne ? oe++ : os++;
-            if (o < (uint32_t)ev.feat_stride) fs[o] = v[e];
+            if (o < (uint32_t)ev.feat_stride) {
+                fs[o] = v[e];
+                const float4 f = ev.feat[(size_t)b * ev.feat_stride + v[e]];
+                ev.featp[(size_t)b * ev.feat_stride + o] = make_float4(f.x, f.y, f.z, __int_as_float(v[e]));
+            }
         }
         base_e += tot & 0xffffu;
         base_s += tot >> 16;

@@ -810,12 +810,12 @@ __global__ __launch_bounds__(256) void match_memo_kernel(GridView ge, GridView g
 #pragma unroll
     for (int e = 0; e < kPacket; ++e) P[e] = 0.0;
     if (need) {
-        const size_t pos = (size_t)b * F + i;
-        const int q = bv.fslot[pos];
+        const size_t pos = (size_t)b * F + i;   // search position: memo state and records live here
+        const float4 p = bv.featp[pos];
+        const int q = __float_as_int(p.w);
         const float4 pw = bv.prevw[pos];
         if (q >= 0 && q < nq && pw.w > 0.f) {
-            const size_t slot = (size_t)b * F + q;
-            const float4 p = bv.feat[slot];
+            const size_t slot = pos;
             const float3 w = associate(Ps, p);
             const double dx = (double)w.x - pw.x, dy = (double)w.y - pw.y, dz = (double)w.z - pw.z;
             const double dd = sqrt(dx * dx + dy * dy + dz * dz);
@@ -981,11 +981,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
             lim = bv.wlim[at];
         }
         const size_t ppos = (size_t)b * F + pos;
-        const int qq = bv.fslot[ppos];
+        const float4 p = bv.featp[ppos];        // the feature at this search position, w = its slot
+        const int qq = __float_as_int(p.w);
         const bool is_edge = qq < ne;
         const GridView g = pick_grid(is_edge, ge, gs);
-        const size_t slot = (size_t)b * F + qq;
-        const float4 p = bv.feat[slot];
+        const size_t slot = (size_t)b * F + qq;   // nnp (lmsf_match diagnostics) stays slot-indexed
         const float3 w = associate(Ps, p);
         const double sentinel = key_as_double(kSentinel);
         double k[kNK];
@@ -1043,7 +1043,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
             }
         }
 #endif
-        store_record(bv, slot, p, kind, v0, v1x, v1y, v1z);
+        store_record(bv, ppos, p, kind, v0, v1x, v1y, v1z);   // records by search position
         record_packet(kind, p, v0, v1x, v1y, v1z, Ps, P);
     }
     if (bx * 256 + wave * 64 < total)

@@ -82,6 +82,8 @@ struct BatchView {
     const int* n_pos;        // [B] ring positions per slot (with qslot)
     int pos_stride;
     const int* fslot;        // [B][feat_stride] edge slots then surf slots, each in ring order (with qslot)
+    const float4* featp;     // [B][feat_stride] feat in fslot order, w = slot bits (the fused path reads these
+                             //   coalesced and stores its records by search position, not by slot)
     int write_nn;            // fused search + fit also writes nnp (lmsf_match diagnostics)
     // Query memo of the fused path (outer iterations > 0 of one solve), indexed by search position i
     // (fslot order, so one lane per position reads them coalesced):
@@ -156,6 +158,7 @@ struct ExtractView {
     int* qcode;                  // [B][raw_stride] per ring position: ring-local edge index, kQSurf | surf index, -1
     int* qslot;                  // [B][raw_stride] per ring position: its feature slot or -1 (the search order)
     int* fslot;                  // [B][feat_stride] qslot's valid entries, edge slots first (stable)
+    float4* featp;               // [B][feat_stride] the features in fslot order: xyz, w = slot (int bits)
     int* n_pos;                  // [B] ring positions of the slot (ring_start[n_scans])
     float4* feat;                // [B][feat_stride] output (edges then surfs)
     int* feat_src;               // [B][feat_stride]

@@ -160,3 +160,14 @@ def test_single_hip_runtime_in_process():
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip() == "1"
+
+
+def test_pcl_adapter_header_guarded(tmp_path):
+    """include/lmsf/lmsf_pcl.hpp (the reference-side adapters of INTEGRATION.md) is compiled only where
+    PCL and the reference's headers are on the include path: here (no PCL) it must compile to nothing."""
+    src = tmp_path / "use_pcl_adapter.cpp"
+    src.write_text('#include "lmsf/lmsf_pcl.hpp"\n#ifdef LMSF_HAVE_PCL_REFERENCE\n#error unexpected\n#endif\nint main() { return 0; }\n')
+    subprocess.run(["g++", "-std=c++14", "-fsyntax-only", "-I", os.path.join(REPO, "include"), str(src)], check=True)
+    text = open(os.path.join(REPO, "include", "lmsf", "lmsf_pcl.hpp")).read()
+    for cls in ("HipEdgeSurfFeatureRegistration", "HipLOAMFeatureProcessor", "HipPointCloudCommonProcess"):
+        assert f"class {cls}" in text

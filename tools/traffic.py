@@ -5,7 +5,11 @@
 The FETCH_SIZE pass also carries --kernel-trace: the kernel's mean duration in that same run is kept
 as rocprof_mean_us, so bench.py's roofline can be recomputed from the committed files alone.
 
-Usage: python tools/traffic.py <fetch_dir> <write_dir> <hitmiss_dir> <kernel-substring> <out.json> [k=v ...]
+Usage: python tools/traffic.py <fetch_dir> <write_dir> <hitmiss_dir> <kernels> <out.json> [k=v ...]
+       kernels: comma-separated name substrings of the kernels one "launch" (one outer iteration of the
+       neighbour search) runs, the first naming the kernel that runs exactly once per launch (e.g.
+       match_fit_kernel,match_memo_kernel: the memo pass runs in outer iterations > 0 only); per-launch
+       figures = sums over all their dispatches / dispatches of the first.
        (k=v: the workload the passes ran -- config, batch, streams, map_points, unique_scans, profile)
 """
 import csv
@@ -14,46 +18,53 @@ import json
 import sys
 
 
-def per_dispatch(d, kernel):
+def counter_rows(d):
     f = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)[0]
-    vals = {}
-    for r in csv.DictReader(open(f)):
-        if kernel in r["Kernel_Name"]:
-            key = (r["Dispatch_Id"], r["Counter_Name"])
-            vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
-    out = {}
-    for (disp, name), v in vals.items():
-        out.setdefault(name, []).append(v)
-    return out
+    return list(csv.DictReader(open(f)))
 
 
-def mean_duration_us(d, kernel):
+def per_launch(d, kernels, counter):
+    """(sum of `counter` over the dispatches of every kernel in `kernels`, dispatches of kernels[0])."""
+    tot, first = 0.0, set()
+    for r in counter_rows(d):
+        if r["Counter_Name"] != counter or not any(k in r["Kernel_Name"] for k in kernels):
+            continue
+        tot += float(r["Counter_Value"])
+        if kernels[0] in r["Kernel_Name"]:
+            first.add(r["Dispatch_Id"])
+    return tot, len(first)
+
+
+def mean_duration_us(d, kernels):
     files = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)
     if not files:
         return None
-    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(files[0]))
-            if kernel in r["Kernel_Name"]]
-    return sum(durs) / len(durs) / 1e3 if durs else None
+    tot, n = 0, 0
+    for r in csv.DictReader(open(files[0])):
+        if any(k in r["Kernel_Name"] for k in kernels):
+            tot += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            n += kernels[0] in r["Kernel_Name"]
+    return tot / n / 1e3 if n else None
 
 
 def main():
-    fetch_dir, write_dir, hm_dir, kernel, out = sys.argv[1:6]
+    fetch_dir, write_dir, hm_dir, kernel_list, out = sys.argv[1:6]
+    kernels = kernel_list.split(",")
     extra = dict(a.split("=", 1) for a in sys.argv[6:])
-    fe = per_dispatch(fetch_dir, kernel)["FETCH_SIZE"]
-    wr = per_dispatch(write_dir, kernel)["WRITE_SIZE"]
-    hm = per_dispatch(hm_dir, kernel)
-    fetch_kb = sum(fe) / len(fe)
-    write_kb = sum(wr) / len(wr)
-    hit, miss = sum(hm["TCC_HIT_sum"]), sum(hm["TCC_MISS_sum"])
+    fe, n_fe = per_launch(fetch_dir, kernels, "FETCH_SIZE")
+    wr, n_wr = per_launch(write_dir, kernels, "WRITE_SIZE")
+    hit, _ = per_launch(hm_dir, kernels, "TCC_HIT_sum")
+    miss, _ = per_launch(hm_dir, kernels, "TCC_MISS_sum")
+    fetch_kb, write_kb = fe / n_fe, wr / n_wr
     res = {
-        "kernel": kernel,
-        "dispatches": len(fe),
+        "kernel": kernel_list,
+        "dispatches": n_fe,
         "fetch_size_kb_per_launch": fetch_kb,
         "write_size_kb_per_launch": write_kb,
         "hbm_bytes_per_launch": int((2 * fetch_kb + write_kb) * 1024),
         "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE counts 128-B requests at 64 B)",
         "l2_hit_rate": hit / max(hit + miss, 1.0),
-        "rocprof_mean_us": mean_duration_us(fetch_dir, kernel),
+        "rocprof_mean_us": mean_duration_us(fetch_dir, kernels),
     }
     for k, v in extra.items():
         res[k] = int(v) if v.isdigit() else v
