@@ -1,0 +1,67 @@
+/*
+ * lmsf_dist.h -- multi-GPU plumbing of the registration hot path for C / C++ callers
+ * (liblmsf_dist.so, RCCL over xGMI).
+ *
+ * The reference runs one MultiLidarSystem per process (INC/System/ML_System.hpp:130-156) and has no
+ * multi-device path; the build's scaling protocol -- one process (or thread) per GPU, each with its
+ * own lmsf_ctx -- needs three exchanges, the same ones lmsf-slam_amd/lmsf/multi.py runs over
+ * torch.distributed for bench.py:
+ *   C2 / C5  scans (pairs) sharded with no data-path collective, then an all-gather of the 6-DoF
+ *            poses (7 doubles each);
+ *   C4       the shared map broadcast from rank 0 once (into device memory, then lmsf_set_map /
+ *            lmsf_tracker_set_prior_map from it), and per tracking step an all-gather of every
+ *            stream's (pose, keyframe flag, feature counts) followed -- only when some stream
+ *            keyframed -- by an all-gather of the padded feature buffers, so every replica appends
+ *            the same keyframes in rank order.
+ * Every call is collective (all ranks, same order) and returns when its result is usable: host
+ * results are written, device results are complete on the device.
+ */
+#ifndef LMSF_LMSF_DIST_H_
+#define LMSF_LMSF_DIST_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "lmsf.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LMSF_GROUP_ID_BYTES 128
+
+typedef struct lmsf_group lmsf_group;
+
+/* Rank 0 creates the group id and hands it to every rank out of band (a file, the ROS parameter
+ * server, MPI, ...). */
+lmsf_status lmsf_group_unique_id(uint8_t id[LMSF_GROUP_ID_BYTES]);
+/* Join the group as `rank` of `nranks` on HIP device `device` (one device per rank). */
+lmsf_status lmsf_group_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t id[LMSF_GROUP_ID_BYTES],
+                              lmsf_group** out);
+void lmsf_group_destroy(lmsf_group* g);
+int32_t lmsf_group_rank(const lmsf_group* g);
+int32_t lmsf_group_size(const lmsf_group* g);
+
+/* C2 / C5: every rank's n poses (qx qy qz qw tx ty tz, host) -> all[rank][n][7] (host). */
+lmsf_status lmsf_group_allgather_poses(lmsf_group* g, const double* mine, int32_t n, double* all);
+
+/* C4: the root's cloud (xyzi rows in device memory, *n rows at the root) replicated into every rank's
+ * device buffer xyzi_dev of cap rows; *n = rows on return (LMSF_ERR_CAPACITY when cap is too small). */
+lmsf_status lmsf_group_broadcast_cloud(lmsf_group* g, int32_t root, float* xyzi_dev, size_t cap, size_t* n);
+
+/* C4 keyframe exchange.  In: this rank's pose (4x4 row-major), update type (0: none), feature counts
+ * and feat_dev = [edges (cap rows) | surfs (cap rows)] xyzi in device memory.  Out: info[rank][19] =
+ * (pose[16], update type, n_edge, n_surf) of every rank (host); *any = 1 when some rank keyframed, and
+ * then gathered_dev[rank][2 * cap][4] holds every rank's buffer (device). */
+lmsf_status lmsf_group_exchange_keyframes(lmsf_group* g, const double pose[16], int32_t update_type, int64_t n_edge,
+                                          int64_t n_surf, const float* feat_dev, size_t cap, double* info,
+                                          float* gathered_dev, int32_t* any);
+
+/* Max over ranks of a host double (the bench's max-over-ranks timing). */
+lmsf_status lmsf_group_max(lmsf_group* g, double* value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LMSF_LMSF_DIST_H_ */

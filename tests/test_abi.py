@@ -171,3 +171,34 @@ def test_pcl_adapter_header_guarded(tmp_path):
     text = open(os.path.join(REPO, "include", "lmsf", "lmsf_pcl.hpp")).read()
     for cls in ("HipEdgeSurfFeatureRegistration", "HipLOAMFeatureProcessor", "HipPointCloudCommonProcess"):
         assert f"class {cls}" in text
+
+
+def build_dist_example(out_dir):
+    """Compile tests/cpp/dist_example.cpp (a C caller of lmsf_dist.h + lmsf.h) against liblmsf_dist.so and
+    liblmsf_hip.so."""
+    lib_dir = os.path.join(REPO, "lmsf-slam_amd")
+    exe = os.path.join(str(out_dir), "dist_example")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(REPO, "include"),
+                    "-I", "/opt/rocm/include", os.path.join(REPO, "tests", "cpp", "dist_example.cpp"), "-L", lib_dir,
+                    "-llmsf_dist", "-llmsf_hip", "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{lib_dir}",
+                    "-Wl,-rpath,/opt/rocm/lib", "-o", exe], check=True)
+    return exe
+
+
+def test_dist_library_exports_and_example_links(lib, tmp_path):
+    """liblmsf_dist.so (RCCL) exports every entry point of include/lmsf/lmsf_dist.h; the C example
+    that runs one rank's C2 / C4 protocol through it links."""
+    import re
+    dist = os.path.join(REPO, "lmsf-slam_amd", "liblmsf_dist.so")
+    if not os.path.exists(dist):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "lmsf-slam_amd"), "liblmsf_dist.so"], check=True)
+    text = open(os.path.join(REPO, "include", "lmsf", "lmsf_dist.h")).read()
+    syms = set(re.findall(r"^\s*(?:lmsf_status|void|int32_t)\s+(lmsf_group_\w+)\s*\(", text, re.M))
+    assert len(syms) >= 8
+    out = subprocess.run(["nm", "-D", "--defined-only", dist], capture_output=True, text=True).stdout
+    assert syms <= {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert "ncclAllGather" in subprocess.run(["nm", "-D", "-u", dist], capture_output=True, text=True).stdout
+    exe = build_dist_example(tmp_path)
+    undefined = subprocess.run(["nm", "-u", exe], capture_output=True, text=True).stdout
+    for s in ("lmsf_group_create", "lmsf_group_allgather_poses", "lmsf_group_exchange_keyframes", "lmsf_solve"):
+        assert s in undefined

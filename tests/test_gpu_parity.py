@@ -811,3 +811,37 @@ def test_sparse_point_plane_icp_tracking(lib, oracle_mod, sequence_workload):
         R.PointCloudCommonProcessHIP().SetVoxelGrid("ApproximateVoxelGrid", 0.5)
     reg = R.make_registration("sparse_point_plane_icp_hip", max_features=70000)
     assert (reg.edge_name, reg.surf_name) == ("", "filtered")
+
+
+def test_dist_example(lib, oracle_mod, small_workload, tmp_path):
+    """The C multi-GPU plumbing (liblmsf_dist.so over RCCL) driven by a C program, one rank: map broadcast
+    into device memory, extraction + registration from it, pose all-gather, keyframe exchange, max --
+    the pose equals the oracle's, the gathered pose and keyframe buffer equal the rank's own."""
+    import subprocess
+    from test_abi import build_dist_example
+    wl = small_workload
+    exe = build_dist_example(tmp_path)
+    paths = []
+    for name, arr in (("scan", wl.scans[0]), ("edge", wl.edge_map), ("surf", wl.surf_map)):
+        p = tmp_path / f"{name}.bin"
+        np.ascontiguousarray(arr, np.float32).tofile(p)
+        paths.append(str(p))
+    g = wl.guess[0]
+    out = subprocess.run([exe, "1", "0", str(tmp_path / "group.id"), *paths, *[repr(float(v)) for v in g], "5"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    f = out.stdout.strip().splitlines()[-1].split()     # RCCL may print its banner first
+    x = np.array([float(v) for v in f[2:9]])
+    assert f[9] == "1" and f[10] == "1" and float(f[11]) == 1.5
+    e, s = _features(oracle_mod, wl.scans[0])
+    assert (int(f[0]), int(f[1])) == (len(e), len(s))
+    reg = oracle_mod.Registration()
+    reg.set_map(1, wl.edge_map)
+    reg.set_map(2, wl.surf_map)
+    reg.set_scan(1, e)
+    reg.set_scan(2, s)
+    reg.set_fixed_schedule(True)
+    reg.set_max_iterations(5)
+    ox, _, _ = reg.solve(g)
+    dt, dr = pose_err(x, ox)
+    assert dt <= POSE_TOL and dr <= POSE_TOL
