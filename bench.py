@@ -223,10 +223,11 @@ def shared_map(d, make):
 
 
 def kernel_name(ks):
-    """The timed neighbour-search launch: the fused search + fit kernel (batch launches) or knn_kernel."""
+    """The timed neighbour-search launch: the fused search + fit kernels (batch launches) or knn_kernel."""
     if ks.launches and ks.fused_launches == ks.launches:
-        return "match_fit_kernel (fused 5-NN search + line/plane fit + first evaluation)"
-    return "knn_kernel"
+        return ("match_memo_kernel + match_fit_kernel (query memo pass, then the fused 5-NN search + line/plane "
+                "fit + first evaluation of the queries it lists; one outer iteration)")
+    return "knn_kernel (8-lane 5-NN search with the slot memo; fit_eval_kernel follows)"
 
 
 def load_traffic(traffic_json, **match):
@@ -264,10 +265,11 @@ def knn_roofline(ks, mean_n27, tj, elapsed_s, note):
     traffic = int(tj["hbm_bytes_per_launch"]) if tj else None
     if traffic:
         achieved, basis = traffic / (avg_launch_ms * 1e-3) / 1e9, "pmc"
-    else:
-        achieved, basis = model_gbs, "model (no PMC profile of this workload under profiles/)"
-    out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "basis": basis,
+    else:   # never the model: it counts cache-served candidate reads as HBM bytes
+        achieved, basis = None, "unmeasured (no PMC profile of this workload under profiles/)"
+    out = {"bound": "hbm", "achieved": round(achieved, 1) if achieved is not None else None, "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved is not None else None,
+           "traffic": traffic, "basis": basis,
            "kernel": kernel_name(ks), "avg_launch_ms": round(avg_launch_ms, 4), "launches": int(ks.launches),
            "queries_per_launch": int(ks.queries / launches),
            "reused_query_frac": round(reused / max(int(ks.queries), 1), 4),

@@ -57,7 +57,8 @@ def test_roofline_measured_and_model():
     assert r["model"]["exceeds_peak"] is False
     # a model figure above the HBM peak is flagged
     r2 = bench.knn_roofline(types.SimpleNamespace(**dict(vars(ks), total_ms=0.01)), 50.0, None, 0.02, "n")
-    assert r2["basis"].startswith("model") and r2["model"]["exceeds_peak"] is True and r2["traffic"] is None
+    assert r2["basis"].startswith("unmeasured") and r2["achieved"] is None and r2["frac"] is None
+    assert r2["model"]["exceeds_peak"] is True and r2["traffic"] is None
 
 
 def test_load_traffic_matches_workload(tmp_path):
