@@ -31,6 +31,11 @@ struct DevMap {
     size_t scan_tmp_bytes = 0;
     int ox = 0, oy = 0, oz = 0, nx = 0, ny = 0, nz = 0, sx = 1;
     float lim1 = 1.f;
+    // occupied-slice count of the last build, read back without blocking: lim1 (the pruned walk's
+    // first radius) is resolved only by a launch that can take the pruned one-lane walk
+    unsigned long long* h_occ = nullptr;   // pinned
+    hipEvent_t ev_occ = nullptr;
+    bool occ_pending = false;
 
     GridView view() const {
         GridView g;
@@ -338,11 +343,34 @@ lmsf_status build_grid(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, int 
     unsigned long long* d_occ = reinterpret_cast<unsigned long long*>(c->d_error + 16);   // scratch after the bbox
     HIPCHK(c, hipMemsetAsync(d_occ, 0, sizeof(unsigned long long), s));
     HIPCHK(c, launch_count_nonzero(m.counts, cells, d_occ, s));
-    unsigned long long occ = 0;
-    HIPCHK(c, hipMemcpyAsync(&occ, d_occ, sizeof occ, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    m.lim1 = knn_first_radius2(n, occ);
+    if (!m.h_occ) {
+        HIPCHK(c, hipHostMalloc((void**)&m.h_occ, sizeof(unsigned long long), hipHostMallocDefault));
+        HIPCHK(c, hipEventCreateWithFlags(&m.ev_occ, hipEventDisableTiming));
+    }
+    HIPCHK(c, hipMemcpyAsync(m.h_occ, d_occ, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipEventRecord(m.ev_occ, s));
+    m.occ_pending = true;
+    m.lim1 = 1.f;   // provisional (plain walk) until resolve_lim1
     m.n = (int)n;
+    return LMSF_OK;
+}
+
+// The density-chosen first radius of the pruned walk, once a launch may use it (one-lane launches).
+lmsf_status resolve_lim1(lmsf_ctx* c, DevMap& m) {
+    if (!m.occ_pending) return LMSF_OK;
+    HIPCHK(c, hipEventSynchronize(m.ev_occ));
+    m.lim1 = knn_first_radius2((size_t)m.n, *m.h_occ);
+    m.occ_pending = false;
+    return LMSF_OK;
+}
+
+lmsf_status resolve_all_lim1(lmsf_ctx* c, size_t query_slots) {
+    if (knn_team_for(query_slots) != 1) return LMSF_OK;   // the 8-lane walk never prunes
+    for (DevMap* ms : {c->map, c->prior})
+        for (int k = 0; k < 3; ++k) {
+            lmsf_status rc = resolve_lim1(c, ms[k]);
+            if (rc) return rc;
+        }
     return LMSF_OK;
 }
 
@@ -376,6 +404,8 @@ lmsf_status sync_slot0_features(lmsf_ctx* c) {
 
 // Enqueue the registration of slots [0, nb): outer iterations of match + solver control.
 lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
+    lmsf_status rl = resolve_all_lim1(c, (size_t)c->F * nb);
+    if (rl) return rl;
     const BatchView bv = c->bview(nb);
     const GridView ge = c->map[LMSF_EDGE].view(), gs = c->map[LMSF_SURF].view();
     const GridView ge2 = c->prior[LMSF_EDGE].view(), gs2 = c->prior[LMSF_SURF].view();
@@ -484,6 +514,8 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
             DevMap& m = ms[k];
             hipFree(m.orig); hipFree(m.pts); hipFree(m.cell); hipFree(m.counts); hipFree(m.off); hipFree(m.fill);
             hipFree(m.scan_tmp);
+            if (m.h_occ) hipHostFree(m.h_occ);
+            if (m.ev_occ) hipEventDestroy(m.ev_occ);
         }
     }
     void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->prevw, c->memo_nbr, c->wl, c->wlim, c->wcount, c->n_search, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
@@ -689,12 +721,14 @@ lmsf_status lmsf_solve_trace(lmsf_ctx* c, double* trace, int32_t cap, int32_t* n
     return LMSF_OK;
 }
 
+static lmsf_status load_scans(lmsf_ctx* c, const float* xyzi, const int64_t* counts, int32_t n, bool sync);
+
 lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf_feature_counts* counts) {
     if (!c || (n && !xyzi)) return LMSF_ERR_ARG;
     if (n > (size_t)c->R) return c->fail(LMSF_ERR_CAPACITY, "%zu points exceed max_scan_points %d", n, c->R);
     HIPCHK(c, hipSetDevice(c->cfg.device));
     const int64_t counts_in[1] = {(int64_t)n};
-    lmsf_status rc = lmsf_batch_load_scans(c, xyzi, counts_in, 1);
+    lmsf_status rc = load_scans(c, xyzi, counts_in, 1, false);   // synchronised below
     if (rc) return rc;
     HIPCHK(c, hipMemsetAsync(c->d_error, 0, sizeof(int), c->stream));
     HIPCHK(c, launch_extract(c->eview(1), c->stream));
@@ -779,9 +813,14 @@ lmsf_status lmsf_common_process(lmsf_ctx* c, const float* xyzi, size_t n, const 
 static lmsf_status copy_slot_features(lmsf_ctx* c, int slot, int32_t kind, float* out, int32_t* src, size_t cap,
                                       size_t* n_out) {
     int hc[2];
-    HIPCHK(c, hipMemcpyAsync(&hc[0], c->n_edge + slot, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&hc[1], c->n_surf + slot, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (slot == 0 && c->features_on_device) {   // counts of the last extraction are known on the host
+        hc[0] = (int)c->slot0_ne;
+        hc[1] = (int)c->slot0_ns;
+    } else {
+        HIPCHK(c, hipMemcpyAsync(&hc[0], c->n_edge + slot, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&hc[1], c->n_surf + slot, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     const size_t n = kind == LMSF_EDGE ? hc[0] : hc[1];
     const size_t off = (size_t)slot * c->F + (kind == LMSF_EDGE ? 0 : hc[0]);
     if (n_out) *n_out = n;
@@ -937,6 +976,11 @@ lmsf_status lmsf_batch_copy_features(lmsf_ctx* c, int32_t slot, int32_t kind, fl
 }
 
 lmsf_status lmsf_batch_load_scans(lmsf_ctx* c, const float* xyzi, const int64_t* counts, int32_t n) {
+    return load_scans(c, xyzi, counts, n, true);
+}
+
+// sync = false: the caller synchronises the stream before h_counts is written again
+static lmsf_status load_scans(lmsf_ctx* c, const float* xyzi, const int64_t* counts, int32_t n, bool sync) {
     if (!c || !counts || n < 1 || n > c->B) return LMSF_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->cfg.device));
     if (c->raw_pending) {   // a streamed upload not yet consumed: this copy replaces it, after it
@@ -954,7 +998,7 @@ lmsf_status lmsf_batch_load_scans(lmsf_ctx* c, const float* xyzi, const int64_t*
         off += (size_t)counts[i];
     }
     HIPCHK(c, hipMemcpyAsync(c->raw_count, c->h_counts, n * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (sync) HIPCHK(c, hipStreamSynchronize(c->stream));
     return LMSF_OK;
 }
 
@@ -1046,6 +1090,8 @@ lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int3
     if (nq > cap) return c->fail(LMSF_ERR_CAPACITY, "output capacity %zu < %zu queries", cap, nq);
     std::memcpy(c->h_poses, pose, 7 * sizeof(double));
     HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    rc = resolve_all_lim1(c, (size_t)c->F);
+    if (rc) return rc;
     BatchView bv = c->bview(1);
     bv.write_nn = 1;
     HIPCHK(c, launch_state_init(bv, c->d_poses, c->stream));

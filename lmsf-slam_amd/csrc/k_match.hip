@@ -1141,6 +1141,8 @@ static int knn_team(size_t query_slots) {
     if (forced) return forced;
     return query_slots >= ((size_t)1 << 20) ? 1 : 8;
 }
+int knn_team_for(size_t query_slots) { return knn_team(query_slots); }
+
 static int knn_remap() {
     static int r = [] {
         const char* e = getenv("LMSF_XCD_REMAP");

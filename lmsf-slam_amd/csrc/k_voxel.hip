@@ -39,16 +39,24 @@ __global__ void __launch_bounds__(256) voxel_bbox_kernel(const float4* pts, int 
     block_bbox_commit<256>(lo, hi, bbox);
 }
 
-__global__ void voxel_key_kernel(const float4* pts, int n, float inv, const int* bbox, uint32_t dx, uint32_t dy,
-                                 uint32_t* keys, int* idx) {
+// Linear voxel key from the device-side bounding box (no host round trip).  When div_x*div_y*div_z
+// exceeds INT32_MAX PCL refuses and returns the input unchanged: every point then gets its own key
+// (its index), so each "voxel" is one point and the centroid pass reproduces the input exactly.
+__global__ void voxel_key_kernel(const float4* pts, int n, float inv, const int* bbox, uint32_t* keys, int* idx) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    const int64_t dx = (int64_t)bbox[3] - bbox[0] + 1, dy = (int64_t)bbox[4] - bbox[1] + 1,
+                  dz = (int64_t)bbox[5] - bbox[2] + 1;
+    idx[i] = i;
+    if (dx * dy * dz > (int64_t)INT32_MAX) {
+        keys[i] = (uint32_t)i;
+        return;
+    }
     const float4 p = pts[i];
     const uint32_t cx = (uint32_t)(vox_coord(p.x, inv) - bbox[0]);
     const uint32_t cy = (uint32_t)(vox_coord(p.y, inv) - bbox[1]);
     const uint32_t cz = (uint32_t)(vox_coord(p.z, inv) - bbox[2]);
-    keys[i] = (cz * dy + cy) * dx + cx;        // < 2^31 (checked on the host)
-    idx[i] = i;
+    keys[i] = (cz * (uint32_t)dy + cy) * (uint32_t)dx + cx;   // < 2^31
 }
 
 // start[s] = first sorted position of voxel s (heads scanned into segment ids).
@@ -94,6 +102,11 @@ __global__ __launch_bounds__(256) void voxel_mean_kernel(const float4* pts, cons
     }
 }
 
+__global__ void bbox_init_kernel(int* bbox) {
+    if (threadIdx.x < 3) bbox[threadIdx.x] = INT_MAX;
+    else if (threadIdx.x < 6) bbox[threadIdx.x] = INT_MIN;
+}
+
 void VoxelFilter::release() {
     void* bufs[] = {keys, keys_sorted, idx, idx_sorted, head, seg, start, bbox, nseg, tmp};
     for (void* p : bufs) hipFree(p);
@@ -131,24 +144,12 @@ hipError_t VoxelFilter::run(const float4* in, int n, float leaf, float4* out, in
     hipError_t e = reserve((size_t)n);
     if (e != hipSuccess) return e;
     const float inv = 1.0f / leaf;
-    const int init[6] = {INT_MAX, INT_MAX, INT_MAX, INT_MIN, INT_MIN, INT_MIN};
-    int hb[6];
-    if ((e = hipMemcpyAsync(bbox, init, sizeof init, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(bbox_init_kernel, dim3(1), dim3(64), 0, s, bbox);
     hipLaunchKernelGGL(voxel_bbox_kernel, dim3(min(max((n + 255) / 256, 1), 512)), dim3(256), 0, s, in, n, inv, bbox);
-    if ((e = hipMemcpyAsync(hb, bbox, sizeof hb, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    const int64_t dx = (int64_t)hb[3] - hb[0] + 1, dy = (int64_t)hb[4] - hb[1] + 1, dz = (int64_t)hb[5] - hb[2] + 1;
-    if (dx * dy * dz > (int64_t)INT32_MAX) {      // PCL: indices would overflow -> input unchanged
-        if ((e = hipMemcpyAsync(out, in, (size_t)n * sizeof(float4), hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
-        *n_out = n;
-        return hipStreamSynchronize(s);
-    }
-    int bits = 1;
-    while (bits < 31 && (int64_t{1} << bits) < dx * dy * dz) ++bits;
     const dim3 g((n + 255) / 256), b(256);
-    hipLaunchKernelGGL(voxel_key_kernel, g, b, 0, s, in, n, inv, bbox, (uint32_t)dx, (uint32_t)dy, keys, idx);
-    size_t tb = tmp_bytes;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys_sorted, idx, idx_sorted, n, 0, bits, s)) != hipSuccess)
+    hipLaunchKernelGGL(voxel_key_kernel, g, b, 0, s, in, n, inv, bbox, keys, idx);
+    size_t tb = tmp_bytes;   // keys < 2^31: 31 key bits (one host round trip fewer than sizing the sort to the box)
+    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys_sorted, idx, idx_sorted, n, 0, 31, s)) != hipSuccess)
         return e;
     hipLaunchKernelGGL(voxel_head_kernel, g, b, 0, s, keys_sorted, n, head);
     tb = tmp_bytes;

@@ -125,6 +125,7 @@ hipError_t launch_lm_eval_step(const BatchView& bv, int outer, int is_last, hipS
 hipError_t launch_lm_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
 hipError_t launch_gn_solve(const BatchView& bv, int outer, hipStream_t s);
 int fit_per_thread_default();
+int knn_team_for(size_t query_slots);   // lanes per query of a search launch over that many query slots
 // Fused 5-NN search + fit + first evaluation (one lane per query, queries in fslot order); false:
 // not applicable to this launch (caller runs launch_knn + launch_fit_eval).
 bool match_fit_applies(const GridView& edge2, const GridView& surf2, const BatchView& bv, int solver);
