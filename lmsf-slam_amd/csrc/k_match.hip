@@ -845,9 +845,19 @@ __global__ __launch_bounds__(256) void match_memo_kernel(GridView ge, GridView g
                         const RecV v = bv.rec_v[slot];
                         v0 = mk(v.v[0], v.v[1], v.v[2]);
                         v1x = v.v[3];
-                        if (kind == LMSF_SURF) {   // surf_fit's orientation test at the new query (the stored
-                            const d3 cp = mk((double)w.x, (double)w.y, (double)w.z);   // n, D were flipped to
-                            reuse = (float)(dot(v0, cp) + v1x) > 0.f;                   // make it >= 0 at w0)
+                        if (kind == LMSF_SURF) {
+                            // surf_fit keeps its plane (n, D) when (float)(n . w + D) >= 0 and flips it
+                            // otherwise; the stored record is that plane up to sign, and negation is exact,
+                            // so t = (float)(n_s . w + D_s) = +-(the fit's test): t > 0 -> the stored record
+                            // is the fit's answer at w, t < 0 -> its negation; t == 0 is ambiguous (search)
+                            const d3 cp = mk((double)w.x, (double)w.y, (double)w.z);
+                            const float t = (float)(dot(v0, cp) + v1x);
+                            reuse = t != 0.f;
+                            if (t < 0.f) {
+                                v0 = mk(-v0.x, -v0.y, -v0.z);
+                                v1x = -v1x;
+                                store_record(bv, slot, p, kind, v0, v1x, 0.0, 0.0);
+                            }
                         } else {
                             const double2 e = bv.rec_e[slot];
                             v1y = e.x;
