@@ -148,6 +148,7 @@ __global__ __launch_bounds__(256) void ring_scatter_kernel(ExtractView ev) {
         __syncthreads();
         const int i = t * kTile + c0 + threadIdx.x;
         const int r = i < n ? (int)rid[i] : -1;
+        const float4 pt = r >= 0 ? raw[i] : make_float4(0, 0, 0, 0);   // in flight across the rank pass
         int rank = 0;
         unsigned long long remaining = __ballot(r >= 0);
         while (remaining) {
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(256) void ring_scatter_kernel(ExtractView ev) {
             int base = running[r];
             for (int w = 0; w < wave; ++w) base += wcnt[w][r];
             const int dst = toff[(size_t)r * ev.n_tiles + t] + base + rank;
-            out[dst] = raw[i];
+            out[dst] = pt;
             osrc[dst] = i;
         }
         __syncthreads();
@@ -382,7 +383,9 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
     __shared__ double key[kSortMax];
     __shared__ int kidx[kSortMax];
     __shared__ int scan_part[256];
+    __shared__ int pick[20];
     __shared__ int sh_ec, sh_sc, sh_err;
+    constexpr int kSurfPer = 3;   // sector points per thread held in registers by the surf compaction
     const int r = blockIdx.x, b = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63;
     const int* rs = ev.ring_start + (size_t)b * (kMaxRings + 1);
@@ -440,8 +443,7 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
                 ++picked;
                 if (picked > 20) break;
                 if (lane == 0) {
-                    estage[ec] = pts[ind];
-                    estage_src[ec] = psrc[ind];
+                    pick[picked - 1] = ind;   // staged after the loop: no load -> store round trip per pick
                     flag[ind] = 1;
                     qc[ind] = ec;
                 }
@@ -451,6 +453,12 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
                 pos = pos - f - 1;
             }
             if (lane == 0) sh_ec = ec;
+            const int ec0 = ec - min(picked, 20);
+            for (int t = lane; t < ec - ec0; t += 64) {
+                const int ind = pick[t];
+                estage[ec0 + t] = pts[ind];
+                estage_src[ec0 + t] = psrc[ind];
+            }
         }
         __syncthreads();
         // surf: every sector point not picked as edge, ascending curvature (FX:197-206);
@@ -470,13 +478,37 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
         int wbase = 0;
         for (int w2 = 0; w2 < (tid >> 6); ++w2) wbase += scan_part[w2];
         int o = sh_sc + wbase + incl - cntv;
-        for (int i = lo; i < hi; ++i) {
-            const int ind = kidx[i];
-            if (flag[ind] == 0) {
-                sstage[o] = pts[ind];
-                sstage_src[o] = psrc[ind];
-                qc[ind] = kQSurf | o;
-                ++o;
+        if (per <= kSurfPer) {   // every point load in flight before the first store
+            int ind[kSurfPer];
+            float4 sp[kSurfPer];
+            int ss[kSurfPer];
+#pragma unroll
+            for (int u = 0; u < kSurfPer; ++u) {
+                const int i = lo + u;
+                ind[u] = i < hi && flag[kidx[i]] == 0 ? kidx[i] : -1;
+                if (ind[u] >= 0) {
+                    sp[u] = pts[ind[u]];
+                    ss[u] = psrc[ind[u]];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kSurfPer; ++u) {
+                if (ind[u] >= 0) {
+                    sstage[o] = sp[u];
+                    sstage_src[o] = ss[u];
+                    qc[ind[u]] = kQSurf | o;
+                    ++o;
+                }
+            }
+        } else {
+            for (int i = lo; i < hi; ++i) {
+                const int ind1 = kidx[i];
+                if (flag[ind1] == 0) {
+                    sstage[o] = pts[ind1];
+                    sstage_src[o] = psrc[ind1];
+                    qc[ind1] = kQSurf | o;
+                    ++o;
+                }
             }
         }
         __syncthreads();
@@ -558,10 +590,10 @@ __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
 // search neighbouring ring points, and a wave runs one fit kind).  One block per (ring, slot): a
 // ring's valid positions are exactly its ring_edge_cnt edges and ring_surf_cnt surfs (concat_kernel),
 // so ring r writes edges from epre[r] and surfs from n_edge + spre[r]; inside the ring a block-wide
-// exclusive scan of the packed (edge, surf) counts (16 bits each) of 4 consecutive positions per
-// thread, 1024 positions per chunk.
+// exclusive scan of the packed (edge, surf) counts (16 bits each) of 8 consecutive positions per
+// thread, 2048 positions per chunk.
 __global__ __launch_bounds__(256) void order_kernel(ExtractView ev) {
-    constexpr int E = 4;
+    constexpr int E = 8;
     __shared__ uint32_t wsum[4];
     __shared__ int pre[2];
     const int r = blockIdx.x, b = blockIdx.y;
@@ -614,14 +646,20 @@ __global__ __launch_bounds__(256) void order_kernel(ExtractView ev) {
         }
         const uint32_t ex = wpre + x - cnt;
         uint32_t oe = base_e + (ex & 0xffffu), os = base_s + (ex >> 16);
+        // all E feature loads first, then the stores (a load after a store to featp, which the compiler
+        // cannot prove distinct from feat, would wait for it: E serial round trips per chunk)
+        uint32_t o[E];
+        float4 f[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            if (v[e] < 0) continue;
-            const uint32_t o = v[e] < ne ? oe++ : os++;
-            if (o < (uint32_t)ev.feat_stride) {
-                fs[o] = v[e];
-                const float4 f = ev.feat[(size_t)b * ev.feat_stride + v[e]];
-                ev.featp[(size_t)b * ev.feat_stride + o] = make_float4(f.x, f.y, f.z, __int_as_float(v[e]));
+            o[e] = v[e] < 0 ? 0xffffffffu : (v[e] < ne ? oe++ : os++);
+            f[e] = o[e] < (uint32_t)ev.feat_stride ? ev.feat[(size_t)b * ev.feat_stride + v[e]] : make_float4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if (o[e] < (uint32_t)ev.feat_stride) {
+                fs[o[e]] = v[e];
+                ev.featp[(size_t)b * ev.feat_stride + o[e]] = make_float4(f[e].x, f[e].y, f[e].z, __int_as_float(v[e]));
             }
         }
         base_e += tot & 0xffffu;
@@ -636,7 +674,7 @@ hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
     hipLaunchKernelGGL(ring_scatter_kernel, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(sector_sort_kernel, dim3(ev.n_scans * 6, ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(ring_features_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
-    const int cblocks = min(64, (ev.raw_stride + 255) / 256);
+    const int cblocks = min(256, (ev.raw_stride + 255) / 256);   // ~one feature and one position per thread
     hipLaunchKernelGGL(concat_kernel, dim3(max(cblocks, 1), ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(order_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
     return hipGetLastError();

@@ -1080,6 +1080,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
 // agent-scope ticket with sc1 packet stores, measured slower in r02 on C2 / C3 / C4 -- 20.9k vs 22.1k
 // scans/s, 1.95 vs 1.73 ms per C3 frame, 2.12 vs 2.05 ms per C4 scan: the step code capped the
 // kernel at 128 VGPRs and its serial step lands on the launch's tail -- and was removed.)
+__device__ __forceinline__ void eval_record(const Pose& Ps, bool valid, const float4 rp, const RecV& v, const double2 e,
+                                            double* P) {
+    const int kind = __float_as_int(rp.w);
+    if (valid && kind != 0) {
+        double J[6], res;
+        const d3 pp = mk((double)rp.x, (double)rp.y, (double)rp.z);
+        if (kind == LMSF_EDGE)
+            res = edge_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), mk(v.v[3], e.x, e.y), J);
+        else
+            res = surf_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), v.v[3], J);
+        huber_accumulate(P, res, J);
+    }
+}
+
 __global__ __launch_bounds__(256) void lm_eval_kernel(BatchView bv) {
     const int b = blockIdx.y;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
@@ -1089,32 +1103,48 @@ __global__ __launch_bounds__(256) void lm_eval_kernel(BatchView bv) {
     double P[kPacket];
 #pragma unroll
     for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
+    const size_t base = (size_t)b * bv.feat_stride;
+    const int q0 = blockIdx.x * kEvalBlock + threadIdx.x;
+    auto slot_of = [&](int k) { return base + (q0 + k * 256 < nq ? q0 + k * 256 : 0); };
+#if LMSF_EVAL_PIPE
+    // Software pipeline, one record per step: rec_p / rec_v of record k + 2 and rec_e of record k + 1
+    // (edges only; its kind arrived a step earlier) are in flight while record k is evaluated.
+    const double2 ez = make_double2(0.0, 0.0);
+    float4 p0 = bv.rec_p[slot_of(0)], p1 = p0;
+    RecV v0 = bv.rec_v[slot_of(0)], v1 = v0;
+    if (kEvalPerThread > 1) {
+        p1 = bv.rec_p[slot_of(1)];
+        v1 = bv.rec_v[slot_of(1)];
+    }
+    double2 e0 = __float_as_int(p0.w) == LMSF_EDGE ? bv.rec_e[slot_of(0)] : ez;
+#pragma unroll
+    for (int k = 0; k < kEvalPerThread; ++k) {
+        float4 pn = p1;
+        RecV vn = v1;
+        if (k + 2 < kEvalPerThread) {
+            pn = bv.rec_p[slot_of(k + 2)];
+            vn = bv.rec_v[slot_of(k + 2)];
+        }
+        double2 en = ez;
+        if (k + 1 < kEvalPerThread && __float_as_int(p1.w) == LMSF_EDGE) en = bv.rec_e[slot_of(k + 1)];
+        eval_record(Ps, q0 + k * 256 < nq, p0, v0, e0, P);
+        p0 = p1; v0 = v1; e0 = en;
+        p1 = pn; v1 = vn;
+    }
+#else
     float4 rp[kEvalPerThread];
     RecV rv[kEvalPerThread];
 #pragma unroll
     for (int k = 0; k < kEvalPerThread; ++k) {
-        const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
-        const size_t slot = (size_t)b * bv.feat_stride + (q < nq ? q : 0);
-        rp[k] = bv.rec_p[slot];
-        rv[k] = bv.rec_v[slot];
+        rp[k] = bv.rec_p[slot_of(k)];
+        rv[k] = bv.rec_v[slot_of(k)];
     }
 #pragma unroll
     for (int k = 0; k < kEvalPerThread; ++k) {
-        const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
-        const int kind = __float_as_int(rp[k].w);
-        if (q < nq && kind != 0) {
-            double J[6], res;
-            const d3 pp = mk((double)rp[k].x, (double)rp[k].y, (double)rp[k].z);
-            const RecV& v = rv[k];
-            if (kind == LMSF_EDGE) {
-                const double2 e = bv.rec_e[(size_t)b * bv.feat_stride + q];
-                res = edge_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), mk(v.v[3], e.x, e.y), J);
-            } else {
-                res = surf_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), v.v[3], J);
-            }
-            huber_accumulate(P, res, J);
-        }
+        const bool edge = __float_as_int(rp[k].w) == LMSF_EDGE;
+        eval_record(Ps, q0 + k * 256 < nq, rp[k], rv[k], edge ? bv.rec_e[slot_of(k)] : make_double2(0.0, 0.0), P);
     }
+#endif
     block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + blockIdx.x) * kPacket);
 }
 

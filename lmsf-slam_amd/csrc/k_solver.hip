@@ -38,7 +38,7 @@ __global__ void state_init_kernel(BatchView bv, const double* poses) {
 }
 
 // After fit_eval: IterationZero (evaluate at x0, jacobi scaling, gradient check) + first step.
-__global__ __launch_bounds__(64) void lm_begin_kernel(BatchView bv) {
+__global__ __launch_bounds__(kBeginThreads) void lm_begin_kernel(BatchView bv) {
     const int b = blockIdx.x;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
     double tot[kPacket];
@@ -280,7 +280,7 @@ hipError_t launch_state_init(const BatchView& bv, const double* poses, hipStream
 }
 
 hipError_t launch_lm_begin(const BatchView& bv, hipStream_t s) {
-    hipLaunchKernelGGL(lm_begin_kernel, dim3(bv.B), dim3(64), 0, s, bv);
+    hipLaunchKernelGGL(lm_begin_kernel, dim3(bv.B), dim3(kBeginThreads), 0, s, bv);
     return hipGetLastError();
 }
 

@@ -10,34 +10,45 @@
 #include "lmsf_internal.h"
 
 namespace lmsf {
+constexpr int kBeginThreads = 512;   // lm_begin_kernel block: 8 waves share the packet loads
+
 namespace {
 
 constexpr int kMaxInner = 4;  // options.max_num_iterations (ceres_...:118)
 
 // Sum the packets [0, nparts) and [base2, base2 + n2) of slot b in a fixed order; result valid in
-// every lane.  Lane l owns entry l % 32 of the packets p = l / 32 (mod 2): the loads are coalesced
-// and all in flight at once (one latency, not one per entry), then the two halves add in one shuffle.
+// every thread.  Wave w, lane l owns entry l % 32 of the packets p = 2 w + l / 32 (mod 2 waves): the
+// loads are coalesced and 8 per lane in flight, the two halves add in one shuffle and the waves'
+// sums in wave order through LDS.  Every wave of the block loads (lm_begin: kBeginThreads, 1.5k
+// packets per slot at C2 -- one wave took 60 us, latency-bound).
 __device__ void reduce_parts(const BatchView& bv, int b, int nparts, double* tot, int base2 = 0, int n2 = 0) {
     static_assert(kPacket == 32, "one packet entry per half-wave lane");
-    __shared__ double red[kPacket];
-    const int lane = threadIdx.x, e = lane & 31;
+    constexpr int kMaxWaves = 16;
+    __shared__ double red[kMaxWaves][kPacket];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 31;
+    const int nw = min((int)(blockDim.x >> 6), kMaxWaves);
+    const int stride = 2 * nw;   // a wave reads two packets per load (one per half-wave)
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int range = 0; range < 2 && lane < 64; ++range) {   // wave 0 loads; every thread reaches the barrier
+    for (int range = 0; range < 2 && wave < nw; ++range) {   // every thread reaches the barrier
         const int np = range ? n2 : nparts;
         const double* base = bv.partials + ((size_t)b * bv.max_parts + (range ? base2 : 0)) * kPacket;
-        int p = lane >> 5;
-        for (; p + 14 < np; p += 16) {   // 8 independent loads in flight per lane
+        int p = 2 * wave + (lane >> 5);
+        for (; p + 7 * stride < np; p += 8 * stride) {   // 8 independent loads in flight per lane
 #pragma unroll
-            for (int u = 0; u < 8; ++u) acc[u] += base[(size_t)(p + 2 * u) * kPacket + e];
+            for (int u = 0; u < 8; ++u) acc[u] += base[(size_t)(p + u * stride) * kPacket + e];
         }
-        for (; p < np; p += 2) acc[0] += base[(size_t)p * kPacket + e];
+        for (; p < np; p += stride) acc[0] += base[(size_t)p * kPacket + e];
     }
     double v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     v += __shfl_xor(v, 32, 64);
-    if (lane < 32) red[e] = v;   // wave 0's first half
+    if (lane < 32 && wave < nw) red[wave][e] = v;
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < kPacket; ++i) tot[i] = red[i];
+    for (int i = 0; i < kPacket; ++i) {
+        double t = red[0][i];
+        for (int w = 1; w < nw; ++w) t += red[w][i];
+        tot[i] = t;
+    }
 }
 
 __device__ double norm7(const double* x) {

@@ -11,7 +11,13 @@ constexpr int kMaxOuter = 32;        // trace rows kept per solve
 constexpr int kPacket = 32;          // doubles per partial packet (29 used + edge/surf counts)
 constexpr int kFitMaxPerThread = 4;  // queries per thread in the fit / first-evaluation kernel (1..4)
 constexpr int kFitBlockMax = 256 * kFitMaxPerThread;
-constexpr int kEvalPerThread = 4;    // records per thread in the LM evaluation kernel
+#ifndef LMSF_EVAL_PER_THREAD
+#define LMSF_EVAL_PER_THREAD 4
+#endif
+#ifndef LMSF_EVAL_PIPE
+#define LMSF_EVAL_PIPE 0
+#endif
+constexpr int kEvalPerThread = LMSF_EVAL_PER_THREAD;   // records per thread in the LM evaluation kernel
 constexpr int kEvalBlock = 256 * kEvalPerThread;
 // Workspace growth: when a request exceeds the capacity, allocate 1.5x (a growing or jittering
 // request -- the keyframe window, a varying scan size -- then reallocates rarely: hipFree
