@@ -208,7 +208,7 @@ def sum_stats(stats):
     import types
     return types.SimpleNamespace(**{f: sum(getattr(k, f) for k in stats)
                                     for f in ("launches", "total_ms", "queries", "n27_sum", "fused_launches",
-                                              "reused_queries")})
+                                              "reused_queries", "refit_queries")})
 
 
 def shared_map(d, make):
@@ -251,15 +251,17 @@ def knn_roofline(ks, mean_n27, tj, elapsed_s, note):
     dispatch, MI355X_MICROARCH.md's gfx950 correction, from the committed rocprofv3 passes `tj`) /
     average HIP-event launch time.  `rocprof` recomputes the same from the profiler's own mean duration
     of that kernel in the PMC run.  `model` is SURVEY 8(d)'s algorithmic figure, sum over the queries
-    that searched of [16 (query) + 27*8 (cell ranges) + 16 n27(q)] + 16 B per memo-reused query (n27 per
+    that searched of [16 (query) + 27*8 (cell ranges) + 16 n27(q)] + 16 B per memo-reused query + 16 + 5*16 B
+    per refitted query (its 5 neighbours gathered, no walk) (n27 per
     searched query from the counted untimed step); it counts every candidate read as an HBM read while
     the 16 MB map + index stay in L2 / Infinity Cache, hence `exceeds_peak` when it would imply more
     than the HBM peak (per launch or over the whole timed window)."""
     launches = max(int(ks.launches), 1)
     avg_launch_ms = ks.total_ms / launches
     reused = int(getattr(ks, "reused_queries", 0))
-    searched = int(ks.queries) - reused
-    model_bytes = (searched * (16 + 27 * 8 + 16 * mean_n27) + reused * 16) / launches
+    refit = int(getattr(ks, "refit_queries", 0))
+    searched = int(ks.queries) - reused - refit
+    model_bytes = (searched * (16 + 27 * 8 + 16 * mean_n27) + reused * 16 + refit * (16 + 5 * 16)) / launches
     model_gbs = model_bytes / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     model_wall_gbs = model_bytes * launches / elapsed_s / 1e9 if elapsed_s > 0 else 0.0
     traffic = int(tj["hbm_bytes_per_launch"]) if tj else None
@@ -273,6 +275,7 @@ def knn_roofline(ks, mean_n27, tj, elapsed_s, note):
            "kernel": kernel_name(ks), "avg_launch_ms": round(avg_launch_ms, 4), "launches": int(ks.launches),
            "queries_per_launch": int(ks.queries / launches),
            "reused_query_frac": round(reused / max(int(ks.queries), 1), 4),
+           "refit_query_frac": round(refit / max(int(ks.queries), 1), 4),
            "l2_hit_rate": round(tj["l2_hit_rate"], 3) if tj and tj.get("l2_hit_rate") is not None else None,
            "model": {"bytes_per_launch": int(model_bytes), "searched_queries_per_launch": int(searched / launches),
                      "mean_n27": round(mean_n27, 1), "gbs": round(model_gbs, 1),

@@ -219,7 +219,8 @@ lmsf_status lmsf_eval(lmsf_ctx* ctx, const double pose[7], double out[29]);
  * kernel (batch launches with the Ceres-LM solver; the fit is then inside the timed launch).
  * reused_queries: queries of those launches (outer iterations > 0) that moved less than half the
  * neighbour-distance gap of their last full search, so their 5-NN set and fit were reused without a
- * search (counted with the queries; DESIGN.md "Query memo"). */
+ * search (counted with the queries; DESIGN.md "Query memo"); refit_queries: queries whose 5-NN set was
+ * unchanged but reordered, refitted from the memo without a walk. */
 #define LMSF_STATS_TIMING 1
 #define LMSF_STATS_N27 2
 typedef struct {
@@ -229,6 +230,7 @@ typedef struct {
     int64_t n27_sum;
     int64_t fused_launches;
     int64_t reused_queries;
+    int64_t refit_queries;
 } lmsf_kernel_stats;
 lmsf_status lmsf_kernel_stats_get(lmsf_ctx* ctx, lmsf_kernel_stats* out);
 lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* ctx, int32_t mode);

@@ -89,6 +89,18 @@ bool memo_bound_enabled() {
     return v;
 }
 
+// LMSF_MEMO_REFIT = 0 | 1 (A/B, default 1): memo hits whose neighbours changed order are refitted from the
+// memo pass's list without a walk (k_match.hip); 0 sends them to the search.
+bool memo_exact_enabled() {   // LMSF_MEMO_EXACT = 0 | 1 (A/B, default 1), read per launch
+    const char* e = getenv("LMSF_MEMO_EXACT");
+    return e ? atoi(e) != 0 : true;
+}
+
+bool memo_refit_enabled() {   // read per launch, so a test can compare both in one process
+    const char* e = getenv("LMSF_MEMO_REFIT");
+    return e ? atoi(e) != 0 : true;
+}
+
 template <typename T>
 hipError_t dalloc(T** p, size_t count) {
     *p = nullptr;
@@ -211,6 +223,8 @@ struct lmsf_ctx {
         v.wl = wl;
         v.wlim = wlim;
         v.memo_bound = memo_bound_enabled() ? 1 : 0;
+        v.memo_refit = memo_refit_enabled() ? 1 : 0;
+        v.memo_exact = memo_exact_enabled() ? 1 : 0;
         v.wcount = wcount;
         v.n_search = n_search;
         v.fused_parts = 0;            // set for the fused path's lm_begin (enqueue_register)
@@ -1188,11 +1202,12 @@ lmsf_status lmsf_kernel_stats_get(lmsf_ctx* c, lmsf_kernel_stats* out) {
     if (rc) return rc;
     std::vector<unsigned long long> sh((size_t)kCounterShards * 16, 0);
     HIPCHK(c, hipMemcpy(sh.data(), c->d_n27, sh.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    unsigned long long n27 = 0, q = 0, r = 0;
+    unsigned long long n27 = 0, q = 0, r = 0, rf = 0;
     for (int i = 0; i < kCounterShards; ++i) {
         n27 += sh[(size_t)i * 16];
         q += sh[(size_t)i * 16 + 1];
         r += sh[(size_t)i * 16 + 2];
+        rf += sh[(size_t)i * 16 + 3];
     }
     out->launches = c->knn_launches;
     out->fused_launches = c->fused_launches;
@@ -1200,6 +1215,7 @@ lmsf_status lmsf_kernel_stats_get(lmsf_ctx* c, lmsf_kernel_stats* out) {
     out->queries = (int64_t)q;
     out->n27_sum = (int64_t)n27;
     out->reused_queries = (int64_t)r;
+    out->refit_queries = (int64_t)rf;
     return LMSF_OK;
 }
 

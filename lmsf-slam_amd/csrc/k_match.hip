@@ -417,27 +417,39 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
         float lim = kFullLim;
         if (MEMO && bv.memo) {   // every lane of the team decides alike (same loads, same arithmetic)
             const float4 pw = bv.prevw[slot];
-            if (pw.w > 0.f) {
+            if (pw.w >= 0.f) {
                 const double dx = (double)w.x - pw.x, dy = (double)w.y - pw.y, dz = (double)w.z - pw.z;
                 const double dd = sqrt(dx * dx + dy * dy + dz * dz);
-                const double r6 = (double)__int_as_float(bv.memo_nbr[((size_t)b * kMemoWords + 5) * bv.feat_stride + q]) +
-                                  dd + 1e-5;
+                const double s6 = (double)__int_as_float(bv.memo_nbr[((size_t)b * kMemoWords + 5) * bv.feat_stride + q]);
+                const double r6 = s6 + dd + 1e-5;
                 if (r6 < 1.0 && bv.memo_bound) lim = fminf(kFullLim, (float)(r6 * r6) + 1e-5f);
-                if (2.0 * dd + 1e-5 < (double)pw.w) {
-                    double k5[5];
-                    uint32_t idx[5];
+                double k5[5];
+                float4 m[5];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    m[j] = nn_out[j];
+                    k5[j] = nn_key(w, m[j], (uint32_t)__float_as_int(m[j].w));
+                }
+                key_cswap(k5[0], k5[1]); key_cswap(k5[3], k5[4]); key_cswap(k5[2], k5[4]);
+                key_cswap(k5[2], k5[3]); key_cswap(k5[0], k5[3]); key_cswap(k5[0], k5[2]);
+                key_cswap(k5[1], k5[4]); key_cswap(k5[1], k5[3]); key_cswap(k5[1], k5[2]);
+                // the stored 5 are still the 5 nearest when the farthest of them is nearer than any
+                // other point can have come (those were >= s6 from w0, so >= s6 - d from w)
+                bool same = true;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) same = same && (uint32_t)key_bits(k5[j]) == (uint32_t)__float_as_int(m[j].w);
+                reuse = key_bits(k5[4]) < kSentinel &&
+                        (bv.memo_exact ? sqrt((double)key_d2(k5[4])) + dd + 1e-5 < s6   // A/B: r01's gap test
+                                       : same && 2.0 * dd + 1e-5 < (double)pw.w);
+                if (reuse && !same && lane == 0) {   // a new order of the same set: what the walk would write
 #pragma unroll
                     for (int j = 0; j < 5; ++j) {
-                        const float4 m = nn_out[j];
-                        idx[j] = (uint32_t)__float_as_int(m.w);
-                        k5[j] = nn_key(w, m, idx[j]);
-                    }
-                    key_cswap(k5[0], k5[1]); key_cswap(k5[3], k5[4]); key_cswap(k5[2], k5[4]);
-                    key_cswap(k5[2], k5[3]); key_cswap(k5[0], k5[3]); key_cswap(k5[0], k5[2]);
-                    key_cswap(k5[1], k5[4]); key_cswap(k5[1], k5[3]); key_cswap(k5[1], k5[2]);
-                    reuse = key_bits(k5[4]) < kSentinel;
+                        float4 o = m[0];
 #pragma unroll
-                    for (int j = 0; j < 5; ++j) reuse = reuse && (uint32_t)key_bits(k5[j]) == idx[j];
+                        for (int i = 1; i < 5; ++i)
+                            if ((uint32_t)__float_as_int(m[i].w) == (uint32_t)key_bits(k5[j])) o = m[i];
+                        nn_out[j] = o;
+                    }
                 }
             }
         }
@@ -794,7 +806,7 @@ __host__ __device__ __forceinline__ size_t memo_blocks(size_t feat_stride) { ret
 // so the new 6 nearest do too, and a walk over the rows / x-slices within min(1 m, s6 + d) (+ margin)
 // returns the same 6 keys as the full 1 m walk.  One packet per wave at partial index 4 bx + wave.
 __global__ __launch_bounds__(256) void match_memo_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
-    __shared__ int wcnt[4];
+    __shared__ int wcnt[8];
     int bx, b;
     block_coords(remap, gx, bx, b);
     const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
@@ -804,6 +816,8 @@ __global__ __launch_bounds__(256) void match_memo_kernel(GridView ge, GridView g
     const Pose Ps = load_pose(bv.st[b].x);
     const int i = bx * 256 + threadIdx.x;
     bool need = i < nq;
+    bool refit = false;   // same 5 neighbours in a new order: fit without a walk
+    unsigned int n_refit = 0;
     unsigned int n_reused = 0;
     float lim = kFullLim;   // a miss's search radius^2: the 6 nearest at w0 are within s6 + d of w
     double P[kPacket];
@@ -814,14 +828,15 @@ __global__ __launch_bounds__(256) void match_memo_kernel(GridView ge, GridView g
         const float4 p = bv.featp[pos];
         const int q = __float_as_int(p.w);
         const float4 pw = bv.prevw[pos];
-        if (q >= 0 && q < nq && pw.w > 0.f) {
+        if (q >= 0 && q < nq && pw.w >= 0.f) {
             const size_t slot = pos;
             const float3 w = associate(Ps, p);
             const double dx = (double)w.x - pw.x, dy = (double)w.y - pw.y, dz = (double)w.z - pw.z;
             const double dd = sqrt(dx * dx + dy * dy + dz * dz);
-            const double r6 = (double)__int_as_float(bv.memo_nbr[((size_t)b * kMemoWords + 5) * F + i]) + dd + 1e-5;
+            const double s6 = (double)__int_as_float(bv.memo_nbr[((size_t)b * kMemoWords + 5) * F + i]);
+            const double r6 = s6 + dd + 1e-5;
             if (r6 < 1.0 && bv.memo_bound) lim = fminf(kFullLim, (float)(r6 * r6) + 1e-5f);
-            if (2.0 * dd + 1e-5 < (double)pw.w) {
+            if (bv.memo_exact || 2.0 * dd + 1e-5 < (double)pw.w) {
                 const float4* orig = q < ne ? ge.orig : gs.orig;
                 uint32_t idx[5];
                 double k[5];
@@ -833,9 +848,13 @@ __global__ __launch_bounds__(256) void match_memo_kernel(GridView ge, GridView g
                 key_cswap(k[0], k[1]); key_cswap(k[3], k[4]); key_cswap(k[2], k[4]);
                 key_cswap(k[2], k[3]); key_cswap(k[0], k[3]); key_cswap(k[0], k[2]);
                 key_cswap(k[1], k[4]); key_cswap(k[1], k[3]); key_cswap(k[1], k[2]);
-                bool same = key_bits(k[4]) < kSentinel;   // all five still inside the radius
+                // all five still inside the radius and still the 5 nearest: the farthest of them is nearer
+                // than any other point can have come (those were >= s6 from w0, so >= s6 - d from w)
+                const bool inside = key_bits(k[4]) < kSentinel && sqrt((double)key_d2(k[4])) + dd + 1e-5 < s6;
+                bool same = inside;
 #pragma unroll
                 for (int j = 0; j < 5; ++j) same = same && (uint32_t)key_bits(k[j]) == idx[j];
+                refit = inside && bv.memo_refit;   // cleared below when the stored record is reused
                 if (same) {
                     const int kind = __float_as_int(bv.rec_p[slot].w);
                     d3 v0 = mk(0, 0, 0);
@@ -867,41 +886,62 @@ __global__ __launch_bounds__(256) void match_memo_kernel(GridView ge, GridView g
                     if (reuse) {
                         record_packet(kind, p, v0, v1x, v1y, v1z, Ps, P);
                         need = false;
+                        refit = false;
                         n_reused = 1;
                     }
+                }
+                if (refit) {   // the set's new order is what a search would return: keep it for the fit
+#pragma unroll
+                    for (int j = 0; j < 5; ++j)
+                        bv.memo_nbr[((size_t)b * kMemoWords + j) * F + i] = (int)(uint32_t)key_bits(k[j]);
+                    need = false;
+                    n_refit = 1;
                 }
             }
         }
     }
     if (bx * 256 + wave * 64 < nq)
         wave_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + (size_t)bx * 4 + wave) * kPacket);
-    // this block's positions still needing a search, in position order (deterministic)
-    const unsigned long long m = __ballot(need);
-    if (lane == 0) wcnt[wave] = __popcll(m);
+    // this block's positions still needing a search, in position order from the front of its segment,
+    // and those needing only a refit, in position order from its back (deterministic)
+    const unsigned long long m = __ballot(need), mr = __ballot(refit);
+    if (lane == 0) {
+        wcnt[wave] = __popcll(m);
+        wcnt[4 + wave] = __popcll(mr);
+    }
     __syncthreads();
-    int before = 0, total = 0;
+    int before = 0, total = 0, before_r = 0, total_r = 0;
 #pragma unroll
     for (int w4 = 0; w4 < 4; ++w4) {
         before += w4 < wave ? wcnt[w4] : 0;
         total += wcnt[w4];
+        before_r += w4 < wave ? wcnt[4 + w4] : 0;
+        total_r += wcnt[4 + w4];
     }
+    const unsigned long long below = (1ull << lane) - 1ull;
     if (need) {
-        const size_t at = (size_t)b * F + (size_t)bx * 256 + before + __popcll(m & ((1ull << lane) - 1ull));
+        const size_t at = (size_t)b * F + (size_t)bx * 256 + before + __popcll(m & below);
         bv.wl[at] = i;
         bv.wlim[at] = lim;
     }
-    if (threadIdx.x == 0) bv.wcount[(size_t)b * memo_blocks(F) + bx] = total;
+    if (refit) {
+        const int seg = min(256, nq - bx * 256);
+        bv.wl[(size_t)b * F + (size_t)bx * 256 + seg - 1 - (before_r + __popcll(mr & below))] = i;
+    }
+    if (threadIdx.x == 0) bv.wcount[(size_t)b * memo_blocks(F) + bx] = total | (total_r << 16);
     if (bv.n27) {   // accounting runs: queries and reused ones
         unsigned int qn = i < nq ? 1u : 0u;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
             qn += __shfl_xor(qn, o, 64);
             n_reused += __shfl_xor(n_reused, o, 64);
+            n_refit += __shfl_xor(n_refit, o, 64);
         }
         if (lane == 0) {
             unsigned long long* shard = bv.n27 + (size_t)((blockIdx.x * 4 + wave) & (kCounterShards - 1)) * 16;
             if (qn) atomicAdd(shard + 1, (unsigned long long)qn);
             if (n_reused) atomicAdd(shard + 2, (unsigned long long)n_reused);
+            if (n_refit) atomicAdd(shard + 3, (unsigned long long)n_refit);
         }
     }
 }
@@ -930,7 +970,7 @@ __global__ __launch_bounds__(256) void match_memo_kernel(GridView ge, GridView g
 #endif
 template <bool PRUNE, bool LIST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void match_fit_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
-    extern __shared__ int soff[];   // LIST: exclusive prefix of the memo blocks' counts, [nblk + 1]
+    extern __shared__ int soff[];   // LIST: exclusive prefixes of the memo blocks' search / refit counts, 2 x [nblk + 1]
     constexpr bool kMemo = !PRUNE;
     constexpr int kNK = kMemo ? 6 : 5;
     int bx, b;
@@ -938,37 +978,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
     const size_t F = bv.feat_stride;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int total = nq, nblk = 0;
-    if constexpr (LIST) {
-        __shared__ int wsum[4];
+    int total = nq, nblk = 0, total_s = nq;
+    int* roff = soff;
+    if constexpr (LIST) {   // block counts: searches in the low 16 bits, refits in the high 16
+        __shared__ int wsum[8];
         nblk = (nq + 255) / 256;
+        roff = soff + nblk + 1;
         const int* wc = bv.wcount + (size_t)b * memo_blocks(F);
         const int per = (nblk + 255) / 256;
         const int j0 = threadIdx.x * per;
-        int mine = 0;
-        for (int j = 0; j < per; ++j) mine += j0 + j < nblk ? wc[j0 + j] : 0;
-        int incl = mine;   // wave inclusive scan
+        int mine = 0, mine_r = 0;
+        for (int j = 0; j < per; ++j) {
+            const int c = j0 + j < nblk ? wc[j0 + j] : 0;
+            mine += c & 0xffff;
+            mine_r += c >> 16;
+        }
+        int incl = mine, incl_r = mine_r;   // wave inclusive scans
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(incl, o, 64);
+            const int t = __shfl_up(incl, o, 64), tr = __shfl_up(incl_r, o, 64);
             incl += lane >= o ? t : 0;
+            incl_r += lane >= o ? tr : 0;
         }
-        if (lane == 63) wsum[wave] = incl;
+        if (lane == 63) {
+            wsum[wave] = incl;
+            wsum[4 + wave] = incl_r;
+        }
         __syncthreads();
-        int run = incl - mine;
+        int run = incl - mine, run_r = incl_r - mine_r;
 #pragma unroll
-        for (int w4 = 0; w4 < 4; ++w4) run += w4 < wave ? wsum[w4] : 0;
+        for (int w4 = 0; w4 < 4; ++w4) {
+            run += w4 < wave ? wsum[w4] : 0;
+            run_r += w4 < wave ? wsum[4 + w4] : 0;
+        }
         for (int j = 0; j < per; ++j) {
             if (j0 + j < nblk) {
+                const int c = wc[j0 + j];
                 soff[j0 + j] = run;
-                run += wc[j0 + j];
+                roff[j0 + j] = run_r;
+                run += c & 0xffff;
+                run_r += c >> 16;
             }
         }
-        total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        if (threadIdx.x == 0) soff[nblk] = total;
+        total_s = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        total = total_s + wsum[4] + wsum[5] + wsum[6] + wsum[7];
+        if (threadIdx.x == 0) {
+            soff[nblk] = total_s;
+            roff[nblk] = total - total_s;
+        }
         __syncthreads();
     }
-    if (bx == 0 && threadIdx.x == 0) bv.n_search[b] = total;
+    if (bx == 0 && threadIdx.x == 0) bv.n_search[b] = total;   // listed entries (packets), refits included
     if (bx * 256 >= total) return;   // uniform per block, after the last barrier
     const Pose Ps = load_pose(bv.st[b].x);
     const int e = bx * 256 + threadIdx.x;
@@ -979,16 +1039,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     if (e < total) {
         int pos = e;
         float lim = kFullLim;
+        bool walk = true;
         if constexpr (LIST) {   // largest block whose list starts at or before e (empty blocks share offsets)
+            const bool rf = e >= total_s;   // refit entries follow the searches
+            const int er = rf ? e - total_s : e;
+            const int* off = rf ? roff : soff;
             int lo = 0, hi = nblk - 1;
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
-                if (soff[mid] <= e) lo = mid;
+                if (off[mid] <= er) lo = mid;
                 else hi = mid - 1;
             }
-            const size_t at = (size_t)b * F + (size_t)lo * 256 + (e - soff[lo]);
-            pos = bv.wl[at];
-            lim = bv.wlim[at];
+            if (!rf) {
+                const size_t at = (size_t)b * F + (size_t)lo * 256 + (er - off[lo]);
+                pos = bv.wl[at];
+                lim = bv.wlim[at];
+            } else {
+                const int seg = min(256, nq - lo * 256);
+                pos = bv.wl[(size_t)b * F + (size_t)lo * 256 + seg - 1 - (er - off[lo])];
+                walk = false;
+            }
         }
         const size_t ppos = (size_t)b * F + pos;
         const float4 p = bv.featp[ppos];        // the feature at this search position, w = its slot
@@ -1001,10 +1071,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         double k[kNK];
 #pragma unroll
         for (int j = 0; j < kNK; ++j) k[j] = sentinel;
+        if (walk) {
 #ifndef LMSF_AB_NOWALK   // A/B ablation builds only (tools/build_variant.sh): no search
-        knn_walk<1, false, PRUNE, LMSF_FUSED_UNROLL, kNK>(g, g, w, 0, bv.count27, k, c27, lim);
+            knn_walk<1, false, PRUNE, LMSF_FUSED_UNROLL, kNK>(g, g, w, 0, bv.count27, k, c27, lim);
 #endif
-        if (kMemo) {   // anchor for the memo pass: gap between the 5th and the 6th neighbour (capped at 1 m)
+        } else {   // refit: the memo pass left the 5 neighbours in their order at w (key bits: index only)
+#pragma unroll
+            for (int j = 0; j < 5; ++j)
+                k[j] = key_as_double((uint64_t)(uint32_t)bv.memo_nbr[((size_t)b * kMemoWords + j) * F + pos]);
+        }
+        if (kMemo && walk) {   // anchor for the memo pass: gap between the 5th and the 6th neighbour (capped at 1 m)
             float gap = -1.f;
             if (key_bits(k[4]) < kSentinel) {
                 const double s6 = sqrt((double)fminf(key_d2(k[5]), 1.0f));
@@ -1291,7 +1367,7 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
         hipLaunchKernelGGL((match_fit_kernel<true, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
     } else if (bv.memo) {
         hipLaunchKernelGGL(match_memo_kernel, grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
-        const size_t lds = (memo_blocks(bv.feat_stride) + 1) * sizeof(int);
+        const size_t lds = 2 * (memo_blocks(bv.feat_stride) + 1) * sizeof(int);
         hipLaunchKernelGGL((match_fit_kernel<false, true>), grid, dim3(256), lds, s, edge, surf, bv, gx, remap);
     } else {
         hipLaunchKernelGGL((match_fit_kernel<false, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);

@@ -101,11 +101,16 @@ struct BatchView {
     float* wlim;             // [B][feat_stride] the listed positions' search radius^2 (knn_walk lim)
     int memo;                // 1: match_memo_kernel ran before match_fit_kernel in this outer iteration
     int* wl;                 // [B][feat_stride] per block of the memo pass: the positions still needing a search
-    int* wcount;             // [B][feat_stride / 256 + 1] their count per memo block
+                             //   (from the front of the block's segment), then those needing a refit (from its back)
+    int* wcount;             // [B][feat_stride / 256 + 1] their counts per memo block: search | refit << 16
     int* n_search;           // [B] positions searched by the last match_fit_kernel (lm_begin's second range)
     int part2_base;          // packet index of match_fit_kernel's first wave packet (memo pass: [0, ceil(nq/64)))
     int fused_parts;         // lm_begin: packets laid out by the fused path (memo pass + search ranges)
     int memo_bound;          // memo misses search within min(1 m, s6 + d) (LMSF_MEMO_BOUND, default 1)
+    int memo_exact;          // memo: the stored 5 are kept when the farthest of them at w is nearer than s6 - d
+                             //   (LMSF_MEMO_EXACT, default 1; 0: r01's 2 d < s6 - s5)
+    int memo_refit;          // memo hits whose 5 neighbours changed order are refitted without a walk
+                             //   (LMSF_MEMO_REFIT, default 1)
 };
 
 // ---- launchers (each enqueues on `stream`, never synchronises)

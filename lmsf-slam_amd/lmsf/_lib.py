@@ -49,7 +49,8 @@ class FeatureCounts(C.Structure):
 
 class KernelStats(C.Structure):
     _fields_ = [("launches", C.c_int64), ("total_ms", C.c_double), ("queries", C.c_int64), ("n27_sum", C.c_int64),
-                ("fused_launches", C.c_int64), ("reused_queries", C.c_int64)]
+                ("fused_launches", C.c_int64), ("reused_queries", C.c_int64),
+                ("refit_queries", C.c_int64)]
 
 
 class ExtractParams(C.Structure):

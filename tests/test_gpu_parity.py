@@ -286,15 +286,18 @@ def test_batch_run_matches_oracle(lib, oracle_mod, small_workload):
     ks = ctx.kernel_stats()
     assert ks.launches == 5 and ks.fused_launches == 5               # the fused search + fit path ran
     assert ks.reused_queries > 0.1 * ks.queries                      # ... and the query memo fired
+    assert ks.refit_queries > 0                                      # ... and refitted reordered sets
     # outer iterations > 0 reuse the 5-NN set and fit of queries that moved less than half their
-    # neighbour-distance gap: same records, packets summed in another grouping (the searching lanes
-    # are packed), so the poses agree with re-searching every query to rounding
-    os.environ["LMSF_MEMO"] = "0"
-    try:
-        poses0, _ = ctx.batch_run(np.stack([wl.guess[i % n] for i in range(16)]))
-    finally:
-        del os.environ["LMSF_MEMO"]
-    assert np.abs(poses0 - poses).max() <= 1e-12
+    # neighbour-distance gap, and refit (without a walk) those whose set only changed order: same
+    # records, packets summed in another grouping (the searching lanes are packed), so the poses
+    # agree with re-searching every query (and with searching the reordered ones) to rounding
+    for var in ("LMSF_MEMO", "LMSF_MEMO_REFIT", "LMSF_MEMO_EXACT"):
+        os.environ[var] = "0"
+        try:
+            poses0, _ = ctx.batch_run(np.stack([wl.guess[i % n] for i in range(16)]))
+        finally:
+            del os.environ[var]
+        assert np.abs(poses0 - poses).max() <= 1e-12, var
     np.testing.assert_array_equal(poses[n:2 * n], poses[:n])          # same scan + guess -> same pose
     for i in range(len(wl.scans)):
         e, s = _features(oracle_mod, wl.scans[i])
