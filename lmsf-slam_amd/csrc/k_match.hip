@@ -31,6 +31,35 @@ constexpr uint64_t kSentinel = (uint64_t)(0x3f800000u + kKeyBias) << 32;  // key
 __device__ __forceinline__ double key_as_double(uint64_t k) { return __longlong_as_double((long long)k); }
 __device__ __forceinline__ uint64_t key_bits(double k) { return (uint64_t)__double_as_longlong(k); }
 __device__ __forceinline__ float key_d2(double k) { return __uint_as_float((uint32_t)(key_bits(k) >> 32) - kKeyBias); }
+// Keys are never NaN, so the min / max need none of the quieting (v_max_f64 x, x, x per operand built
+// from bits or carried around a loop) that fmin / fmax get in IEEE mode: 18 -> 11 f64 ops per candidate
+// of a 6-key insertion (C2 22.35k -> 22.7-22.8k scans/s, C5 2853 -> 2894-2904 pairs/s, r02).
+// LMSF_KEY_ASM = 0 (A/B build): fmin / fmax.  LMSF_KEY_PK = 1 (A/B build): (dx, dy) squared as packed
+// f32 pairs, 97 -> 79 VALU per 4 candidates but measured slower (C2 22.1-22.7k, C5 2847-2857).
+#ifndef LMSF_KEY_ASM
+#define LMSF_KEY_ASM 1
+#endif
+#ifndef LMSF_KEY_PK
+#define LMSF_KEY_PK 0
+#endif
+__device__ __forceinline__ double key_min(double a, double b) {
+#if LMSF_KEY_ASM
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fmin(a, b);
+#endif
+}
+__device__ __forceinline__ double key_max(double a, double b) {
+#if LMSF_KEY_ASM
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fmax(a, b);
+#endif
+}
 #ifndef LMSF_KNN_UNROLL
 #define LMSF_KNN_UNROLL 4
 #endif
@@ -145,13 +174,24 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
         if (count27) c27 += row[xb + 1] - row[xa];
     };
     auto consider = [&](const float4 m, uint32_t /*tagged_pos*/) {
+#if LMSF_KEY_PK
+        // (dx, dy) and their squares as packed pairs (v_pk_add_f32 / v_pk_mul_f32): the same
+        // roundings as the scalar expression, one instruction for two
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const f2v wxy = {w.x, w.y}, mxy = {m.x, m.y};
+        const f2v dxy = wxy - mxy;
+        const f2v sq = dxy * dxy;
+        const float dz = w.z - m.z;
+        const float d2 = (sq.x + sq.y) + dz * dz;
+#else
         const float dx = w.x - m.x, dy = w.y - m.y, dz = w.z - m.z;
         const float d2 = dx * dx + dy * dy + dz * dz;
+#endif
         double x = key_as_double(((uint64_t)(__float_as_uint(d2) + kKeyBias) << 32) | (uint32_t)__float_as_int(m.w));
 #pragma unroll
         for (int i = 0; i < NK; ++i) {
-            const double lo = fmin(k[i], x);
-            x = fmax(k[i], x);
+            const double lo = key_min(k[i], x);
+            x = key_max(k[i], x);
             k[i] = lo;
         }
     };
@@ -369,8 +409,8 @@ __device__ __forceinline__ double nn_key(const float3 w, const float4 m, uint32_
 }
 
 __device__ __forceinline__ void key_cswap(double& a, double& b) {
-    const double lo = fmin(a, b);
-    b = fmax(a, b);
+    const double lo = key_min(a, b);
+    b = key_max(a, b);
     a = lo;
 }
 
@@ -466,7 +506,7 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
             for (int i = 0; i < NK; ++i) {
                 double mn = k[0];
 #pragma unroll
-                for (int o = T / 2; o >= 1; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o, T));
+                for (int o = T / 2; o >= 1; o >>= 1) mn = key_min(mn, __shfl_xor(mn, o, T));
                 res[i] = mn;
                 if (key_bits(k[0]) == key_bits(mn)) {
 #pragma unroll

@@ -7,6 +7,6 @@ P=$R/lmsf-slam_amd
 B=$P/build_ab/$1
 mkdir -p $B $P/ab
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -w -I$R/include -I$P/csrc $2"
-ls $P/csrc/*.cpp $P/csrc/*.hip | xargs -P 8 -I{} sh -c "/opt/rocm/bin/hipcc $FL -x hip -c {} -o $B/\$(basename {}).o"
+ls $P/csrc/*.cpp $P/csrc/*.hip | grep -v /dist.cpp | xargs -P 8 -I{} sh -c "/opt/rocm/bin/hipcc $FL -x hip -c {} -o $B/\$(basename {}).o"
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $P/ab/liblmsf_$1.so $B/*.o
 echo "built $P/ab/liblmsf_$1.so"
