@@ -425,6 +425,7 @@ def run_batch(args, d):
     map_points = int(em_t.shape[0] + sm_t.shape[0])
     gathered = torch.zeros((world, n_units, 7), dtype=torch.float64, device=d.dev)
     poses = np.zeros((n_units, 7))
+    matches = np.zeros(n_units, np.int64)                    # residual blocks of each unit's last outer iteration
     stream_in = {"on": False}
     host_bufs = []
 
@@ -437,7 +438,8 @@ def run_batch(args, d):
                 if stream_in["on"]:                          # next step's scans, overlapped with this launch
                     cx.load_scans_async(*host_bufs[i])
             for i, cx, a, m in parts:
-                poses[a:a + m], _ = cx.batch_wait(m)
+                poses[a:a + m], st = cx.batch_wait(m)
+                matches[a:a + m] = [s.edge_matches + s.surf_matches for s in st]
         exchange_poses(cfg, poses, gathered, args.pairs, world, d.dev)
         return poses
 
@@ -534,6 +536,8 @@ def run_batch(args, d):
                   f"({U} distinct) over {S} context stream(s), scans HBM-resident")
             extra = {"batch_per_gpu": args.batch, "distinct_scans_per_gpu": U, "map_points": map_points,
                      "outer_iterations": args.outer, "parallelism": f"scan-sharded x{world}"}
+            if ks.launches and roof is not None:   # residual blocks the LM evaluations stream, over the features (queries) of the batch
+                roof["matched_record_frac"] = round(float(matches.sum()) / (ks.queries / ks.launches * S), 4)
             unit, scaling = "scans/s", "weak"
         else:
             metric = "LiDAR scan pairs/sec re-registered (128-beam 254k-pt scan, 10M-pt map, 1k pairs)"

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void ring_count_kernel(ExtractView ev) {
     if (t * kTile >= n && t > 0) return;
     for (int r = threadIdx.x; r < ev.n_scans; r += 256) cnt[r] = 0;
     __syncthreads();
-    const float4* raw = ev.raw + (size_t)b * ev.raw_stride;
+    const float4* raw = ev.raw + ev.raw_off[b];
     int8_t* rid = ev.ring_id + (size_t)b * ev.raw_stride;
     for (int k = threadIdx.x; k < kTile; k += 256) {
         const int i = t * kTile + k;
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void ring_scatter_kernel(ExtractView ev) {
     const int nt = (n + kTile - 1) / kTile;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int r = threadIdx.x; r < kMaxRings; r += 256) running[r] = 0;
-    const float4* raw = ev.raw + (size_t)b * ev.raw_stride;
+    const float4* raw = ev.raw + ev.raw_off[b];
     const int8_t* rid = ev.ring_id + (size_t)b * ev.raw_stride;
     const int* toff = ev.tile_counts + (size_t)b * kMaxRings * ev.n_tiles;
     float4* out = ev.ring_pts + (size_t)b * ev.raw_stride;

@@ -151,8 +151,9 @@ hipError_t launch_eval_at(const BatchView& bv, const double* pose_dev, double* o
 struct ExtractView {
     int B;
     int raw_stride;              // raw points per slot (capacity)
-    const float4* raw;           // [B][raw_stride]
+    const float4* raw;           // scans packed back to back: slot b's raw_count[b] points at raw + raw_off[b]
     const int* raw_count;        // [B]
+    const int64_t* raw_off;      // [B]
     int8_t* ring_id;             // [B][raw_stride]  (-1 rejected)
     int n_tiles;                 // tiles per slot (capacity)
     int* tile_counts;            // [B][kMaxRings][n_tiles]
