@@ -426,24 +426,30 @@ def run_batch(args, d):
     gathered = torch.zeros((world, n_units, 7), dtype=torch.float64, device=d.dev)
     poses = np.zeros((n_units, 7))
     matches = np.zeros(n_units, np.int64)                    # residual blocks of each unit's last outer iteration
+    enqueue_s = []                                           # host time inside lmsf_batch_launch, per step
     stream_in = {"on": False}
     host_bufs = []
 
     def step():
+        enq = 0.0
         for c0 in range(0, n_units, chunk):
             nb = min(chunk, n_units - c0)
             parts = [(i, cx, c0 + i * sub_b, min(sub_b, nb - i * sub_b)) for i, cx in enumerate(ctxs) if nb > i * sub_b]
             for i, cx, a, m in parts:                        # every context's batch enqueued before any wait
+                t_enq = time.perf_counter()
                 cx.batch_launch(guesses[a:a + m])
+                enq += time.perf_counter() - t_enq
                 if stream_in["on"]:                          # next step's scans, overlapped with this launch
                     cx.load_scans_async(*host_bufs[i])
             for i, cx, a, m in parts:
                 poses[a:a + m], st = cx.batch_wait(m)
                 matches[a:a + m] = [s.edge_matches + s.surf_matches for s in st]
         exchange_poses(cfg, poses, gathered, args.pairs, world, d.dev)
+        enqueue_s.append(enq)
         return poses
 
     elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, ctxs, not args.no_n27)
+    enqueue_ms = float(np.median(enqueue_s)) * 1e3
     ks = sum_stats([timed_stats(cx) for cx in ctxs])
     total_units = (args.batch * world if cfg == "C2" else args.pairs) * args.steps
     terr = [synth.pose_delta(poses[i], truth_u[unit_scan[i]]) for i in range(n_units)]
@@ -538,6 +544,7 @@ def run_batch(args, d):
                      "outer_iterations": args.outer, "parallelism": f"scan-sharded x{world}"}
             if ks.launches and roof is not None:   # residual blocks the LM evaluations stream, over the features (queries) of the batch
                 roof["matched_record_frac"] = round(float(matches.sum()) / (ks.queries / ks.launches * S), 4)
+            extra["host_enqueue_ms_per_step"] = round(enqueue_ms, 3)   # lmsf_batch_launch calls, all contexts
             unit, scaling = "scans/s", "weak"
         else:
             metric = "LiDAR scan pairs/sec re-registered (128-beam 254k-pt scan, 10M-pt map, 1k pairs)"

@@ -38,7 +38,7 @@ struct DevMap {
     bool occ_pending = false;
 
     GridView view() const {
-        GridView g;
+        GridView g{};   // zeroed padding: views are compared bytewise (SolveGraph key)
         g.ox = ox; g.oy = oy; g.oz = oz; g.nx = nx; g.ny = ny; g.nz = nz; g.sx = sx;
         g.off = off; g.pts = pts; g.orig = orig; g.n = n; g.lim1 = lim1;
         return g;
@@ -186,10 +186,20 @@ struct lmsf_ctx {
     // kernel accounting
     bool timing = false;    // LMSF_STATS_TIMING: HIP events around each neighbour-search launch
     bool count27 = false;   // LMSF_STATS_N27: n27 accounting inside the launch
-    hipEvent_t ev[2 * kEventPairs];
+    unsigned long long* d_stamps = nullptr;   // [2 * kEventPairs] wall-clock stamps around each search launch
+    unsigned long long* h_stamps = nullptr;   // pinned copy
+    double wall_khz = 0.0;
     int ev_used = 0;
     double knn_ms = 0.0;
     int64_t knn_launches = 0, knn_queries = 0, fused_launches = 0;
+    // state init + registration (lmsf_solve, lmsf_batch_launch) replayed as one HIP graph while nothing
+    // it captured by value changed: key = the batch and grid views, iterations and accounting modes
+    struct SolveGraph {
+        hipGraphExec_t exec = nullptr;
+        std::vector<unsigned char> key;
+        int64_t launches = 0, fused = 0;   // host accounting of one replay
+        int ev_used = 0;
+    } sg;
     // lmsf_voxel_filter workspace (grown on demand)
     VoxelFilter voxel;
     float4* vox_in = nullptr;
@@ -214,7 +224,7 @@ struct lmsf_ctx {
     }
 
     BatchView bview(int nb) const {
-        BatchView v;
+        BatchView v{};
         v.B = nb;
         v.feat_stride = F;
         v.feat = feat;
@@ -431,7 +441,7 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
     const bool gn = c->cfg.solver == LMSF_SOLVER_GN;
     for (int o = 0; o < iters; ++o) {
         const bool t = c->timing && c->ev_used + 2 <= 2 * kEventPairs;
-        if (t) HIPCHK(c, hipEventRecord(c->ev[c->ev_used], s));
+        if (t) HIPCHK(c, launch_stamp(c->d_stamps + c->ev_used, s));
         // batch launches: one fused search + fit kernel (it is then the timed neighbour-search launch)
         const bool fused = match_fit_applies(ge2, gs2, bv, c->cfg.solver);
         if (fused) {
@@ -446,7 +456,7 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
                                  bvk, gn ? 1 : 0, s, !gn && match_memo_enabled()));
         }
         if (t) {
-            HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 1], s));
+            HIPCHK(c, launch_stamp(c->d_stamps + c->ev_used + 1, s));
             c->ev_used += 2;
         }
         c->knn_launches++;
@@ -467,6 +477,84 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
     return LMSF_OK;
 }
 
+// LMSF_GRAPH = 0 | 1 (default 0; A/B): state init + registration as a replayed HIP graph.  A C2
+// context launch is ~65 dependent kernels: replay cuts its host enqueue (0.39 ms per C2 step for both
+// contexts) and the per-kernel dispatch gap (tools/graphprobe: 60 small kernels 160 -> 108 us on the
+// GPU, 159 -> 9 us to enqueue).  Measured r02 (tools/gpu_graph_ab.sh): C2 22.46k / 22.35k scans/s with
+// graphs vs 22.52k without (the step is GPU-bound, the enqueue already hidden); C4 2.00 vs 1.76 ms and
+// C3 1.83-1.90 vs 1.73 ms per scan (every keyframe moves the window grid, so the graph is re-captured and
+// re-instantiated).  Off by default.
+bool graphs_enabled() {
+    static bool v = [] {
+        const char* e = getenv("LMSF_GRAPH");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return v;
+}
+
+std::vector<unsigned char> solve_key(lmsf_ctx* c, int nb, int iters) {
+    std::vector<unsigned char> k;
+    auto put = [&](const void* p, size_t n) {
+        const unsigned char* b = static_cast<const unsigned char*>(p);
+        k.insert(k.end(), b, b + n);
+    };
+    const BatchView bv = c->bview(nb);
+    put(&bv, sizeof bv);
+    for (DevMap* ms : {c->map, c->prior})
+        for (int kind = 0; kind < 3; ++kind) {
+            const GridView g = ms[kind].view();
+            put(&g, sizeof g);
+        }
+    const int flags[] = {nb, iters, c->timing ? 1 : 0, c->count27 ? 1 : 0, match_memo_enabled() ? 1 : 0, c->cfg.solver};
+    put(flags, sizeof flags);
+    return k;
+}
+
+// State init from d_poses + the registration of slots [0, nb) on c->stream.
+lmsf_status enqueue_solve(lmsf_ctx* c, int nb, int iters) {
+    lmsf_status rl = resolve_all_lim1(c, (size_t)c->F * nb);   // host read-back: never inside a capture
+    if (rl) return rl;
+    hipStream_t s = c->stream;
+    if (!graphs_enabled() || c->ev_used != 0) {   // timing events not yet collected: direct launches
+        HIPCHK(c, launch_state_init(c->bview(nb), c->d_poses, s));
+        return enqueue_register(c, nb, iters);
+    }
+    std::vector<unsigned char> key = solve_key(c, nb, iters);
+    if (!c->sg.exec || key != c->sg.key) {
+        if (c->sg.exec) HIPCHK(c, hipGraphExecDestroy(c->sg.exec));
+        c->sg.exec = nullptr;
+        const int64_t l0 = c->knn_launches, f0 = c->fused_launches;
+        HIPCHK(c, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        const hipError_t e = launch_state_init(c->bview(nb), c->d_poses, s);
+        const lmsf_status rc = e == hipSuccess ? enqueue_register(c, nb, iters) : LMSF_ERR_HIP;
+        hipGraph_t g = nullptr;
+        const hipError_t ee = hipStreamEndCapture(s, &g);
+        c->sg.launches = c->knn_launches - l0;
+        c->sg.fused = c->fused_launches - f0;
+        c->sg.ev_used = c->ev_used;
+        c->knn_launches = l0;          // counted at each replay below
+        c->fused_launches = f0;
+        c->ev_used = 0;
+        if (rc || e != hipSuccess || ee != hipSuccess) {
+            if (g) hipGraphDestroy(g);
+            if (rc) return rc;
+            return c->fail(LMSF_ERR_HIP, "graph capture: %s", hipGetErrorString(e != hipSuccess ? e : ee));
+        }
+        const hipError_t ie = hipGraphInstantiate(&c->sg.exec, g, nullptr, nullptr, 0);
+        hipGraphDestroy(g);
+        if (ie != hipSuccess) {
+            c->sg.exec = nullptr;
+            return c->fail(LMSF_ERR_HIP, "graph instantiate: %s", hipGetErrorString(ie));
+        }
+        c->sg.key = std::move(key);
+    }
+    HIPCHK(c, hipGraphLaunch(c->sg.exec, s));
+    c->knn_launches += c->sg.launches;
+    c->fused_launches += c->sg.fused;
+    c->ev_used = c->sg.ev_used;
+    return LMSF_OK;
+}
+
 void fill_stats(const SolveState& S, lmsf_solve_stats* st) {
     st->outer_iterations = S.outer_run;
     st->edge_matches = S.edge_matches;
@@ -480,11 +568,11 @@ void fill_stats(const SolveState& S, lmsf_solve_stats* st) {
 
 lmsf_status collect_timing(lmsf_ctx* c) {
     if (!c->timing) return LMSF_OK;
-    for (int i = 0; i + 1 < c->ev_used; i += 2) {
-        float ms = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
-        c->knn_ms += ms;
-    }
+    if (c->ev_used < 2) return LMSF_OK;
+    HIPCHK(c, hipMemcpyAsync(c->h_stamps, c->d_stamps, c->ev_used * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i + 1 < c->ev_used; i += 2) c->knn_ms += (double)(c->h_stamps[i + 1] - c->h_stamps[i]) / c->wall_khz;
     c->ev_used = 0;
     return LMSF_OK;
 }
@@ -527,6 +615,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (!c) return;
     hipSetDevice(c->cfg.device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->sg.exec) hipGraphExecDestroy(c->sg.exec);
     for (DevMap* ms : {c->map, c->prior}) {
         for (int k = 0; k < 3; ++k) {
             DevMap& m = ms[k];
@@ -559,8 +648,8 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (c->ev_raw_free) hipEventDestroy(c->ev_raw_free);
     if (c->ev_raw_ready) hipEventDestroy(c->ev_raw_ready);
     if (c->copy_stream) hipStreamDestroy(c->copy_stream);
-    for (int i = 0; i < 2 * kEventPairs; ++i)
-        if (c->ev[i]) hipEventDestroy(c->ev[i]);
+    if (c->d_stamps) hipFree(c->d_stamps);
+    if (c->h_stamps) hipHostFree(c->h_stamps);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -574,7 +663,6 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || cfg->device < 0 || cfg->device >= ndev) return LMSF_ERR_HIP;
     lmsf_ctx* c = new lmsf_ctx();
-    std::memset(c->ev, 0, sizeof c->ev);
     c->cfg = *cfg;
     c->optimization_count = cfg->max_iterations;
     c->B = cfg->max_batch;
@@ -721,8 +809,7 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     const int iters = outer_iterations_for_solve(c);
     std::memcpy(c->h_poses, pose, 7 * sizeof(double));
     HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, launch_state_init(c->bview(1), c->d_poses, c->stream));
-    rc = enqueue_register(c, 1, iters);
+    rc = enqueue_solve(c, 1, iters);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1064,13 +1151,12 @@ lmsf_status lmsf_batch_launch(lmsf_ctx* c, int32_t n, const double* poses) {
     HIPCHK(c, launch_extract(c->eview(n), c->stream));
     HIPCHK(c, hipEventRecord(c->ev_raw_free, c->stream));
     c->qorder_valid = true;
-    HIPCHK(c, launch_state_init(c->bview(n), c->d_poses, c->stream));
     // every slot behaves as one Solve on a fresh registration object (ceres_...:100-101)
     int iters = c->optimization_count;
     if (c->cfg.solver == LMSF_SOLVER_CERES_LM && c->cfg.schedule == LMSF_SCHEDULE_REFERENCE_DECAY && iters > 2) --iters;
     iters = std::min(iters, kMaxOuter);
     c->features_on_device = false;
-    return enqueue_register(c, n, iters);
+    return enqueue_solve(c, n, iters);
 }
 
 lmsf_status lmsf_batch_wait(lmsf_ctx* c, int32_t n, double* poses, lmsf_solve_stats* stats) {
@@ -1192,8 +1278,13 @@ lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* c, int32_t mode) {
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const bool timing = (mode & LMSF_STATS_TIMING) != 0;
-    if (timing && !c->ev[0]) {
-        for (int i = 0; i < 2 * kEventPairs; ++i) HIPCHK(c, hipEventCreate(&c->ev[i]));
+    if (timing && !c->d_stamps) {
+        int khz = 0;
+        HIPCHK(c, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->cfg.device));
+        if (khz <= 0) return c->fail(LMSF_ERR_HIP, "device reports no wall-clock rate");
+        c->wall_khz = khz;
+        HIPCHK(c, dalloc(&c->d_stamps, 2 * kEventPairs));
+        HIPCHK(c, hipHostMalloc((void**)&c->h_stamps, 2 * kEventPairs * sizeof(unsigned long long), hipHostMallocDefault));
     }
     c->timing = timing;
     c->count27 = (mode & LMSF_STATS_N27) != 0;

@@ -274,6 +274,18 @@ __global__ __launch_bounds__(256) void gn_accum_kernel(BatchView bv) {
     }
 }
 
+// Kernel accounting (LMSF_STATS_TIMING): the device's constant-rate wall clock at this point of the
+// stream (every earlier kernel of the stream has finished).  Replaces HIP events, whose elapsed time
+// is not available for records made by graph nodes on this runtime.
+__global__ void stamp_kernel(unsigned long long* out) {
+    if (threadIdx.x == 0) out[0] = (unsigned long long)wall_clock64();
+}
+
+hipError_t launch_stamp(unsigned long long* out, hipStream_t s) {
+    hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, s, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_state_init(const BatchView& bv, const double* poses, hipStream_t s) {
     hipLaunchKernelGGL(state_init_kernel, dim3((bv.B + 63) / 64), dim3(64), 0, s, bv, poses);
     return hipGetLastError();

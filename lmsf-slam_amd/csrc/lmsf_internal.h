@@ -144,6 +144,7 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
 bool match_fit_prune(const GridView& edge, const GridView& surf);   // dense map: pruned walk, no memo
 bool match_memo_enabled();   // LMSF_MEMO (default 1)
 hipError_t launch_state_init(const BatchView& bv, const double* poses, hipStream_t s);
+hipError_t launch_stamp(unsigned long long* out, hipStream_t s);   // wall clock after the stream's prior work
 // Standalone evaluation at one pose (diagnostics): packet of slot 0 into out29 (device).
 hipError_t launch_eval_at(const BatchView& bv, const double* pose_dev, double* out_dev, hipStream_t s);
 
