@@ -46,8 +46,11 @@ DEFAULTS = {   # per configuration: batch (scans per launch), map points, column
     # over 2 context streams of 128 (measured, r01, with the query memo: 128 x 1 stream 19.0k scans/s,
     # 128 x 2 19.8k, 256 x 2 20.9k; before it 64 x 1 17.3k, 64 x 2 17.8k; 4 streams lose): one launch
     # per context is ~12 ms of latency, well inside a 10 Hz LiDAR's 100 ms
-    # 40 steps = ~0.5 s timed (a 4-step window is dominated by clock ramp / host jitter)
-    "C2": dict(batch=256, map_points=1_000_000, cols=4096, steps=40, warmup=2, streams=2),
+    # 40 steps = ~0.9 s timed (a 4-step window is dominated by clock ramp / host jitter)
+    # r02 (tools/gpu_ab_batch.sh, 128 slots per context): 256 x 2 streams 22.37-22.39k scans/s, 384 x 3
+    # 22.84k, 512 x 4 23.06-23.13k, 768 x 6 23.07k, 1024 x 8 22.92k, 1024 x 4 (256 per context) 22.92k,
+    # 512 x 8 (64 per context) 22.27k: four contexts of 128 fill the chip's gaps best (22 ms per step)
+    "C2": dict(batch=512, map_points=1_000_000, cols=4096, steps=40, warmup=2, streams=4),
     "C3": dict(batch=1, map_points=0, cols=4096, steps=20, warmup=3),
     "C4": dict(batch=1, map_points=5_000_000, cols=4096, steps=20, warmup=3),
     "C5": dict(batch=125, map_points=10_000_000, cols=2048, steps=2, warmup=1),
