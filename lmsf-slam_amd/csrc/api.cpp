@@ -91,6 +91,11 @@ bool memo_bound_enabled() {
 
 // LMSF_MEMO_REFIT = 0 | 1 (A/B, default 1): memo hits whose neighbours changed order are refitted from the
 // memo pass's list without a walk (k_match.hip); 0 sends them to the search.
+bool memo_order_enabled() {   // LMSF_MEMO_ORDER = 0 | 1 (A/B, default 1), read per launch
+    const char* e = getenv("LMSF_MEMO_ORDER");
+    return e ? atoi(e) != 0 : true;
+}
+
 bool memo_exact_enabled() {   // LMSF_MEMO_EXACT = 0 | 1 (A/B, default 1), read per launch
     const char* e = getenv("LMSF_MEMO_EXACT");
     return e ? atoi(e) != 0 : true;
@@ -238,6 +243,7 @@ struct lmsf_ctx {
         v.memo_bound = memo_bound_enabled() ? 1 : 0;
         v.memo_refit = memo_refit_enabled() ? 1 : 0;
         v.memo_exact = memo_exact_enabled() ? 1 : 0;
+        v.memo_order = memo_order_enabled() ? 1 : 0;
         v.wcount = wcount;
         v.n_search = n_search;
         v.fused_parts = 0;            // set for the fused path's lm_begin (enqueue_register)

@@ -832,6 +832,9 @@ __device__ __forceinline__ void record_packet(int kind, const float4 p, const d3
 // Entries of one memo block's work list per scan: wcount stride.
 __host__ __device__ __forceinline__ size_t memo_blocks(size_t feat_stride) { return feat_stride / 256 + 1; }
 
+#ifndef LMSF_MEMO_WAVES   // waves per SIMD the memo pass is compiled for (A/B)
+#define LMSF_MEMO_WAVES 5
+#endif
 // Query memo pass (outer iterations > 0 of a batch solve, sparse maps): one lane per search position
 // i (fslot order).  Position i's last full search left its anchor w0, gap = s6 - s5 and the 5
 // neighbour indices.  Every map point's distance to the query changes by at most d = |w - w0|, and
@@ -845,7 +848,7 @@ __host__ __device__ __forceinline__ size_t memo_blocks(size_t feat_stride) { ret
 // match_fit_kernel<., true>, with a search radius: the 6 nearest points at w0 lie within s6 + d of w,
 // so the new 6 nearest do too, and a walk over the rows / x-slices within min(1 m, s6 + d) (+ margin)
 // returns the same 6 keys as the full 1 m walk.  One packet per wave at partial index 4 bx + wave.
-__global__ __launch_bounds__(256) void match_memo_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_WAVES))) void match_memo_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
     __shared__ int wcnt[8];
     int bx, b;
     block_coords(remap, gx, bx, b);
@@ -876,7 +879,12 @@ __global__ __launch_bounds__(256) void match_memo_kernel(GridView ge, GridView g
             const double s6 = (double)__int_as_float(bv.memo_nbr[((size_t)b * kMemoWords + 5) * F + i]);
             const double r6 = s6 + dd + 1e-5;
             if (r6 < 1.0 && bv.memo_bound) lim = fminf(kFullLim, (float)(r6 * r6) + 1e-5f);
-            if (bv.memo_exact || 2.0 * dd + 1e-5 < (double)pw.w) {
+            // every distance moved by at most dd: with 2 dd + 1e-5 below every gap between consecutive
+            // neighbours and below s6 - s5, neither the set nor the order of the 5 nearest changed, and a
+            // search would return the stored keys -- no re-keying (r01's test, ahead of the exact one)
+            const double gord = (double)__int_as_float(bv.memo_nbr[((size_t)b * kMemoWords + 6) * F + i]);
+            bool same = bv.memo_order && 2.0 * dd + 1e-5 < gord;
+            if (!same && (bv.memo_exact || 2.0 * dd + 1e-5 < (double)pw.w)) {
                 const float4* orig = q < ne ? ge.orig : gs.orig;
                 uint32_t idx[5];
                 double k[5];
@@ -891,51 +899,52 @@ __global__ __launch_bounds__(256) void match_memo_kernel(GridView ge, GridView g
                 // all five still inside the radius and still the 5 nearest: the farthest of them is nearer
                 // than any other point can have come (those were >= s6 from w0, so >= s6 - d from w)
                 const bool inside = key_bits(k[4]) < kSentinel && sqrt((double)key_d2(k[4])) + dd + 1e-5 < s6;
-                bool same = inside;
+                same = inside;
 #pragma unroll
                 for (int j = 0; j < 5; ++j) same = same && (uint32_t)key_bits(k[j]) == idx[j];
-                refit = inside && bv.memo_refit;   // cleared below when the stored record is reused
-                if (same) {
-                    const int kind = __float_as_int(bv.rec_p[slot].w);
-                    d3 v0 = mk(0, 0, 0);
-                    double v1x = 0.0, v1y = 0.0, v1z = 0.0;
-                    bool reuse = true;
-                    if (kind != 0) {
-                        const RecV v = bv.rec_v[slot];
-                        v0 = mk(v.v[0], v.v[1], v.v[2]);
-                        v1x = v.v[3];
-                        if (kind == LMSF_SURF) {
-                            // surf_fit keeps its plane (n, D) when (float)(n . w + D) >= 0 and flips it
-                            // otherwise; the stored record is that plane up to sign, and negation is exact,
-                            // so t = (float)(n_s . w + D_s) = +-(the fit's test): t > 0 -> the stored record
-                            // is the fit's answer at w, t < 0 -> its negation; t == 0 is ambiguous (search)
-                            const d3 cp = mk((double)w.x, (double)w.y, (double)w.z);
-                            const float t = (float)(dot(v0, cp) + v1x);
-                            reuse = t != 0.f;
-                            if (t < 0.f) {
-                                v0 = mk(-v0.x, -v0.y, -v0.z);
-                                v1x = -v1x;
-                                store_record(bv, slot, p, kind, v0, v1x, 0.0, 0.0);
-                            }
-                        } else {
-                            const double2 e = bv.rec_e[slot];
-                            v1y = e.x;
-                            v1z = e.y;
-                        }
-                    }
-                    if (reuse) {
-                        record_packet(kind, p, v0, v1x, v1y, v1z, Ps, P);
-                        need = false;
-                        refit = false;
-                        n_reused = 1;
-                    }
-                }
+                refit = inside && !same && bv.memo_refit;
                 if (refit) {   // the set's new order is what a search would return: keep it for the fit
 #pragma unroll
                     for (int j = 0; j < 5; ++j)
                         bv.memo_nbr[((size_t)b * kMemoWords + j) * F + i] = (int)(uint32_t)key_bits(k[j]);
+                    bv.memo_nbr[((size_t)b * kMemoWords + 6) * F + i] = __float_as_int(-1.f);   // gaps are w0's order
                     need = false;
                     n_refit = 1;
+                }
+            }
+            if (same) {
+                const int kind = __float_as_int(bv.rec_p[slot].w);
+                d3 v0 = mk(0, 0, 0);
+                double v1x = 0.0, v1y = 0.0, v1z = 0.0;
+                bool reuse = true;
+                if (kind != 0) {
+                    const RecV v = bv.rec_v[slot];
+                    v0 = mk(v.v[0], v.v[1], v.v[2]);
+                    v1x = v.v[3];
+                    if (kind == LMSF_SURF) {
+                        // surf_fit keeps its plane (n, D) when (float)(n . w + D) >= 0 and flips it
+                        // otherwise; the stored record is that plane up to sign, and negation is exact,
+                        // so t = (float)(n_s . w + D_s) = +-(the fit's test): t > 0 -> the stored record
+                        // is the fit's answer at w, t < 0 -> its negation; t == 0 is ambiguous (search)
+                        const d3 cp = mk((double)w.x, (double)w.y, (double)w.z);
+                        const float t = (float)(dot(v0, cp) + v1x);
+                        reuse = t != 0.f;
+                        if (t < 0.f) {
+                            v0 = mk(-v0.x, -v0.y, -v0.z);
+                            v1x = -v1x;
+                            store_record(bv, slot, p, kind, v0, v1x, 0.0, 0.0);
+                        }
+                    } else {
+                        const double2 e = bv.rec_e[slot];
+                        v1y = e.x;
+                        v1z = e.y;
+                    }
+                }
+                if (reuse) {
+                    record_packet(kind, p, v0, v1x, v1y, v1z, Ps, P);
+                    need = false;
+                    refit = false;
+                    n_reused = 1;
                 }
             }
         }
@@ -1124,10 +1133,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
             float gap = -1.f;
             if (key_bits(k[4]) < kSentinel) {
                 const double s6 = sqrt((double)fminf(key_d2(k[5]), 1.0f));
-                gap = (float)(s6 - sqrt((double)key_d2(k[4])));
+                double sj = sqrt((double)key_d2(k[0])), gord = 1.0;
+#pragma unroll
+                for (int j = 1; j < 5; ++j) {   // the smallest gap between consecutive neighbours
+                    const double sn = sqrt((double)key_d2(k[j]));
+                    gord = fmin(gord, sn - sj);
+                    sj = sn;
+                }
+                gap = (float)(s6 - sj);
 #pragma unroll
                 for (int j = 0; j < 5; ++j) bv.memo_nbr[((size_t)b * kMemoWords + j) * F + pos] = (int)(uint32_t)key_bits(k[j]);
                 bv.memo_nbr[((size_t)b * kMemoWords + 5) * F + pos] = __float_as_int((float)s6);
+                bv.memo_nbr[((size_t)b * kMemoWords + 6) * F + pos] = __float_as_int((float)fmin(gord, s6 - sj));
             }
             bv.prevw[ppos] = make_float4(w.x, w.y, w.z, gap);
         }

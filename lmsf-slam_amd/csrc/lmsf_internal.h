@@ -30,7 +30,7 @@ constexpr int kEdgePerRing = 120;    // 20 per sector x 6 sectors (FX:172)
 constexpr int kQSurf = 0x40000000;  // ExtractView::qcode tag of a surf feature
 constexpr int kTile = 2048;          // raw points per ring-split tile
 constexpr int kCounterShards = 64;   // candidate / query counters, 16 u64 (128 B) apart
-constexpr int kMemoWords = 6;        // memo words per search position: 5 neighbour indices + s6
+constexpr int kMemoWords = 7;        // memo words per search position: 5 neighbour indices, s6, order gap
 
 // Dense cell grid over one feature map: cell = floor(coord) - origin, 1 m cells (the match
 // radius: search_thresh_ = 1.0 squared metres, REG/FeatureMatch/FeatureMatchBase.hpp:29).
@@ -97,7 +97,8 @@ struct BatchView {
                              //   and gap = s6 - s5 (s = distance of the k-th neighbour, the 6th capped at
                              //   the 1 m radius); w = -1 when fewer than 5 neighbours were found
     int* memo_nbr;           // [B][kMemoWords][feat_stride] that search's 5 neighbour map indices, nearest
-                             //   first, then s6 (float bits)
+                             //   first, then s6 (float bits), then (batch path) the order gap: min(s6 - s5,
+                             //   s(j+1) - s(j)) (float bits; -1 once a refit reordered the indices)
     float* wlim;             // [B][feat_stride] the listed positions' search radius^2 (knn_walk lim)
     int memo;                // 1: match_memo_kernel ran before match_fit_kernel in this outer iteration
     int* wl;                 // [B][feat_stride] per block of the memo pass: the positions still needing a search
@@ -107,6 +108,7 @@ struct BatchView {
     int part2_base;          // packet index of match_fit_kernel's first wave packet (memo pass: [0, ceil(nq/64)))
     int fused_parts;         // lm_begin: packets laid out by the fused path (memo pass + search ranges)
     int memo_bound;          // memo misses search within min(1 m, s6 + d) (LMSF_MEMO_BOUND, default 1)
+    int memo_order;          // memo: consecutive-gap test first (no re-keying when every gap exceeds 2 d)
     int memo_exact;          // memo: the stored 5 are kept when the farthest of them at w is nearer than s6 - d
                              //   (LMSF_MEMO_EXACT, default 1; 0: r01's 2 d < s6 - s5)
     int memo_refit;          // memo hits whose 5 neighbours changed order are refitted without a walk
