@@ -1213,6 +1213,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
 // agent-scope ticket with sc1 packet stores, measured slower in r02 on C2 / C3 / C4 -- 20.9k vs 22.1k
 // scans/s, 1.95 vs 1.73 ms per C3 frame, 2.12 vs 2.05 ms per C4 scan: the step code capped the
 // kernel at 128 VGPRs and its serial step lands on the launch's tail -- and was removed.)
+// Records per thread / occupancy (A/B, r02, tools/gpu_eval_ab.sh, C2 512 x 4): 4 records at 4 waves
+// (124 VGPRs) 22.69k scans/s; 2 records at 5 waves (96) 21.67-21.86k; 1 record at 6 waves (79) 21.03k --
+// fewer bytes in flight per lane and more block packets lose more than the occupancy gains.
+#ifndef LMSF_EVAL_WAVES   // waves per SIMD lm_eval_kernel is compiled for (A/B)
+#define LMSF_EVAL_WAVES 4
+#endif
 __device__ __forceinline__ void eval_record(const Pose& Ps, bool valid, const float4 rp, const RecV& v, const double2 e,
                                             double* P) {
     const int kind = __float_as_int(rp.w);
@@ -1227,7 +1233,7 @@ __device__ __forceinline__ void eval_record(const Pose& Ps, bool valid, const fl
     }
 }
 
-__global__ __launch_bounds__(256) void lm_eval_kernel(BatchView bv) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_EVAL_WAVES))) void lm_eval_kernel(BatchView bv) {
     const int b = blockIdx.y;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
     if (blockIdx.x * kEvalBlock >= nq) return;
