@@ -37,19 +37,8 @@ __global__ void state_init_kernel(BatchView bv, const double* poses) {
     S.edge_matches = S.surf_matches = S.nmatch = 0;
 }
 
-// After fit_eval: IterationZero (evaluate at x0, jacobi scaling, gradient check) + first step.
-__global__ __launch_bounds__(kBeginThreads) void lm_begin_kernel(BatchView bv) {
-    const int b = blockIdx.x;
-    const int nq = bv.n_edge[b] + bv.n_surf[b];
-    double tot[kPacket];
-    if (bv.fused_parts) {   // fused path: the memo pass's wave packets (when it ran), then the search's
-        reduce_parts(bv, b, bv.memo ? (nq + 63) / 64 : 0, tot, bv.part2_base, (bv.n_search[b] + 63) / 64);
-    } else {
-        const int fb = bv.part_q;
-        reduce_parts(bv, b, (nq + fb - 1) / fb, tot);
-    }
-    if (threadIdx.x != 0) return;
-    SolveState& S = bv.st[b];
+// IterationZero on the reduced first evaluation (tot) + the first step; one lane, S in LDS.
+__device__ __forceinline__ void lm_begin_apply(SolveState& S, const double* tot) {
     S.iteration = 0;
     S.need_eval = 0;
     S.done = 0;
@@ -78,6 +67,25 @@ __global__ __launch_bounds__(kBeginThreads) void lm_begin_kernel(BatchView bv) {
     compute_step(S);
 }
 
+
+// After fit_eval: IterationZero (evaluate at x0, jacobi scaling, gradient check) + first step.
+__global__ __launch_bounds__(kBeginThreads) void lm_begin_kernel(BatchView bv) {
+    const int b = blockIdx.x;
+    const int nq = bv.n_edge[b] + bv.n_surf[b];
+    __shared__ SolveState sS;
+    state_copy(sS, bv.st[b]);
+    __shared__ double tot[kPacket];
+    if (bv.fused_parts) {   // fused path: the memo pass's wave packets (when it ran), then the search's
+        reduce_parts(bv, b, bv.memo ? (nq + 63) / 64 : 0, tot, bv.part2_base, (bv.n_search[b] + 63) / 64);
+    } else {
+        const int fb = bv.part_q;
+        reduce_parts(bv, b, (nq + fb - 1) / fb, tot);
+    }   // (reduce_parts ends with a barrier: sS is in place)
+    if (threadIdx.x == 0) lm_begin_apply(sS, tot);
+    __syncthreads();
+    state_copy(bv.st[b], sS);
+}
+
 // After lm_eval_kernel at the candidate (LMSF_LM_FUSED=0): the reduction and lm_step_apply.
 __global__ __launch_bounds__(64) void lm_step_kernel(BatchView bv, int outer, int is_last) {
     const int b = blockIdx.x;
@@ -86,10 +94,14 @@ __global__ __launch_bounds__(64) void lm_step_kernel(BatchView bv, int outer, in
         if (is_last && threadIdx.x == 0) finish_outer(S, outer);
         return;
     }
+    __shared__ SolveState sS;
+    state_copy(sS, S);
     const int nq = bv.n_edge[b] + bv.n_surf[b];
-    double tot[kPacket];
-    reduce_parts(bv, b, (nq + kEvalBlock - 1) / kEvalBlock, tot);
-    if (threadIdx.x == 0) lm_step_apply(S, tot, outer, is_last);
+    __shared__ double tot[kPacket];
+    reduce_parts(bv, b, (nq + kEvalBlock - 1) / kEvalBlock, tot);   // ends with a barrier
+    if (threadIdx.x == 0) lm_step_apply(sS, tot, outer, is_last);
+    __syncthreads();
+    state_copy(S, sS);
 }
 
 // ---------------------------------------------------------------- GN (edgeSurfFeatureRegistration)
@@ -110,7 +122,7 @@ __global__ __launch_bounds__(64) void gn_solve_kernel(BatchView bv, int outer) {
     const int nq = bv.n_edge[b] + bv.n_surf[b];
     const int fb = 256 * bv.fit_per_thread;
     const int nparts = (nq + fb - 1) / fb;
-    double tot[kPacket];
+    __shared__ double tot[kPacket];
     BatchView g = bv;
     g.partials = bv.partials_gn;
     reduce_parts(g, b, nparts, tot);

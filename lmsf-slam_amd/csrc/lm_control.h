@@ -16,8 +16,8 @@ namespace {
 
 constexpr int kMaxInner = 4;  // options.max_num_iterations (ceres_...:118)
 
-// Sum the packets [0, nparts) and [base2, base2 + n2) of slot b in a fixed order; result valid in
-// every thread.  Wave w, lane l owns entry l % 32 of the packets p = 2 w + l / 32 (mod 2 waves): the
+// Sum the packets [0, nparts) and [base2, base2 + n2) of slot b in a fixed order into tot (LDS, valid
+// after the closing barrier; entry i summed by thread i, over the waves in wave order).  Wave w, lane l owns entry l % 32 of the packets p = 2 w + l / 32 (mod 2 waves): the
 // loads are coalesced and 8 per lane in flight, the two halves add in one shuffle and the waves'
 // sums in wave order through LDS.  Every wave of the block loads (lm_begin: kBeginThreads, 1.5k
 // packets per slot at C2 -- one wave took 60 us, latency-bound).
@@ -43,12 +43,23 @@ __device__ void reduce_parts(const BatchView& bv, int b, int nparts, double* tot
     v += __shfl_xor(v, 32, 64);
     if (lane < 32 && wave < nw) red[wave][e] = v;
     __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kPacket; ++i) {
+    if (threadIdx.x < kPacket) {
+        const int i = threadIdx.x;
         double t = red[0][i];
         for (int w = 1; w < nw; ++w) t += red[w][i];
         tot[i] = t;
     }
+    __syncthreads();
+}
+
+// A slot's SolveState staged in LDS around the one-lane LM control: every field access of the serial
+// step is then an LDS access instead of a dependent global-memory round trip.  Copied in / out by the
+// whole block (8-byte words); callers put a barrier between the copy and the lane that uses it.
+__device__ __forceinline__ void state_copy(SolveState& dst, const SolveState& src) {
+    static_assert(sizeof(SolveState) % 8 == 0, "SolveState copied as 8-byte words");
+    const long long* s = reinterpret_cast<const long long*>(&src);
+    long long* d = reinterpret_cast<long long*>(&dst);
+    for (int i = threadIdx.x; i < (int)(sizeof(SolveState) / 8); i += blockDim.x) d[i] = s[i];
 }
 
 __device__ double norm7(const double* x) {
@@ -69,24 +80,26 @@ __device__ __forceinline__ double grad_max_norm(const double* x, const double* g
     return m;
 }
 
-__device__ __forceinline__ bool chol_solve6(const double* A, const double* b, double* x) {
-    double L[36];
-#pragma unroll
-    for (int i = 0; i < 36; ++i) L[i] = 0.0;
+// Cholesky solve of the 6x6 SPD system in packed lower-triangular storage, in place (A[lidx(i, j)],
+// j <= i, becomes L): the arithmetic of the dense version, in 21 doubles instead of 2 x 36 -- the
+// one-lane LM control kernels then fit in fewer VGPRs and find a slot beside the search waves sooner.
+__device__ __forceinline__ constexpr int lidx(int i, int j) { return i * (i + 1) / 2 + j; }
+
+__device__ __forceinline__ bool chol_solve6(double* A, const double* b, double* x) {
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-        double s = A[j * 6 + j];
+        double s = A[lidx(j, j)];
 #pragma unroll
-        for (int k = 0; k < j; ++k) s -= L[j * 6 + k] * L[j * 6 + k];
+        for (int k = 0; k < j; ++k) s -= A[lidx(j, k)] * A[lidx(j, k)];
         if (!(s > 0.0)) return false;
-        double ljj = sqrt(s);
-        L[j * 6 + j] = ljj;
+        const double ljj = sqrt(s);
+        A[lidx(j, j)] = ljj;
 #pragma unroll
         for (int i = j + 1; i < 6; ++i) {
-            double t = A[i * 6 + j];
+            double t = A[lidx(i, j)];
 #pragma unroll
-            for (int k = 0; k < j; ++k) t -= L[i * 6 + k] * L[j * 6 + k];
-            L[i * 6 + j] = t / ljj;
+            for (int k = 0; k < j; ++k) t -= A[lidx(i, k)] * A[lidx(j, k)];
+            A[lidx(i, j)] = t / ljj;
         }
     }
     double y[6];
@@ -94,15 +107,15 @@ __device__ __forceinline__ bool chol_solve6(const double* A, const double* b, do
     for (int i = 0; i < 6; ++i) {
         double t = b[i];
 #pragma unroll
-        for (int k = 0; k < i; ++k) t -= L[i * 6 + k] * y[k];
-        y[i] = t / L[i * 6 + i];
+        for (int k = 0; k < i; ++k) t -= A[lidx(i, k)] * y[k];
+        y[i] = t / A[lidx(i, i)];
     }
 #pragma unroll
     for (int i = 5; i >= 0; --i) {
         double t = y[i];
 #pragma unroll
-        for (int k = i + 1; k < 6; ++k) t -= L[k * 6 + i] * x[k];
-        x[i] = t / L[i * 6 + i];
+        for (int k = i + 1; k < 6; ++k) t -= A[lidx(k, i)] * x[k];
+        x[i] = t / A[lidx(i, i)];
     }
 #pragma unroll
     for (int i = 0; i < 6; ++i)
@@ -117,21 +130,19 @@ __device__ __forceinline__ void compute_step(SolveState& S) {
         if (S.iteration >= kMaxInner) { S.done = 1; S.term = LMSF_TERM_MAX_ITERATIONS; return; }
         if (S.radius < 1e-32) { S.done = 1; S.term = LMSF_TERM_PARAMETER_TOL; return; }
         ++S.iteration;
-        double A[36], Hs[36], gs[6], nb[6], step[6];
+        // Hs = D H D (D = diag(s)) and A = Hs + diag(clamp(Hs_ii, 1e-6, 1e32)) / radius, lower triangle
+        double A[21], gs[6], nb[6], step[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             gs[i] = S.g[i] * S.s[i];
 #pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                const int a = i <= j ? hidx(i, j) : hidx(j, i);
-                Hs[i * 6 + j] = S.H[a] * S.s[i] * S.s[j];
-                A[i * 6 + j] = Hs[i * 6 + j];
-            }
+            for (int j = 0; j <= i; ++j) A[lidx(i, j)] = S.H[hidx(j, i)] * S.s[i] * S.s[j];
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            const double dg = fmin(fmax(Hs[i * 6 + i], 1e-6), 1e32);
-            A[i * 6 + i] += dg / S.radius;
+            const double hs = S.H[hidx(i, i)] * S.s[i] * S.s[i];
+            const double dg = fmin(fmax(hs, 1e-6), 1e32);
+            A[lidx(i, i)] = hs + dg / S.radius;
             nb[i] = -gs[i];
         }
         const bool ok = chol_solve6(A, nb, step);
@@ -143,7 +154,7 @@ __device__ __forceinline__ void compute_step(SolveState& S) {
                 sg += step[i] * gs[i];
                 double t = 0.0;
 #pragma unroll
-                for (int j = 0; j < 6; ++j) t += Hs[i * 6 + j] * step[j];
+                for (int j = 0; j < 6; ++j) t += S.H[i <= j ? hidx(i, j) : hidx(j, i)] * S.s[i] * S.s[j] * step[j];
                 sHs += step[i] * t;
             }
             mcc = -(sg + 0.5 * sHs);
