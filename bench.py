@@ -28,6 +28,7 @@ SURVEY 8(d) byte model (counted over the queries that actually searched) is repo
 `roofline.model`, flagged when it would exceed the HBM peak.
 """
 import argparse
+import collections
 import json
 import math
 import os
@@ -599,21 +600,36 @@ def run_streams(args, d):
     xchg = multi.KeyframeExchange(cap, world, d.dev)
     state = {"i": 0, "kf": 0, "err": []}
 
+    phases = collections.defaultdict(float) if os.environ.get("LMSF_BENCH_PHASES") else None
+
+    def mark(name, t0):   # host time per call (diagnostics: LMSF_BENCH_PHASES=1 prints the means to stderr)
+        t1 = time.perf_counter()
+        if phases is not None:
+            phases[name] += t1 - t0
+        return t1
+
     def step():
         i = state["i"]
+        t = time.perf_counter()
         ctx.extract(scans_dev[i])
+        t = mark("extract", t)
         _, r = tr.solve_extracted(0.1 * i)
+        t = mark("solve", t)
         P = tr.pose()
         ne = ns = 0
         if r.update_type:
             ne = ctx.copy_features_into(_lib.EDGE, fbuf[:cap])
             ns = ctx.copy_features_into(_lib.SURF, fbuf[cap:])
+        t = mark("copy_features", t)
         kfs = xchg.exchange(P, r.update_type, ne, ns, fbuf)           # same list, same order everywhere
+        t = mark("exchange", t)
         for _, fe, fs, pose in kfs:
             tr.add_keyframe(fe, fs, pose)
+        t = mark("add_keyframe", t)
         if kfs:
             tr.commit_map()
             state["kf"] += len(kfs)
+        t = mark("commit", t)
         Tt = np.eye(4)
         Tt[:3, :3] = synth.quat_to_mat(truth[i][:4])
         Tt[:3, 3] = truth[i][4:]
@@ -622,6 +638,9 @@ def run_streams(args, d):
         return P
 
     elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx], not args.no_n27)
+    if phases is not None:
+        nst = state["i"]
+        print("phases ms/step: " + "  ".join(f"{k} {1e3 * v / nst:.3f}" for k, v in phases.items()), file=sys.stderr)
     ks = timed_stats(ctx)
     roof = knn_roofline(ks, mean_n27, load_traffic(args.traffic_json, config="C4", batch=1, map_points=map_points),
                         elapsed, "one 63k-query scan per launch (8 lanes per query): latency-bound launches")

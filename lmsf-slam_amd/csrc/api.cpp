@@ -36,6 +36,9 @@ struct DevMap {
     unsigned long long* h_occ = nullptr;   // pinned
     hipEvent_t ev_occ = nullptr;
     bool occ_pending = false;
+    // build scratch: d_bb = [box 0..5, count 6, -, occupied u64 at 8..9], read back into pinned h_bb
+    int* d_bb = nullptr;
+    int* h_bb = nullptr;
 
     GridView view() const {
         GridView g{};   // zeroed padding: views are compared bytewise (SolveGraph key)
@@ -105,6 +108,26 @@ bool memo_refit_enabled() {   // read per launch, so a test can compare both in 
     const char* e = getenv("LMSF_MEMO_REFIT");
     return e ? atoi(e) != 0 : true;
 }
+
+}  // namespace
+
+// Host wait on a stream of the latency-bound single-scan paths (extraction read-back, solve, tracker
+// commit).  LMSF_SPIN_SYNC=1 polls hipStreamQuery instead of hipStreamSynchronize: A/B on one box (C4 /
+// C3 ms per scan, two runs each: 1.55, 1.74 / 1.50, 1.73 spinning vs 1.63, 1.71 / 1.52, 1.50 blocking)
+// within the noise, so the blocking wait stays the default.
+hipError_t lmsf::stream_wait(hipStream_t s) {
+    static const bool spin = [] {
+        const char* e = getenv("LMSF_SPIN_SYNC");
+        return e ? atoi(e) != 0 : false;
+    }();
+    if (!spin) return hipStreamSynchronize(s);
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e != hipErrorNotReady) return e;
+    }
+}
+
+namespace {
 
 template <typename T>
 hipError_t dalloc(T** p, size_t count) {
@@ -181,6 +204,7 @@ struct lmsf_ctx {
     double* h_poses = nullptr;        // pinned [B*7]
     SolveState* h_st = nullptr;       // pinned [B]
     int* h_counts = nullptr;          // pinned [2*B]
+    int* h_pack = nullptr;            // pinned [4]: packed single-scan read-back (counts, error flag)
     std::vector<float> host_scan[3];  // SetInputTarget copies (slot 0)
     bool scan_dirty = false;
     bool features_on_device = false;  // slot 0 features came from lmsf_extract_features
@@ -324,10 +348,17 @@ struct lmsf_ctx {
 
 namespace {
 
-// Cell grid of one cloud into m; sorted points carry w = base + original index.
-lmsf_status build_grid(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, int base) {
-    hipStream_t s = c->stream;
+// Cell grid of one cloud into m, in two stages so that several grids can be built with one host wait:
+// grid_stage (no wait) copies the cloud into m.orig and reads its box + count back into pinned m.h_bb;
+// once the stream has drained that, grid_finish sizes the grid and sorts the points into cells.
+// n bounds the count, n_dev (device) gives it when the producer's size is still on the device.
+// Sorted points carry w = base + original index.
+lmsf_status grid_stage(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, const int* n_dev, hipStream_t s) {
     if (n > (size_t)INT32_MAX) return c->fail(LMSF_ERR_CAPACITY, "map too large (%zu points)", n);
+    if (!m.d_bb) {
+        HIPCHK(c, hipMalloc((void**)&m.d_bb, 16 * sizeof(int)));
+        HIPCHK(c, hipHostMalloc((void**)&m.h_bb, 8 * sizeof(int), hipHostMallocDefault));
+    }
     if (n > m.cap) {
         hipFree(m.orig); hipFree(m.pts); hipFree(m.cell);
         m.orig = nullptr; m.pts = nullptr; m.cell = nullptr;
@@ -340,14 +371,22 @@ lmsf_status build_grid(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, int 
     }
     // host or device source (unified addressing): the tracker rebuilds from device-resident maps
     HIPCHK(c, hipMemcpyAsync(m.orig, xyzi, n * sizeof(float4), hipMemcpyDefault, s));
-    int* d_bbox = c->d_error + 4;  // scratch ints after the error word
-    const int init[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
-    HIPCHK(c, hipMemcpyAsync(d_bbox, init, sizeof init, hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_map_bbox(m.orig, (int)n, n_dev, grid_slices(), m.d_bb, s));
+    HIPCHK(c, hipMemcpyAsync(m.h_bb, m.d_bb, 7 * sizeof(int), hipMemcpyDeviceToHost, s));
+    return LMSF_OK;
+}
+
+// density: also count the occupied slices (lim1 of the pruned one-lane walk); keyframe windows skip it
+// (lim1 stays 1, the plain walk -- speed only, results do not depend on it).
+lmsf_status grid_finish(lmsf_ctx* c, DevMap& m, int base, hipStream_t s, bool density = true) {
+    const int* bb = m.h_bb;
+    const int n = bb[6];
+    if (n == 0) {
+        m.n = 0;
+        m.occ_pending = false;
+        return LMSF_OK;
+    }
     const int sx = grid_slices();
-    HIPCHK(c, launch_map_bbox(m.orig, (int)n, sx, d_bbox, s));
-    int bb[6];
-    HIPCHK(c, hipMemcpyAsync(bb, d_bbox, sizeof bb, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
     const int nx = bb[3] - bb[0] + 1, ny = bb[4] - bb[1] + 1, nz = bb[5] - bb[2] + 1;
     const size_t cells = (size_t)nx * ny * nz;
     if (nx <= 0 || ny <= 0 || nz <= 0 || cells > kMaxCells)
@@ -368,14 +407,18 @@ lmsf_status build_grid(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, int 
     }
     m.ox = bb[0]; m.oy = bb[1]; m.oz = bb[2];
     m.nx = nx; m.ny = ny; m.nz = nz; m.sx = sx;
-    HIPCHK(c, hipMemsetAsync(m.counts, 0, (cells + 1) * sizeof(uint32_t), s));
-    HIPCHK(c, hipMemsetAsync(m.fill, 0, (cells + 1) * sizeof(uint32_t), s));
-    HIPCHK(c, launch_map_count(m.orig, (int)n, sx, m.ox, m.oy, m.oz, nx, ny, nz, m.cell, m.counts, s));
+    unsigned long long* d_occ = reinterpret_cast<unsigned long long*>(m.d_bb + 8);
+    HIPCHK(c, launch_grid_clear(m.counts, m.fill, cells + 1, d_occ, s));
+    HIPCHK(c, launch_map_count(m.orig, n, sx, m.ox, m.oy, m.oz, nx, ny, nz, m.cell, m.counts, s));
     size_t tb = m.scan_tmp_bytes;
     HIPCHK(c, exclusive_scan_u32(m.counts, m.off, cells + 1, m.scan_tmp, tb, s));
-    HIPCHK(c, launch_map_scatter(m.orig, (int)n, m.cell, m.off, m.fill, m.pts, base, s));
-    unsigned long long* d_occ = reinterpret_cast<unsigned long long*>(c->d_error + 16);   // scratch after the bbox
-    HIPCHK(c, hipMemsetAsync(d_occ, 0, sizeof(unsigned long long), s));
+    HIPCHK(c, launch_map_scatter(m.orig, n, m.cell, m.off, m.fill, m.pts, base, s));
+    m.lim1 = 1.f;   // provisional (plain walk) until resolve_lim1
+    m.n = n;
+    if (!density) {
+        m.occ_pending = false;
+        return LMSF_OK;
+    }
     HIPCHK(c, launch_count_nonzero(m.counts, cells, d_occ, s));
     if (!m.h_occ) {
         HIPCHK(c, hipHostMalloc((void**)&m.h_occ, sizeof(unsigned long long), hipHostMallocDefault));
@@ -384,9 +427,14 @@ lmsf_status build_grid(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, int 
     HIPCHK(c, hipMemcpyAsync(m.h_occ, d_occ, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipEventRecord(m.ev_occ, s));
     m.occ_pending = true;
-    m.lim1 = 1.f;   // provisional (plain walk) until resolve_lim1
-    m.n = (int)n;
     return LMSF_OK;
+}
+
+lmsf_status build_grid(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, int base) {
+    lmsf_status rc = grid_stage(c, m, xyzi, n, nullptr, c->stream);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return grid_finish(c, m, base, c->stream);
 }
 
 // The density-chosen first radius of the pruned walk, once a launch may use it (one-lane launches).
@@ -629,6 +677,8 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
             hipFree(m.scan_tmp);
             if (m.h_occ) hipHostFree(m.h_occ);
             if (m.ev_occ) hipEventDestroy(m.ev_occ);
+            hipFree(m.d_bb);
+            if (m.h_bb) hipHostFree(m.h_bb);
         }
     }
     void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->prevw, c->memo_nbr, c->wl, c->wlim, c->wcount, c->n_search, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
@@ -647,6 +697,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (c->h_poses) hipHostFree(c->h_poses);
     if (c->h_st) hipHostFree(c->h_st);
     if (c->h_counts) hipHostFree(c->h_counts);
+    if (c->h_pack) hipHostFree(c->h_pack);
     if (c->h_raw_counts) hipHostFree(c->h_raw_counts);
     if (c->h_raw_off) hipHostFree(c->h_raw_off);
     if (c->h_off) hipHostFree(c->h_off);
@@ -738,6 +789,7 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(hipHostMalloc((void**)&c->h_poses, B * 7 * sizeof(double), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_st, B * sizeof(SolveState), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_counts, 2 * B * sizeof(int), hipHostMallocDefault));
+    CHK(hipHostMalloc((void**)&c->h_pack, 4 * sizeof(int), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_raw_counts, B * sizeof(int), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_raw_off, B * sizeof(int64_t), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_off, B * sizeof(int64_t), hipHostMallocDefault));
@@ -818,7 +870,7 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     rc = enqueue_solve(c, 1, iters);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c->stream));
     rc = collect_timing(c);
     if (rc) return rc;
     const SolveState& S = c->h_st[0];
@@ -850,11 +902,11 @@ lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf
     HIPCHK(c, launch_extract(c->eview(1), c->stream));
     HIPCHK(c, hipEventRecord(c->ev_raw_free, c->stream));
     c->qorder_valid = true;
-    int hc[3];
-    HIPCHK(c, hipMemcpyAsync(&hc[0], c->n_edge, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&hc[1], c->n_surf, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&hc[2], c->d_error, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // counts + error flag gathered on the device, one read-back into pinned memory
+    HIPCHK(c, launch_pack3(c->n_edge, c->n_surf, c->d_error, c->d_error + 8, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_pack, c->d_error + 8, 3 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, stream_wait(c->stream));
+    const int* hc = c->h_pack;
     if (hc[2]) return c->fail(LMSF_ERR_CAPACITY, "ring or sector larger than the extraction kernel supports (flags %d)", hc[2]);
     c->slot0_ne = hc[0];
     c->slot0_ns = hc[1];
@@ -943,7 +995,7 @@ static lmsf_status copy_slot_features(lmsf_ctx* c, int slot, int32_t kind, float
     if (n > cap) return c->fail(LMSF_ERR_CAPACITY, "output capacity %zu < %zu features", cap, n);
     if (n && out) HIPCHK(c, hipMemcpyAsync(out, c->feat + off, n * sizeof(float4), hipMemcpyDefault, c->stream));
     if (n && src) HIPCHK(c, hipMemcpyAsync(src, c->feat_src + off, n * sizeof(int), hipMemcpyDefault, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c->stream));
     return LMSF_OK;
 }
 
@@ -1359,6 +1411,24 @@ lmsf_status ctx_set_window_device(lmsf_ctx* c, int kind, const float4* d_pts, si
         if (rc) return rc;
     }
     c->map_set[kind] = c->prior[kind].n > 0 || c->map[kind].n > 0;
+    return LMSF_OK;
+}
+
+lmsf_status ctx_window_stage(lmsf_ctx* c, int kind, const float4* d_pts, size_t n_max, const int* n_dev, hipStream_t s) {
+    if (n_max == 0) return LMSF_OK;
+    return grid_stage(c, c->map[kind], reinterpret_cast<const float*>(d_pts), n_max, n_dev, s);
+}
+
+lmsf_status ctx_window_finish(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s, size_t* n_out) {
+    DevMap& m = c->map[kind];
+    if (n_max == 0) {
+        m.n = 0;
+    } else {
+        lmsf_status rc = grid_finish(c, m, c->prior[kind].n, s, false);
+        if (rc) return rc;
+    }
+    *n_out = (size_t)m.n;
+    c->map_set[kind] = c->prior[kind].n > 0 || m.n > 0;
     return LMSF_OK;
 }
 

@@ -17,7 +17,16 @@
 
 namespace lmsf {
 
-__global__ void __launch_bounds__(256) map_bbox_kernel(const float4* pts, int n, float sx, int* bbox) {
+// bbox[0..5] = slice / row / level box of the first n points; with n_dev (a producer's count still on the
+// device, e.g. the voxel filter's) n = min(n, *n_dev); bbox[6] = that n, so one read-back carries both.
+__global__ void map_bbox_init_kernel(int* bbox) {
+    if (threadIdx.x < 3) bbox[threadIdx.x] = INT_MAX;
+    else if (threadIdx.x < 6) bbox[threadIdx.x] = INT_MIN;
+}
+
+__global__ void __launch_bounds__(256) map_bbox_kernel(const float4* pts, int n, const int* n_dev, float sx, int* bbox) {
+    if (n_dev) n = min(n, *n_dev);
+    if (blockIdx.x == 0 && threadIdx.x == 0) bbox[6] = n;
     int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const float4 p = pts[i];
@@ -118,9 +127,12 @@ hipError_t launch_gather_slots(const SlotTable& tab, float4* out, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_map_bbox(const float4* pts, int n, int sx, int* bbox, hipStream_t s) {
-    const int blocks = min((n + 255) / 256, 512);
-    hipLaunchKernelGGL(map_bbox_kernel, dim3(max(blocks, 1)), dim3(256), 0, s, pts, n, (float)sx, bbox);
+hipError_t launch_map_bbox(const float4* pts, int n, const int* n_dev, int sx, int* bbox, hipStream_t s) {
+    hipLaunchKernelGGL(map_bbox_init_kernel, dim3(1), dim3(64), 0, s, bbox);
+    // >= 16 points per thread, <= 512 blocks: each block commits 6 atomics to the same 6 words (512 blocks
+    // serialise ~35 us on them, which only a multi-million-point cloud amortises)
+    const int blocks = min((n + 4095) / 4096, 512);
+    hipLaunchKernelGGL(map_bbox_kernel, dim3(max(blocks, 1)), dim3(256), 0, s, pts, n, n_dev, (float)sx, bbox);
     return hipGetLastError();
 }
 
@@ -135,6 +147,36 @@ hipError_t launch_map_scatter(const float4* pts, int n, const int* cell, const u
                               float4* sorted, int base, hipStream_t s) {
     hipLaunchKernelGGL(map_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pts, n, cell, off, fill, sorted,
                        base);
+    return hipGetLastError();
+}
+
+// out[0..2] = *a, *b, *c: several device words gathered for one read-back
+__global__ void pack3_kernel(const int* a, const int* b, const int* c, int* out) {
+    if (threadIdx.x == 0) {
+        out[0] = *a;
+        out[1] = *b;
+        out[2] = *c;
+    }
+}
+
+hipError_t launch_pack3(const int* a, const int* b, const int* c, int* out, hipStream_t s) {
+    hipLaunchKernelGGL(pack3_kernel, dim3(1), dim3(64), 0, s, a, b, c, out);
+    return hipGetLastError();
+}
+
+// counts[0..n) = fill[0..n) = 0 and *occ = 0 (one launch for the three resets of a grid build)
+__global__ void grid_clear_kernel(uint32_t* counts, uint32_t* fill, size_t n, unsigned long long* occ) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        counts[i] = 0u;
+        fill[i] = 0u;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *occ = 0ull;
+}
+
+hipError_t launch_grid_clear(uint32_t* counts, uint32_t* fill, size_t n, unsigned long long* occ, hipStream_t s) {
+    const size_t blocks = std::min<size_t>(2048, (n + 255) / 256);
+    hipLaunchKernelGGL(grid_clear_kernel, dim3((unsigned)std::max<size_t>(blocks, 1)), dim3(256), 0, s, counts, fill, n, occ);
     return hipGetLastError();
 }
 

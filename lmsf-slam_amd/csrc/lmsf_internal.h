@@ -116,7 +116,10 @@ struct BatchView {
 };
 
 // ---- launchers (each enqueues on `stream`, never synchronises)
-hipError_t launch_map_bbox(const float4* pts, int n, int sx, int* bbox, hipStream_t s);
+// bbox[0..6] = the map box of the first n points (min(n, *n_dev) when n_dev) and that count; resets bbox first.
+hipError_t launch_pack3(const int* a, const int* b, const int* c, int* out, hipStream_t s);
+hipError_t launch_grid_clear(uint32_t* counts, uint32_t* fill, size_t n, unsigned long long* occ, hipStream_t s);
+hipError_t launch_map_bbox(const float4* pts, int n, const int* n_dev, int sx, int* bbox, hipStream_t s);
 hipError_t launch_map_count(const float4* pts, int n, int sx, int ox, int oy, int oz, int nx, int ny, int nz,
                             int* cell, uint32_t* counts, hipStream_t s);
 // sorted[] w = base + original index (base > 0 for a keyframe window behind a prior map)
@@ -220,6 +223,8 @@ struct VoxelFilter {
     size_t tmp_bytes = 0, cap = 0;
     hipError_t reserve(size_t n);
     hipError_t run(const float4* in, int n, float leaf, float4* out, int* n_out, hipStream_t s);
+    // run() without the read-back: the voxel count stays on the device in *nseg (no host wait)
+    hipError_t enqueue(const float4* in, int n, float leaf, float4* out, hipStream_t s);
     void release();
 };
 
@@ -252,6 +257,13 @@ lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg);
 // keyframe commit with indices offset by the prior size; n == 0 clears that part.
 lmsf_status ctx_set_prior_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n);
 lmsf_status ctx_set_window_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n);
+// host wait of the single-scan paths (spins on hipStreamQuery unless LMSF_SPIN_SYNC=0)
+hipError_t stream_wait(hipStream_t s);
+// the same in two stages on stream s, so several windows share one host wait: stage (no wait; n_dev, on the
+// device, bounds the count n_max when the producer's size is not known on the host yet), then -- once s has
+// drained -- finish (n_out = the window's point count)
+lmsf_status ctx_window_stage(lmsf_ctx* c, int kind, const float4* d_pts, size_t n_max, const int* n_dev, hipStream_t s);
+lmsf_status ctx_window_finish(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s, size_t* n_out);
 lmsf_status ctx_slot0_features(lmsf_ctx* c, const float4** d_feat, int64_t* ne, int64_t* ns);
 
 }  // namespace lmsf

@@ -139,7 +139,9 @@ struct lmsf_tracker {
     Iso origin, curr, prev, motion, last_kf;
     double last_kf_time = 0.0;
     Window win[3];
-    VoxelFilter voxel;
+    VoxelFilter voxel[3];       // per kind: the two windows are filtered concurrently
+    hipStream_t aux = nullptr;  // the surf window's commit runs here beside the edge window's on the context stream
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     float4* stage = nullptr;   // host/device keyframe input staged before the transform
     int cap = 0;               // points per keyframe slot
 };
@@ -184,10 +186,22 @@ lmsf_status push_frame(lmsf_tracker* t, int kind, const float4* src, int64_t n, 
     return LMSF_OK;
 }
 
-// SetInputSource(GetLocalMap()) (:229) for every kind whose window changed.
+// SetInputSource(GetLocalMap()) (:229) for every kind whose window changed.  Both kinds are committed
+// together with one host wait: per kind (surf on the tracker's aux stream when both changed, edge on the
+// context stream) the keyframes are gathered, voxel-filtered and the grid's box + count read back
+// without waiting; after one wait on both streams the grids are sized and filled, and the context stream
+// joins the aux stream before the next search.
 lmsf_status commit(lmsf_tracker* t) {
     hipStream_t s = ctx_stream(t->ctx);
-    for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) {
+    const bool both = t->win[LMSF_EDGE].dirty && t->win[LMSF_SURF].dirty;
+    hipStream_t ks[3] = {s, s, both ? t->aux : s};
+    if (both) {
+        TCHK(t, hipEventRecord(t->ev_fork, s));   // the keyframe transforms queued on s
+        TCHK(t, hipStreamWaitEvent(t->aux, t->ev_fork, 0));
+    }
+    size_t nmax[3] = {0, 0, 0};
+    // surf first: its chain (the larger window, its sort) runs on the GPU while the edge chain is enqueued
+    for (int kind : {LMSF_SURF, LMSF_EDGE}) {
         Window& w = t->win[kind];
         if (!w.dirty) continue;
         const int W = (int)w.slots.size();
@@ -201,20 +215,34 @@ lmsf_status commit(lmsf_tracker* t) {
                 tab.src[i] = w.slots[k];
                 tab.start[i + 1] = tab.start[i] + w.sizes[k];
             }
-            TCHK(t, launch_gather_slots(tab, dst + nw, s));
+            TCHK(t, launch_gather_slots(tab, dst + nw, ks[kind]));
             nw += (size_t)tab.start[tab.n];
         }
-        if (w.leaf > 0 && nw) {                                   // VoxelGrid of the window
-            int nv = 0;
-            TCHK(t, t->voxel.run(w.wcat, (int)nw, (float)w.leaf, w.concat, &nv, s));
-            nw = (size_t)nv;
+        const int* n_dev = nullptr;
+        if (w.leaf > 0 && nw) {                                   // VoxelGrid of the window (count stays on the device)
+            TCHK(t, t->voxel[kind].enqueue(w.wcat, (int)nw, (float)w.leaf, w.concat, ks[kind]));
+            n_dev = t->voxel[kind].nseg;
         }
-        w.window_n = nw;
-        w.total = w.prior_n + nw;
-        w.dirty = false;
+        nmax[kind] = nw;
         // only the window's grid is rebuilt; the prior's grid was built once (set_prior_map)
-        lmsf_status rc = ctx_set_window_device(t->ctx, kind, w.concat, nw);
+        lmsf_status rc = ctx_window_stage(t->ctx, kind, w.concat, nw, n_dev, ks[kind]);
         if (rc) return rc;
+    }
+    if (both) TCHK(t, stream_wait(t->aux));
+    TCHK(t, stream_wait(s));
+    for (int kind : {LMSF_SURF, LMSF_EDGE}) {
+        Window& w = t->win[kind];
+        if (!w.dirty) continue;
+        size_t n = 0;
+        lmsf_status rc = ctx_window_finish(t->ctx, kind, nmax[kind], ks[kind], &n);
+        if (rc) return rc;
+        w.window_n = n;
+        w.total = w.prior_n + n;
+        w.dirty = false;
+    }
+    if (both) {
+        TCHK(t, hipEventRecord(t->ev_join, t->aux));
+        TCHK(t, hipStreamWaitEvent(s, t->ev_join, 0));
     }
     return LMSF_OK;
 }
@@ -276,7 +304,13 @@ void lmsf_tracker_destroy(lmsf_tracker* t) {
         hipFree(w.wcat);
         hipFree(w.prior);
     }
-    t->voxel.release();
+    for (auto& v : t->voxel) v.release();
+    if (t->aux) {
+        hipStreamSynchronize(t->aux);
+        hipStreamDestroy(t->aux);
+    }
+    if (t->ev_fork) hipEventDestroy(t->ev_fork);
+    if (t->ev_join) hipEventDestroy(t->ev_join);
     hipFree(t->stage);
     delete t;
 }
@@ -289,6 +323,12 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
     t->cfg = *cfg;
     t->cap = ctx_feature_capacity(ctx);
     if (hipSetDevice(ctx_device(ctx)) != hipSuccess) { delete t; return LMSF_ERR_HIP; }
+    if (hipStreamCreateWithFlags(&t->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&t->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming) != hipSuccess) {
+        lmsf_tracker_destroy(t);
+        return LMSF_ERR_HIP;
+    }
     for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) {
         Window& w = t->win[kind];
         w.slots.assign(cfg->window_frames, nullptr);
