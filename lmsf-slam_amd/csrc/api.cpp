@@ -495,31 +495,36 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
     const bool gn = c->cfg.solver == LMSF_SOLVER_GN;
     for (int o = 0; o < iters; ++o) {
         const bool t = c->timing && c->ev_used + 2 <= 2 * kEventPairs;
-        if (t) HIPCHK(c, launch_stamp(c->d_stamps + c->ev_used, s));
+        unsigned long long* st0 = t ? c->d_stamps + c->ev_used : nullptr;   // search entry / exit stamps
+        unsigned long long* st1 = t ? st0 + 1 : nullptr;
         // batch launches: one fused search + fit kernel (it is then the timed neighbour-search launch)
         const bool fused = match_fit_applies(ge2, gs2, bv, c->cfg.solver);
         if (fused) {
             BatchView bvo = bv;
+            bvo.stamp_start = st0;
             bvo.memo = o > 0 && !c->count27 && match_memo_enabled() ? 1 : 0;   // within one solve only
             HIPCHK(c, launch_match_fit(ge, gs, bvo, s));
         }
         else {   // single-scan launches: the 8-lane search, with the slot memo under the Ceres-LM solver
             BatchView bvk = bv;
+            bvk.stamp_start = st0;
             bvk.memo = !gn && o > 0 && !c->count27 && match_memo_enabled() ? 1 : 0;
             HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{},
                                  bvk, gn ? 1 : 0, s, !gn && match_memo_enabled()));
         }
-        if (t) {
-            HIPCHK(c, launch_stamp(c->d_stamps + c->ev_used + 1, s));
-            c->ev_used += 2;
-        }
+        if (t) c->ev_used += 2;
         c->knn_launches++;
         if (fused) c->fused_launches++;
-        if (!fused) HIPCHK(c, launch_fit_eval(ge, gs, bv, c->cfg.solver, s));
+        if (!fused) {
+            BatchView bvf = bv;
+            bvf.stamp_end = st1;   // fit_eval starts when the search has drained
+            HIPCHK(c, launch_fit_eval(ge, gs, bvf, c->cfg.solver, s));
+        }
         if (gn) {
             HIPCHK(c, launch_gn_solve(bv, o, s));
         } else {
             BatchView bvb = bv;
+            if (fused) bvb.stamp_end = st1;
             if (fused) {   // packets: memo pass [0, ceil(nq / 64)) when it ran, search [part2_base, + ceil(n_search / 64))
                 bvb.fused_parts = 1;
                 bvb.memo = o > 0 && !c->count27 && match_memo_enabled() && !match_fit_prune(ge, gs) ? 1 : 0;

@@ -426,6 +426,7 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
     constexpr int NK = MEMO ? 6 : 5;
     __shared__ unsigned long long blk_n27;
     __shared__ unsigned int blk_q, blk_r;
+    stamp_if(bv.stamp_start, blockIdx.x == 0);
     int bx, b;
     block_coords(remap, gx, bx, b);
     if (threadIdx.x == 0) { blk_n27 = 0; blk_q = 0; blk_r = 0; }
@@ -775,6 +776,7 @@ __device__ __forceinline__ void fit_one(const BatchView& bv, int solver, int b, 
 // FPT queries per thread (block = 256 * FPT queries): one packet reduction per block.
 template <int FPT>
 __global__ __launch_bounds__(256) void fit_eval_kernel(BatchView bv, int solver) {
+    stamp_if(bv.stamp_end, blockIdx.x == 0 && blockIdx.y == 0);
     const int b = blockIdx.y;
     const int ne = bv.n_edge[b], ns = bv.n_surf[b];
     const int nq = ne + ns;
@@ -850,6 +852,7 @@ __host__ __device__ __forceinline__ size_t memo_blocks(size_t feat_stride) { ret
 // returns the same 6 keys as the full 1 m walk.  One packet per wave at partial index 4 bx + wave.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_WAVES))) void match_memo_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
     __shared__ int wcnt[8];
+    stamp_if(bv.stamp_start, blockIdx.x == 0);
     int bx, b;
     block_coords(remap, gx, bx, b);
     const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
@@ -1022,6 +1025,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     extern __shared__ int soff[];   // LIST: exclusive prefixes of the memo blocks' search / refit counts, 2 x [nblk + 1]
     constexpr bool kMemo = !PRUNE;
     constexpr int kNK = kMemo ? 6 : 5;
+    stamp_if(bv.stamp_start, blockIdx.x == 0);
     int bx, b;
     block_coords(remap, gx, bx, b);
     const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
@@ -1431,7 +1435,9 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
     } else if (bv.memo) {
         hipLaunchKernelGGL(match_memo_kernel, grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
         const size_t lds = 2 * (memo_blocks(bv.feat_stride) + 1) * sizeof(int);
-        hipLaunchKernelGGL((match_fit_kernel<false, true>), grid, dim3(256), lds, s, edge, surf, bv, gx, remap);
+        BatchView bl = bv;
+        bl.stamp_start = nullptr;   // the memo pass opened the timed span
+        hipLaunchKernelGGL((match_fit_kernel<false, true>), grid, dim3(256), lds, s, edge, surf, bl, gx, remap);
     } else {
         hipLaunchKernelGGL((match_fit_kernel<false, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
     }

@@ -70,6 +70,7 @@ __device__ __forceinline__ void lm_begin_apply(SolveState& S, const double* tot)
 
 // After fit_eval: IterationZero (evaluate at x0, jacobi scaling, gradient check) + first step.
 __global__ __launch_bounds__(kBeginThreads) void lm_begin_kernel(BatchView bv) {
+    stamp_if(bv.stamp_end, blockIdx.x == 0);
     const int b = blockIdx.x;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
     __shared__ SolveState sS;
