@@ -306,6 +306,11 @@ lmsf_status lmsf_tracker_set_initial_pose(lmsf_tracker* t, const double pose[16]
 lmsf_status lmsf_tracker_set_prior_map(lmsf_tracker* t, int32_t kind, const float* xyzi, size_t n);
 lmsf_status lmsf_tracker_add_keyframe(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf,
                                       size_t n_surf, const double pose[16]);
+/* Rebuilds the local map from the appended keyframes.  Returns once the rebuild is enqueued on the
+ * tracker's own streams; the next lmsf_tracker_* call on t completes it, so context work enqueued in
+ * between (lmsf_extract_features of the next scan, lmsf_copy_features) runs beside the rebuild.  Direct
+ * map consumers on the same context (lmsf_solve, lmsf_match, lmsf_align_score, lmsf_set_map) are
+ * called after a tracker call, not between this and the next one. */
 lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t);
 
 /* VoxelGridFilter::Filter (INC/Algorithm/PointClouds/processing/Filter/voxel_grid.hpp:25-34,

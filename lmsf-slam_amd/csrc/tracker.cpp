@@ -140,8 +140,11 @@ struct lmsf_tracker {
     double last_kf_time = 0.0;
     Window win[3];
     VoxelFilter voxel[3];       // per kind: the two windows are filtered concurrently
-    hipStream_t aux = nullptr;  // the surf window's commit runs here beside the edge window's on the context stream
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t aux[2] = {nullptr, nullptr};   // the windows' commits (surf, edge), beside the context stream
+    hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
+    hipStream_t ks[3] = {nullptr, nullptr, nullptr};   // staged commit: stream per kind (null: unchanged)
+    size_t nmax[3] = {0, 0, 0};
+    bool pending = false;                               // staged, not yet finished
     float4* stage = nullptr;   // host/device keyframe input staged before the transform
     int cap = 0;               // points per keyframe slot
 };
@@ -186,24 +189,25 @@ lmsf_status push_frame(lmsf_tracker* t, int kind, const float4* src, int64_t n, 
     return LMSF_OK;
 }
 
-// SetInputSource(GetLocalMap()) (:229) for every kind whose window changed.  Both kinds are committed
-// together with one host wait: per kind (surf on the tracker's aux stream when both changed, edge on the
-// context stream) the keyframes are gathered, voxel-filtered and the grid's box + count read back
-// without waiting; after one wait on both streams the grids are sized and filled, and the context stream
-// joins the aux stream before the next search.
-lmsf_status commit(lmsf_tracker* t) {
+// SetInputSource(GetLocalMap()) (:229) for every kind whose window changed, in two halves.
+// commit_stage (no host wait): each changed kind on a stream of its own (surf on aux[0], edge on aux[1],
+// both after the keyframe transforms queued on the context stream) gathers its keyframes, voxel-filters
+// them and reads the grid's box + count back.  commit_finish: one wait on those streams, the grids sized
+// and filled on them, and the context stream joins them before its next search.  The context stream
+// stays free in between, so the next scan's extraction runs beside the map rebuild when the caller
+// defers the finish (lmsf_tracker_commit_map; settle() completes it at the next tracker call).
+lmsf_status commit_stage(lmsf_tracker* t) {
     hipStream_t s = ctx_stream(t->ctx);
-    const bool both = t->win[LMSF_EDGE].dirty && t->win[LMSF_SURF].dirty;
-    hipStream_t ks[3] = {s, s, both ? t->aux : s};
-    if (both) {
-        TCHK(t, hipEventRecord(t->ev_fork, s));   // the keyframe transforms queued on s
-        TCHK(t, hipStreamWaitEvent(t->aux, t->ev_fork, 0));
-    }
-    size_t nmax[3] = {0, 0, 0};
-    // surf first: its chain (the larger window, its sort) runs on the GPU while the edge chain is enqueued
-    for (int kind : {LMSF_SURF, LMSF_EDGE}) {
+    TCHK(t, hipEventRecord(t->ev_fork, s));   // the keyframe transforms queued on s
+    int k = 0;
+    for (int kind : {LMSF_SURF, LMSF_EDGE}) {   // surf first: the larger window and its sort
         Window& w = t->win[kind];
+        t->ks[kind] = nullptr;
+        t->nmax[kind] = 0;
         if (!w.dirty) continue;
+        hipStream_t ks = t->aux[k++];
+        t->ks[kind] = ks;
+        TCHK(t, hipStreamWaitEvent(ks, t->ev_fork, 0));
         const int W = (int)w.slots.size();
         float4* dst = w.leaf > 0 ? w.wcat : w.concat;
         size_t nw = 0;
@@ -211,41 +215,56 @@ lmsf_status commit(lmsf_tracker* t) {
             SlotTable tab{};
             tab.n = std::min(kSlotTable, w.count - i0);
             for (int i = 0; i < tab.n; ++i) {
-                const int k = (w.head + i0 + i) % W;
-                tab.src[i] = w.slots[k];
-                tab.start[i + 1] = tab.start[i] + w.sizes[k];
+                const int j = (w.head + i0 + i) % W;
+                tab.src[i] = w.slots[j];
+                tab.start[i + 1] = tab.start[i] + w.sizes[j];
             }
-            TCHK(t, launch_gather_slots(tab, dst + nw, ks[kind]));
+            TCHK(t, launch_gather_slots(tab, dst + nw, ks));
             nw += (size_t)tab.start[tab.n];
         }
         const int* n_dev = nullptr;
         if (w.leaf > 0 && nw) {                                   // VoxelGrid of the window (count stays on the device)
-            TCHK(t, t->voxel[kind].enqueue(w.wcat, (int)nw, (float)w.leaf, w.concat, ks[kind]));
+            TCHK(t, t->voxel[kind].enqueue(w.wcat, (int)nw, (float)w.leaf, w.concat, ks));
             n_dev = t->voxel[kind].nseg;
         }
-        nmax[kind] = nw;
+        t->nmax[kind] = nw;
         // only the window's grid is rebuilt; the prior's grid was built once (set_prior_map)
-        lmsf_status rc = ctx_window_stage(t->ctx, kind, w.concat, nw, n_dev, ks[kind]);
+        lmsf_status rc = ctx_window_stage(t->ctx, kind, w.concat, nw, n_dev, ks);
         if (rc) return rc;
     }
-    if (both) TCHK(t, stream_wait(t->aux));
-    TCHK(t, stream_wait(s));
+    t->pending = true;
+    return LMSF_OK;
+}
+
+lmsf_status commit_finish(lmsf_tracker* t) {
+    if (!t->pending) return LMSF_OK;
+    t->pending = false;
+    hipStream_t s = ctx_stream(t->ctx);
+    for (int kind : {LMSF_SURF, LMSF_EDGE})
+        if (t->ks[kind]) TCHK(t, stream_wait(t->ks[kind]));
     for (int kind : {LMSF_SURF, LMSF_EDGE}) {
         Window& w = t->win[kind];
-        if (!w.dirty) continue;
+        if (!t->ks[kind]) continue;
         size_t n = 0;
-        lmsf_status rc = ctx_window_finish(t->ctx, kind, nmax[kind], ks[kind], &n);
+        lmsf_status rc = ctx_window_finish(t->ctx, kind, t->nmax[kind], t->ks[kind], &n);
         if (rc) return rc;
         w.window_n = n;
         w.total = w.prior_n + n;
         w.dirty = false;
-    }
-    if (both) {
-        TCHK(t, hipEventRecord(t->ev_join, t->aux));
-        TCHK(t, hipStreamWaitEvent(s, t->ev_join, 0));
+        TCHK(t, hipEventRecord(t->ev_join[kind], t->ks[kind]));
+        TCHK(t, hipStreamWaitEvent(s, t->ev_join[kind], 0));
     }
     return LMSF_OK;
 }
+
+lmsf_status commit(lmsf_tracker* t) {
+    lmsf_status rc = commit_stage(t);
+    if (rc) return rc;
+    return commit_finish(t);
+}
+
+// A deferred commit completed before anything that reads or rewrites the windows or the map.
+lmsf_status settle(lmsf_tracker* t) { return commit_finish(t); }
 
 // updateLocalMap (:205-232) with the current scan's features (context slot 0).
 lmsf_status update_local_map(lmsf_tracker* t, const Iso& T) {
@@ -305,12 +324,14 @@ void lmsf_tracker_destroy(lmsf_tracker* t) {
         hipFree(w.prior);
     }
     for (auto& v : t->voxel) v.release();
-    if (t->aux) {
-        hipStreamSynchronize(t->aux);
-        hipStreamDestroy(t->aux);
-    }
+    for (hipStream_t a : t->aux)
+        if (a) {
+            hipStreamSynchronize(a);
+            hipStreamDestroy(a);
+        }
     if (t->ev_fork) hipEventDestroy(t->ev_fork);
-    if (t->ev_join) hipEventDestroy(t->ev_join);
+    for (hipEvent_t e : t->ev_join)
+        if (e) hipEventDestroy(e);
     hipFree(t->stage);
     delete t;
 }
@@ -323,9 +344,11 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
     t->cfg = *cfg;
     t->cap = ctx_feature_capacity(ctx);
     if (hipSetDevice(ctx_device(ctx)) != hipSuccess) { delete t; return LMSF_ERR_HIP; }
-    if (hipStreamCreateWithFlags(&t->aux, hipStreamNonBlocking) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&t->aux[0], hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&t->aux[1], hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&t->ev_join[LMSF_EDGE], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&t->ev_join[LMSF_SURF], hipEventDisableTiming) != hipSuccess) {
         lmsf_tracker_destroy(t);
         return LMSF_ERR_HIP;
     }
@@ -358,6 +381,8 @@ namespace {
 
 // Solve (:107-160) on the features currently in the context's slot 0.
 lmsf_status solve_current(lmsf_tracker* t, double timestamp, double deltaT[16], lmsf_tracker_result* res) {
+    lmsf_status rc0 = settle(t);   // a deferred keyframe commit completes before the search reads the map
+    if (rc0) return rc0;
     lmsf_tracker_result r;
     std::memset(&r, 0, sizeof r);
     lmsf_status rc;
@@ -442,6 +467,10 @@ lmsf_status lmsf_tracker_set_initial_pose(lmsf_tracker* t, const double pose[16]
 lmsf_status lmsf_tracker_set_prior_map(lmsf_tracker* t, int32_t kind, const float* xyzi, size_t n) {
     if (!t || (kind != LMSF_EDGE && kind != LMSF_SURF) || (n && !xyzi)) return LMSF_ERR_ARG;
     if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    {
+        lmsf_status rs = settle(t);
+        if (rs) return rs;
+    }
     Window& w = t->win[kind];
     hipStream_t s = ctx_stream(t->ctx);
     TCHK(t, hipStreamSynchronize(s));
@@ -463,6 +492,10 @@ lmsf_status lmsf_tracker_add_keyframe(lmsf_tracker* t, const float* edge, size_t
                                       size_t n_surf, const double pose[16]) {
     if (!t || !pose || (n_edge && !edge) || (n_surf && !surf)) return LMSF_ERR_ARG;
     if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    {
+        lmsf_status rs = settle(t);
+        if (rs) return rs;
+    }
     hipStream_t s = ctx_stream(t->ctx);
     const Iso T = iso_from16(pose);
     const float* src[3] = {nullptr, edge, surf};
@@ -477,16 +510,24 @@ lmsf_status lmsf_tracker_add_keyframe(lmsf_tracker* t, const float* edge, size_t
     return LMSF_OK;
 }
 
+// Returns once the rebuild is enqueued (commit_stage); the next tracker call completes it (settle), so
+// work the caller enqueues on the context in between (the next scan's extraction) runs beside it.
 lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t) {
     if (!t) return LMSF_ERR_ARG;
     if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
-    return commit(t);
+    lmsf_status rc = settle(t);
+    if (rc) return rc;
+    return commit_stage(t);
 }
 
 lmsf_status lmsf_tracker_register(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf,
                                   size_t n_surf, double pose[16], lmsf_solve_stats* stats) {
     if (!t || !pose) return LMSF_ERR_ARG;
     if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    {
+        lmsf_status rs = settle(t);
+        if (rs) return rs;
+    }
     lmsf_status rc = set_features(t, edge, n_edge, surf, n_surf);
     if (rc) return rc;
     Iso T = iso_from16(pose);
@@ -501,6 +542,10 @@ lmsf_status lmsf_tracker_register(lmsf_tracker* t, const float* edge, size_t n_e
 lmsf_status lmsf_tracker_register_extracted(lmsf_tracker* t, double pose[16], lmsf_solve_stats* stats) {
     if (!t || !pose) return LMSF_ERR_ARG;
     if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    {
+        lmsf_status rs = settle(t);
+        if (rs) return rs;
+    }
     if (!ctx_features_on_device(t->ctx)) return fail(t, LMSF_ERR_STATE, "no extracted features on the device");
     Iso T = iso_from16(pose);
     lmsf_solve_stats st;
@@ -519,11 +564,13 @@ lmsf_status lmsf_tracker_pose(const lmsf_tracker* t, double T[16]) {
 
 lmsf_status lmsf_tracker_local_map(lmsf_tracker* t, int32_t kind, float* out, size_t cap, size_t* n_out) {
     if (!t || (kind != LMSF_EDGE && kind != LMSF_SURF)) return LMSF_ERR_ARG;
+    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    lmsf_status rs = settle(t);   // the window sizes of a deferred commit
+    if (rs) return rs;
     const Window& w = t->win[kind];
     if (n_out) *n_out = w.total;
     if (!out) return LMSF_OK;
     if (w.total > cap) return fail(t, LMSF_ERR_CAPACITY, "output capacity smaller than the local map");
-    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
     hipStream_t s = ctx_stream(t->ctx);
     if (w.prior_n) TCHK(t, hipMemcpyAsync(out, w.prior, w.prior_n * sizeof(float4), hipMemcpyDefault, s));
     if (w.window_n)
