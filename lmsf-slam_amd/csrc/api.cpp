@@ -530,7 +530,15 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
                 bvb.memo = o > 0 && !c->count27 && match_memo_enabled() && !match_fit_prune(ge, gs) ? 1 : 0;
             }
             HIPCHK(c, launch_lm_begin(bvb, s));
-            for (int i = 0; i < 4; ++i) HIPCHK(c, launch_lm_eval_step(bv, o, i == 3 ? 1 : 0, s));
+            // a memo pass opens the next outer iteration's search: its start stamp is the exit of this last
+            // lm_step (the memo kernel itself has no register to spare for it)
+            const bool next_memo = fused && o + 1 < iters && !c->count27 && match_memo_enabled() && !match_fit_prune(ge, gs);
+            for (int i = 0; i < 4; ++i) {
+                BatchView bve = bv;
+                if (i == 3 && next_memo && c->timing && c->ev_used + 2 <= 2 * kEventPairs)
+                    bve.stamp_exit = c->d_stamps + c->ev_used;
+                HIPCHK(c, launch_lm_eval_step(bve, o, i == 3 ? 1 : 0, s));
+            }
         }
     }
     return LMSF_OK;

@@ -526,17 +526,28 @@ __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
     __shared__ int epre[kMaxRings + 1], spre[kMaxRings + 1];
     const int b = blockIdx.y;
     const int nr = ev.n_scans;
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {   // ring-count prefixes by one wave: lane r loads ring r's counts, shuffle scan
+        const int r = threadIdx.x;
         int e = 0, s = 0;
-        for (int r = 0; r < nr; ++r) {
-            epre[r] = e; spre[r] = s;
-            e += ev.ring_edge_cnt[(size_t)b * kMaxRings + r];
-            s += ev.ring_surf_cnt[(size_t)b * kMaxRings + r];
+        for (int r0 = 0; r0 < nr; r0 += 64) {
+            const int ce = r0 + r < nr ? ev.ring_edge_cnt[(size_t)b * kMaxRings + r0 + r] : 0;
+            const int cs = r0 + r < nr ? ev.ring_surf_cnt[(size_t)b * kMaxRings + r0 + r] : 0;
+            int xe = ce, xs = cs;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int ye = __shfl_up(xe, o, 64), ys = __shfl_up(xs, o, 64);
+                if (r >= o) { xe += ye; xs += ys; }
+            }
+            if (r0 + r < nr) { epre[r0 + r] = e + xe - ce; spre[r0 + r] = s + xs - cs; }
+            e += __shfl(xe, 63, 64);
+            s += __shfl(xs, 63, 64);
         }
-        epre[nr] = e; spre[nr] = s;
-        if (blockIdx.x == 0) {
-            ev.n_edge[b] = e;
-            ev.n_surf[b] = s;
+        if (r == 0) {
+            epre[nr] = e; spre[nr] = s;
+            if (blockIdx.x == 0) {
+                ev.n_edge[b] = e;
+                ev.n_surf[b] = s;
+            }
         }
     }
     __syncthreads();
@@ -674,7 +685,13 @@ hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
     hipLaunchKernelGGL(ring_scatter_kernel, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(sector_sort_kernel, dim3(ev.n_scans * 6, ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(ring_features_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
-    const int cblocks = min(256, (ev.raw_stride + 255) / 256);   // ~one feature and one position per thread
+    // blocks per scan (LMSF_CONCAT_BLOCKS, A/B; default 256: ~one feature and one position per thread)
+    static const int cmax = [] {
+        const char* e = getenv("LMSF_CONCAT_BLOCKS");
+        const int v = e ? atoi(e) : 256;
+        return v >= 1 && v <= 1024 ? v : 256;
+    }();
+    const int cblocks = min(cmax, (ev.raw_stride + 255) / 256);
     hipLaunchKernelGGL(concat_kernel, dim3(max(cblocks, 1), ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(order_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
     return hipGetLastError();

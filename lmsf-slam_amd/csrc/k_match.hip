@@ -852,7 +852,7 @@ __host__ __device__ __forceinline__ size_t memo_blocks(size_t feat_stride) { ret
 // returns the same 6 keys as the full 1 m walk.  One packet per wave at partial index 4 bx + wave.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_WAVES))) void match_memo_kernel(GridView ge, GridView gs, BatchView bv, int gx, int remap) {
     __shared__ int wcnt[8];
-    stamp_if(bv.stamp_start, blockIdx.x == 0);
+
     int bx, b;
     block_coords(remap, gx, bx, b);
     const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
@@ -981,6 +981,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_W
         bv.wl[(size_t)b * F + (size_t)bx * 256 + seg - 1 - (before_r + __popcll(mr & below))] = i;
     }
     if (threadIdx.x == 0) bv.wcount[(size_t)b * memo_blocks(F) + bx] = total | (total_r << 16);
+
     if (bv.n27) {   // accounting runs: queries and reused ones
         unsigned int qn = i < nq ? 1u : 0u;
 #pragma unroll

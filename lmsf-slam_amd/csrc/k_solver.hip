@@ -93,6 +93,7 @@ __global__ __launch_bounds__(64) void lm_step_kernel(BatchView bv, int outer, in
     SolveState& S = bv.st[b];
     if (!S.need_eval) {
         if (is_last && threadIdx.x == 0) finish_outer(S, outer);
+        stamp_if(bv.stamp_exit, b == 0);
         return;
     }
     __shared__ SolveState sS;
@@ -103,6 +104,7 @@ __global__ __launch_bounds__(64) void lm_step_kernel(BatchView bv, int outer, in
     if (threadIdx.x == 0) lm_step_apply(sS, tot, outer, is_last);
     __syncthreads();
     state_copy(S, sS);
+    stamp_if(bv.stamp_exit, b == 0);
 }
 
 // ---------------------------------------------------------------- GN (edgeSurfFeatureRegistration)

@@ -114,17 +114,21 @@ struct BatchView {
     int memo_refit;          // memo hits whose 5 neighbours changed order are refitted without a walk
                              //   (LMSF_MEMO_REFIT, default 1)
     // LMSF_STATS_TIMING: device wall-clock stamps of one neighbour-search launch, written by the first
-    // block of the search's first kernel at entry (stamp_start) and by the first block of the kernel that
-    // follows it in the stream at entry (stamp_end: lm_begin / fit_eval, which start once the search has
-    // drained); null: no stamps.  (r02 timed with a one-lane stamp kernel on each side: 2 x ~4.5 us of
-    // serialised dispatch per outer iteration, ~2.5% of a C4 scan.)
+    // block of the search kernel at entry (stamp_start), or -- before a memo pass, which has no register
+    // to spare (a store at its entry raised its spill 12 -> 20 B) -- by block 0 of the preceding lm_step
+    // at exit (stamp_exit); and by the first block of the kernel that follows the search at entry
+    // (stamp_end: lm_begin / fit_eval, which start once the search has drained); null: no stamps.
+    // (r02 timed with a one-lane stamp kernel on each side: 2 x ~4.5 us of serialised dispatch per outer
+    // iteration, ~2.5% of a C4 scan.)
     unsigned long long* stamp_start;
     unsigned long long* stamp_end;
+    unsigned long long* stamp_exit;
 };
 
 __device__ __forceinline__ void stamp_if(unsigned long long* at, bool first_block) {
     if (at && first_block && threadIdx.x == 0) *at = (unsigned long long)wall_clock64();
 }
+
 
 // ---- launchers (each enqueues on `stream`, never synchronises)
 // bbox[0..6] = the map box of the first n points (min(n, *n_dev) when n_dev) and that count; resets bbox first.
