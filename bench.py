@@ -269,8 +269,10 @@ def knn_roofline(ks, mean_n27, tj, elapsed_s, note):
     model_gbs = model_bytes / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     model_wall_gbs = model_bytes * launches / elapsed_s / 1e9 if elapsed_s > 0 else 0.0
     traffic = int(tj["hbm_bytes_per_launch"]) if tj else None
-    if traffic:
+    if traffic and avg_launch_ms > 0:
         achieved, basis = traffic / (avg_launch_ms * 1e-3) / 1e9, "pmc"
+    elif traffic:
+        achieved, basis = None, "untimed (no search-launch stamps in this build)"
     else:   # never the model: it counts cache-served candidate reads as HBM bytes
         achieved, basis = None, "unmeasured (no PMC profile of this workload under profiles/)"
     out = {"bound": "hbm", "achieved": round(achieved, 1) if achieved is not None else None, "peak": HBM_PEAK_GBS,

@@ -499,9 +499,15 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
         unsigned long long* st1 = t ? st0 + 1 : nullptr;
         // batch launches: one fused search + fit kernel (it is then the timed neighbour-search launch)
         const bool fused = match_fit_applies(ge2, gs2, bv, c->cfg.solver);
+        // Stamps: batch (fused) launches are timed by a one-lane stamp kernel on each side, single-scan
+        // launches in-kernel (knn_kernel's first block at entry, fit_eval's at entry).  Measured r02: the
+        // stamp kernels cost ~2.5% of a C4 scan (2 x ~4.5 us of serialised dispatch per outer iteration)
+        // and nothing at C2 (hidden by the other context streams), where in-kernel stamps (search entry /
+        // lm_step exit, lm_begin entry) measured 0.6-0.9% slower on one box (22.62-22.63k vs 22.76-22.81k
+        // scans/s without the clock reads).
+        if (fused && t) HIPCHK(c, launch_stamp(st0, s));
         if (fused) {
             BatchView bvo = bv;
-            bvo.stamp_start = st0;
             bvo.memo = o > 0 && !c->count27 && match_memo_enabled() ? 1 : 0;   // within one solve only
             HIPCHK(c, launch_match_fit(ge, gs, bvo, s));
         }
@@ -512,6 +518,7 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
             HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{},
                                  bvk, gn ? 1 : 0, s, !gn && match_memo_enabled()));
         }
+        if (fused && t) HIPCHK(c, launch_stamp(st1, s));
         if (t) c->ev_used += 2;
         c->knn_launches++;
         if (fused) c->fused_launches++;
@@ -524,21 +531,12 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
             HIPCHK(c, launch_gn_solve(bv, o, s));
         } else {
             BatchView bvb = bv;
-            if (fused) bvb.stamp_end = st1;
             if (fused) {   // packets: memo pass [0, ceil(nq / 64)) when it ran, search [part2_base, + ceil(n_search / 64))
                 bvb.fused_parts = 1;
                 bvb.memo = o > 0 && !c->count27 && match_memo_enabled() && !match_fit_prune(ge, gs) ? 1 : 0;
             }
             HIPCHK(c, launch_lm_begin(bvb, s));
-            // a memo pass opens the next outer iteration's search: its start stamp is the exit of this last
-            // lm_step (the memo kernel itself has no register to spare for it)
-            const bool next_memo = fused && o + 1 < iters && !c->count27 && match_memo_enabled() && !match_fit_prune(ge, gs);
-            for (int i = 0; i < 4; ++i) {
-                BatchView bve = bv;
-                if (i == 3 && next_memo && c->timing && c->ev_used + 2 <= 2 * kEventPairs)
-                    bve.stamp_exit = c->d_stamps + c->ev_used;
-                HIPCHK(c, launch_lm_eval_step(bve, o, i == 3 ? 1 : 0, s));
-            }
+            for (int i = 0; i < 4; ++i) HIPCHK(c, launch_lm_eval_step(bv, o, i == 3 ? 1 : 0, s));
         }
     }
     return LMSF_OK;

@@ -526,7 +526,24 @@ __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
     __shared__ int epre[kMaxRings + 1], spre[kMaxRings + 1];
     const int b = blockIdx.y;
     const int nr = ev.n_scans;
+#ifdef LMSF_CONCAT_SERIAL   // A/B build: r02 first-half prologue (one thread sums the ring counts)
+    if (threadIdx.x == 0) {
+        int e = 0, s = 0;
+        for (int r = 0; r < nr; ++r) {
+            epre[r] = e; spre[r] = s;
+            e += ev.ring_edge_cnt[(size_t)b * kMaxRings + r];
+            s += ev.ring_surf_cnt[(size_t)b * kMaxRings + r];
+        }
+        epre[nr] = e; spre[nr] = s;
+        if (blockIdx.x == 0) {
+            ev.n_edge[b] = e;
+            ev.n_surf[b] = s;
+        }
+    }
+    if (false) {
+#else
     if (threadIdx.x < 64) {   // ring-count prefixes by one wave: lane r loads ring r's counts, shuffle scan
+#endif
         const int r = threadIdx.x;
         int e = 0, s = 0;
         for (int r0 = 0; r0 < nr; r0 += 64) {

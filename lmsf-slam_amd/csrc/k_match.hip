@@ -1026,7 +1026,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     extern __shared__ int soff[];   // LIST: exclusive prefixes of the memo blocks' search / refit counts, 2 x [nblk + 1]
     constexpr bool kMemo = !PRUNE;
     constexpr int kNK = kMemo ? 6 : 5;
-    stamp_if(bv.stamp_start, blockIdx.x == 0);
     int bx, b;
     block_coords(remap, gx, bx, b);
     const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
@@ -1436,9 +1435,7 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
     } else if (bv.memo) {
         hipLaunchKernelGGL(match_memo_kernel, grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
         const size_t lds = 2 * (memo_blocks(bv.feat_stride) + 1) * sizeof(int);
-        BatchView bl = bv;
-        bl.stamp_start = nullptr;   // the memo pass opened the timed span
-        hipLaunchKernelGGL((match_fit_kernel<false, true>), grid, dim3(256), lds, s, edge, surf, bl, gx, remap);
+        hipLaunchKernelGGL((match_fit_kernel<false, true>), grid, dim3(256), lds, s, edge, surf, bv, gx, remap);
     } else {
         hipLaunchKernelGGL((match_fit_kernel<false, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
     }

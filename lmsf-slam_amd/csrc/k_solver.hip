@@ -70,7 +70,6 @@ __device__ __forceinline__ void lm_begin_apply(SolveState& S, const double* tot)
 
 // After fit_eval: IterationZero (evaluate at x0, jacobi scaling, gradient check) + first step.
 __global__ __launch_bounds__(kBeginThreads) void lm_begin_kernel(BatchView bv) {
-    stamp_if(bv.stamp_end, blockIdx.x == 0);
     const int b = blockIdx.x;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
     __shared__ SolveState sS;
@@ -93,7 +92,6 @@ __global__ __launch_bounds__(64) void lm_step_kernel(BatchView bv, int outer, in
     SolveState& S = bv.st[b];
     if (!S.need_eval) {
         if (is_last && threadIdx.x == 0) finish_outer(S, outer);
-        stamp_if(bv.stamp_exit, b == 0);
         return;
     }
     __shared__ SolveState sS;
@@ -104,7 +102,6 @@ __global__ __launch_bounds__(64) void lm_step_kernel(BatchView bv, int outer, in
     if (threadIdx.x == 0) lm_step_apply(sS, tot, outer, is_last);
     __syncthreads();
     state_copy(S, sS);
-    stamp_if(bv.stamp_exit, b == 0);
 }
 
 // ---------------------------------------------------------------- GN (edgeSurfFeatureRegistration)

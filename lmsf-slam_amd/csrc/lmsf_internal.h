@@ -113,20 +113,20 @@ struct BatchView {
                              //   (LMSF_MEMO_EXACT, default 1; 0: r01's 2 d < s6 - s5)
     int memo_refit;          // memo hits whose 5 neighbours changed order are refitted without a walk
                              //   (LMSF_MEMO_REFIT, default 1)
-    // LMSF_STATS_TIMING: device wall-clock stamps of one neighbour-search launch, written by the first
-    // block of the search kernel at entry (stamp_start), or -- before a memo pass, which has no register
-    // to spare (a store at its entry raised its spill 12 -> 20 B) -- by block 0 of the preceding lm_step
-    // at exit (stamp_exit); and by the first block of the kernel that follows the search at entry
-    // (stamp_end: lm_begin / fit_eval, which start once the search has drained); null: no stamps.
-    // (r02 timed with a one-lane stamp kernel on each side: 2 x ~4.5 us of serialised dispatch per outer
-    // iteration, ~2.5% of a C4 scan.)
+    // LMSF_STATS_TIMING, single-scan launches: device wall-clock stamps of one neighbour-search launch,
+    // written by knn_kernel's first block at entry (stamp_start) and by the first block of the fit_eval
+    // that follows it at entry (stamp_end: it starts once the search has drained); null: none.  Batch
+    // launches are timed by stamp kernels (enqueue_register).
     unsigned long long* stamp_start;
     unsigned long long* stamp_end;
-    unsigned long long* stamp_exit;
 };
 
 __device__ __forceinline__ void stamp_if(unsigned long long* at, bool first_block) {
+#ifndef LMSF_NO_STAMPS
     if (at && first_block && threadIdx.x == 0) *at = (unsigned long long)wall_clock64();
+#else   // A/B build without the clock read: every stamp 0 (the timing line then reads 0)
+    if (at && first_block && threadIdx.x == 0) *at = 0ull;
+#endif
 }
 
 
