@@ -804,7 +804,12 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(hipHostMalloc((void**)&c->h_raw_counts, B * sizeof(int), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_raw_off, B * sizeof(int64_t), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_off, B * sizeof(int64_t), hipHostMallocDefault));
-    CHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    // Created here, not at the first streamed upload: streams take the process's GPU_MAX_HW_QUEUES (4)
+    // hardware queues round-robin at creation, so with a copy stream per context the four C2 contexts'
+    // compute streams share two queues -- measured faster than one queue each (LMSF_LAZY_COPY_STREAM=1:
+    // 22.50 / 22.58 / 22.62k vs 23.07 / 22.85 / 23.11k scans/s, one box, alternating).
+    if (!(getenv("LMSF_LAZY_COPY_STREAM") && atoi(getenv("LMSF_LAZY_COPY_STREAM"))))
+        CHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     CHK(hipEventCreateWithFlags(&c->ev_raw_free, hipEventDisableTiming));
     CHK(hipEventCreateWithFlags(&c->ev_raw_ready, hipEventDisableTiming));
     CHK(hipEventRecord(c->ev_raw_free, c->stream));
@@ -1188,6 +1193,7 @@ lmsf_status lmsf_batch_load_scans_async(lmsf_ctx* c, const float* xyzi, const in
     for (int i = 0; i < n; ++i)
         if (counts[i] < 0 || counts[i] > c->R)
             return c->fail(LMSF_ERR_CAPACITY, "scan %d has %lld points (max_scan_points %d)", i, (long long)counts[i], c->R);
+    if (!c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     HIPCHK(c, hipStreamSynchronize(c->copy_stream));   // the previous upload (normally long done) owns h_raw_counts
     HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->ev_raw_free, 0));     // the last extraction has read raw
     size_t off = 0;
