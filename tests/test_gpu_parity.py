@@ -597,6 +597,22 @@ def test_voxel_filter_bitexact(lib, oracle_mod, small_workload):
     assert ctx.voxel_filter(far, 0.01).tobytes() == far.tobytes()
 
 
+def test_voxel_filter_small_bitexact(lib, oracle_mod, small_workload):
+    """Window-sized clouds (a C4 edge window is ~4.5k points) == oracle/voxel.cpp: random subsets from 1 to
+    9000 points, long voxels of duplicated points and the int32 key-overflow case (input returned)."""
+    ctx = _ctx(lib)
+    _, s, _, _ = oracle_mod.extract(small_workload.scans[0])
+    rng = np.random.default_rng(5)
+    for n in (1, 2, 63, 100, 1000, 4550, 8191, 8192, 8193, 9000):
+        pts = s[rng.permutation(len(s))[:n]] if n <= len(s) else s
+        for leaf in (0.2, 0.4, 2.0):
+            assert ctx.voxel_filter(pts, leaf).tobytes() == oracle_mod.voxel_filter(pts, leaf).tobytes(), (n, leaf)
+    dup = np.repeat(s[:50], 40, axis=0)                      # 40 copies of each point: long voxels
+    assert ctx.voxel_filter(dup, 0.4).tobytes() == oracle_mod.voxel_filter(dup, 0.4).tobytes()
+    far = np.concatenate([s[:500], np.array([[1e5, -1e5, 1e5, 2]], np.float32)])   # key range overflows
+    assert ctx.voxel_filter(far, 0.001).tobytes() == oracle_mod.voxel_filter(far, 0.001).tobytes()
+
+
 def test_ingest_pointcloud2_parity(lib, oracle_mod, small_workload):
     """lmsf_ingest_pointcloud2 / lmsf_extract_pointcloud2 vs oracle/ingest.cpp: decode + removeNaN
     and the distance filter bit-exact; rotary relative time (double atan2 rounded to float on both
