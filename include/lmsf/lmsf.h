@@ -308,9 +308,9 @@ lmsf_status lmsf_tracker_add_keyframe(lmsf_tracker* t, const float* edge, size_t
                                       size_t n_surf, const double pose[16]);
 /* Rebuilds the local map from the appended keyframes.  Returns once the rebuild is enqueued on the
  * tracker's own streams; the next lmsf_tracker_* call on t completes it, so context work enqueued in
- * between (lmsf_extract_features of the next scan, lmsf_copy_features) runs beside the rebuild.  Direct
- * map consumers on the same context (lmsf_solve, lmsf_match, lmsf_align_score, lmsf_set_map) are
- * called after a tracker call, not between this and the next one. */
+ * between (lmsf_extract_features of the next scan, lmsf_copy_features) runs beside the rebuild; map
+ * consumers of the same context (lmsf_solve, lmsf_match, lmsf_batch_launch, lmsf_set_map) complete it
+ * first as well. */
 lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t);
 
 /* VoxelGridFilter::Filter (INC/Algorithm/PointClouds/processing/Filter/voxel_grid.hpp:25-34,

@@ -208,6 +208,9 @@ struct lmsf_ctx {
     std::vector<float> host_scan[3];  // SetInputTarget copies (slot 0)
     bool scan_dirty = false;
     bool features_on_device = false;  // slot 0 features came from lmsf_extract_features
+    // trackers on this context with a deferred keyframe commit (lmsf_tracker_commit_map): completed
+    // before any map consumer of the context (resolve_all_lim1) or a map replacement
+    std::vector<std::pair<lmsf_status (*)(void*), void*>> settle_hooks;
     int64_t slot0_ne = 0, slot0_ns = 0;
     int last_outer = 0;
     int batch_done = 0;               // slots whose SolveState the last lmsf_batch_wait read back into h_st
@@ -446,7 +449,19 @@ lmsf_status resolve_lim1(lmsf_ctx* c, DevMap& m) {
     return LMSF_OK;
 }
 
+lmsf_status ctx_settle(lmsf_ctx* c) {
+    for (auto& h : c->settle_hooks) {
+        lmsf_status rc = h.first(h.second);
+        if (rc) return rc;
+    }
+    return LMSF_OK;
+}
+
+// Entry of every map consumer (enqueue_register / enqueue_solve / lmsf_match): deferred tracker commits
+// complete first.
 lmsf_status resolve_all_lim1(lmsf_ctx* c, size_t query_slots) {
+    lmsf_status rs = ctx_settle(c);
+    if (rs) return rs;
     if (knn_team_for(query_slots) != 1) return LMSF_OK;   // the 8-lane walk never prunes
     for (DevMap* ms : {c->map, c->prior})
         for (int k = 0; k < 3; ++k) {
@@ -825,6 +840,8 @@ lmsf_status lmsf_set_map(lmsf_ctx* c, int32_t kind, const float* xyzi, size_t n)
     if (n == 0) return LMSF_OK;  // empty source ignored (ceres_...:60)
     if (!xyzi) return c->fail(LMSF_ERR_ARG, "null map pointer");
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    lmsf_status rs = ctx_settle(c);
+    if (rs) return rs;
     return build_map(c, kind, xyzi, n);
 }
 
@@ -1407,6 +1424,17 @@ int ctx_device(const lmsf_ctx* c) { return c->cfg.device; }
 int ctx_feature_capacity(const lmsf_ctx* c) { return c->F; }
 bool ctx_features_on_device(const lmsf_ctx* c) { return c->features_on_device; }
 lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg) { return c->fail(code, "%s", msg); }
+
+void ctx_add_settle(lmsf_ctx* c, lmsf_status (*fn)(void*), void* arg) { c->settle_hooks.emplace_back(fn, arg); }
+
+void ctx_remove_settle(lmsf_ctx* c, void* arg) {
+    auto& v = c->settle_hooks;
+    for (size_t i = 0; i < v.size(); ++i)
+        if (v[i].second == arg) {
+            v.erase(v.begin() + (long)i);
+            return;
+        }
+}
 
 // SetInputSource from device-resident points (local-map rebuild without a host round trip).
 lmsf_status ctx_set_prior_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n) {

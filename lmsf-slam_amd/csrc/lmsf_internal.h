@@ -268,6 +268,9 @@ int ctx_device(const lmsf_ctx* c);
 int ctx_feature_capacity(const lmsf_ctx* c);
 bool ctx_features_on_device(const lmsf_ctx* c);
 lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg);
+// a tracker's deferred-commit completion, run by the context before its map consumers
+void ctx_add_settle(lmsf_ctx* c, lmsf_status (*fn)(void*), void* arg);
+void ctx_remove_settle(lmsf_ctx* c, void* arg);
 // map of a kind = [prior | window]: the prior grid is built once (static), the window grid at every
 // keyframe commit with indices offset by the prior size; n == 0 clears that part.
 lmsf_status ctx_set_prior_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n);

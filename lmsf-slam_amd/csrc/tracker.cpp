@@ -315,6 +315,7 @@ lmsf_status lmsf_tracker_config_init(lmsf_tracker_config* cfg) {
 
 void lmsf_tracker_destroy(lmsf_tracker* t) {
     if (!t) return;
+    ctx_remove_settle(t->ctx, t);
     hipSetDevice(ctx_device(t->ctx));
     hipStreamSynchronize(ctx_stream(t->ctx));
     for (auto& w : t->win) {
@@ -371,6 +372,7 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
         return LMSF_ERR_HIP;
     }
     t->origin = t->curr = t->prev = t->motion = t->last_kf = iso_identity();
+    ctx_add_settle(ctx, [](void* p) { return settle(static_cast<lmsf_tracker*>(p)); }, t);
     *out = t;
     return LMSF_OK;
 }
