@@ -694,6 +694,7 @@ def test_tracker_shared_map_streams(lib, oracle_mod, sequence_workload):
         ots[s].set_prior_map(1, wl.edge_map)
         ots[s].set_prior_map(2, wl.surf_map)
     buf = {k: torch.zeros((70000, 4), dtype=torch.float32, device=dev) for k in (lib.EDGE, lib.SURF)}
+    nq = {}
     for step in range(5):
         kfs_g, kfs_o = [], []
         for s, idx in enumerate(streams):
@@ -703,6 +704,7 @@ def test_tracker_shared_map_streams(lib, oracle_mod, sequence_workload):
             _, r = gts[s].solve_extracted(wl.dt * step)
             _, otyp, _ = ots[s].solve(e, su, wl.dt * step)
             assert r.update_type == otyp
+            nq[s] = len(e) + len(su)
             dt, dr = mat_err(gts[s].pose(), ots[s].curr)
             assert dt <= POSE_TOL and dr <= POSE_TOL, (step, s, dt, dr)
             dt, dr = mat_err(gts[s].pose(), pose_matrix(wl.truth[idx[step]]))
@@ -718,8 +720,13 @@ def test_tracker_shared_map_streams(lib, oracle_mod, sequence_workload):
                 gts[s].add_keyframe(*g)
                 ots[s].add_keyframe(*o)
         for s in range(len(streams)):
-            gts[s].commit_map()
+            gts[s].commit_map()                     # returns with the rebuild enqueued (deferred finish)
             ots[s].commit()
+            if s == 0 and kfs_g:                    # a context-level map consumer completes it first
+                rec_a, nn_a = ctxs[0].match(wl.truth[streams[0][step]], nq[0])
+                gts[0].local_map(lib.EDGE)
+                rec_b, nn_b = ctxs[0].match(wl.truth[streams[0][step]], nq[0])
+                assert rec_a.tobytes() == rec_b.tobytes() and (nn_a == nn_b).all()
             assert len(gts[s].local_map(lib.SURF)) == len(ots[s].local_map(2))
     np.testing.assert_allclose(gts[0].local_map(lib.SURF), gts[1].local_map(lib.SURF), atol=0)
     np.testing.assert_allclose(gts[0].local_map(lib.EDGE), ots[0].local_map(1), atol=1e-4)
