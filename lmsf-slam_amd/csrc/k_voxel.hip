@@ -25,7 +25,7 @@ namespace lmsf {
 // launch instead of ~13) was bit-exact but slower on the tracker's ~4.5k-point edge window: C4 1.65-1.89
 // vs 1.55-1.85 ms/scan, C3 1.68-1.72 vs 1.58-1.62 ms/frame (91 barrier-separated sort stages): removed.
 // hipcub's default dispatch (merge sort below 2^20 items).  Measured on a C4 commit: rocprim onesweep
-// (radix_sort_config merge limit 0) took 4 x ~25 us + 8 lookback resets for the ~3e5-point surf window
+// (radix_sort_config merge limit 0) took 4 x ~25 us + 8 lookback resets for the ~6e5-point surf window
 // (merge sort ~130 us) and 4 x ~18 us for the edge window (merge sort ~25 us): not used.
 static hipError_t voxel_sort(void* tmp, size_t& bytes, const uint32_t* k_in, uint32_t* k_out, const int* v_in,
                              int* v_out, int n, hipStream_t s) {
