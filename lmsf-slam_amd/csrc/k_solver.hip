@@ -69,7 +69,20 @@ __device__ __forceinline__ void lm_begin_apply(SolveState& S, const double* tot)
 
 
 // After fit_eval: IterationZero (evaluate at x0, jacobi scaling, gradient check) + first step.
-__global__ __launch_bounds__(kBeginThreads) void lm_begin_kernel(BatchView bv) {
+// LMSF_CTL_WAVES: waves per SIMD the LM control kernels are compiled for; 0 = the compiler's choice
+// (lm_begin 195 VGPRs, lm_step 256).  At 8, lm_begin fits 64 VGPRs (604 B of scratch for its serial lane)
+// and finds a slot beside the other contexts' search waves (4 x 121 VGPRs per SIMD) sooner; lm_step
+// stays at 256.  A/B on one box (tools/gpu_ab_lib2.sh, C2, alternating): 23.31-23.40k scans/s vs
+// 23.14-23.25k at 0; 4 (128 VGPRs, 380 / 576 B scratch) 23.18-23.25k.  C4 within its noise.
+#ifndef LMSF_CTL_WAVES
+#define LMSF_CTL_WAVES 8
+#endif
+#if LMSF_CTL_WAVES > 0
+#define LMSF_CTL_ATTR __attribute__((amdgpu_waves_per_eu(LMSF_CTL_WAVES)))
+#else
+#define LMSF_CTL_ATTR
+#endif
+__global__ __launch_bounds__(kBeginThreads) LMSF_CTL_ATTR void lm_begin_kernel(BatchView bv) {
     const int b = blockIdx.x;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
     __shared__ SolveState sS;
@@ -87,7 +100,7 @@ __global__ __launch_bounds__(kBeginThreads) void lm_begin_kernel(BatchView bv) {
 }
 
 // After lm_eval_kernel at the candidate (LMSF_LM_FUSED=0): the reduction and lm_step_apply.
-__global__ __launch_bounds__(64) void lm_step_kernel(BatchView bv, int outer, int is_last) {
+__global__ __launch_bounds__(64) LMSF_CTL_ATTR void lm_step_kernel(BatchView bv, int outer, int is_last) {
     const int b = blockIdx.x;
     SolveState& S = bv.st[b];
     if (!S.need_eval) {
