@@ -85,6 +85,9 @@ def parse(argv=None):
                          "(lmsf_batch_load_scans_async, overlapped with the previous launch) -- reported as "
                          "`h2d_inclusive` beside the HBM-resident headline")
     ap.add_argument("--workers", type=int, default=None, help="processes generating the synthetic scans")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=V",
+                    help="context option (lmsf_set_option, e.g. MEMO_BOUND=2 or QUERY_MEMO=0) for A/B runs; the "
+                         "line records it under config.options")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend of the ranks (nccl = RCCL)")
     ap.add_argument("--launch-check", action="store_true",
                     help="no GPU work: ranks join the process group, run the C2 pose all-gather on CPU tensors and "
@@ -296,7 +299,18 @@ def knn_roofline(ks, mean_n27, tj, elapsed_s, note):
     return out
 
 
+def apply_options(args, ctxs):
+    """--opt NAME=V on every context (lmsf_set_option)."""
+    from lmsf import _lib
+    for o in args.opt:
+        name, v = o.split("=", 1)
+        for c in ctxs:
+            c.set_option(getattr(_lib, "OPT_" + name.upper()), int(v))
+
+
 def line(args, d, metric, value, unit, elapsed, scaling, workload, extra_cfg, roofline, cpu, **extra):
+    if args.opt:
+        extra_cfg = dict(extra_cfg, options=list(args.opt))
     out = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": d.world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
            "scaling": scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
@@ -423,6 +437,7 @@ def run_batch(args, d):
     max_pts = max(len(s) for s in scans_u)
     ctxs = [_lib.Context(device=d.local, max_batch=sub_b, max_scan_points=max_pts + 64, max_features=max_pts + 64,
                          schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer, **c["extract"]) for _ in range(S)]
+    apply_options(args, ctxs)
     ctx_scans = [[scans_u[j % U] for j in range(i * sub_b, min((i + 1) * sub_b, chunk))] for i in range(S)]
     for cx, sc in zip(ctxs, ctx_scans):
         cx.set_map(_lib.EDGE, em_t)
@@ -589,6 +604,7 @@ def run_streams(args, d):
     max_pts = max(len(s) for s in scans)
     ctx = _lib.Context(device=d.local, max_batch=1, max_scan_points=max_pts + 64, max_features=max_pts + 64,
                        schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer)
+    apply_options(args, [ctx])
     tr = _lib.Tracker(ctx, manual_map_update=True)
     T0 = np.eye(4)
     T0[:3, :3] = synth.quat_to_mat(truth[0][:4])
@@ -707,6 +723,7 @@ def run_dual(args, d):
     sub_dev = [torch.from_numpy(s).to(d.dev) for s in ds.sub]
     max_pts = max(max(len(s) for s in ds.primary), max(len(s) for s in ds.sub))
     ctx = _lib.Context(device=d.local, max_batch=1, max_scan_points=max_pts + 64, max_features=max_pts + 64)
+    apply_options(args, [ctx])
     system = dual.DualLidarSystem(ctx, extrinsic=X0)
     state = {"i": 0}
 

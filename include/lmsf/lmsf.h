@@ -193,6 +193,8 @@ lmsf_status lmsf_batch_load_scans(lmsf_ctx* ctx, const float* xyzi, const int64_
  * xyzi (page-locked host memory for a truly asynchronous copy) and counts' values unchanged until
  * the lmsf_batch_wait of that next launch returns. */
 lmsf_status lmsf_batch_load_scans_async(lmsf_ctx* ctx, const float* xyzi, const int64_t* counts, int32_t n);
+/* n may not exceed the scans of the last load (LMSF_ERR_STATE): a load of fewer scans -- including
+ * lmsf_extract_features, which loads one scan into slot 0 -- replaces a streamed batch not yet launched. */
 lmsf_status lmsf_batch_run(lmsf_ctx* ctx, int32_t n, double* poses, lmsf_solve_stats* stats);
 /* Same, but without blocking: poses are read back by lmsf_batch_wait. */
 lmsf_status lmsf_batch_launch(lmsf_ctx* ctx, int32_t n, const double* poses);
@@ -204,7 +206,34 @@ lmsf_status lmsf_batch_trace(lmsf_ctx* ctx, int32_t slot, double* trace, int32_t
 lmsf_status lmsf_batch_copy_features(lmsf_ctx* ctx, int32_t slot, int32_t kind, float* out, int32_t* src,
                                      size_t cap, size_t* n_out);
 
+/* ---- context options (not on the reference surface): algorithm switches of the build.
+ * Results do not depend on them (the memo switches are exact, DESIGN.md section 4 "Query memo"); they
+ * exist so tests can compare the paths in one process and a caller can rule a path out.  Values 0 | 1
+ * (LMSF_OPT_MEMO_BOUND: 0 | 1 | 2); defaults 1, LMSF_OPT_GRAPH 0. */
+#define LMSF_OPT_QUERY_MEMO 0   /* 1: outer iterations > 0 reuse 5-NN sets that provably did not change */
+#define LMSF_OPT_MEMO_REFIT 1   /* 1: a reused set in a new order is refitted without a walk */
+#define LMSF_OPT_MEMO_EXACT 2   /* 1: keep the set when its farthest point is nearer than s6 - d (0: 2d < s6 - s5) */
+#define LMSF_OPT_MEMO_ORDER 3   /* 1: consecutive-gap test first (no re-keying when every gap exceeds 2d) */
+#define LMSF_OPT_MEMO_BOUND 4   /* memo misses walk a bounded radius: 1 = min(1 m, s6 + d, the farthest of the
+                                   stored 5 at the new query), 2 = min(1 m, s6 + d) (r02), 0 = the full 1 m */
+#define LMSF_OPT_GRAPH 5        /* 1: replay state init + registration as a HIP graph (default 0) */
+#define LMSF_OPT_COUNT 6
+lmsf_status lmsf_set_option(lmsf_ctx* ctx, int32_t option, int32_t value);
+
 /* ---- diagnostics used by the parity tests and the roofline report (not on the reference surface) */
+/* Record capture: for the following launches (lmsf_batch_launch / lmsf_batch_run / lmsf_solve), the
+ * correspondence records and 5-NN indices of up to LMSF_MAX_CAPTURE batch slots are copied aside on the
+ * device after every outer iteration's matching (the first 10), with the pose they were matched at --
+ * the records the solver then reads, including those the query memo reused or refitted.  n = 0 stops it.
+ * The capture makes the search kernels also store their neighbours (stores only; the same kernels). */
+#define LMSF_MAX_CAPTURE 4
+lmsf_status lmsf_batch_capture(lmsf_ctx* ctx, const int32_t* slots, int32_t n);
+/* Captured rows of `slot` at outer iteration `iter` of the last launch, in slot order (edges then surfs,
+ * as lmsf_match): records, neighbour indices (5 per query, -1: rank not found within 1 m; nullable), the
+ * linearisation pose (nullable); *n_out = queries.  Host or device memory. */
+lmsf_status lmsf_batch_records(lmsf_ctx* ctx, int32_t slot, int32_t iter, lmsf_record* out, int32_t* nn, size_t cap,
+                               double pose[7], size_t* n_out);
+
 /* Matching only at a pose: n_edge + n_surf records (edges first) and the 5 neighbour map indices. */
 lmsf_status lmsf_match(lmsf_ctx* ctx, const double pose[7], lmsf_record* out, int32_t* nn, size_t cap);
 /* Weighted normal-equation packet of the current records at a pose: cost, H (21 upper, row-major),

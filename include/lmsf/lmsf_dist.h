@@ -14,7 +14,14 @@
  *            keyframed -- by an all-gather of the padded feature buffers, so every replica appends
  *            the same keyframes in rank order.
  * Every call is collective (all ranks, same order) and returns when its result is usable: host
- * results are written, device results are complete on the device.
+ * results are written, device results are complete on the device.  Every rank takes the same path
+ * through a call: an argument problem only one rank can see (a null buffer, a too-small capacity)
+ * travels in the call's first exchange, so every rank returns the same error and none is left inside
+ * a collective the others skipped.
+ *
+ * Transports: RCCL (lmsf_group_create; "device" buffers below are device memory of the group's GPU), or
+ * the caller's own host collectives (lmsf_group_create_transport; the same buffers are then host
+ * memory) -- the same protocol code either way, which is how the CPU tests run it over gloo.
  */
 #ifndef LMSF_LMSF_DIST_H_
 #define LMSF_LMSF_DIST_H_
@@ -38,6 +45,15 @@ lmsf_status lmsf_group_unique_id(uint8_t id[LMSF_GROUP_ID_BYTES]);
 /* Join the group as `rank` of `nranks` on HIP device `device` (one device per rank). */
 lmsf_status lmsf_group_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t id[LMSF_GROUP_ID_BYTES],
                               lmsf_group** out);
+/* Caller-supplied collectives on host memory (MPI, a torch.distributed group, ...); each returns 0 on
+ * success.  allgather: bytes_per_rank from send -> recv[nranks][bytes_per_rank] in rank order;
+ * broadcast: bytes of buf from root to every rank.  The struct is copied; `user` is passed back. */
+typedef struct {
+    void* user;
+    int32_t (*allgather)(void* user, const void* send, void* recv, size_t bytes_per_rank);
+    int32_t (*broadcast)(void* user, void* buf, size_t bytes, int32_t root);
+} lmsf_transport;
+lmsf_status lmsf_group_create_transport(int32_t nranks, int32_t rank, const lmsf_transport* tp, lmsf_group** out);
 void lmsf_group_destroy(lmsf_group* g);
 int32_t lmsf_group_rank(const lmsf_group* g);
 int32_t lmsf_group_size(const lmsf_group* g);
@@ -45,17 +61,21 @@ int32_t lmsf_group_size(const lmsf_group* g);
 /* C2 / C5: every rank's n poses (qx qy qz qw tx ty tz, host) -> all[rank][n][7] (host). */
 lmsf_status lmsf_group_allgather_poses(lmsf_group* g, const double* mine, int32_t n, double* all);
 
-/* C4: the root's cloud (xyzi rows in device memory, *n rows at the root) replicated into every rank's
- * device buffer xyzi_dev of cap rows; *n = rows on return (LMSF_ERR_CAPACITY when cap is too small). */
-lmsf_status lmsf_group_broadcast_cloud(lmsf_group* g, int32_t root, float* xyzi_dev, size_t cap, size_t* n);
+/* C4: the root's cloud (xyzi rows, *n rows at the root) replicated into every rank's buffer xyzi of cap
+ * rows (device memory for RCCL groups); *n = rows on return.  Every rank returns LMSF_ERR_CAPACITY when
+ * some rank's cap is too small, LMSF_ERR_ARG when some rank passed no buffer for a non-empty cloud. */
+lmsf_status lmsf_group_broadcast_cloud(lmsf_group* g, int32_t root, float* xyzi, size_t cap, size_t* n);
 
 /* C4 keyframe exchange.  In: this rank's pose (4x4 row-major), update type (0: none), feature counts
- * and feat_dev = [edges (cap rows) | surfs (cap rows)] xyzi in device memory.  Out: info[rank][19] =
- * (pose[16], update type, n_edge, n_surf) of every rank (host); *any = 1 when some rank keyframed, and
- * then gathered_dev[rank][2 * cap][4] holds every rank's buffer (device). */
+ * and feat = [edges (cap rows) | surfs (cap rows)] xyzi (device memory for RCCL groups).  Out: info[rank]
+ * [19] = (pose[16], update type, n_edge, n_surf) of every rank (host); *any = 1 when some rank keyframed,
+ * and then gathered[rank][2 * cap][4] holds every rank's buffer.  Every replica appends rank r's
+ * keyframe (gathered[r] rows [0, n_edge) and [cap, cap + n_surf)) for r = 0, 1, ... with a non-zero
+ * update type: the same keyframes in the same order on every rank.  Counts above cap or a null feat /
+ * gathered on any rank: LMSF_ERR_ARG on every rank (*any = 0).  g, pose, info and any are required. */
 lmsf_status lmsf_group_exchange_keyframes(lmsf_group* g, const double pose[16], int32_t update_type, int64_t n_edge,
-                                          int64_t n_surf, const float* feat_dev, size_t cap, double* info,
-                                          float* gathered_dev, int32_t* any);
+                                          int64_t n_surf, const float* feat, size_t cap, double* info, float* gathered,
+                                          int32_t* any);
 
 /* Max over ranks of a host double (the bench's max-over-ranks timing). */
 lmsf_status lmsf_group_max(lmsf_group* g, double* value);

@@ -51,11 +51,10 @@ struct DevMap {
 constexpr size_t kMaxCells = (size_t)1 << 30;   // 4 GiB of offsets: refuse larger map extents
 constexpr int kEventPairs = 4096;
 
-// x-slices per metre of the map grids (LMSF_GRID_SX = 1 | 2 | 4 | 8 overrides; measured in DESIGN.md)
+// x-slices per metre of the map grids (A/B builds: LMSF_GRID_SX = 1 | 2 | 4 | 8; measured in DESIGN.md)
 int grid_slices() {
     static const int sx = [] {
-        const char* e = getenv("LMSF_GRID_SX");
-        const int v = e ? atoi(e) : 4;
+        const int v = ab_int("LMSF_GRID_SX", 4);
         return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 4;
     }();
     return sx;
@@ -65,17 +64,11 @@ int grid_slices() {
 // x-slice: dense maps (rho >= 8; C5's 10M-point map: 19 surf / 38 edge) get lim1 = 1 / rho m^2,
 // between the median and the 90th percentile of the 5th-neighbour distance^2 (0.037 / 0.085 m^2 on
 // C5's surf map; per C5 knn launch: 2 / rho 7.04 ms, 0.05 for both kinds 6.52 ms); sparse
-// maps (C2's 1M-point map: 2.3 / 4.3) keep lim1 = 1, the plain walk.  LMSF_KNN_LIM1 forces a value
-// and LMSF_KNN_PRUNE_RHO the density threshold (A/B).  Speed only: results do not depend on it.
+// maps (C2's 1M-point map: 2.3 / 4.3) keep lim1 = 1, the plain walk.  A/B builds: LMSF_KNN_LIM1 forces a
+// value (in 1/1000 m^2) and LMSF_KNN_PRUNE_RHO the density threshold.  Speed only: results do not depend on it.
 float knn_first_radius2(size_t n, unsigned long long occupied) {
-    static const float forced = [] {
-        const char* e = getenv("LMSF_KNN_LIM1");
-        return e ? (float)atof(e) : -1.f;
-    }();
-    static const double rho_min = [] {
-        const char* e = getenv("LMSF_KNN_PRUNE_RHO");
-        return e ? atof(e) : 8.0;
-    }();
+    static const float forced = (float)ab_int("LMSF_KNN_LIM1", -1) * 1e-3f;
+    static const double rho_min = (double)ab_int("LMSF_KNN_PRUNE_RHO", 8);
     if (forced > 0.f) return forced;
     if (occupied == 0) return 1.f;
     const double rho = (double)n / (double)occupied;
@@ -83,43 +76,14 @@ float knn_first_radius2(size_t n, unsigned long long occupied) {
     return (float)std::min(1.0, std::max(0.01, 1.0 / rho));
 }
 
-// LMSF_MEMO_BOUND = 0 | 1 (A/B, default 1): memo misses search a bounded radius (k_match.hip).
-bool memo_bound_enabled() {
-    static const bool v = [] {
-        const char* e = getenv("LMSF_MEMO_BOUND");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
-
-// LMSF_MEMO_REFIT = 0 | 1 (A/B, default 1): memo hits whose neighbours changed order are refitted from the
-// memo pass's list without a walk (k_match.hip); 0 sends them to the search.
-bool memo_order_enabled() {   // LMSF_MEMO_ORDER = 0 | 1 (A/B, default 1), read per launch
-    const char* e = getenv("LMSF_MEMO_ORDER");
-    return e ? atoi(e) != 0 : true;
-}
-
-bool memo_exact_enabled() {   // LMSF_MEMO_EXACT = 0 | 1 (A/B, default 1), read per launch
-    const char* e = getenv("LMSF_MEMO_EXACT");
-    return e ? atoi(e) != 0 : true;
-}
-
-bool memo_refit_enabled() {   // read per launch, so a test can compare both in one process
-    const char* e = getenv("LMSF_MEMO_REFIT");
-    return e ? atoi(e) != 0 : true;
-}
-
 }  // namespace
 
 // Host wait on a stream of the latency-bound single-scan paths (extraction read-back, solve, tracker
-// commit).  LMSF_SPIN_SYNC=1 polls hipStreamQuery instead of hipStreamSynchronize: A/B on one box (C4 /
-// C3 ms per scan, two runs each: 1.55, 1.74 / 1.50, 1.73 spinning vs 1.63, 1.71 / 1.52, 1.50 blocking)
+// commit).  A/B builds: LMSF_SPIN_SYNC=1 polls hipStreamQuery instead of hipStreamSynchronize: on one box (C4
+// / C3 ms per scan, two runs each: 1.55, 1.74 / 1.50, 1.73 spinning vs 1.63, 1.71 / 1.52, 1.50 blocking)
 // within the noise, so the blocking wait stays the default.
 hipError_t lmsf::stream_wait(hipStream_t s) {
-    static const bool spin = [] {
-        const char* e = getenv("LMSF_SPIN_SYNC");
-        return e ? atoi(e) != 0 : false;
-    }();
+    static const bool spin = ab_int("LMSF_SPIN_SYNC", 0) != 0;
     if (!spin) return hipStreamSynchronize(s);
     for (;;) {
         const hipError_t e = hipStreamQuery(s);
@@ -141,6 +105,16 @@ hipError_t dalloc(T** p, size_t count) {
 struct lmsf_ctx {
     lmsf_config cfg;
     std::string err;
+    int opt[LMSF_OPT_COUNT] = {1, 1, 1, 1, 1, 0};   // lmsf_set_option (defaults: lmsf.h)
+    // record capture (lmsf_batch_capture): device rows [n_cap][kCaptureIters][F] of the captured slots
+    std::vector<int> cap_slots;
+    lmsf_record* cap_rec = nullptr;
+    int32_t* cap_nn = nullptr;        // [n_cap][kCaptureIters][F][5]
+    double* cap_pose = nullptr;       // [n_cap][kCaptureIters][7]
+    int cap_alloc = 0;                // captured slots the buffers hold
+    int cap_iters = 0;                // outer iterations captured by the last launch
+    int cap_by_pos = 0;
+    int raw_loaded = 0;               // slots of the last (or pending streamed) load
     hipStream_t stream = nullptr;
     int B = 1, R = 0, F = 0, max_parts = 0, n_tiles = 0;
     int optimization_count = 10;
@@ -267,10 +241,10 @@ struct lmsf_ctx {
         v.memo_nbr = memo_nbr;
         v.wl = wl;
         v.wlim = wlim;
-        v.memo_bound = memo_bound_enabled() ? 1 : 0;
-        v.memo_refit = memo_refit_enabled() ? 1 : 0;
-        v.memo_exact = memo_exact_enabled() ? 1 : 0;
-        v.memo_order = memo_order_enabled() ? 1 : 0;
+        v.memo_bound = opt[LMSF_OPT_MEMO_BOUND];
+        v.memo_refit = opt[LMSF_OPT_MEMO_REFIT];
+        v.memo_exact = opt[LMSF_OPT_MEMO_EXACT];
+        v.memo_order = opt[LMSF_OPT_MEMO_ORDER];
         v.wcount = wcount;
         v.n_search = n_search;
         v.fused_parts = 0;            // set for the fused path's lm_begin (enqueue_register)
@@ -503,11 +477,17 @@ lmsf_status sync_slot0_features(lmsf_ctx* c) {
 lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
     lmsf_status rl = resolve_all_lim1(c, (size_t)c->F * nb);
     if (rl) return rl;
-    const BatchView bv = c->bview(nb);
+    BatchView bv = c->bview(nb);
     const GridView ge = c->map[LMSF_EDGE].view(), gs = c->map[LMSF_SURF].view();
     const GridView ge2 = c->prior[LMSF_EDGE].view(), gs2 = c->prior[LMSF_SURF].view();
     hipStream_t s = c->stream;
     const bool gn = c->cfg.solver == LMSF_SOLVER_GN;
+    const bool memo_on = c->opt[LMSF_OPT_QUERY_MEMO] != 0;
+    // record capture: every launch of this solve writes nnp (stores only: the same kernels, the same
+    // results), so a captured slot's neighbours are readable after each outer iteration
+    const bool capture = !c->cap_slots.empty();
+    if (capture) bv.write_nn = 1;
+    c->cap_iters = 0;
     for (int o = 0; o < iters; ++o) {
         const bool t = c->timing && c->ev_used + 2 <= 2 * kEventPairs;
         unsigned long long* st0 = t ? c->d_stamps + c->ev_used : nullptr;   // search entry / exit stamps
@@ -523,15 +503,15 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
         if (fused && t) HIPCHK(c, launch_stamp(st0, s));
         if (fused) {
             BatchView bvo = bv;
-            bvo.memo = o > 0 && !c->count27 && match_memo_enabled() ? 1 : 0;   // within one solve only
+            bvo.memo = o > 0 && !c->count27 && memo_on ? 1 : 0;   // within one solve only
             HIPCHK(c, launch_match_fit(ge, gs, bvo, s));
         }
         else {   // single-scan launches: the 8-lane search, with the slot memo under the Ceres-LM solver
             BatchView bvk = bv;
             bvk.stamp_start = st0;
-            bvk.memo = !gn && o > 0 && !c->count27 && match_memo_enabled() ? 1 : 0;
+            bvk.memo = !gn && o > 0 && !c->count27 && memo_on ? 1 : 0;
             HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{},
-                                 bvk, gn ? 1 : 0, s, !gn && match_memo_enabled()));
+                                 bvk, gn ? 1 : 0, s, !gn && memo_on));
         }
         if (fused && t) HIPCHK(c, launch_stamp(st1, s));
         if (t) c->ev_used += 2;
@@ -542,13 +522,25 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
             bvf.stamp_end = st1;   // fit_eval starts when the search has drained
             HIPCHK(c, launch_fit_eval(ge, gs, bvf, c->cfg.solver, s));
         }
+        if (capture && o < kCaptureIters) {   // this iteration's records, before the solver reads them
+            const size_t F = (size_t)c->F;
+            for (size_t k = 0; k < c->cap_slots.size(); ++k) {
+                const int b = c->cap_slots[k];
+                if (b >= nb) continue;
+                const size_t row = k * kCaptureIters + (size_t)o;
+                HIPCHK(c, launch_capture(bv, b, fused ? 1 : 0, c->cap_rec + row * F, c->cap_nn + row * F * 5,
+                                         c->cap_pose + row * 7, s));
+            }
+            c->cap_iters = o + 1;
+            c->cap_by_pos = fused ? 1 : 0;
+        }
         if (gn) {
             HIPCHK(c, launch_gn_solve(bv, o, s));
         } else {
             BatchView bvb = bv;
             if (fused) {   // packets: memo pass [0, ceil(nq / 64)) when it ran, search [part2_base, + ceil(n_search / 64))
                 bvb.fused_parts = 1;
-                bvb.memo = o > 0 && !c->count27 && match_memo_enabled() && !match_fit_prune(ge, gs) ? 1 : 0;
+                bvb.memo = o > 0 && !c->count27 && memo_on && !match_fit_prune(ge, gs) ? 1 : 0;
             }
             HIPCHK(c, launch_lm_begin(bvb, s));
             for (int i = 0; i < 4; ++i) HIPCHK(c, launch_lm_eval_step(bv, o, i == 3 ? 1 : 0, s));
@@ -557,20 +549,13 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
     return LMSF_OK;
 }
 
-// LMSF_GRAPH = 0 | 1 (default 0; A/B): state init + registration as a replayed HIP graph.  A C2
+// LMSF_OPT_GRAPH = 0 | 1 (default 0): state init + registration as a replayed HIP graph.  A C2
 // context launch is ~65 dependent kernels: replay cuts its host enqueue (0.39 ms per C2 step for both
 // contexts) and the per-kernel dispatch gap (tools/graphprobe: 60 small kernels 160 -> 108 us on the
 // GPU, 159 -> 9 us to enqueue).  Measured r02 (tools/gpu_graph_ab.sh): C2 22.46k / 22.35k scans/s with
 // graphs vs 22.52k without (the step is GPU-bound, the enqueue already hidden); C4 2.00 vs 1.76 ms and
 // C3 1.83-1.90 vs 1.73 ms per scan (every keyframe moves the window grid, so the graph is re-captured and
 // re-instantiated).  Off by default.
-bool graphs_enabled() {
-    static bool v = [] {
-        const char* e = getenv("LMSF_GRAPH");
-        return e ? atoi(e) != 0 : false;
-    }();
-    return v;
-}
 
 std::vector<unsigned char> solve_key(lmsf_ctx* c, int nb, int iters) {
     std::vector<unsigned char> k;
@@ -585,7 +570,7 @@ std::vector<unsigned char> solve_key(lmsf_ctx* c, int nb, int iters) {
             const GridView g = ms[kind].view();
             put(&g, sizeof g);
         }
-    const int flags[] = {nb, iters, c->timing ? 1 : 0, c->count27 ? 1 : 0, match_memo_enabled() ? 1 : 0, c->cfg.solver};
+    const int flags[] = {nb, iters, c->timing ? 1 : 0, c->count27 ? 1 : 0, c->opt[LMSF_OPT_QUERY_MEMO], c->cfg.solver};
     put(flags, sizeof flags);
     return k;
 }
@@ -595,7 +580,8 @@ lmsf_status enqueue_solve(lmsf_ctx* c, int nb, int iters) {
     lmsf_status rl = resolve_all_lim1(c, (size_t)c->F * nb);   // host read-back: never inside a capture
     if (rl) return rl;
     hipStream_t s = c->stream;
-    if (!graphs_enabled() || c->ev_used != 0) {   // timing events not yet collected: direct launches
+    // direct launches: graphs off, timing events not yet collected, or a record capture
+    if (!c->opt[LMSF_OPT_GRAPH] || c->ev_used != 0 || !c->cap_slots.empty()) {
         HIPCHK(c, launch_state_init(c->bview(nb), c->d_poses, s));
         return enqueue_register(c, nb, iters);
     }
@@ -712,6 +698,9 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->sort_key,
                     c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->featp, c->n_pos, c->d_error};
     for (void* p : bufs) hipFree(p);
+    hipFree(c->cap_rec);
+    hipFree(c->cap_nn);
+    hipFree(c->cap_pose);
     c->voxel.release();
     hipFree(c->vox_in);
     hipFree(c->vox_out);
@@ -823,7 +812,7 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     // hardware queues round-robin at creation, so with a copy stream per context the four C2 contexts'
     // compute streams share two queues -- measured faster than one queue each (LMSF_LAZY_COPY_STREAM=1:
     // 22.50 / 22.58 / 22.62k vs 23.07 / 22.85 / 23.11k scans/s, one box, alternating).
-    if (!(getenv("LMSF_LAZY_COPY_STREAM") && atoi(getenv("LMSF_LAZY_COPY_STREAM"))))
+    if (!ab_int("LMSF_LAZY_COPY_STREAM", 0))
         CHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     CHK(hipEventCreateWithFlags(&c->ev_raw_free, hipEventDisableTiming));
     CHK(hipEventCreateWithFlags(&c->ev_raw_ready, hipEventDisableTiming));
@@ -893,9 +882,12 @@ lmsf_status lmsf_set_extract_params(lmsf_ctx* c, const lmsf_extract_params* p) {
 lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     if (!c || !pose) return LMSF_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    lmsf_status rc = ctx_settle(c);   // a deferred tracker commit may be the first map of this context
+    if (rc) return rc;
     if (!c->map_set[LMSF_EDGE] && !c->map_set[LMSF_SURF])
         return c->fail(LMSF_ERR_NO_MAP, "Solve before SetInputSource: no map");
-    lmsf_status rc = sync_slot0_features(c);
+    c->batch_done = 0;                // h_st[0] now holds this solve's state, not a batch slot's
+    rc = sync_slot0_features(c);
     if (rc) return rc;
     const int iters = outer_iterations_for_solve(c);
     std::memcpy(c->h_poses, pose, 7 * sizeof(double));
@@ -1189,9 +1181,11 @@ static lmsf_status load_scans(lmsf_ctx* c, const float* xyzi, const int64_t* cou
         c->raw_pending = false;
     }
     size_t off = 0;
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n; ++i)
         if (counts[i] < 0 || counts[i] > c->R)
             return c->fail(LMSF_ERR_CAPACITY, "scan %d has %lld points (max_scan_points %d)", i, (long long)counts[i], c->R);
+    c->raw_loaded = n;   // replaces any streamed batch: slots >= n hold nothing a launch may extract
+    for (int i = 0; i < n; ++i) {
         c->h_counts[i] = (int)counts[i];
         c->h_off[i] = (int64_t)off;
         off += (size_t)counts[i];
@@ -1226,13 +1220,18 @@ lmsf_status lmsf_batch_load_scans_async(lmsf_ctx* c, const float* xyzi, const in
     HIPCHK(c, hipMemcpyAsync(c->raw_off, c->h_raw_off, n * sizeof(int64_t), hipMemcpyHostToDevice, c->copy_stream));
     HIPCHK(c, hipEventRecord(c->ev_raw_ready, c->copy_stream));
     c->raw_pending = true;
+    c->raw_loaded = n;
     return LMSF_OK;
 }
 
 lmsf_status lmsf_batch_launch(lmsf_ctx* c, int32_t n, const double* poses) {
     if (!c || !poses || n < 1 || n > c->B) return LMSF_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    lmsf_status rs = ctx_settle(c);   // a deferred tracker commit may be the first map of this context
+    if (rs) return rs;
     if (!c->map_set[LMSF_EDGE] && !c->map_set[LMSF_SURF]) return c->fail(LMSF_ERR_NO_MAP, "no map set");
+    if (n > c->raw_loaded)   // e.g. lmsf_extract_features (one scan into slot 0) after a batch load
+        return c->fail(LMSF_ERR_STATE, "launch of %d slots but the last scan load filled %d", n, c->raw_loaded);
     std::memcpy(c->h_poses, poses, (size_t)n * 7 * sizeof(double));
     HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, (size_t)n * 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_error, 0, sizeof(int), c->stream));   // capacity flags of this batch only
@@ -1283,6 +1282,61 @@ lmsf_status lmsf_batch_run(lmsf_ctx* c, int32_t n, double* poses, lmsf_solve_sta
     lmsf_status rc = lmsf_batch_launch(c, n, poses);
     if (rc) return rc;
     return lmsf_batch_wait(c, n, poses, stats);
+}
+
+lmsf_status lmsf_set_option(lmsf_ctx* c, int32_t option, int32_t value) {
+    if (!c || option < 0 || option >= LMSF_OPT_COUNT || value < 0 || value > (option == LMSF_OPT_MEMO_BOUND ? 2 : 1))
+        return LMSF_ERR_ARG;
+    c->opt[option] = value;
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_batch_capture(lmsf_ctx* c, const int32_t* slots, int32_t n) {
+    if (!c || n < 0 || n > LMSF_MAX_CAPTURE || (n && !slots)) return LMSF_ERR_ARG;
+    for (int i = 0; i < n; ++i)
+        if (slots[i] < 0 || slots[i] >= c->B) return c->fail(LMSF_ERR_ARG, "capture slot %d outside the batch", slots[i]);
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    c->cap_slots.assign(slots, slots + n);
+    c->cap_iters = 0;
+    if (n > c->cap_alloc) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        hipFree(c->cap_rec);
+        hipFree(c->cap_nn);
+        hipFree(c->cap_pose);
+        c->cap_rec = nullptr;
+        c->cap_nn = nullptr;
+        c->cap_pose = nullptr;
+        c->cap_alloc = 0;
+        const size_t rows = (size_t)n * kCaptureIters;
+        HIPCHK(c, dalloc(&c->cap_rec, rows * c->F));
+        HIPCHK(c, dalloc(&c->cap_nn, rows * c->F * 5));
+        HIPCHK(c, dalloc(&c->cap_pose, rows * 7));
+        c->cap_alloc = n;
+    }
+    return LMSF_OK;
+}
+
+lmsf_status lmsf_batch_records(lmsf_ctx* c, int32_t slot, int32_t iter, lmsf_record* out, int32_t* nn, size_t cap,
+                               double pose[7], size_t* n_out) {
+    if (!c || iter < 0) return LMSF_ERR_ARG;
+    size_t k = 0;
+    while (k < c->cap_slots.size() && c->cap_slots[k] != slot) ++k;
+    if (k == c->cap_slots.size()) return c->fail(LMSF_ERR_STATE, "slot %d is not captured", slot);
+    if (iter >= c->cap_iters) return c->fail(LMSF_ERR_STATE, "outer iteration %d not captured (%d)", iter, c->cap_iters);
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    int hc[2];
+    HIPCHK(c, hipMemcpyAsync(&hc[0], c->n_edge + slot, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&hc[1], c->n_surf + slot, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t nq = (size_t)hc[0] + (size_t)hc[1];
+    if (n_out) *n_out = nq;
+    if ((out || nn) && nq > cap) return c->fail(LMSF_ERR_CAPACITY, "output capacity %zu < %zu queries", cap, nq);
+    const size_t row = k * kCaptureIters + (size_t)iter, F = (size_t)c->F;
+    if (out && nq) HIPCHK(c, hipMemcpyAsync(out, c->cap_rec + row * F, nq * sizeof(lmsf_record), hipMemcpyDefault, c->stream));
+    if (nn && nq) HIPCHK(c, hipMemcpyAsync(nn, c->cap_nn + row * F * 5, nq * 5 * sizeof(int32_t), hipMemcpyDefault, c->stream));
+    if (pose) HIPCHK(c, hipMemcpyAsync(pose, c->cap_pose + row * 7, 7 * sizeof(double), hipMemcpyDefault, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return LMSF_OK;
 }
 
 lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int32_t* nn, size_t cap) {

@@ -1,8 +1,15 @@
-// liblmsf_dist.so: the multi-GPU exchanges of include/lmsf/lmsf_dist.h on RCCL (one communicator per
-// group, its own HIP stream; every call synchronises that stream before returning).
+// liblmsf_dist.so: the multi-GPU exchanges of include/lmsf/lmsf_dist.h.  One protocol, two transports:
+// RCCL (one communicator per group, its own HIP stream; every call synchronises that stream before
+// returning) or the caller's own host collectives (lmsf_group_create_transport: MPI, a torch.distributed
+// group, ... -- and the CPU tests, which drive this same code over gloo).
+//
+// Every call is collective and every rank takes the same path through it: argument problems a rank can
+// only see locally (a null buffer, a capacity) travel in the first exchange, so all ranks return the same
+// error instead of some entering a collective the others skipped.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -12,9 +19,11 @@ static_assert(sizeof(ncclUniqueId) == LMSF_GROUP_ID_BYTES, "RCCL unique id size"
 
 struct lmsf_group {
     int device = 0, nranks = 1, rank = 0;
+    bool custom = false;              // caller-supplied host collectives instead of RCCL
+    lmsf_transport tp{};
     ncclComm_t comm = nullptr;
     hipStream_t stream = nullptr;
-    double* d_small = nullptr;        // device staging for host-sized exchanges
+    double* d_small = nullptr;        // device staging for host-sized exchanges (RCCL)
     size_t small_cap = 0;             // doubles
 };
 
@@ -38,8 +47,13 @@ lmsf_status reserve_small(lmsf_group* g, size_t doubles) {
     return LMSF_OK;
 }
 
-// all-gather of `count` doubles per rank between host arrays (staged through the device)
+// all-gather of `count` doubles per rank between host arrays (RCCL: staged through the device)
 lmsf_status allgather_host(lmsf_group* g, const double* mine, size_t count, double* all) {
+    if (g->custom) {
+        if (count && g->tp.allgather(g->tp.user, mine, all, count * sizeof(double)) != 0) return LMSF_ERR_HIP;
+        return LMSF_OK;
+    }
+    LCHK(hipSetDevice(g->device));
     lmsf_status rc = reserve_small(g, count * (size_t)(g->nranks + 1));
     if (rc) return rc;
     double* d_in = g->d_small;
@@ -49,6 +63,25 @@ lmsf_status allgather_host(lmsf_group* g, const double* mine, size_t count, doub
         LCHK(ncclAllGather(d_in, d_out, count, ncclFloat64, g->comm, g->stream));
         LCHK(hipMemcpyAsync(all, d_out, count * g->nranks * sizeof(double), hipMemcpyDeviceToHost, g->stream));
     }
+    LCHK(hipStreamSynchronize(g->stream));
+    return LMSF_OK;
+}
+
+// all-gather of `count` floats per rank between buffers of the group's memory space (device for RCCL)
+lmsf_status allgather_buffers(lmsf_group* g, const float* mine, size_t count, float* all) {
+    if (!count) return LMSF_OK;
+    if (g->custom) return g->tp.allgather(g->tp.user, mine, all, count * sizeof(float)) == 0 ? LMSF_OK : LMSF_ERR_HIP;
+    LCHK(hipSetDevice(g->device));
+    LCHK(ncclAllGather(mine, all, count, ncclFloat32, g->comm, g->stream));
+    LCHK(hipStreamSynchronize(g->stream));
+    return LMSF_OK;
+}
+
+lmsf_status broadcast_buffer(lmsf_group* g, float* buf, size_t count, int root) {
+    if (!count) return LMSF_OK;
+    if (g->custom) return g->tp.broadcast(g->tp.user, buf, count * sizeof(float), root) == 0 ? LMSF_OK : LMSF_ERR_HIP;
+    LCHK(hipSetDevice(g->device));
+    LCHK(ncclBroadcast(buf, buf, count, ncclFloat32, root, g->comm, g->stream));
     LCHK(hipStreamSynchronize(g->stream));
     return LMSF_OK;
 }
@@ -85,13 +118,26 @@ lmsf_status lmsf_group_create(int32_t device, int32_t nranks, int32_t rank, cons
     return LMSF_OK;
 }
 
+lmsf_status lmsf_group_create_transport(int32_t nranks, int32_t rank, const lmsf_transport* tp, lmsf_group** out) {
+    if (!out || !tp || !tp->allgather || !tp->broadcast || nranks < 1 || rank < 0 || rank >= nranks) return LMSF_ERR_ARG;
+    lmsf_group* g = new lmsf_group();
+    g->custom = true;
+    g->tp = *tp;
+    g->nranks = nranks;
+    g->rank = rank;
+    *out = g;
+    return LMSF_OK;
+}
+
 void lmsf_group_destroy(lmsf_group* g) {
     if (!g) return;
-    hipSetDevice(g->device);
-    if (g->stream) hipStreamSynchronize(g->stream);
-    if (g->comm) ncclCommDestroy(g->comm);
-    if (g->d_small) hipFree(g->d_small);
-    if (g->stream) hipStreamDestroy(g->stream);
+    if (!g->custom) {
+        hipSetDevice(g->device);
+        if (g->stream) hipStreamSynchronize(g->stream);
+        if (g->comm) ncclCommDestroy(g->comm);
+        if (g->d_small) hipFree(g->d_small);
+        if (g->stream) hipStreamDestroy(g->stream);
+    }
     delete g;
 }
 
@@ -100,63 +146,64 @@ int32_t lmsf_group_size(const lmsf_group* g) { return g ? g->nranks : 0; }
 
 lmsf_status lmsf_group_allgather_poses(lmsf_group* g, const double* mine, int32_t n, double* all) {
     if (!g || n < 0 || (n && (!mine || !all))) return LMSF_ERR_ARG;
-    LCHK(hipSetDevice(g->device));
     return allgather_host(g, mine, (size_t)n * 7, all);
 }
 
-lmsf_status lmsf_group_broadcast_cloud(lmsf_group* g, int32_t root, float* xyzi_dev, size_t cap, size_t* n) {
+lmsf_status lmsf_group_broadcast_cloud(lmsf_group* g, int32_t root, float* xyzi, size_t cap, size_t* n) {
     if (!g || !n || root < 0 || root >= g->nranks) return LMSF_ERR_ARG;
-    LCHK(hipSetDevice(g->device));
-    lmsf_status rc = reserve_small(g, 1);
+    // one exchange of (rows at the root, this rank's receive capacity; -1: no buffer): every rank then
+    // knows the row count and whether every rank can take it
+    const double mine[2] = {g->rank == root ? (double)*n : 0.0, xyzi ? (double)cap : -1.0};   // < 2^53 rows
+    std::vector<double> all((size_t)2 * g->nranks);
+    lmsf_status rc = allgather_host(g, mine, 2, all.data());
     if (rc) return rc;
-    double cnt = g->rank == root ? (double)*n : 0.0;   // < 2^53 rows
-    LCHK(hipMemcpyAsync(g->d_small, &cnt, sizeof cnt, hipMemcpyHostToDevice, g->stream));
-    LCHK(ncclBroadcast(g->d_small, g->d_small, 1, ncclFloat64, root, g->comm, g->stream));
-    LCHK(hipMemcpyAsync(&cnt, g->d_small, sizeof cnt, hipMemcpyDeviceToHost, g->stream));
-    LCHK(hipStreamSynchronize(g->stream));
-    const size_t rows = (size_t)cnt;
+    const size_t rows = (size_t)all[(size_t)2 * root];
     *n = rows;
-    if (rows > cap) return LMSF_ERR_CAPACITY;   // collective: every rank sees the same count first
-    if (rows) {
-        if (!xyzi_dev) return LMSF_ERR_ARG;
-        LCHK(ncclBroadcast(xyzi_dev, xyzi_dev, rows * 4, ncclFloat32, root, g->comm, g->stream));
+    if (rows == 0) return LMSF_OK;
+    for (int r = 0; r < g->nranks; ++r) {
+        if (all[(size_t)2 * r + 1] < 0.0) return LMSF_ERR_ARG;
+        if (all[(size_t)2 * r + 1] < (double)rows) return LMSF_ERR_CAPACITY;
     }
-    LCHK(hipStreamSynchronize(g->stream));
-    return LMSF_OK;
+    return broadcast_buffer(g, xyzi, rows * 4, root);
 }
 
 lmsf_status lmsf_group_exchange_keyframes(lmsf_group* g, const double pose[16], int32_t update_type, int64_t n_edge,
-                                          int64_t n_surf, const float* feat_dev, size_t cap, double* info,
-                                          float* gathered_dev, int32_t* any) {
-    if (!g || !pose || !info || !any || n_edge < 0 || n_surf < 0 || (size_t)n_edge > cap || (size_t)n_surf > cap)
-        return LMSF_ERR_ARG;
-    LCHK(hipSetDevice(g->device));
-    double mine[19];
+                                          int64_t n_surf, const float* feat, size_t cap, double* info, float* gathered,
+                                          int32_t* any) {
+    if (!g || !pose || !info || !any) return LMSF_ERR_ARG;
+    // local argument state travels with the info row, so a bad argument on one rank fails every rank
+    const bool args_ok = n_edge >= 0 && n_surf >= 0 && (size_t)n_edge <= cap && (size_t)n_surf <= cap && feat && gathered;
+    constexpr int kRow = 20;   // pose[16], update type, n_edge, n_surf, args ok
+    double mine[kRow];
     std::memcpy(mine, pose, 16 * sizeof(double));
     mine[16] = (double)update_type;
     mine[17] = (double)n_edge;
     mine[18] = (double)n_surf;
-    lmsf_status rc = allgather_host(g, mine, 19, info);
+    mine[19] = args_ok ? 1.0 : 0.0;
+    std::vector<double> all((size_t)kRow * g->nranks);
+    lmsf_status rc = allgather_host(g, mine, kRow, all.data());
     if (rc) return rc;
+    bool all_ok = true;
     *any = 0;
-    for (int r = 0; r < g->nranks; ++r)
-        if (info[(size_t)r * 19 + 16] != 0.0) *any = 1;
+    for (int r = 0; r < g->nranks; ++r) {
+        std::memcpy(info + (size_t)r * 19, &all[(size_t)r * kRow], 19 * sizeof(double));
+        if (all[(size_t)r * kRow + 16] != 0.0) *any = 1;
+        all_ok = all_ok && all[(size_t)r * kRow + 19] != 0.0;
+    }
+    if (!all_ok) {
+        *any = 0;
+        return LMSF_ERR_ARG;
+    }
     if (!*any) return LMSF_OK;
-    if (!feat_dev || !gathered_dev) return LMSF_ERR_ARG;
-    LCHK(ncclAllGather(feat_dev, gathered_dev, 2 * cap * 4, ncclFloat32, g->comm, g->stream));
-    LCHK(hipStreamSynchronize(g->stream));
-    return LMSF_OK;
+    return allgather_buffers(g, feat, 2 * cap * 4, gathered);
 }
 
 lmsf_status lmsf_group_max(lmsf_group* g, double* value) {
     if (!g || !value) return LMSF_ERR_ARG;
-    LCHK(hipSetDevice(g->device));
-    lmsf_status rc = reserve_small(g, 1);
+    std::vector<double> all((size_t)g->nranks);
+    lmsf_status rc = allgather_host(g, value, 1, all.data());
     if (rc) return rc;
-    LCHK(hipMemcpyAsync(g->d_small, value, sizeof(double), hipMemcpyHostToDevice, g->stream));
-    LCHK(ncclAllReduce(g->d_small, g->d_small, 1, ncclFloat64, ncclMax, g->comm, g->stream));
-    LCHK(hipMemcpyAsync(value, g->d_small, sizeof(double), hipMemcpyDeviceToHost, g->stream));
-    LCHK(hipStreamSynchronize(g->stream));
+    *value = *std::max_element(all.begin(), all.end());
     return LMSF_OK;
 }
 

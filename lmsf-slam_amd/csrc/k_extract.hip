@@ -704,8 +704,7 @@ hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
     hipLaunchKernelGGL(ring_features_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
     // blocks per scan (LMSF_CONCAT_BLOCKS, A/B; default 256: ~one feature and one position per thread)
     static const int cmax = [] {
-        const char* e = getenv("LMSF_CONCAT_BLOCKS");
-        const int v = e ? atoi(e) : 256;
+        const int v = ab_int("LMSF_CONCAT_BLOCKS", 256);
         return v >= 1 && v <= 1024 ? v : 256;
     }();
     const int cblocks = min(cmax, (ev.raw_stride + 255) / 256);

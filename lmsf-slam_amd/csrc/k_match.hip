@@ -902,6 +902,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_W
                 // all five still inside the radius and still the 5 nearest: the farthest of them is nearer
                 // than any other point can have come (those were >= s6 from w0, so >= s6 - d from w)
                 const bool inside = key_bits(k[4]) < kSentinel && sqrt((double)key_d2(k[4])) + dd + 1e-5 < s6;
+                // a miss walks at most the radius of the farthest stored neighbour at w: those are 5 points within
+                // it, so the 5 nearest are too (r03; the search then knows the 6th only as >= that radius)
+                if (bv.memo_bound == 1 && key_bits(k[4]) < kSentinel) lim = fminf(lim, key_d2(k[4]) + 1e-5f);
                 same = inside;
 #pragma unroll
                 for (int j = 0; j < 5; ++j) same = same && (uint32_t)key_bits(k[j]) == idx[j];
@@ -1136,7 +1139,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         if (kMemo && walk) {   // anchor for the memo pass: gap between the 5th and the 6th neighbour (capped at 1 m)
             float gap = -1.f;
             if (key_bits(k[4]) < kSentinel) {
-                const double s6 = sqrt((double)fminf(key_d2(k[5]), 1.0f));
+                // s6: the 6th distance, or the walk's radius when it found no 6th -- a lower bound, which is all the
+                // memo's tests need (lim - 1e-5 = 1 for a full walk: the r02 cap)
+                const double s6 = sqrt((double)fminf(key_d2(k[5]), fminf(1.0f, lim - 1e-5f)));
                 double sj = sqrt((double)key_d2(k[0])), gord = 1.0;
 #pragma unroll
                 for (int j = 1; j < 5; ++j) {   // the smallest gap between consecutive neighbours
@@ -1310,6 +1315,51 @@ __global__ __launch_bounds__(256) void eval_at_kernel(BatchView bv, const double
     block_reduce_packet(P, bv.partials + (size_t)blockIdx.x * kPacket);
 }
 
+// Record capture (diagnostics, lmsf_batch_capture): one lane per search position (by_pos: records stored
+// by position, featp w = its slot) or slot; the record goes out in slot order in the lmsf_record layout
+// lmsf_match returns (value fields of unmatched records zero), with the 5 neighbour indices of nnp.
+__global__ __launch_bounds__(256) void capture_kernel(BatchView bv, int b, int by_pos, lmsf_record* out, int32_t* nn,
+                                                      double* pose) {
+    if (blockIdx.x == 0 && threadIdx.x < 7) pose[threadIdx.x] = bv.st[b].x[threadIdx.x];
+    const int nq = bv.n_edge[b] + bv.n_surf[b];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= nq) return;
+    const size_t pos = (size_t)b * bv.feat_stride + i;
+    const int q = by_pos ? __float_as_int(bv.featp[pos].w) : i;
+    if (q < 0 || q >= nq) return;
+    const float4 p = bv.rec_p[pos];
+    lmsf_record r;
+    r.px = p.x;
+    r.py = p.y;
+    r.pz = p.z;
+    r.kind = __float_as_int(p.w);
+    r.v0[0] = r.v0[1] = r.v0[2] = 0.0;
+    r.v1[0] = r.v1[1] = r.v1[2] = 0.0;
+    if (r.kind != 0) {
+        const RecV v = bv.rec_v[pos];
+        r.v0[0] = v.v[0];
+        r.v0[1] = v.v[1];
+        r.v0[2] = v.v[2];
+        r.v1[0] = v.v[3];
+        if (r.kind == LMSF_EDGE) {
+            const double2 e = bv.rec_e[pos];
+            r.v1[1] = e.x;
+            r.v1[2] = e.y;
+        }
+    }
+    out[q] = r;
+    const float4* np = bv.nnp + ((size_t)b * bv.feat_stride + q) * 5;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) nn[(size_t)q * 5 + j] = __float_as_int(np[j].w);
+}
+
+hipError_t launch_capture(const BatchView& bv, int b, int by_pos, lmsf_record* rec, int32_t* nn, double* pose,
+                          hipStream_t s) {
+    const dim3 grid((bv.feat_stride + 255) / 256);
+    hipLaunchKernelGGL(capture_kernel, grid, dim3(256), 0, s, bv, b, by_pos, rec, nn, pose);
+    return hipGetLastError();
+}
+
 // Team size and XCD remap are tunables (LMSF_KNN_TEAM = 1 | 2 | 4 | 8 | 16 | 32, LMSF_XCD_REMAP =
 // 0 | 1) for A/B measurement.  Default (measured, r01): one lane per query when a launch carries
 // >= 2^20 query slots (C2 batch of 64: 10.8k scans/s vs 7.1k at T = 8); 8 lanes per query for
@@ -1317,8 +1367,7 @@ __global__ __launch_bounds__(256) void eval_at_kernel(BatchView bv, const double
 // us on the C3 local map), where one lane per query leaves most of the chip idle.
 static int knn_team(size_t query_slots) {
     static int forced = [] {
-        const char* e = getenv("LMSF_KNN_TEAM");
-        int v = e ? atoi(e) : 0;
+        const int v = ab_int("LMSF_KNN_TEAM", 0);
         return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 0;
     }();
     if (forced) return forced;
@@ -1327,10 +1376,7 @@ static int knn_team(size_t query_slots) {
 int knn_team_for(size_t query_slots) { return knn_team(query_slots); }
 
 static int knn_remap() {
-    static int r = [] {
-        const char* e = getenv("LMSF_XCD_REMAP");
-        return e ? atoi(e) : 1;
-    }();
+    static int r = ab_int("LMSF_XCD_REMAP", 1);
     return r;
 }
 
@@ -1394,26 +1440,16 @@ hipError_t launch_fit_eval(const GridView& edge, const GridView& surf, const Bat
 // VGPRs, 4 waves/SIMD) since the butterfly packet reduction: C2 16.8k vs 16.5k scans/s at 2 (165 VGPRs).
 int fit_per_thread_default() {
     static int v = [] {
-        const char* e = getenv("LMSF_FIT_PER_THREAD");
-        int x = e ? atoi(e) : 1;
+        const int x = ab_int("LMSF_FIT_PER_THREAD", 1);
         return (x == 1 || x == 2 || x == 4) ? x : 1;
     }();
     return v;
 }
 
-// LMSF_FUSED = 0 | 1 (A/B): the fused search + fit for batch launches (default 1).
+// LMSF_FUSED = 0 | 1 (A/B builds): the fused search + fit for batch launches (default 1).
 static bool fused_enabled() {
-    static bool v = [] {
-        const char* e = getenv("LMSF_FUSED");
-        return e ? atoi(e) != 0 : true;
-    }();
+    static bool v = ab_int("LMSF_FUSED", 1) != 0;
     return v;
-}
-
-// LMSF_MEMO = 0 | 1 (default 1), read at every launch so a test can compare both in one process.
-bool match_memo_enabled() {
-    const char* e = getenv("LMSF_MEMO");
-    return e ? atoi(e) != 0 : true;
 }
 
 bool match_fit_applies(const GridView& edge2, const GridView& surf2, const BatchView& bv, int solver) {

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/lmsf/lmsf.h"
 
@@ -31,6 +32,21 @@ constexpr int kQSurf = 0x40000000;  // ExtractView::qcode tag of a surf feature
 constexpr int kTile = 2048;          // raw points per ring-split tile
 constexpr int kCounterShards = 64;   // candidate / query counters, 16 u64 (128 B) apart
 constexpr int kMemoWords = 7;        // memo words per search position: 5 neighbour indices, s6, order gap
+constexpr int kCaptureIters = 10;    // outer iterations kept per captured slot (lmsf_batch_capture)
+
+// Tuning knobs measured by A/B builds.  The shipped library reads no environment:
+// ab_int returns the default unless the library was built with -DLMSF_AB (tools/build_variant.sh), which
+// lets one build take an override from the environment.  Algorithm switches a caller may legitimately
+// want (the query memo and its tests, HIP graphs) are context options instead (lmsf_set_option).
+inline int ab_int(const char* name, int def) {
+#ifdef LMSF_AB
+    const char* e = getenv(name);
+    return e ? atoi(e) : def;
+#else
+    (void)name;
+    return def;
+#endif
+}
 
 // Dense cell grid over one feature map: cell = floor(coord) - origin, 1 m cells (the match
 // radius: search_thresh_ = 1.0 squared metres, REG/FeatureMatch/FeatureMatchBase.hpp:29).
@@ -107,7 +123,8 @@ struct BatchView {
     int* n_search;           // [B] positions searched by the last match_fit_kernel (lm_begin's second range)
     int part2_base;          // packet index of match_fit_kernel's first wave packet (memo pass: [0, ceil(nq/64)))
     int fused_parts;         // lm_begin: packets laid out by the fused path (memo pass + search ranges)
-    int memo_bound;          // memo misses search within min(1 m, s6 + d) (LMSF_MEMO_BOUND, default 1)
+    int memo_bound;          // memo misses walk a bounded radius (LMSF_OPT_MEMO_BOUND): 1 = min(1 m, s6 + d, the
+                             //   farthest stored neighbour at w) (default), 2 = min(1 m, s6 + d) (r02), 0 = 1 m
     int memo_order;          // memo: consecutive-gap test first (no re-keying when every gap exceeds 2 d)
     int memo_exact;          // memo: the stored 5 are kept when the farthest of them at w is nearer than s6 - d
                              //   (LMSF_MEMO_EXACT, default 1; 0: r01's 2 d < s6 - s5)
@@ -162,7 +179,11 @@ int knn_team_for(size_t query_slots);   // lanes per query of a search launch ov
 bool match_fit_applies(const GridView& edge2, const GridView& surf2, const BatchView& bv, int solver);
 hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const BatchView& bv, hipStream_t s);
 bool match_fit_prune(const GridView& edge, const GridView& surf);   // dense map: pruned walk, no memo
-bool match_memo_enabled();   // LMSF_MEMO (default 1)
+// Record capture (lmsf_batch_capture): slot b's records after an outer iteration's matching as lmsf_record
+// rows in slot order, its 5 neighbour indices (nnp w bits, -1: none) and the linearisation pose (7 doubles).
+// by_pos: records are stored by search position (fused path), else by slot.
+hipError_t launch_capture(const BatchView& bv, int b, int by_pos, lmsf_record* rec, int32_t* nn, double* pose,
+                          hipStream_t s);
 hipError_t launch_state_init(const BatchView& bv, const double* poses, hipStream_t s);
 hipError_t launch_stamp(unsigned long long* out, hipStream_t s);   // wall clock after the stream's prior work
 // Standalone evaluation at one pose (diagnostics): packet of slot 0 into out29 (device).

@@ -4,7 +4,7 @@
 // src/MultiSensorFusionEstimator3D/include): first scan seeds the local map (:112-122), constant
 // velocity prediction `prev * motion_increment` when deltaT is exactly identity (:125-129),
 // RegistrationLocalMap (:168-177), motion increment (:133-135), keyframe gate needUpdataLocalMap
-// (:239-262: dt > 10 s -> TIME, |dp| > 0.3 m or 2 acos(|q.w|) > 0.1 rad -> MOTION), and
+// (:239-262: dt > 10 s -> TIME, |dp| > 0.3 m or 2 acos(q.w / |q|) > 0.1 rad -> MOTION; no abs, as :254), and
 // updateLocalMap (:205-232: transformPointCloud, add frame, SetInputSource(local map)).
 // The local-map class itself is missing from the reference snapshot (factory/Map/LocalMap_factory.hpp);
 // "sliding_Localmap" is defined here as a device-resident window of the last W keyframes
@@ -315,8 +315,13 @@ lmsf_status lmsf_tracker_config_init(lmsf_tracker_config* cfg) {
 
 void lmsf_tracker_destroy(lmsf_tracker* t) {
     if (!t) return;
-    ctx_remove_settle(t->ctx, t);
     hipSetDevice(ctx_device(t->ctx));
+    // A deferred commit is completed first: its staging already rewrote the context's window grids (points,
+    // box read-back), so the context must not keep searching the old sizes and offsets.  If it cannot be
+    // completed, the windows are dropped (the context keeps its prior maps).
+    if (commit_finish(t) != LMSF_OK)
+        for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) ctx_set_window_device(t->ctx, kind, nullptr, 0);
+    ctx_remove_settle(t->ctx, t);
     hipStreamSynchronize(ctx_stream(t->ctx));
     for (auto& w : t->win) {
         for (float4* p : w.slots) hipFree(p);

@@ -20,6 +20,7 @@ EDGE, SURF = 1, 2
 UPDATE_NONE, UPDATE_MOTION, UPDATE_TIME = 0, 1, 2
 SOLVER_CERES_LM, SOLVER_GN = 0, 1
 SCHEDULE_REFERENCE_DECAY, SCHEDULE_FIXED = 0, 1
+OPT_QUERY_MEMO, OPT_MEMO_REFIT, OPT_MEMO_EXACT, OPT_MEMO_ORDER, OPT_MEMO_BOUND, OPT_GRAPH = range(6)
 TERM_NAMES = {0: "max_iterations", 1: "function_tol", 2: "parameter_tol", 3: "gradient_tol",
               4: "no_residuals", 5: "gn_converged", 6: "gn_too_few"}
 
@@ -112,6 +113,9 @@ _SIGS = {
     "lmsf_batch_wait": (C.c_int32, [_P, C.c_int32, _P, _P]),
     "lmsf_batch_trace": (C.c_int32, [_P, C.c_int32, _P, C.c_int32, C.POINTER(C.c_int32)]),
     "lmsf_batch_copy_features": (C.c_int32, [_P, C.c_int32, C.c_int32, _P, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "lmsf_set_option": (C.c_int32, [_P, C.c_int32, C.c_int32]),
+    "lmsf_batch_capture": (C.c_int32, [_P, _P, C.c_int32]),
+    "lmsf_batch_records": (C.c_int32, [_P, C.c_int32, C.c_int32, _P, _P, C.c_size_t, _P, C.POINTER(C.c_size_t)]),
     "lmsf_match": (C.c_int32, [_P, _P, _P, _P, C.c_size_t]),
     "lmsf_eval": (C.c_int32, [_P, _P, _P]),
     "lmsf_kernel_stats_get": (C.c_int32, [_P, C.POINTER(KernelStats)]),
@@ -395,7 +399,28 @@ class Context:
         self._check(load().lmsf_batch_trace(self.h, int(slot), out.ctypes.data, cap, C.byref(n)))
         return out[:min(n.value, cap)].copy()
 
+    def set_option(self, option, value):
+        """lmsf_set_option (OPT_* switches, 0 | 1)."""
+        self._check(load().lmsf_set_option(self.h, int(option), int(bool(value))))
+
     # ---- diagnostics
+    def batch_capture(self, slots):
+        """Capture the records / neighbour indices of these batch slots after every outer iteration of
+        the following launches ([] stops it)."""
+        s = np.ascontiguousarray(slots, dtype=np.int32)
+        self._check(load().lmsf_batch_capture(self.h, s.ctypes.data if len(s) else None, len(s)))
+
+    def batch_records(self, slot, it):
+        """(records, nn (n, 5), pose) of a captured slot at outer iteration `it` of the last launch."""
+        n = C.c_size_t()
+        self._check(load().lmsf_batch_records(self.h, int(slot), int(it), None, None, 0, None, C.byref(n)))
+        rec = np.zeros(n.value, RECORD_DTYPE)
+        nn = np.zeros((n.value, 5), np.int32)
+        pose = np.zeros(7, np.float64)
+        self._check(load().lmsf_batch_records(self.h, int(slot), int(it), rec.ctypes.data, nn.ctypes.data, n.value,
+                                              pose.ctypes.data, C.byref(n)))
+        return rec, nn, pose
+
     def match(self, pose, n_queries):
         rec = np.zeros(n_queries, RECORD_DTYPE)
         nn = np.zeros((n_queries, 5), np.int32)

@@ -118,3 +118,109 @@ class KeyframeExchange:
                 ne, ns = int(allinfo[q, 17]), int(allinfo[q, 18])
                 out.append((q, self.gbuf[q, :ne], self.gbuf[q, self.cap:self.cap + ns], allinfo[q, :16].reshape(4, 4)))
         return out
+
+
+# ---- the C library's protocol (liblmsf_dist.so, include/lmsf/lmsf_dist.h) over a torch.distributed group
+class CGroup:
+    """lmsf_group over caller-supplied host collectives (lmsf_group_create_transport) that run on the
+    current torch.distributed process group (gloo on CPU): the C / C++ callers' exchange protocol --
+    argument agreement, info layout, keyframe order -- executed by the same compiled code the RCCL
+    groups use, without GPUs.  Buffers are host memory (numpy)."""
+
+    _AG = None
+    _BC = None
+
+    def __init__(self, lib_path=None):
+        import ctypes as C
+        import os
+        import torch.distributed as dist
+        from . import _lib
+        _lib._share_torch_hip_runtime()
+        path = lib_path or os.path.join(_lib.PKG_ROOT, "liblmsf_dist.so")
+        L = C.CDLL(path)
+        P = C.c_void_p
+        CGroup._AG = C.CFUNCTYPE(C.c_int32, P, P, P, C.c_size_t)
+        CGroup._BC = C.CFUNCTYPE(C.c_int32, P, P, C.c_size_t, C.c_int32)
+
+        class Transport(C.Structure):
+            _fields_ = [("user", P), ("allgather", CGroup._AG), ("broadcast", CGroup._BC)]
+
+        L.lmsf_group_create_transport.argtypes = [C.c_int32, C.c_int32, C.POINTER(Transport), C.POINTER(P)]
+        L.lmsf_group_create_transport.restype = C.c_int32
+        L.lmsf_group_destroy.argtypes = [P]
+        L.lmsf_group_destroy.restype = None
+        L.lmsf_group_allgather_poses.argtypes = [P, P, C.c_int32, P]
+        L.lmsf_group_broadcast_cloud.argtypes = [P, C.c_int32, P, C.c_size_t, C.POINTER(C.c_size_t)]
+        L.lmsf_group_exchange_keyframes.argtypes = [P, P, C.c_int32, C.c_int64, C.c_int64, P, C.c_size_t, P, P,
+                                                    C.POINTER(C.c_int32)]
+        L.lmsf_group_max.argtypes = [P, C.POINTER(C.c_double)]
+        for f in ("lmsf_group_allgather_poses", "lmsf_group_broadcast_cloud", "lmsf_group_exchange_keyframes",
+                  "lmsf_group_max"):
+            getattr(L, f).restype = C.c_int32
+        self.C, self.L = C, L
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+
+        def allgather(user, send, recv, nbytes):
+            try:
+                import torch
+                src = torch.frombuffer(bytearray(C.string_at(send, nbytes)), dtype=torch.uint8)
+                outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.world)]
+                dist.all_gather(outs, src)
+                cat = torch.cat(outs).numpy()
+                C.memmove(recv, cat.ctypes.data, nbytes * self.world)
+                return 0
+            except Exception:   # noqa: BLE001 -- reported to the library as a transport failure
+                return 1
+
+        def broadcast(user, buf, nbytes, root):
+            try:
+                import torch
+                t = torch.frombuffer(bytearray(C.string_at(buf, nbytes)), dtype=torch.uint8)
+                dist.broadcast(t, int(root))
+                C.memmove(buf, t.numpy().ctypes.data, nbytes)
+                return 0
+            except Exception:   # noqa: BLE001
+                return 1
+
+        self._cbs = (CGroup._AG(allgather), CGroup._BC(broadcast))   # kept alive with the group
+        self._tp = Transport(None, self._cbs[0], self._cbs[1])
+        h = P()
+        rc = L.lmsf_group_create_transport(self.world, self.rank, C.byref(self._tp), C.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"lmsf_group_create_transport: {rc}")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.lmsf_group_destroy(self.h)
+            self.h = None
+
+    def allgather_poses(self, poses):
+        p = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 7)
+        out = np.zeros((self.world, len(p), 7))
+        rc = self.L.lmsf_group_allgather_poses(self.h, p.ctypes.data, len(p), out.ctypes.data)
+        return rc, out
+
+    def broadcast_cloud(self, root, buf, n):
+        """buf: (cap, 4) float32 numpy array (the root's holds n rows); returns (status, rows)."""
+        nn = self.C.c_size_t(n)
+        rc = self.L.lmsf_group_broadcast_cloud(self.h, root, buf.ctypes.data if buf is not None else None,
+                                               0 if buf is None else len(buf), self.C.byref(nn))
+        return rc, nn.value
+
+    def exchange_keyframes(self, pose, update_type, n_edge, n_surf, feat, cap, gathered):
+        """feat: (2 cap, 4) float32 or None; gathered: (world, 2 cap, 4) float32 or None.
+        Returns (status, info (world, 19), any)."""
+        info = np.zeros((self.world, 19))
+        anyk = self.C.c_int32(-1)
+        P = np.ascontiguousarray(pose, dtype=np.float64)
+        rc = self.L.lmsf_group_exchange_keyframes(self.h, P.ctypes.data, int(update_type), int(n_edge), int(n_surf),
+                                                  feat.ctypes.data if feat is not None else None, cap, info.ctypes.data,
+                                                  gathered.ctypes.data if gathered is not None else None,
+                                                  self.C.byref(anyk))
+        return rc, info, anyk.value
+
+    def max(self, v):
+        d = self.C.c_double(v)
+        rc = self.L.lmsf_group_max(self.h, self.C.byref(d))
+        return rc, d.value

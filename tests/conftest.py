@@ -103,3 +103,28 @@ def libm_probe_scan():
     scan = np.concatenate(rows, 0).astype(np.float32)
     odd = np.array([[80.0, 0.0221, 80.0 * np.tan(np.radians(-15.0)), 0.5]], np.float32)
     return np.concatenate([scan[:900], odd, scan[900:]], 0)
+
+
+def assert_captured_records(ctx, reg, slot, iters, min_matched=0.2):
+    """Records and 5-NN indices the batch path kept after each outer iteration of `slot` (lmsf_batch_capture:
+    fresh searches, memo reuses and refits alike) against the oracle's fresh match at the exact pose the GPU
+    matched at (REG/FeatureMatch/EdgeFeatureMatch.hpp:38-80, surfFeatureMatch.hpp:37-83).  reg holds the
+    slot's scan.  Byte-identical records; equal neighbour indices on every rank found within 1 m.
+    Returns the per-iteration count of matched records."""
+    matched = []
+    for it in range(iters):
+        grec, gnn, gpose = ctx.batch_records(slot, it)
+        orec, onn = reg.match(gpose)
+        assert len(grec) == len(orec), (slot, it)
+        found = gnn >= 0
+        assert np.array_equal(gnn[found], onn[found]), (slot, it, int((gnn[found] != onn[found]).sum()))
+        matched5 = orec["kind"] > 0                              # a record needs the 5 found within 1 m
+        assert found[matched5].all(), (slot, it)
+        if grec.tobytes() != orec.tobytes():
+            diff = np.nonzero((grec.view(np.uint8).reshape(len(grec), -1) !=
+                               orec.view(np.uint8).reshape(len(orec), -1)).any(1))[0]
+            raise AssertionError(f"slot {slot} outer iteration {it}: {len(diff)} records differ, first {diff[:5]}: "
+                                 f"gpu {grec[diff[:2]]} oracle {orec[diff[:2]]}")
+        assert matched5.sum() > min_matched * len(orec), (slot, it)
+        matched.append(int(matched5.sum()))
+    return matched

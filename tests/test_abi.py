@@ -202,3 +202,27 @@ def test_dist_library_exports_and_example_links(lib, tmp_path):
     undefined = subprocess.run(["nm", "-u", exe], capture_output=True, text=True).stdout
     for s in ("lmsf_group_create", "lmsf_group_allgather_poses", "lmsf_group_exchange_keyframes", "lmsf_solve"):
         assert s in undefined
+
+
+def test_shipped_library_reads_no_environment_knobs(lib):
+    """Verdict r02: no A/B switch of the shipped library comes from the caller's environment.  The
+    measured tuning knobs are compile-time (ab_int, -DLMSF_AB builds only) and the algorithm switches
+    are context options (lmsf_set_option): no LMSF_* variable name is left in the built objects."""
+    import re
+    for so in (lib.LIB_PATH, os.path.join(REPO, "lmsf-slam_amd", "liblmsf_dist.so")):
+        blob = open(so, "rb").read()
+        header = open(os.path.join(REPO, "include", "lmsf", "lmsf.h"), "rb").read()
+        abi = set(re.findall(rb"#define (LMSF_[A-Z0-9_]+)", header))   # ABI constants in error-message text
+        names = set(re.findall(rb"LMSF_[A-Z0-9_]{3,}", blob)) - abi
+        assert not names, (so, sorted(names)[:10])
+    src = os.path.join(REPO, "lmsf-slam_amd", "csrc")
+    for f in os.listdir(src):
+        text = open(os.path.join(src, f)).read()
+        assert len(re.findall(r"\bgetenv\s*\(", text)) == (1 if f == "lmsf_internal.h" else 0), f
+
+
+def test_set_option_validates(lib):
+    """lmsf_set_option: known options, 0 | 1 only (no device needed for the argument checks)."""
+    L = lib.load()
+    assert L.lmsf_set_option(None, lib.OPT_QUERY_MEMO, 1) == lib.ERR_ARG
+    assert L.lmsf_batch_capture(None, None, 0) == lib.ERR_ARG

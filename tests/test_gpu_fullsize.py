@@ -16,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import mat_err, pose_err, pose_matrix
+from conftest import assert_captured_records, mat_err, pose_err, pose_matrix
 
 pytestmark = pytest.mark.gpu
 
@@ -101,6 +101,19 @@ def test_c2_fullsize_memo_batch(lib, oracle_mt, c2_workload):
         assert (stats[i].edge_matches, stats[i].surf_matches) == (ost.edge_matches, ost.surf_matches)
         dt, dr = pose_err(poses[i], wl.truth[unit[i]])
         assert dt < 0.05 and dr < 0.01
+    # byte level on the timed path: records + 5-NN indices of two slots after each of the 5 outer iterations
+    # (memo reuses, refits and bounded re-searches included) vs the oracle's fresh match at the GPU's pose
+    cap_slots = [1, 6]
+    ctx.batch_capture(cap_slots)
+    ctx.kernel_stats_reset(timing=True)
+    posesc, _ = ctx.batch_run(guesses)
+    ksc = ctx.kernel_stats()
+    assert np.array_equal(posesc, poses) and ksc.reused_queries > 0.1 * ksc.queries and ksc.refit_queries > 0
+    for i in cap_slots:
+        e, s, _, _ = feats[unit[i]]
+        reg.set_scan(1, e)
+        reg.set_scan(2, s)
+        assert_captured_records(ctx, reg, i, 5)
     ctx.close()
     _records_bitexact(lib, oracle_mt, wl, wl.scans[1], guesses[1], dict(max_scan_points=70000), {})
 
@@ -138,6 +151,14 @@ def test_c5_fullsize_pruned_batch(lib, oracle_mt, c5_workload):
         ox, otr, ost = reg.solve(wl.guess[i])
         _check_trace(ctx.batch_trace(i), otr, ("C5 pair", i))
         assert (stats[i].edge_matches, stats[i].surf_matches) == (ost.edge_matches, ost.surf_matches)
+    # byte level: the pruned walk's records + 5-NN indices after each outer iteration (pair 1)
+    ctx.batch_capture([1])
+    posesc, _ = ctx.batch_run(wl.guess[:n])
+    assert np.array_equal(posesc, poses)
+    e, s, _, _ = oracle_mt.extract(wl.scans[1], **c["extract"])
+    reg.set_scan(1, e)
+    reg.set_scan(2, s)
+    assert_captured_records(ctx, reg, 1, 5)
     ctx.close()
     _records_bitexact(lib, oracle_mt, wl, wl.scans[0], wl.guess[0], dict(max_scan_points=R, **c["extract"]),
                       c["extract"])

@@ -6,12 +6,11 @@ Bars (DESIGN.md "Parity"):
 * the 29-double normal-equation packet differs only by summation order -> rel 1e-9;
 * poses per outer iteration <= 1e-4 m / 1e-4 rad (north_star tolerance).
 """
-import os
 
 import numpy as np
 import pytest
 
-from conftest import mat_err, pose_err
+from conftest import assert_captured_records, mat_err, pose_err
 
 pytestmark = pytest.mark.gpu
 
@@ -291,13 +290,29 @@ def test_batch_run_matches_oracle(lib, oracle_mod, small_workload):
     # neighbour-distance gap, and refit (without a walk) those whose set only changed order: same
     # records, packets summed in another grouping (the searching lanes are packed), so the poses
     # agree with re-searching every query (and with searching the reordered ones) to rounding
-    for var in ("LMSF_MEMO", "LMSF_MEMO_REFIT", "LMSF_MEMO_EXACT"):
-        os.environ[var] = "0"
+    for opt in (lib.OPT_QUERY_MEMO, lib.OPT_MEMO_REFIT, lib.OPT_MEMO_EXACT, lib.OPT_MEMO_ORDER, lib.OPT_MEMO_BOUND):
+        ctx.set_option(opt, 0)
         try:
             poses0, _ = ctx.batch_run(np.stack([wl.guess[i % n] for i in range(16)]))
         finally:
-            del os.environ[var]
-        assert np.abs(poses0 - poses).max() <= 1e-12, var
+            ctx.set_option(opt, 1)
+        assert np.abs(poses0 - poses).max() <= 1e-12, opt
+    # byte-level: every outer iteration's records of two slots (memo reuses, refits and bounded searches
+    # included) equal the oracle's fresh match at the pose the GPU matched at
+    ctx.batch_capture([1, 4])
+    ctx.kernel_stats_reset(timing=True)
+    posesc, _ = ctx.batch_run(np.stack([wl.guess[i % n] for i in range(16)]))
+    ksc = ctx.kernel_stats()
+    assert ksc.reused_queries > 0 and np.array_equal(posesc, poses)   # capture changes nothing
+    for slot in (1, 4):
+        e, s = _features(oracle_mod, wl.scans[slot % n])
+        reg = oracle_mod.Registration()
+        reg.set_map(1, wl.edge_map)
+        reg.set_map(2, wl.surf_map)
+        reg.set_scan(1, e)
+        reg.set_scan(2, s)
+        assert_captured_records(ctx, reg, slot, 5)
+    ctx.batch_capture([])
     np.testing.assert_array_equal(poses[n:2 * n], poses[:n])          # same scan + guess -> same pose
     for i in range(len(wl.scans)):
         e, s = _features(oracle_mod, wl.scans[i])
@@ -391,11 +406,11 @@ def test_batch_memo_dense(lib, oracle_mod, dense_workload):
     poses, _ = ctx.batch_run(guesses)
     ks = ctx.kernel_stats()
     assert ks.fused_launches == 5 and ks.reused_queries == 0   # the pruned walk keeps 5 keys: no memo
-    os.environ["LMSF_MEMO"] = "0"
+    ctx.set_option(lib.OPT_QUERY_MEMO, 0)
     try:
         poses0, _ = ctx.batch_run(guesses)
     finally:
-        del os.environ["LMSF_MEMO"]
+        ctx.set_option(lib.OPT_QUERY_MEMO, 1)
     assert np.abs(poses0 - poses).max() <= 1e-12
     e, s = _features(oracle_mod, wl.scans[0])
     reg = oracle_mod.Registration()
@@ -732,6 +747,63 @@ def test_tracker_shared_map_streams(lib, oracle_mod, sequence_workload):
     np.testing.assert_allclose(gts[0].local_map(lib.EDGE), ots[0].local_map(1), atol=1e-4)
     for t in gts:
         t.close()
+
+
+def test_deferred_commit_settles(lib, oracle_mod, sequence_workload):
+    """A keyframe commit left pending by lmsf_tracker_commit_map completes (a) before lmsf_solve's map check on
+    a context whose only map is that first commit, and (b) when the tracker is destroyed, so the context keeps
+    searching a consistent window grid.  Both equal the explicitly completed commit."""
+    from conftest import pose_matrix
+    wl = sequence_workload
+    scan = wl.scans[1]
+    e, su, _, _ = oracle_mod.extract(wl.scans[0], n_scans=wl.n_scans)
+    T0 = pose_matrix(wl.truth[0])
+    guess = wl.truth[1]
+
+    def setup(finish):
+        ctx = _ctx(lib, n_scans=wl.n_scans)
+        t = lib.Tracker(ctx, window_frames=3, manual_map_update=True)
+        t.add_keyframe(e, su, T0)
+        t.commit_map()                                   # deferred finish
+        if finish:
+            t.local_map(lib.SURF)                        # any tracker call completes it
+        return ctx, t
+
+    ref_ctx, ref_t = setup(True)
+    ref_ctx.extract(scan)
+    ref_pose, _ = ref_ctx.solve(guess)
+    ctx, t = setup(False)
+    ctx.extract(scan)
+    pose, _ = ctx.solve(guess)                           # (a): no LMSF_ERR_NO_MAP
+    assert np.array_equal(pose, ref_pose)
+    ctx2, t2 = setup(False)
+    t2.close()                                           # (b): completes the pending rebuild first
+    nq = sum(ctx2.extract(scan))
+    rec_a, nn_a = ctx2.match(guess, nq)
+    ref_ctx.extract(scan)
+    rec_b, nn_b = ref_ctx.match(guess, nq)
+    assert rec_a.tobytes() == rec_b.tobytes() and np.array_equal(nn_a, nn_b)
+    assert (rec_a["kind"] > 0).sum() > 0.2 * nq
+    for x in (ref_t, t):
+        x.close()
+
+
+def test_batch_launch_after_single_load_refused(lib, small_workload):
+    """lmsf_extract_features loads one scan into slot 0: a following launch of more slots (whose streamed or
+    loaded scans it replaced) fails with LMSF_ERR_STATE instead of extracting stale offsets."""
+    import torch
+    wl = small_workload
+    ctx = _ctx(lib, schedule=1, max_iterations=2, max_batch=2)
+    ctx.set_map(lib.EDGE, wl.edge_map)
+    ctx.set_map(lib.SURF, wl.surf_map)
+    buf = torch.from_numpy(np.concatenate([wl.scans[0], wl.scans[1]], 0)).pin_memory()
+    ctx.load_scans_async(buf, np.array([len(wl.scans[0]), len(wl.scans[1])]))
+    ctx.extract(wl.scans[2])
+    with pytest.raises(lib.LmsfError) as ei:
+        ctx.batch_launch(np.stack([wl.guess[0], wl.guess[1]]))
+    assert ei.value.code == lib.ERR_STATE
+    poses, st = ctx.batch_run(np.stack([wl.guess[2]]))  # one slot: the extracted scan
+    assert st[0].surf_matches > 0
 
 
 @pytest.mark.parametrize("cols", [1800, 4096])

@@ -132,3 +132,96 @@ def test_gloo_world2_pairs_map_and_keyframe_exchange():
         assert len(a) == len(b)
         for x, y in zip(a, b):
             assert x[0] == y[0] and x[1].tobytes() == y[1].tobytes() and x[2].tobytes() == y[2].tobytes()
+
+
+def _worker_cdist(rank, world, port, out_q):
+    """The C library's protocol (liblmsf_dist.so) over gloo: pose gather, map broadcast, 3 keyframe-exchange
+    steps, error agreement (one rank passes a bad buffer: every rank gets the error, none hangs)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lmsf-slam_amd"))
+    import torch.distributed as dist
+    from lmsf import multi
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = multi.CGroup()
+    res = {}
+    res["poses"] = g.allgather_poses(np.stack([np.full(7, 10.0 * rank + i) for i in range(3)]))
+    rng = np.random.default_rng(5)
+    cloud = rng.random((13, 4)).astype(np.float32)
+    buf = np.zeros((16, 4), np.float32)
+    if rank == 0:
+        buf[:13] = cloud
+    res["bcast"] = (g.broadcast_cloud(0, buf, 13 if rank == 0 else 0), buf.copy())
+    small = np.zeros((8 if rank == 1 else 16, 4), np.float32)   # rank 1 cannot hold 13 rows
+    res["bcast_small"] = g.broadcast_cloud(0, small, 13 if rank == 0 else 0)
+    cap = 8
+    gathered = np.zeros((world, 2 * cap, 4), np.float32)
+    replica = []                                                # the keyframes this replica appends, in order
+    steps = []
+    for step, kf in enumerate([(1, 1), (0, 0), (0, 2)]):
+        typ = kf[rank]
+        ne, ns = 2 + rank, 3 + step
+        feat = np.zeros((2 * cap, 4), np.float32)
+        feat[:ne] = 10 * rank + step
+        feat[cap:cap + ns] = -(10 * rank + step)
+        pose = np.eye(4)
+        pose[0, 3] = 100 * rank + step
+        rc, info, anyk = g.exchange_keyframes(pose, typ, ne if typ else 0, ns if typ else 0, feat, cap, gathered)
+        steps.append((rc, info.copy(), anyk))
+        if rc == 0 and anyk:
+            for q in range(world):
+                if info[q, 16] != 0:
+                    ne_q, ns_q = int(info[q, 17]), int(info[q, 18])
+                    replica.append((q, gathered[q, :ne_q].copy(), gathered[q, cap:cap + ns_q].copy(),
+                                    info[q, :16].reshape(4, 4).copy()))
+    res["steps"] = steps
+    res["replica"] = replica
+    # rank 1 passes no gathered buffer while rank 0 keyframes: both must return LMSF_ERR_ARG (-1)
+    feat = np.zeros((2 * cap, 4), np.float32)
+    rc, _, anyk = g.exchange_keyframes(np.eye(4), 1 if rank == 0 else 0, 1, 1, feat, cap,
+                                       gathered if rank == 0 else None)
+    res["bad_args"] = (rc, anyk)
+    res["max"] = g.max(1.5 + rank)
+    g.close()
+    out_q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_c_library_protocol():
+    """Verdict r02 item 7: the C library's keyframe-exchange protocol (lmsf_group_exchange_keyframes and the
+    info / padded-buffer layout of include/lmsf/lmsf_dist.h) rehearsed on 2 CPU ranks through its own code,
+    over a caller-supplied transport: identical keyframe order on both replicas, and every rank takes the
+    same error path."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_cdist, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cloud = np.random.default_rng(5).random((13, 4)).astype(np.float32)
+    for rank in (0, 1):
+        r = res[rank]
+        rc, poses = r["poses"]
+        assert rc == 0
+        for q2 in (0, 1):
+            np.testing.assert_array_equal(poses[q2], np.stack([np.full(7, 10.0 * q2 + i) for i in range(3)]))
+        (rc, rows), buf = r["bcast"]
+        assert rc == 0 and rows == 13 and buf[:13].tobytes() == cloud.tobytes()
+        assert r["bcast_small"] == (-4, 13)                      # LMSF_ERR_CAPACITY on both ranks
+        assert [s[0] for s in r["steps"]] == [0, 0, 0]
+        assert [s[2] for s in r["steps"]] == [1, 0, 1]
+        assert r["bad_args"] == (-1, 0)
+        assert r["max"] == (0, 2.5)
+        assert [q2 for q2, *_ in r["replica"]] == [0, 1, 1]
+    for (rc0, i0, _), (rc1, i1, _) in zip(res[0]["steps"], res[1]["steps"]):
+        assert i0.tobytes() == i1.tobytes()                      # the same info table on every rank
+    for a, b in zip(res[0]["replica"], res[1]["replica"]):
+        assert a[0] == b[0] and all(x.tobytes() == y.tobytes() for x, y in zip(a[1:], b[1:]))
+    q2, fe, fs, P = res[0]["replica"][2]                          # step 2: rank 1's keyframe
+    assert fe.shape == (3, 4) and (fe == 12).all() and fs.shape == (5, 4) and (fs == -12).all() and P[0, 3] == 102

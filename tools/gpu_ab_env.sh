@@ -1,5 +1,6 @@
 # A/B of runtime switches in one box session: each ENVS entry (space-free "A=1,B=0" lists, "-" = none)
-# runs the default C2 bench once; one JSON line per entry under gpurun_out/ab_env_<i>.json.
+# runs the default C2 bench once; one JSON line per entry under gpurun_out/ab_env_<i>.json.  The knobs are read
+# only by -DLMSF_AB builds (tools/build_variant.sh): set LMSF_LIB to one.
 set -u
 cd "$GRAFT_REPO_ROOT"
 i=0

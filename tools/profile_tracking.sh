@@ -2,7 +2,7 @@
 # latency breakdown (tools/gaps.py), each bench under its own limit.
 set -u
 R="$GRAFT_REPO_ROOT"
-O="$R/gpurun_out/r02"
+O="$R/gpurun_out/${ROUND:-r03}"
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 for cfg in ${CONFIGS:-C4 C3}; do
