@@ -251,29 +251,37 @@ def load_traffic(traffic_json, **match):
     return tj
 
 
-def knn_roofline(ks, mean_n27, tj, elapsed_s, note):
-    """Roofline of the dominant (neighbour-search) kernel over the HIP-event-timed launches.
+def knn_roofline(ks, mean_n27, tj, elapsed_s, note, solo=None):
+    """Roofline of the dominant (neighbour-search) kernel.
 
-    achieved = PMC-measured HBM bytes per launch (`traffic`: (2 FETCH_SIZE + WRITE_SIZE) KiB per
-    dispatch, MI355X_MICROARCH.md's gfx950 correction, from the committed rocprofv3 passes `tj`) /
-    average HIP-event launch time.  `rocprof` recomputes the same from the profiler's own mean duration
-    of that kernel in the PMC run.  `model` is SURVEY 8(d)'s algorithmic figure, sum over the queries
-    that searched of [16 (query) + 27*8 (cell ranges) + 16 n27(q)] + 16 B per memo-reused query + 16 + 5*16 B
-    per refitted query (its 5 neighbours gathered, no walk) (n27 per
-    searched query from the counted untimed step); it counts every candidate read as an HBM read while
-    the 16 MB map + index stay in L2 / Infinity Cache, hence `exceeds_peak` when it would imply more
-    than the HBM peak (per launch or over the whole timed window)."""
-    launches = max(int(ks.launches), 1)
-    avg_launch_ms = ks.total_ms / launches
-    reused = int(getattr(ks, "reused_queries", 0))
-    refit = int(getattr(ks, "refit_queries", 0))
-    searched = int(ks.queries) - reused - refit
+    The launch time is `solo` when given: the HIP-stamped span of each search launch (memo pass + fused
+    search) measured live in an untimed pass that runs the context streams one at a time, i.e. the kernel
+    alone on the chip -- the condition of the committed rocprofv3 profile.  (The timed region runs several
+    context streams at once; a launch's span there includes time it shares the chip with other streams'
+    kernels, reported as `concurrent`.)  Without `solo` the timed launches' own spans are used (single-
+    stream configurations).
+
+    achieved = PMC-measured HBM bytes per launch (`traffic`: (2 FETCH_SIZE + WRITE_SIZE) KiB per outer
+    iteration, MI355X_MICROARCH.md's gfx950 correction, from the committed rocprofv3 passes `tj`) / that
+    launch time.  `rocprof` recomputes it with the profiler's own mean duration in the PMC run (the two
+    agree when the profile is of the current library).  `model` is SURVEY 8(d)'s algorithmic figure over
+    the same launch time: sum over the queries that searched of [16 (query) + 27*8 (cell ranges) +
+    16 n27(q)] + 16 B per memo-reused query + 16 + 5*16 B per refitted query (its 5 neighbours gathered,
+    no walk), n27 per searched query from the counted untimed step; it counts every candidate read as an
+    HBM read while the 16 MB map + index stay in L2 / Infinity Cache."""
+    t = solo if solo is not None else ks
+    launches = max(int(t.launches), 1)
+    avg_launch_ms = t.total_ms / launches
+    reused = int(getattr(t, "reused_queries", 0))
+    refit = int(getattr(t, "refit_queries", 0))
+    searched = int(t.queries) - reused - refit
     model_bytes = (searched * (16 + 27 * 8 + 16 * mean_n27) + reused * 16 + refit * (16 + 5 * 16)) / launches
     model_gbs = model_bytes / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
-    model_wall_gbs = model_bytes * launches / elapsed_s / 1e9 if elapsed_s > 0 else 0.0
+    model_wall_gbs = model_bytes * int(ks.launches) / elapsed_s / 1e9 if elapsed_s > 0 else 0.0
     traffic = int(tj["hbm_bytes_per_launch"]) if tj else None
     if traffic and avg_launch_ms > 0:
-        achieved, basis = traffic / (avg_launch_ms * 1e-3) / 1e9, "pmc"
+        achieved, basis = traffic / (avg_launch_ms * 1e-3) / 1e9, "pmc bytes / live " + ("solo" if solo else "timed") + \
+            " launch span"
     elif traffic:
         achieved, basis = None, "untimed (no search-launch stamps in this build)"
     else:   # never the model: it counts cache-served candidate reads as HBM bytes
@@ -281,22 +289,44 @@ def knn_roofline(ks, mean_n27, tj, elapsed_s, note):
     out = {"bound": "hbm", "achieved": round(achieved, 1) if achieved is not None else None, "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved is not None else None,
            "traffic": traffic, "basis": basis,
-           "kernel": kernel_name(ks), "avg_launch_ms": round(avg_launch_ms, 4), "launches": int(ks.launches),
-           "queries_per_launch": int(ks.queries / launches),
-           "reused_query_frac": round(reused / max(int(ks.queries), 1), 4),
-           "refit_query_frac": round(refit / max(int(ks.queries), 1), 4),
+           "kernel": kernel_name(ks), "avg_launch_ms": round(avg_launch_ms, 4), "launches": int(t.launches),
+           "queries_per_launch": int(t.queries / launches),
+           "reused_query_frac": round(reused / max(int(t.queries), 1), 4),
+           "refit_query_frac": round(refit / max(int(t.queries), 1), 4),
            "l2_hit_rate": round(tj["l2_hit_rate"], 3) if tj and tj.get("l2_hit_rate") is not None else None,
            "model": {"bytes_per_launch": int(model_bytes), "searched_queries_per_launch": int(searched / launches),
                      "mean_n27": round(mean_n27, 1), "gbs": round(model_gbs, 1),
                      "frac": round(model_gbs / HBM_PEAK_GBS, 4), "gbs_over_timed_window": round(model_wall_gbs, 1),
                      "exceeds_peak": bool(model_gbs > HBM_PEAK_GBS or model_wall_gbs > HBM_PEAK_GBS)},
            "note": note}
+    if solo is not None:
+        span = ks.total_ms / max(int(ks.launches), 1)
+        out["concurrent"] = {"avg_launch_ms": round(span, 4), "launches": int(ks.launches),
+                             "note": "timed region: search-launch spans with the other context streams' kernels "
+                                     "sharing the chip (not a kernel duration)"}
     if tj:
         mean_us = tj.get("rocprof_mean_us")
         out["rocprof"] = {"profile": tj.get("profile"), "mean_us": mean_us,
                           "frac": round(traffic / (mean_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if mean_us else None,
+                          "model_frac": round(model_bytes / (mean_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if mean_us else None,
+                          "live_over_rocprof": round(avg_launch_ms * 1e3 / mean_us, 3) if mean_us else None,
                           "dispatches": tj.get("dispatches")}
     return out
+
+
+def solo_launches(ctxs, guesses_of):
+    """One untimed pass over the context streams one at a time (launch + wait each: the search kernels
+    run alone on the chip, as in the rocprofv3 profile) with the launch stamps on; their summed accounting."""
+    stats = []
+    for i, c in enumerate(ctxs):
+        g = guesses_of(i)
+        if g is None:
+            continue
+        c.kernel_stats_reset(timing=True)
+        c.batch_launch(g)
+        c.batch_wait(len(g))
+        stats.append(c.kernel_stats())
+    return sum_stats(stats) if stats else None
 
 
 def apply_options(args, ctxs):
@@ -476,10 +506,16 @@ def run_batch(args, d):
     terr = [synth.pose_delta(poses[i], truth_u[unit_scan[i]]) for i in range(n_units)]
     tj = load_traffic(args.traffic_json, config=cfg, batch=sub_b, streams=1, map_points=map_points,
                       unique_scans=min(U, sub_b))
+    solo = None
+    if S > 1:   # kernel time alone on the chip (the profile's condition), live, after the timed region
+        c0 = 0
+        solo = solo_launches(ctxs, lambda i: guesses[c0 + i * sub_b:c0 + min((i + 1) * sub_b, chunk)]
+                             if i * sub_b < chunk else None)
     roof = knn_roofline(ks, mean_n27, tj, elapsed,
-                        "traffic: PMC bytes per dispatch from a one-stream run of the same per-context batch "
-                        "(device-wide counters); avg_launch_ms: HIP events on the context streams (with two "
-                        "streams a launch's span includes time it shares the chip with the other stream's kernels)")
+                        "traffic: PMC bytes per outer iteration (memo pass + search) from a one-stream rocprofv3 run "
+                        "of the same per-context batch (device-wide counters, profiles/); avg_launch_ms: device "
+                        "wall-clock stamps around each search launch of a live untimed pass running one context "
+                        "stream at a time", solo=solo)
     h2d = None
     if cfg == "C2" and (args.h2d == "on" or (args.h2d == "auto" and U == n_units)):
         # SURVEY 8(d) "including ... H2D of the scan": the same K steps with every step's scans streamed

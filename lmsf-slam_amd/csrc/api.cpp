@@ -1285,8 +1285,7 @@ lmsf_status lmsf_batch_run(lmsf_ctx* c, int32_t n, double* poses, lmsf_solve_sta
 }
 
 lmsf_status lmsf_set_option(lmsf_ctx* c, int32_t option, int32_t value) {
-    if (!c || option < 0 || option >= LMSF_OPT_COUNT || value < 0 || value > (option == LMSF_OPT_MEMO_BOUND ? 2 : 1))
-        return LMSF_ERR_ARG;
+    if (!c || option < 0 || option >= LMSF_OPT_COUNT || (value != 0 && value != 1)) return LMSF_ERR_ARG;
     c->opt[option] = value;
     return LMSF_OK;
 }

@@ -902,9 +902,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_W
                 // all five still inside the radius and still the 5 nearest: the farthest of them is nearer
                 // than any other point can have come (those were >= s6 from w0, so >= s6 - d from w)
                 const bool inside = key_bits(k[4]) < kSentinel && sqrt((double)key_d2(k[4])) + dd + 1e-5 < s6;
-                // a miss walks at most the radius of the farthest stored neighbour at w: those are 5 points within
-                // it, so the 5 nearest are too (r03; the search then knows the 6th only as >= that radius)
-                if (bv.memo_bound == 1 && key_bits(k[4]) < kSentinel) lim = fminf(lim, key_d2(k[4]) + 1e-5f);
                 same = inside;
 #pragma unroll
                 for (int j = 0; j < 5; ++j) same = same && (uint32_t)key_bits(k[j]) == idx[j];
@@ -1139,9 +1136,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         if (kMemo && walk) {   // anchor for the memo pass: gap between the 5th and the 6th neighbour (capped at 1 m)
             float gap = -1.f;
             if (key_bits(k[4]) < kSentinel) {
-                // s6: the 6th distance, or the walk's radius when it found no 6th -- a lower bound, which is all the
-                // memo's tests need (lim - 1e-5 = 1 for a full walk: the r02 cap)
-                const double s6 = sqrt((double)fminf(key_d2(k[5]), fminf(1.0f, lim - 1e-5f)));
+                const double s6 = sqrt((double)fminf(key_d2(k[5]), 1.0f));
                 double sj = sqrt((double)key_d2(k[0])), gord = 1.0;
 #pragma unroll
                 for (int j = 1; j < 5; ++j) {   // the smallest gap between consecutive neighbours

@@ -99,8 +99,14 @@ __global__ __launch_bounds__(kBeginThreads) LMSF_CTL_ATTR void lm_begin_kernel(B
     state_copy(bv.st[b], sS);
 }
 
-// After lm_eval_kernel at the candidate (LMSF_LM_FUSED=0): the reduction and lm_step_apply.
-__global__ __launch_bounds__(64) LMSF_CTL_ATTR void lm_step_kernel(BatchView bv, int outer, int is_last) {
+// After lm_eval_kernel at the candidate: the reduction and lm_step_apply.  kStepThreads: one wave.  Four
+// waves sharing the packet loads (A/B r03, tools/gpu_ab_lib.sh, two rounds): C3 1.81 vs 1.52-1.57 ms per
+// frame, C4 1.69-1.70 vs 1.64-1.66 ms per scan -- slower: a 4 x 256-VGPR block waits for a whole CU.
+#ifndef LMSF_STEP_THREADS
+#define LMSF_STEP_THREADS 64
+#endif
+constexpr int kStepThreads = LMSF_STEP_THREADS;
+__global__ __launch_bounds__(kStepThreads) LMSF_CTL_ATTR void lm_step_kernel(BatchView bv, int outer, int is_last) {
     const int b = blockIdx.x;
     SolveState& S = bv.st[b];
     if (!S.need_eval) {
@@ -322,7 +328,7 @@ hipError_t launch_lm_begin(const BatchView& bv, hipStream_t s) {
 }
 
 hipError_t launch_lm_step(const BatchView& bv, int outer, int is_last, hipStream_t s) {
-    hipLaunchKernelGGL(lm_step_kernel, dim3(bv.B), dim3(64), 0, s, bv, outer, is_last);
+    hipLaunchKernelGGL(lm_step_kernel, dim3(bv.B), dim3(kStepThreads), 0, s, bv, outer, is_last);
     return hipGetLastError();
 }
 

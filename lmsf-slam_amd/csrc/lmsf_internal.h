@@ -123,8 +123,7 @@ struct BatchView {
     int* n_search;           // [B] positions searched by the last match_fit_kernel (lm_begin's second range)
     int part2_base;          // packet index of match_fit_kernel's first wave packet (memo pass: [0, ceil(nq/64)))
     int fused_parts;         // lm_begin: packets laid out by the fused path (memo pass + search ranges)
-    int memo_bound;          // memo misses walk a bounded radius (LMSF_OPT_MEMO_BOUND): 1 = min(1 m, s6 + d, the
-                             //   farthest stored neighbour at w) (default), 2 = min(1 m, s6 + d) (r02), 0 = 1 m
+    int memo_bound;          // memo misses walk min(1 m, s6 + d) instead of 1 m (LMSF_OPT_MEMO_BOUND, default 1)
     int memo_order;          // memo: consecutive-gap test first (no re-keying when every gap exceeds 2 d)
     int memo_exact;          // memo: the stored 5 are kept when the farthest of them at w is nearer than s6 - d
                              //   (LMSF_MEMO_EXACT, default 1; 0: r01's 2 d < s6 - s5)

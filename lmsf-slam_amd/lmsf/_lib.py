@@ -401,7 +401,7 @@ class Context:
 
     def set_option(self, option, value):
         """lmsf_set_option (OPT_* switches, 0 | 1)."""
-        self._check(load().lmsf_set_option(self.h, int(option), int(bool(value))))
+        self._check(load().lmsf_set_option(self.h, int(option), int(value)))
 
     # ---- diagnostics
     def batch_capture(self, slots):
