@@ -49,8 +49,14 @@ def test_roofline_measured_and_model():
           "profile": "profiles/x", "dispatches": 3}
     r = bench.knn_roofline(ks, 50.0, tj, 0.02, "n")
     # 1 GB per 1 ms launch = 1000 GB/s; rocprof: 1 GB / 0.8 ms
-    assert r["basis"] == "pmc" and r["achieved"] == 1000.0 and r["frac"] == 0.125
+    assert r["basis"].startswith("pmc") and r["achieved"] == 1000.0 and r["frac"] == 0.125
     assert abs(r["rocprof"]["frac"] - 1e9 / 0.8e-3 / 1e9 / 8000) < 1e-4
+    assert r["rocprof"]["live_over_rocprof"] == 1.25 and "concurrent" not in r
+    # with a solo pass, achieved / model use its launch spans; the timed (concurrent) spans are reported beside
+    solo = types.SimpleNamespace(**dict(vars(ks), total_ms=8.0))
+    rs = bench.knn_roofline(ks, 50.0, tj, 0.02, "n", solo=solo)
+    assert rs["achieved"] == 1250.0 and rs["avg_launch_ms"] == 0.8 and rs["concurrent"]["avg_launch_ms"] == 1.0
+    assert rs["rocprof"]["live_over_rocprof"] == 1.0 and rs["model"]["frac"] == rs["rocprof"]["model_frac"]
     # model over the 600k searched queries per 10 launches + 16 B per reused query
     mb = (600_000 * (16 + 216 + 16 * 50) + 400_000 * 16) / 10
     assert r["model"]["bytes_per_launch"] == int(mb) and r["model"]["searched_queries_per_launch"] == 60_000
