@@ -671,14 +671,17 @@ def run_streams(args, d):
         t = mark("solve", t)
         P = tr.pose()
         ne = ns = 0
-        if r.update_type:
+        if r.update_type and world > 1:                               # the payload the other streams append
             ne = ctx.copy_features_into(_lib.EDGE, fbuf[:cap])
             ns = ctx.copy_features_into(_lib.SURF, fbuf[cap:])
         t = mark("copy_features", t)
         kfs = xchg.exchange(P, r.update_type, ne, ns, fbuf)           # same list, same order everywhere
         t = mark("exchange", t)
-        for _, fe, fs, pose in kfs:
-            tr.add_keyframe(fe, fs, pose)
+        for q, fe, fs, pose in kfs:
+            if q == rank:                                             # own keyframe: from the context, no copies
+                tr.add_keyframe_extracted(pose)
+            else:
+                tr.add_keyframe(fe, fs, pose)
         t = mark("add_keyframe", t)
         if kfs:
             tr.commit_map()

@@ -334,9 +334,12 @@ lmsf_status lmsf_tracker_set_initial_pose(lmsf_tracker* t, const double pose[16]
 lmsf_status lmsf_tracker_set_prior_map(lmsf_tracker* t, int32_t kind, const float* xyzi, size_t n);
 lmsf_status lmsf_tracker_add_keyframe(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf,
                                       size_t n_surf, const double pose[16]);
+/* add_keyframe of the features lmsf_extract_features left on the context's device (a stream's own
+ * keyframe: no copy out and back). */
+lmsf_status lmsf_tracker_add_keyframe_extracted(lmsf_tracker* t, const double pose[16]);
 /* Rebuilds the local map from the appended keyframes.  Returns once the rebuild is enqueued on the
- * tracker's own streams; the next lmsf_tracker_* call on t completes it, so context work enqueued in
- * between (lmsf_extract_features of the next scan, lmsf_copy_features) runs beside the rebuild; map
+ * tracker's own streams; the next lmsf_tracker_* call on t completes it, and so does the context's next
+ * lmsf_extract_features (after enqueuing the extraction, so the window grids are built beside it); map
  * consumers of the same context (lmsf_solve, lmsf_match, lmsf_batch_launch, lmsf_set_map) complete it
  * first as well. */
 lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t);

@@ -169,6 +169,7 @@ struct lmsf_ctx {
     // streaming ingest (lmsf_batch_load_scans_async): copies on their own stream into the raw slots,
     // ordered after the extraction that last read them (ev_raw_free) and before the next (ev_raw_ready)
     hipStream_t copy_stream = nullptr;
+    hipStream_t pad_stream = nullptr;    // batch contexts: holds a hardware queue slot (see lmsf_ctx_create)
     hipEvent_t ev_raw_free = nullptr, ev_raw_ready = nullptr;
     bool raw_pending = false;
     int* h_raw_counts = nullptr;      // pinned [B]
@@ -720,6 +721,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (c->ev_raw_free) hipEventDestroy(c->ev_raw_free);
     if (c->ev_raw_ready) hipEventDestroy(c->ev_raw_ready);
     if (c->copy_stream) hipStreamDestroy(c->copy_stream);
+    if (c->pad_stream) hipStreamDestroy(c->pad_stream);
     if (c->d_stamps) hipFree(c->d_stamps);
     if (c->h_stamps) hipHostFree(c->h_stamps);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -775,7 +777,10 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
         CHK(dalloc(&c->partials_gn, B * c->max_parts * kPacket));
         CHK(dalloc(&c->gn_rows, B * F * 4));
     }
-    CHK(dalloc(&c->raw, B * R));
+    if (ab_int("LMSF_RAW_UNCACHED", 0))   // A/B builds: raw slots in uncached memory (streamed uploads)
+        CHK(hipExtMallocWithFlags((void**)&c->raw, std::max<size_t>(B * R, 1) * sizeof(float4), hipDeviceMallocUncached));
+    else
+        CHK(dalloc(&c->raw, B * R));
     CHK(dalloc(&c->raw_count, B));
     CHK(dalloc(&c->raw_off, B));
     CHK(dalloc(&c->ring_id, B * R));
@@ -808,12 +813,18 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(hipHostMalloc((void**)&c->h_raw_counts, B * sizeof(int), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_raw_off, B * sizeof(int64_t), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_off, B * sizeof(int64_t), hipHostMallocDefault));
-    // Created here, not at the first streamed upload: streams take the process's GPU_MAX_HW_QUEUES (4)
-    // hardware queues round-robin at creation, so with a copy stream per context the four C2 contexts'
-    // compute streams share two queues -- measured faster than one queue each (LMSF_LAZY_COPY_STREAM=1:
-    // 22.50 / 22.58 / 22.62k vs 23.07 / 22.85 / 23.11k scans/s, one box, alternating).
-    if (!ab_int("LMSF_LAZY_COPY_STREAM", 0))
-        CHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    // Hardware queues.  Streams take the process's GPU_MAX_HW_QUEUES (4) queues at creation, and streams on
+    // one queue run in order.  Batch contexts create one more (otherwise idle) stream here: the four C2
+    // contexts' compute streams then share two queues -- measured faster than one queue each (r02, without
+    // it: 22.50 / 22.58 / 22.62k vs 23.07 / 22.85 / 23.11k scans/s, one box, alternating).  The upload
+    // stream of lmsf_batch_load_scans_async is created at the first streamed upload with the highest
+    // priority, which does not put it behind a context's kernels on a shared queue (r03, tools/gpu_call.sh
+    // A/B, two rounds: H2D-inclusive C2 23.74 / 23.87 ms per step vs 29.28 / 29.40 with the r02 normal-priority
+    // copy stream per context; 28.26 / 28.46 without the extra stream).  Single-scan (tracking) contexts
+    // create neither: the tracker's two commit streams then get queues of their own instead of sharing one
+    // (r03 trace: the surf and edge window rebuilds ran back to back on one queue).
+    if (cfg->max_batch > 1 && ab_int("LMSF_QUEUE_PAD", 1))
+        CHK(hipStreamCreateWithFlags(&c->pad_stream, hipStreamNonBlocking));
     CHK(hipEventCreateWithFlags(&c->ev_raw_free, hipEventDisableTiming));
     CHK(hipEventCreateWithFlags(&c->ev_raw_ready, hipEventDisableTiming));
     CHK(hipEventRecord(c->ev_raw_free, c->stream));
@@ -927,6 +938,10 @@ lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf
     HIPCHK(c, launch_extract(c->eview(1), c->stream));
     HIPCHK(c, hipEventRecord(c->ev_raw_free, c->stream));
     c->qorder_valid = true;
+    // A tracker's deferred keyframe commit completes here, beside this extraction: its window grids are built
+    // on the tracker's streams while the extraction kernels run, and the next search finds them ready.
+    rc = ctx_settle(c);
+    if (rc) return rc;
     // counts + error flag gathered on the device, one read-back into pinned memory
     HIPCHK(c, launch_pack3(c->n_edge, c->n_surf, c->d_error, c->d_error + 8, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->h_pack, c->d_error + 8, 3 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -1204,7 +1219,11 @@ lmsf_status lmsf_batch_load_scans_async(lmsf_ctx* c, const float* xyzi, const in
     for (int i = 0; i < n; ++i)
         if (counts[i] < 0 || counts[i] > c->R)
             return c->fail(LMSF_ERR_CAPACITY, "scan %d has %lld points (max_scan_points %d)", i, (long long)counts[i], c->R);
-    if (!c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    if (!c->copy_stream) {   // highest priority: not queued behind kernels (lmsf_ctx_create)
+        int lo = 0, hi = 0;
+        HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(c, hipStreamCreateWithPriority(&c->copy_stream, hipStreamNonBlocking, hi));
+    }
     HIPCHK(c, hipStreamSynchronize(c->copy_stream));   // the previous upload (normally long done) owns h_raw_counts
     HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->ev_raw_free, 0));     // the last extraction has read raw
     size_t off = 0;

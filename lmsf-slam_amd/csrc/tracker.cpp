@@ -510,11 +510,37 @@ lmsf_status lmsf_tracker_add_keyframe(lmsf_tracker* t, const float* edge, size_t
     for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) {
         if (cnt[kind] == 0) continue;
         if (cnt[kind] > (size_t)t->cap) return fail(t, LMSF_ERR_CAPACITY, "keyframe larger than the tracker slot capacity");
-        TCHK(t, hipMemcpyAsync(t->stage, src[kind], cnt[kind] * sizeof(float4), hipMemcpyDefault, s));
-        lmsf_status rc = push_frame(t, kind, t->stage, (int64_t)cnt[kind], T);
+        // device memory of this GPU is transformed in place; host (or other-device) memory is staged first
+        const float4* from = t->stage;
+        hipPointerAttribute_t pa;
+        if (hipPointerGetAttributes(&pa, src[kind]) == hipSuccess && pa.type == hipMemoryTypeDevice &&
+            pa.device == ctx_device(t->ctx))
+            from = reinterpret_cast<const float4*>(src[kind]);
+        else
+            TCHK(t, hipMemcpyAsync(t->stage, src[kind], cnt[kind] * sizeof(float4), hipMemcpyDefault, s));
+        (void)hipGetLastError();   // a host pointer's failed attribute query leaves an error behind
+        lmsf_status rc = push_frame(t, kind, from, (int64_t)cnt[kind], T);
         if (rc) return rc;
     }
     return LMSF_OK;
+}
+
+lmsf_status lmsf_tracker_add_keyframe_extracted(lmsf_tracker* t, const double pose[16]) {
+    if (!t || !pose) return LMSF_ERR_ARG;
+    if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    {
+        lmsf_status rs = settle(t);
+        if (rs) return rs;
+    }
+    if (!ctx_features_on_device(t->ctx)) return fail(t, LMSF_ERR_STATE, "no extracted features on the device");
+    const float4* feat;
+    int64_t ne, ns;
+    lmsf_status rc = ctx_slot0_features(t->ctx, &feat, &ne, &ns);
+    if (rc) return rc;
+    const Iso T = iso_from16(pose);
+    rc = push_frame(t, LMSF_EDGE, feat, ne, T);
+    if (rc) return rc;
+    return push_frame(t, LMSF_SURF, feat + ne, ns, T);
 }
 
 // Returns once the rebuild is enqueued (commit_stage); the next tracker call completes it (settle), so

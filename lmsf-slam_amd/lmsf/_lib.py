@@ -133,6 +133,7 @@ _SIGS = {
     "lmsf_tracker_set_initial_pose": (C.c_int32, [_P, _P]),
     "lmsf_tracker_set_prior_map": (C.c_int32, [_P, C.c_int32, _P, C.c_size_t]),
     "lmsf_tracker_add_keyframe": (C.c_int32, [_P, _P, C.c_size_t, _P, C.c_size_t, _P]),
+    "lmsf_tracker_add_keyframe_extracted": (C.c_int32, [_P, _P]),
     "lmsf_tracker_commit_map": (C.c_int32, [_P]),
     "lmsf_voxel_filter": (C.c_int32, [_P, _P, C.c_size_t, C.c_float, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "lmsf_ingest_params_init": (C.c_int32, [C.POINTER(IngestParams)]),
@@ -537,6 +538,11 @@ class Tracker:
         ps, ns, ks = _buf(surf)
         T = np.ascontiguousarray(pose, dtype=np.float64)
         self.ctx._check(load().lmsf_tracker_add_keyframe(self.h, pe, ne, ps, ns, T.ctypes.data))
+
+    def add_keyframe_extracted(self, pose):
+        """The context's extracted features (lmsf_extract_features) as a keyframe at pose (4x4)."""
+        T = np.ascontiguousarray(pose, dtype=np.float64)
+        self.ctx._check(load().lmsf_tracker_add_keyframe_extracted(self.h, T.ctypes.data))
 
     def commit_map(self):
         self.ctx._check(load().lmsf_tracker_commit_map(self.h))

@@ -89,7 +89,9 @@ class KeyframeExchange:
     every step, of the transformed-feature payload when a stream emits a keyframe).
 
     feat: (2 * cap, 4) float32 tensor on `device` holding this rank's [edges | surfs] (edges at 0,
-    surfs at cap).  Returns [(rank, edge_view, surf_view, pose4x4)] for the keyframed streams."""
+    surfs at cap).  Returns [(rank, edge_view, surf_view, pose4x4)] for the keyframed streams (a replica adds
+    its own entry from its context, lmsf_tracker_add_keyframe_extracted; with one stream the views are None
+    and feat is not read)."""
 
     def __init__(self, cap: int, world: int, device=None):
         import torch
@@ -108,10 +110,8 @@ class KeyframeExchange:
             allinfo = self.info.cpu().numpy()
             if (allinfo[:, 16] > 0).any():
                 dist.all_gather_into_tensor(self.gbuf, feat.unsqueeze(0))
-        else:
-            allinfo = vec[None]
-            if update_type:
-                self.gbuf[0].copy_(feat)
+        else:   # one stream: nothing to exchange; the caller adds its own keyframe from its context
+            return [(0, None, None, np.asarray(pose, dtype=np.float64).reshape(4, 4))] if update_type else []
         out = []
         for q in range(self.world):
             if allinfo[q, 16] > 0:

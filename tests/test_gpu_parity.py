@@ -728,11 +728,14 @@ def test_tracker_shared_map_streams(lib, oracle_mod, sequence_workload):
                 ne = ctxs[s].copy_features_into(lib.EDGE, buf[lib.EDGE])
                 ns = ctxs[s].copy_features_into(lib.SURF, buf[lib.SURF])
                 assert (ne, ns) == (len(e), len(su))
-                kfs_g.append((buf[lib.EDGE][:ne].clone(), buf[lib.SURF][:ns].clone(), gts[s].pose()))
+                kfs_g.append((s, buf[lib.EDGE][:ne].clone(), buf[lib.SURF][:ns].clone(), gts[s].pose()))
                 kfs_o.append((e, su, ots[s].curr.copy()))
         for g, o in zip(kfs_g, kfs_o):              # every stream appends every keyframe, same order
             for s in range(len(streams)):
-                gts[s].add_keyframe(*g)
+                if g[0] == s:                       # its own: from the context's extracted features
+                    gts[s].add_keyframe_extracted(g[3])
+                else:                               # the other stream's: device tensors (in place)
+                    gts[s].add_keyframe(*g[1:])
                 ots[s].add_keyframe(*o)
         for s in range(len(streams)):
             gts[s].commit_map()                     # returns with the rebuild enqueued (deferred finish)
@@ -743,7 +746,9 @@ def test_tracker_shared_map_streams(lib, oracle_mod, sequence_workload):
                 rec_b, nn_b = ctxs[0].match(wl.truth[streams[0][step]], nq[0])
                 assert rec_a.tobytes() == rec_b.tobytes() and (nn_a == nn_b).all()
             assert len(gts[s].local_map(lib.SURF)) == len(ots[s].local_map(2))
+    # replica 0 added stream 0's keyframes from its context and stream 1's from tensors, replica 1 the reverse
     np.testing.assert_allclose(gts[0].local_map(lib.SURF), gts[1].local_map(lib.SURF), atol=0)
+    np.testing.assert_allclose(gts[0].local_map(lib.EDGE), gts[1].local_map(lib.EDGE), atol=0)
     np.testing.assert_allclose(gts[0].local_map(lib.EDGE), ots[0].local_map(1), atol=1e-4)
     for t in gts:
         t.close()
