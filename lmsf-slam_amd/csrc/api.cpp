@@ -165,7 +165,8 @@ struct lmsf_ctx {
     float4* featp = nullptr;          // [B][F] the features in that order (w = slot)
     int* n_pos = nullptr;
     bool qorder_valid = false;        // the slots' features came from the extraction kernels
-    int* d_error = nullptr;
+    int* d_error = nullptr;           // [0] extraction capacity flags, [8..10] pack3, [16] LM loop wait gave up
+    unsigned* d_lmsync = nullptr;     // [2 B] lm_loop_kernel counters
     // streaming ingest (lmsf_batch_load_scans_async): copies on their own stream into the raw slots,
     // ordered after the extraction that last read them (ev_raw_free) and before the next (ev_raw_ready)
     hipStream_t copy_stream = nullptr;
@@ -543,8 +544,15 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
                 bvb.fused_parts = 1;
                 bvb.memo = o > 0 && !c->count27 && memo_on && !match_fit_prune(ge, gs) ? 1 : 0;
             }
-            HIPCHK(c, launch_lm_begin(bvb, s));
-            for (int i = 0; i < 4; ++i) HIPCHK(c, launch_lm_eval_step(bv, o, i == 3 ? 1 : 0, s));
+            // single-scan launches: the whole LM of this outer iteration in one launch when its grid is
+            // co-resident (lm_loop_kernel; A/B builds: LMSF_LM_LOOP=0 for the 9-launch form)
+            static const bool loop_on = ab_int("LMSF_LM_LOOP", 1) != 0;
+            if (!fused && loop_on && nb * lm_loop_blocks(bv) <= kLoopMaxBlocks) {
+                HIPCHK(c, launch_lm_loop(bv, o, c->d_lmsync, c->d_error + 16, s));
+            } else {
+                HIPCHK(c, launch_lm_begin(bvb, s));
+                for (int i = 0; i < 4; ++i) HIPCHK(c, launch_lm_eval_step(bv, o, i == 3 ? 1 : 0, s));
+            }
         }
     }
     return LMSF_OK;
@@ -644,6 +652,14 @@ lmsf_status collect_timing(lmsf_ctx* c) {
     return LMSF_OK;
 }
 
+// lm_loop_kernel gave up a bounded wait (its blocks were not all resident): the results are not usable.
+lmsf_status loop_fault(lmsf_ctx* c) {
+    HIPCHK(c, hipMemsetAsync(c->d_error + 16, 0, sizeof(int), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->h_pack[3] = 0;
+    return c->fail(LMSF_ERR_HIP, "single-scan LM loop: a block waited past its limit (grid not co-resident)");
+}
+
 int outer_iterations_for_solve(lmsf_ctx* c) {
     if (c->cfg.solver == LMSF_SOLVER_CERES_LM && c->cfg.schedule == LMSF_SCHEDULE_REFERENCE_DECAY) {
         if (c->optimization_count > 2) c->optimization_count--;   // ceres_...:100-101
@@ -697,7 +713,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->prevw, c->memo_nbr, c->wl, c->wlim, c->wcount, c->n_search, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->sort_key,
-                    c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->featp, c->n_pos, c->d_error};
+                    c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->featp, c->n_pos, c->d_error, c->d_lmsync};
     for (void* p : bufs) hipFree(p);
     hipFree(c->cap_rec);
     hipFree(c->cap_nn);
@@ -802,6 +818,8 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->featp, B * c->F));
     CHK(dalloc(&c->n_pos, B));
     CHK(dalloc(&c->d_error, 32));
+    CHK(dalloc(&c->d_lmsync, 2 * B));
+    CHK(hipMemset(c->d_lmsync, 0, 2 * B * sizeof(unsigned)));
     CHK(hipMemset(c->d_error, 0, 32 * sizeof(int)));
     CHK(hipMemset(c->n_edge, 0, B * sizeof(int)));
     CHK(hipMemset(c->n_surf, 0, B * sizeof(int)));
@@ -906,9 +924,11 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     rc = enqueue_solve(c, 1, iters);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, stream_wait(c->stream));
     rc = collect_timing(c);
     if (rc) return rc;
+    if (c->h_pack[3]) return loop_fault(c);
     const SolveState& S = c->h_st[0];
     std::memcpy(pose, S.x, 7 * sizeof(double));
     c->last_outer = std::min(S.outer_run, kMaxOuter);
@@ -1275,9 +1295,11 @@ lmsf_status lmsf_batch_wait(lmsf_ctx* c, int32_t n, double* poses, lmsf_solve_st
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, (size_t)n * sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
     int herr = 0;
     HIPCHK(c, hipMemcpyAsync(&herr, c->d_error, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     lmsf_status rc = collect_timing(c);
     if (rc) return rc;
+    if (c->h_pack[3]) return loop_fault(c);
     for (int i = 0; i < n; ++i) {
         std::memcpy(poses + 7 * i, c->h_st[i].x, 7 * sizeof(double));
         if (stats) fill_stats(c->h_st[i], &stats[i]);

@@ -1291,6 +1291,146 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_EVAL_W
     block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + blockIdx.x) * kPacket);
 }
 
+// ---------------------------------------------------------------- single-scan LM loop in one launch
+// The Ceres LM of one outer iteration (lm_begin + 4 x (lm_eval + lm_step), 9 launches) as one launch for
+// contexts whose whole grid is co-resident (tracking: one scan, ~70 blocks on 256 CUs; kLoopMaxBlocks).  Every block keeps
+// its own LDS copy of the slot's SolveState and runs the one-lane control on identical inputs (the same
+// packets summed in the same order), so all copies stay equal and no block waits for another's step: a
+// block evaluates its 1024 records at the candidate, publishes its packet, and one arrive / wait on a
+// per-slot counter later every block reduces every packet itself.
+//
+// Cross-block visibility (MI355X_MICROARCH.md, correctness boundaries: per-XCD L2s are not coherent):
+// packets are stored and loaded with agent-scope atomic accesses (write-through / L2-bypassing), every
+// storing wave drains its stores before the block's barrier, and the counter is an agent-scope atomic.
+// Packets alternate between two buffers by inner iteration, so a block that runs ahead cannot overwrite a
+// packet another block still reads.  Every wait is bounded: a block that spins past the limit flags
+// err[0] and leaves (the host reports LMSF_ERR_HIP), so no configuration can hang the device.
+// sync[2 b] counts arrivals of slot b across launches; sync[2 b + 1] holds the count at the start of the
+// next launch (written by block 0 after the last wait of this one).
+constexpr unsigned kLoopSpinLimit = 1u << 24;
+
+__device__ __forceinline__ void coherent_store_f64(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double coherent_load_f64(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<double*>(p)),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Every block of the slot arrives once; returns when all nblk of this barrier have (count reaches target).
+__device__ __forceinline__ void slot_barrier(unsigned* cnt, unsigned target, int* err) {
+    __builtin_amdgcn_s_waitcnt(0);   // this wave's packet stores are complete
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kLoopSpinLimit) {
+                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// The packets [p0, p0 + np) of slot b summed in a fixed order into tot (LDS; the same in every block).
+__device__ void reduce_coherent(const BatchView& bv, int b, int p0, int np, double* tot) {
+    __shared__ double red[4][kPacket];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 31;
+    double acc = 0.0;
+    const double* base = bv.partials + ((size_t)b * bv.max_parts + p0) * kPacket;
+    for (int p = 2 * wave + (lane >> 5); p < np; p += 8) acc += coherent_load_f64(base + (size_t)p * kPacket + e);
+    acc += __shfl_xor(acc, 32, 64);
+    if (lane < 32) red[wave][e] = acc;
+    __syncthreads();
+    if (threadIdx.x < kPacket) {
+        const int i = threadIdx.x;
+        tot[i] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, unsigned* sync, int* err) {
+    const int b = blockIdx.y, part = blockIdx.x, nblk = gridDim.x;
+    __shared__ SolveState sS;
+    __shared__ double tot[kPacket];
+    state_copy(sS, bv.st[b]);
+    const int nq = bv.n_edge[b] + bv.n_surf[b];
+    // lm_begin: the first evaluation's packets (fit_eval), IterationZero and the first step
+    reduce_parts(bv, b, (nq + bv.part_q - 1) / bv.part_q, tot);   // ends with a barrier: sS is in place
+    if (threadIdx.x == 0) lm_begin_apply(sS, tot);
+    __syncthreads();
+    const unsigned base = sync[2 * b + 1];
+    unsigned nbar = 0;
+    const int pbuf = bv.max_parts / 2;   // packet buffers [pbuf, pbuf + 2 nblk): above the fit packets
+    const size_t rbase = (size_t)b * bv.feat_stride;
+    for (int i = 0; i < 4; ++i) {
+        const int last = i == 3 ? 1 : 0;
+        if (!sS.need_eval) {
+            if (last && threadIdx.x == 0) finish_outer(sS, outer);
+            __syncthreads();
+            continue;
+        }
+        const Pose Ps = load_pose(sS.xc);
+        double P[kPacket];
+#pragma unroll
+        for (int k = 0; k < kPacket; ++k) P[k] = 0.0;
+        const int q0 = part * kEvalBlock + threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < kEvalPerThread; ++k) {
+            const int q = q0 + k * 256;
+            if (q < nq) {
+                const float4 rp = bv.rec_p[rbase + q];
+                if (__float_as_int(rp.w) != 0) {
+                    const RecV rv = bv.rec_v[rbase + q];
+                    const double2 re = __float_as_int(rp.w) == LMSF_EDGE ? bv.rec_e[rbase + q] : make_double2(0.0, 0.0);
+                    eval_record(Ps, true, rp, rv, re, P);
+                }
+            }
+        }
+        double* slotp = bv.partials + ((size_t)b * bv.max_parts + pbuf + (i & 1) * nblk + part) * kPacket;
+        {   // block packet (block_reduce_packet's order), stored write-through
+            __shared__ double red[4][kPacket];
+            const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+            butterfly_step<16>(P, lane);
+            butterfly_step<8>(P, lane);
+            butterfly_step<4>(P, lane);
+            butterfly_step<2>(P, lane);
+            butterfly_step<1>(P, lane);
+            const double v = P[0] + __shfl_xor(P[0], 1, 64);
+            if ((lane & 1) == 0) red[wave][lane >> 1] = v;
+            __syncthreads();
+            if (threadIdx.x < kPacket) {
+                const int e = threadIdx.x;
+                coherent_store_f64(slotp + e, ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e]);
+            }
+        }
+        ++nbar;
+        slot_barrier(&sync[2 * b], base + nbar * (unsigned)nblk, err);
+        reduce_coherent(bv, b, pbuf + (i & 1) * nblk, nblk, tot);
+        if (threadIdx.x == 0) lm_step_apply(sS, tot, outer, last);
+        __syncthreads();
+    }
+    if (nbar == 0) {   // no wait yet: make sure every block has read st before block 0 rewrites it
+        ++nbar;
+        slot_barrier(&sync[2 * b], base + nbar * (unsigned)nblk, err);
+    }
+    if (part == 0) {
+        state_copy(bv.st[b], sS);
+        if (threadIdx.x == 0) sync[2 * b + 1] = base + nbar * (unsigned)nblk;
+    }
+}
+
+int lm_loop_blocks(const BatchView& bv) { return (bv.feat_stride + kEvalBlock - 1) / kEvalBlock; }
+
+hipError_t launch_lm_loop(const BatchView& bv, int outer, unsigned* sync, int* err, hipStream_t s) {
+    hipLaunchKernelGGL(lm_loop_kernel, dim3(lm_loop_blocks(bv), bv.B), dim3(256), 0, s, bv, outer, sync, err);
+    return hipGetLastError();
+}
+
 // Diagnostics: evaluate slot 0's records at an arbitrary pose into partials of slot 0.
 __global__ __launch_bounds__(256) void eval_at_kernel(BatchView bv, const double* pose) {
     const int nq = bv.n_edge[0] + bv.n_surf[0];

@@ -37,37 +37,6 @@ __global__ void state_init_kernel(BatchView bv, const double* poses) {
     S.edge_matches = S.surf_matches = S.nmatch = 0;
 }
 
-// IterationZero on the reduced first evaluation (tot) + the first step; one lane, S in LDS.
-__device__ __forceinline__ void lm_begin_apply(SolveState& S, const double* tot) {
-    S.iteration = 0;
-    S.need_eval = 0;
-    S.done = 0;
-    S.evals = 1;
-    S.nmatch = (int)tot[28];
-    S.edge_matches = (int)tot[29];
-    S.surf_matches = (int)tot[30];
-    S.cost = tot[0];
-    S.initial_cost = tot[0];
-    for (int i = 0; i < 21; ++i) S.H[i] = tot[1 + i];
-    for (int i = 0; i < 6; ++i) S.g[i] = tot[22 + i];
-    if (S.nmatch == 0) {  // no residual blocks: pose unchanged
-        S.done = 1;
-        S.term = LMSF_TERM_NO_RESIDUALS;
-        return;
-    }
-    for (int j = 0; j < 6; ++j) S.s[j] = 1.0 / (1.0 + sqrt(S.H[hidx(j, j)]));
-    S.radius = 1e4;
-    S.decrease = 2.0;
-    S.x_norm = norm7(S.x);
-    if (grad_max_norm(S.x, S.g) <= 1e-10) {
-        S.done = 1;
-        S.term = LMSF_TERM_GRADIENT_TOL;
-        return;
-    }
-    compute_step(S);
-}
-
-
 // After fit_eval: IterationZero (evaluate at x0, jacobi scaling, gradient check) + first step.
 // LMSF_CTL_WAVES: waves per SIMD the LM control kernels are compiled for; 0 = the compiler's choice
 // (lm_begin 195 VGPRs, lm_step 256).  At 8, lm_begin fits 64 VGPRs (604 B of scratch for its serial lane)

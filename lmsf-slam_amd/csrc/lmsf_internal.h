@@ -169,6 +169,12 @@ hipError_t launch_fit_eval(const GridView& edge, const GridView& surf, const Bat
 hipError_t launch_lm_begin(const BatchView& bv, hipStream_t s);
 // One LM inner iteration: evaluation at the candidate, then the step control.
 hipError_t launch_lm_eval_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
+// lm_begin + the 4 inner iterations of one outer iteration in one launch (k_match.hip, lm_loop_kernel): for
+// launches whose B x lm_loop_blocks blocks are all co-resident (kLoopMaxBlocks).  sync: [2 B] counters
+// (zeroed once), err: set when a bounded wait gave up.
+constexpr int kLoopMaxBlocks = 128;   // half the CUs: room for other streams' launches beside it
+int lm_loop_blocks(const BatchView& bv);
+hipError_t launch_lm_loop(const BatchView& bv, int outer, unsigned* sync, int* err, hipStream_t s);
 hipError_t launch_lm_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
 hipError_t launch_gn_solve(const BatchView& bv, int outer, hipStream_t s);
 int fit_per_thread_default();
