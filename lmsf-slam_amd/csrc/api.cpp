@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -105,6 +106,7 @@ hipError_t dalloc(T** p, size_t count) {
 struct lmsf_ctx {
     lmsf_config cfg;
     std::string err;
+    std::mutex err_mu;                // a tracker's commit worker may report an error beside the caller
     int opt[LMSF_OPT_COUNT] = {1, 1, 1, 1, 1, 0};   // lmsf_set_option (defaults: lmsf.h)
     // record capture (lmsf_batch_capture): device rows [n_cap][kCaptureIters][F] of the captured slots
     std::vector<int> cap_slots;
@@ -227,6 +229,7 @@ struct lmsf_ctx {
         va_start(ap, fmt);
         vsnprintf(buf, sizeof buf, fmt, ap);
         va_end(ap);
+        std::lock_guard<std::mutex> lk(err_mu);
         err = buf;
         return code;
     }

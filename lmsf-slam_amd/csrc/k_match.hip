@@ -1340,9 +1340,19 @@ __device__ __forceinline__ void slot_barrier(unsigned* cnt, unsigned target, int
 __device__ void reduce_coherent(const BatchView& bv, int b, int p0, int np, double* tot) {
     __shared__ double red[4][kPacket];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 31;
-    double acc = 0.0;
     const double* base = bv.partials + ((size_t)b * bv.max_parts + p0) * kPacket;
-    for (int p = 2 * wave + (lane >> 5); p < np; p += 8) acc += coherent_load_f64(base + (size_t)p * kPacket + e);
+    // kLoads loads in flight per lane (the packets of one launch: <= 8 * kLoads), summed in a fixed order
+    constexpr int kLoads = kLoopMaxBlocks / 8;
+    double v[kLoads];
+    const int pl = 2 * wave + (lane >> 5);
+#pragma unroll
+    for (int u = 0; u < kLoads; ++u) {
+        const int p = pl + 8 * u;
+        v[u] = p < np ? coherent_load_f64(base + (size_t)p * kPacket + e) : 0.0;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < kLoads; ++u) acc += v[u];
     acc += __shfl_xor(acc, 32, 64);
     if (lane < 32) red[wave][e] = acc;
     __syncthreads();
@@ -1378,18 +1388,20 @@ __global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, u
         double P[kPacket];
 #pragma unroll
         for (int k = 0; k < kPacket; ++k) P[k] = 0.0;
+        // lm_eval_kernel's form: the records' loads in flight together, then evaluated
         const int q0 = part * kEvalBlock + threadIdx.x;
+        auto rec_at = [&](int k) { return rbase + (q0 + k * 256 < nq ? q0 + k * 256 : 0); };
+        float4 rp[kEvalPerThread];
+        RecV rv[kEvalPerThread];
 #pragma unroll
         for (int k = 0; k < kEvalPerThread; ++k) {
-            const int q = q0 + k * 256;
-            if (q < nq) {
-                const float4 rp = bv.rec_p[rbase + q];
-                if (__float_as_int(rp.w) != 0) {
-                    const RecV rv = bv.rec_v[rbase + q];
-                    const double2 re = __float_as_int(rp.w) == LMSF_EDGE ? bv.rec_e[rbase + q] : make_double2(0.0, 0.0);
-                    eval_record(Ps, true, rp, rv, re, P);
-                }
-            }
+            rp[k] = bv.rec_p[rec_at(k)];
+            rv[k] = bv.rec_v[rec_at(k)];
+        }
+#pragma unroll
+        for (int k = 0; k < kEvalPerThread; ++k) {
+            const bool edge = __float_as_int(rp[k].w) == LMSF_EDGE;
+            eval_record(Ps, q0 + k * 256 < nq, rp[k], rv[k], edge ? bv.rec_e[rec_at(k)] : make_double2(0.0, 0.0), P);
         }
         double* slotp = bv.partials + ((size_t)b * bv.max_parts + pbuf + (i & 1) * nblk + part) * kPacket;
         {   // block packet (block_reduce_packet's order), stored write-through

@@ -15,7 +15,10 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "lmsf_internal.h"
@@ -147,6 +150,16 @@ struct lmsf_tracker {
     bool pending = false;                               // staged, not yet finished
     float4* stage = nullptr;   // host/device keyframe input staged before the transform
     int cap = 0;               // points per keyframe slot
+    // Commit worker (lmsf_tracker_commit_map): enqueues the window rebuild on the aux streams from a host
+    // thread of its own, so the ~50 launches of a rebuild (~0.6 ms of host API time per C4 step, r03) overlap
+    // the caller's next calls instead of preceding them.  `staging`: a job posted and not yet joined.
+    // Two workers, one per window kind / aux stream, so the surf and edge rebuilds are enqueued side by side.
+    std::thread worker[2];
+    std::mutex mu;
+    std::condition_variable cv;
+    int job[2] = {0, 0};          // kind to stage on aux[i] (0: none)
+    bool quit = false, staging = false;
+    lmsf_status job_rc[2] = {LMSF_OK, LMSF_OK};
 };
 
 namespace {
@@ -196,47 +209,90 @@ lmsf_status push_frame(lmsf_tracker* t, int kind, const float4* src, int64_t n, 
 // and filled on them, and the context stream joins them before its next search.  The context stream
 // stays free in between, so the next scan's extraction runs beside the map rebuild when the caller
 // defers the finish (lmsf_tracker_commit_map; settle() completes it at the next tracker call).
-lmsf_status commit_stage(lmsf_tracker* t) {
-    hipStream_t s = ctx_stream(t->ctx);
-    TCHK(t, hipEventRecord(t->ev_fork, s));   // the keyframe transforms queued on s
+// One kind's half of commit_stage on stream ks (after ev_fork).
+lmsf_status commit_stage_kind(lmsf_tracker* t, int kind, hipStream_t ks) {
+    Window& w = t->win[kind];
+    TCHK(t, hipStreamWaitEvent(ks, t->ev_fork, 0));
+    const int W = (int)w.slots.size();
+    float4* dst = w.leaf > 0 ? w.wcat : w.concat;
+    size_t nw = 0;
+    for (int i0 = 0; i0 < w.count; i0 += kSlotTable) {         // keyframes in window order
+        SlotTable tab{};
+        tab.n = std::min(kSlotTable, w.count - i0);
+        for (int i = 0; i < tab.n; ++i) {
+            const int j = (w.head + i0 + i) % W;
+            tab.src[i] = w.slots[j];
+            tab.start[i + 1] = tab.start[i] + w.sizes[j];
+        }
+        TCHK(t, launch_gather_slots(tab, dst + nw, ks));
+        nw += (size_t)tab.start[tab.n];
+    }
+    const int* n_dev = nullptr;
+    if (w.leaf > 0 && nw) {                                   // VoxelGrid of the window (count stays on the device)
+        TCHK(t, t->voxel[kind].enqueue(w.wcat, (int)nw, (float)w.leaf, w.concat, ks));
+        n_dev = t->voxel[kind].nseg;
+    }
+    t->nmax[kind] = nw;
+    // only the window's grid is rebuilt; the prior's grid was built once (set_prior_map)
+    return ctx_window_stage(t->ctx, kind, w.concat, nw, n_dev, ks);
+}
+
+// The aux stream of each changed kind (surf first: the larger window and its sort); returns the count.
+int assign_streams(lmsf_tracker* t) {
     int k = 0;
-    for (int kind : {LMSF_SURF, LMSF_EDGE}) {   // surf first: the larger window and its sort
-        Window& w = t->win[kind];
+    for (int kind : {LMSF_SURF, LMSF_EDGE}) {
         t->ks[kind] = nullptr;
         t->nmax[kind] = 0;
-        if (!w.dirty) continue;
-        hipStream_t ks = t->aux[k++];
-        t->ks[kind] = ks;
-        TCHK(t, hipStreamWaitEvent(ks, t->ev_fork, 0));
-        const int W = (int)w.slots.size();
-        float4* dst = w.leaf > 0 ? w.wcat : w.concat;
-        size_t nw = 0;
-        for (int i0 = 0; i0 < w.count; i0 += kSlotTable) {         // keyframes in window order
-            SlotTable tab{};
-            tab.n = std::min(kSlotTable, w.count - i0);
-            for (int i = 0; i < tab.n; ++i) {
-                const int j = (w.head + i0 + i) % W;
-                tab.src[i] = w.slots[j];
-                tab.start[i + 1] = tab.start[i] + w.sizes[j];
-            }
-            TCHK(t, launch_gather_slots(tab, dst + nw, ks));
-            nw += (size_t)tab.start[tab.n];
-        }
-        const int* n_dev = nullptr;
-        if (w.leaf > 0 && nw) {                                   // VoxelGrid of the window (count stays on the device)
-            TCHK(t, t->voxel[kind].enqueue(w.wcat, (int)nw, (float)w.leaf, w.concat, ks));
-            n_dev = t->voxel[kind].nseg;
-        }
-        t->nmax[kind] = nw;
-        // only the window's grid is rebuilt; the prior's grid was built once (set_prior_map)
-        lmsf_status rc = ctx_window_stage(t->ctx, kind, w.concat, nw, n_dev, ks);
+        if (t->win[kind].dirty) t->ks[kind] = t->aux[k++];
+    }
+    return k;
+}
+
+lmsf_status commit_stage(lmsf_tracker* t) {
+    TCHK(t, hipEventRecord(t->ev_fork, ctx_stream(t->ctx)));   // the keyframe transforms queued on the context
+    assign_streams(t);
+    for (int kind : {LMSF_SURF, LMSF_EDGE}) {
+        if (!t->ks[kind]) continue;
+        lmsf_status rc = commit_stage_kind(t, kind, t->ks[kind]);
         if (rc) return rc;
     }
     t->pending = true;
     return LMSF_OK;
 }
 
+// Wait until the workers have enqueued the posted rebuild (no GPU wait); their status.
+lmsf_status join_worker(lmsf_tracker* t) {
+    if (!t->staging) return LMSF_OK;
+    std::unique_lock<std::mutex> lk(t->mu);
+    t->cv.wait(lk, [t] { return !t->job[0] && !t->job[1]; });
+    t->staging = false;
+    return t->job_rc[0] ? t->job_rc[0] : t->job_rc[1];
+}
+
+void worker_main(lmsf_tracker* t, int i, int device) {
+    hipSetDevice(device);
+    std::unique_lock<std::mutex> lk(t->mu);
+    for (;;) {
+        t->cv.wait(lk, [t, i] { return t->job[i] != 0 || t->quit; });
+        if (t->quit) return;
+        const int kind = t->job[i];
+        lk.unlock();
+        const lmsf_status rc = commit_stage_kind(t, kind, t->aux[i]);
+        lk.lock();
+        t->job_rc[i] = rc;
+        t->job[i] = 0;
+        t->cv.notify_all();
+    }
+}
+
 lmsf_status commit_finish(lmsf_tracker* t) {
+    {
+        lmsf_status rj = join_worker(t);
+        if (rj) {
+            t->pending = false;
+            return rj;
+        }
+    }
     if (!t->pending) return LMSF_OK;
     t->pending = false;
     hipStream_t s = ctx_stream(t->ctx);
@@ -316,6 +372,15 @@ lmsf_status lmsf_tracker_config_init(lmsf_tracker_config* cfg) {
 void lmsf_tracker_destroy(lmsf_tracker* t) {
     if (!t) return;
     hipSetDevice(ctx_device(t->ctx));
+    if (t->worker[0].joinable()) {   // a posted rebuild is enqueued first (commit_finish joins it)
+        join_worker(t);
+        {
+            std::lock_guard<std::mutex> lk(t->mu);
+            t->quit = true;
+        }
+        t->cv.notify_all();
+        for (auto& w : t->worker) w.join();
+    }
     // A deferred commit is completed first: its staging already rewrote the context's window grids (points,
     // box read-back), so the context must not keep searching the old sizes and offsets.  If it cannot be
     // completed, the windows are dropped (the context keeps its prior maps).
@@ -550,7 +615,21 @@ lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t) {
     if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
     lmsf_status rc = settle(t);
     if (rc) return rc;
-    return commit_stage(t);
+    // the keyframe transforms enqueued so far on the context stream, then each changed kind's rebuild enqueued
+    // by its worker on its aux stream
+    TCHK(t, hipEventRecord(t->ev_fork, ctx_stream(t->ctx)));
+    if (assign_streams(t) == 0) return LMSF_OK;
+    if (!t->worker[0].joinable())
+        for (int i = 0; i < 2; ++i) t->worker[i] = std::thread(worker_main, t, i, ctx_device(t->ctx));
+    {
+        std::lock_guard<std::mutex> lk(t->mu);
+        for (int kind : {LMSF_SURF, LMSF_EDGE})
+            if (t->ks[kind]) t->job[t->ks[kind] == t->aux[0] ? 0 : 1] = kind;
+        t->staging = true;
+    }
+    t->cv.notify_all();
+    t->pending = true;
+    return LMSF_OK;
 }
 
 lmsf_status lmsf_tracker_register(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf,

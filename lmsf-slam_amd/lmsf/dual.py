@@ -39,6 +39,10 @@ class DualLidarSystem:
     def __init__(self, ctx_primary: _lib.Context, ctx_sub: _lib.Context | None = None, extrinsic=None,
                  **tracker_kw):
         self.ctx = [ctx_primary, ctx_sub]
+        # the trackers' keyframe appends (updateLocalMap, LidarTrackerLocalMap.hpp:205-232) are made explicitly
+        # after each Solve (_track): the same keyframe at the same pose, but the window rebuild is then enqueued
+        # by the tracker's commit worker and completes beside the next extraction on the context
+        tracker_kw = dict(tracker_kw, manual_map_update=True)
         self.trackers = [_lib.Tracker(ctx_primary, **tracker_kw)]
         if extrinsic is None:
             if ctx_sub is None:
@@ -54,13 +58,21 @@ class DualLidarSystem:
         self.pose = [np.eye(4), np.eye(4)]       # pose_lidar_cur_
         self.last = {}
 
+    def _track(self, i, scan, timestamp):
+        """LidarTrackerLocalMap::Solve of LiDAR i on its device-extracted features, keyframe included."""
+        self.ctx[i].extract(scan)
+        d, r = self.trackers[i].solve_extracted(timestamp)
+        if r.update_type:
+            self.trackers[i].add_keyframe_extracted(self.trackers[i].pose())
+            self.trackers[i].commit_map()
+        return d, r
+
     def process(self, scan_primary, scan_sub, timestamp):
         """One synchronized frame; returns (primary pose, sub pose) in the tracker's local frame."""
         if self.status == 0:
             deltas = []
             for i, scan in enumerate((scan_primary, scan_sub)):
-                self.ctx[i].extract(scan)
-                d, r = self.trackers[i].solve_extracted(timestamp)
+                d, r = self._track(i, scan, timestamp)
                 self.pose[i] = iso_mul(self.pose[i], d)
                 deltas.append(d)
             if self.handeye.add_pose(deltas[0], deltas[1]):              # :268-281
@@ -71,8 +83,7 @@ class DualLidarSystem:
                     self.status = 1
             return self.pose[0], self.pose[1]
         t0 = self.trackers[0]
-        self.ctx[0].extract(scan_primary)
-        d, r = t0.solve_extracted(timestamp)                              # :296-297
+        d, r = self._track(0, scan_primary, timestamp)                    # :296-297
         primary = t0.pose()                                               # :299
         sub0 = iso_mul(primary, self.extrinsic)                                   # :301
         self.pose[0] = iso_mul(self.pose[0], d)                                   # :302
