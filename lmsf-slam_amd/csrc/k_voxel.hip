@@ -121,7 +121,7 @@ __global__ void bbox_init_kernel(int* bbox) {
 }
 
 void VoxelFilter::release() {
-    void* bufs[] = {keys, keys_sorted, idx, idx_sorted, head, seg, start, bbox, nseg, tmp};
+    void* bufs[] = {keys, keys_sorted, idx, idx_sorted, head, seg, start, bbox, nseg, tmp, sort_scratch};
     for (void* p : bufs) hipFree(p);
     *this = VoxelFilter();
 }
@@ -141,6 +141,7 @@ hipError_t VoxelFilter::reserve(size_t need) {
     VALLOC(start, (n + 1) * sizeof(int));
     VALLOC(bbox, 8 * sizeof(int));
     VALLOC(nseg, sizeof(int));
+    VALLOC(sort_scratch, radix_sort_scratch_words(n) * sizeof(uint32_t));
     size_t sort_b = 0, scan_b = 0;
     voxel_sort(nullptr, sort_b, keys, keys_sorted, idx, idx_sorted, (int)n, nullptr);
     hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, head, seg, (int)n);
@@ -161,15 +162,25 @@ hipError_t VoxelFilter::enqueue(const float4* in, int n, float leaf, float4* out
     hipLaunchKernelGGL(voxel_bbox_kernel, dim3(min(max((n + 4095) / 4096, 1), 512)), dim3(256), 0, s, in, n, inv, bbox);
     const dim3 g((n + 255) / 256), b(256);
     hipLaunchKernelGGL(voxel_key_kernel, g, b, 0, s, in, n, inv, bbox, keys, idx);
-    size_t tb = tmp_bytes;   // keys < 2^31: 31 key bits (one host round trip fewer than sizing the sort to the box)
-    if ((e = voxel_sort(tmp, tb, keys, keys_sorted, idx, idx_sorted, n, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(voxel_head_kernel, g, b, 0, s, keys_sorted, n, head);
-    tb = tmp_bytes;
+    // keys < 2^31: 31 key bits (one host round trip fewer than sizing the sort to the box)
+    const uint32_t* ks = keys_sorted;
+    const int* is = idx_sorted;
+    static const bool radix = ab_int("LMSF_VOXEL_RADIX", 1) != 0;
+    if (radix) {   // k_sort.hip: 6 enqueues, in place (r03)
+        if ((e = radix_sort_pairs(keys, idx, keys_sorted, idx_sorted, n, sort_scratch, s)) != hipSuccess) return e;
+        ks = keys;
+        is = idx;
+    } else {
+        size_t tb = tmp_bytes;
+        if ((e = voxel_sort(tmp, tb, keys, keys_sorted, idx, idx_sorted, n, s)) != hipSuccess) return e;
+    }
+    size_t tb = tmp_bytes;
+    hipLaunchKernelGGL(voxel_head_kernel, g, b, 0, s, ks, n, head);
     if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, head, seg, n, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(voxel_start_kernel, g, b, 0, s, head, seg, n, start, nseg);
     // up to one wave per ~4 points (r02: 4096 blocks, 47 vs 40 us on a C4 surf window; the voxel count is on
     // the device and idle waves exit at once)
-    hipLaunchKernelGGL(voxel_mean_kernel, dim3(min((n + 15) / 16, 16384)), b, 0, s, in, idx_sorted, start, nseg, out);
+    hipLaunchKernelGGL(voxel_mean_kernel, dim3(min((n + 15) / 16, 16384)), b, 0, s, in, is, start, nseg, out);
     return hipGetLastError();
 }
 

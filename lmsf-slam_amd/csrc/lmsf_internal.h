@@ -255,10 +255,16 @@ int align_parts(int n);
 hipError_t launch_align(const GridView& g, const float4* src, int n, const Affine34f& M, double thresh,
                         double* part_sum, unsigned int* part_cnt, double* out2, hipStream_t s);
 
+// Stable radix sort of (key < 2^31, value) pairs in place (k_sort.hip): 6 enqueues; scratch of
+// radix_sort_scratch_words(n) uint32 words; k_tmp / v_tmp hold n pairs.
+size_t radix_sort_scratch_words(size_t n);
+hipError_t radix_sort_pairs(uint32_t* keys, int* vals, uint32_t* k_tmp, int* v_tmp, int n, uint32_t* scratch,
+                            hipStream_t s);
+
 // pcl::VoxelGrid centroid downsampling on the device (k_voxel.hip); workspace grows on demand.
 // run() synchronises the stream (the output count is returned to the host).
 struct VoxelFilter {
-    uint32_t *keys = nullptr, *keys_sorted = nullptr, *head = nullptr, *seg = nullptr;
+    uint32_t *keys = nullptr, *keys_sorted = nullptr, *head = nullptr, *seg = nullptr, *sort_scratch = nullptr;
     int *idx = nullptr, *idx_sorted = nullptr, *start = nullptr, *bbox = nullptr, *nseg = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0, cap = 0;
