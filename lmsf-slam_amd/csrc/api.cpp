@@ -52,14 +52,6 @@ struct DevMap {
 constexpr size_t kMaxCells = (size_t)1 << 30;   // 4 GiB of offsets: refuse larger map extents
 constexpr int kEventPairs = 4096;
 
-// x-slices per metre of the map grids (A/B builds: LMSF_GRID_SX = 1 | 2 | 4 | 8; measured in DESIGN.md)
-int grid_slices() {
-    static const int sx = [] {
-        const int v = ab_int("LMSF_GRID_SX", 4);
-        return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 4;
-    }();
-    return sx;
-}
 
 // First-pass radius^2 of the pruned knn walk from the map's density rho = points per occupied
 // x-slice: dense maps (rho >= 8; C5's 10M-point map: 19 surf / 38 edge) get lim1 = 1 / rho m^2,
@@ -335,7 +327,7 @@ namespace {
 // once the stream has drained that, grid_finish sizes the grid and sorts the points into cells.
 // n bounds the count, n_dev (device) gives it when the producer's size is still on the device.
 // Sorted points carry w = base + original index.
-lmsf_status grid_stage(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, const int* n_dev, hipStream_t s) {
+lmsf_status grid_reserve(lmsf_ctx* c, DevMap& m, size_t n) {
     if (n > (size_t)INT32_MAX) return c->fail(LMSF_ERR_CAPACITY, "map too large (%zu points)", n);
     if (!m.d_bb) {
         HIPCHK(c, hipMalloc((void**)&m.d_bb, 16 * sizeof(int)));
@@ -351,9 +343,19 @@ lmsf_status grid_stage(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, cons
         HIPCHK(c, dalloc(&m.cell, cap));
         m.cap = cap;
     }
-    // host or device source (unified addressing): the tracker rebuilds from device-resident maps
-    HIPCHK(c, hipMemcpyAsync(m.orig, xyzi, n * sizeof(float4), hipMemcpyDefault, s));
-    HIPCHK(c, launch_map_bbox(m.orig, (int)n, n_dev, grid_slices(), m.d_bb, s));
+    return LMSF_OK;
+}
+
+// xyzi == nullptr: a producer already wrote the points into m.orig and their box + count into m.d_bb
+// (ctx_window_target), only the read-back is left.
+lmsf_status grid_stage(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, const int* n_dev, hipStream_t s) {
+    lmsf_status rc = grid_reserve(c, m, n);
+    if (rc) return rc;
+    if (xyzi) {
+        // host or device source (unified addressing): the tracker rebuilds from device-resident maps
+        HIPCHK(c, hipMemcpyAsync(m.orig, xyzi, n * sizeof(float4), hipMemcpyDefault, s));
+        HIPCHK(c, launch_map_bbox(m.orig, (int)n, n_dev, grid_slices(), m.d_bb, s));
+    }
     HIPCHK(c, hipMemcpyAsync(m.h_bb, m.d_bb, 7 * sizeof(int), hipMemcpyDeviceToHost, s));
     return LMSF_OK;
 }
@@ -1516,6 +1518,15 @@ lmsf_status lmsf_kernel_stats_get(lmsf_ctx* c, lmsf_kernel_stats* out) {
 // ---------------------------------------------------------------- internal (tracker.cpp)
 namespace lmsf {
 
+// x-slices per metre of the map grids (A/B builds: LMSF_GRID_SX = 1 | 2 | 4 | 8; measured in DESIGN.md)
+int grid_slices() {
+    static const int sx = [] {
+        const int v = ab_int("LMSF_GRID_SX", 4);
+        return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 4;
+    }();
+    return sx;
+}
+
 hipStream_t ctx_stream(lmsf_ctx* c) { return c->stream; }
 int ctx_device(const lmsf_ctx* c) { return c->cfg.device; }
 int ctx_feature_capacity(const lmsf_ctx* c) { return c->F; }
@@ -1560,6 +1571,17 @@ lmsf_status ctx_window_stage(lmsf_ctx* c, int kind, const float4* d_pts, size_t 
     if (n_max == 0) return LMSF_OK;
     return grid_stage(c, c->map[kind], reinterpret_cast<const float*>(d_pts), n_max, n_dev, s);
 }
+
+lmsf_status ctx_window_target(lmsf_ctx* c, int kind, size_t n_max, float4** orig, int** bb) {
+    DevMap& m = c->map[kind];
+    lmsf_status rc = grid_reserve(c, m, n_max);
+    if (rc) return rc;
+    *orig = reinterpret_cast<float4*>(m.orig);
+    *bb = m.d_bb;
+    return LMSF_OK;
+}
+
+const float4* ctx_window_points(const lmsf_ctx* c, int kind) { return reinterpret_cast<const float4*>(c->map[kind].orig); }
 
 lmsf_status ctx_window_finish(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s, size_t* n_out) {
     DevMap& m = c->map[kind];

@@ -1,176 +1,111 @@
-// Stable LSD radix sort of (uint32 key < 2^31, int32 value) pairs for the voxel filter (k_voxel.hip).
+// Stable LSD radix sort of (uint32 key, int32 value) pairs for the voxel filter (k_voxel.hip).
 //
 // Why: the tracker rebuilds its keyframe windows with a VoxelGrid every keyframe, and hipCUB's dispatch of a
 // ~6e5-pair sort is a merge sort of ~20 dependent launches (~70 us of host enqueue time alone, r03 probe,
-// tools/hostcost) on the tracking critical path.  Here: one histogram launch and four single-pass digit
-// launches (8-bit digits; one memset clears the counters first) -- 6 enqueues.
+// tools/hostcost) on the tracking critical path.  Here the caller's key kernel also builds the digit
+// histograms (radix.h), and each 8-bit digit is one launch; digits above the key bound are skipped on the
+// device (a surf window's keys span ~24 bits: 3 passes).
 //
-// Each pass kernel takes tiles of kTile pairs in the order the blocks start (a tile counter, so a block
-// only ever waits for tiles whose blocks are already running), ranks its pairs stably per digit (wave ballots
-// over the 8 digit bits, waves and rounds in input order), publishes its per-digit tile count, finds the
-// count of every earlier tile by decoupled look-back (aggregate / inclusive flags in the top bits, agent-scope
-// atomics: the tiles' blocks run on different XCDs), and scatters.  Equal keys keep their input order, so the
-// result equals any stable sort of the pairs.
+// A pass block takes a tile of 2048 pairs in block start order (a tile counter, so a block only ever waits
+// for tiles whose blocks are already running).  Each wave ranks its own 512 consecutive pairs (8 rounds of
+// 64: ballots over the 8 digit bits, running per-digit counts in the wave's LDS row -- no block barrier per
+// round), one barrier turns the 4 rows into per-wave prefixes and the tile's digit counts, the counts are
+// published and the counts of all earlier tiles found by decoupled look-back (radix.h: 8 predecessors per
+// read, agent-scope words, the tiles' blocks run on different XCDs), and the pairs are scattered.  Tile order
+// = wave, round, lane = input order, so equal keys keep their input order.
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
-#include <utility>
-
 #include "lmsf_internal.h"
+#include "radix.h"
 
 namespace lmsf {
 
 namespace {
 
-constexpr int kSortThreads = 256;
-constexpr int kSortRounds = 8;                         // pairs per thread
-constexpr int kSortTile = kSortThreads * kSortRounds;  // 2048 pairs per tile
-constexpr int kDigits = 256;
-constexpr int kPasses = 4;                             // 32 key bits; keys < 2^31 leave the last digit < 128
-constexpr uint32_t kFlagAgg = 1u << 30, kFlagInc = 2u << 30, kCountMask = (1u << 30) - 1u;
-constexpr unsigned kLookbackSpinLimit = 1u << 26;
-
-__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
-    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// hist[pass][digit] over all n keys (zeroed by the caller's memset).
-__global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(const uint32_t* keys, int n, uint32_t* hist) {
-    __shared__ uint32_t h[kPasses][kDigits];
-    for (int i = threadIdx.x; i < kPasses * kDigits; i += kSortThreads) (&h[0][0])[i] = 0;
-    __syncthreads();
-    for (int i = blockIdx.x * kSortThreads + threadIdx.x; i < n; i += gridDim.x * kSortThreads) {
-        const uint32_t k = keys[i];
-#pragma unroll
-        for (int p = 0; p < kPasses; ++p) atomicAdd(&h[p][(k >> (8 * p)) & 255u], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kPasses * kDigits; i += kSortThreads) {
-        const uint32_t c = (&h[0][0])[i];
-        if (c) atomicAdd(&hist[i], c);
-    }
-}
-
-__global__ __launch_bounds__(kSortThreads) void radix_pass_kernel(const uint32_t* k_in, const int* v_in, uint32_t* k_out,
-                                                                  int* v_out, int n, int shift, const uint32_t* hist,
-                                                                  uint32_t* state, uint32_t* tile_ctr) {
-    __shared__ uint32_t s_run[kDigits], s_base[kDigits], s_off[kDigits];
-    __shared__ uint32_t s_wc[kSortThreads / 64][kDigits];
+__global__ __launch_bounds__(kRadixThreads) void radix_pass_kernel(uint32_t* ka, int* va, uint32_t* kb, int* vb, const int* v0, int n,
+                                                                   int pass, const uint32_t* bound,
+                                                                   const uint32_t* hist, uint32_t* ctr,
+                                                                   unsigned long long* state, uint32_t epoch) {
+    if (pass >= radix_pass_count(*bound)) return;   // keys < 2^(8 pass): this digit is 0 for all of them
+    const uint32_t* ki = pass & 1 ? kb : ka;
+    const int* vi = pass & 1 ? vb : (pass == 0 ? v0 : va);
+    uint32_t* ko = pass & 1 ? ka : kb;
+    int* vo = pass & 1 ? va : vb;
+    const int shift = 8 * pass;
+    __shared__ uint32_t s_cnt[kRadixThreads / 64][kRadixDigits];   // per-wave running counts -> wave prefixes
+    __shared__ uint32_t s_off[kRadixDigits];
+    __shared__ uint32_t s_wave[kRadixThreads / 64];
     __shared__ int s_tile;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_tile = (int)__hip_atomic_fetch_add(tile_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // digit starts of this pass: exclusive scan of the global histogram (Hillis-Steele in LDS)
-    s_base[tid] = hist[tid];
-    s_run[tid] = 0;
-    __syncthreads();
-    for (int o = 1; o < kDigits; o <<= 1) {
-        const uint32_t v = tid >= o ? s_base[tid - o] : 0u;
-        __syncthreads();
-        s_base[tid] += v;
-        __syncthreads();
-    }
-    const uint32_t excl_base = s_base[tid] - hist[tid];
-    __syncthreads();
-    s_base[tid] = excl_base;
-    const int tile = s_tile;
-    const int base = tile * kSortTile;
-    uint32_t key[kSortRounds];
-    int val[kSortRounds];
+    if (tid == 0) s_tile = (int)__hip_atomic_fetch_add(&ctr[pass], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-    for (int r = 0; r < kSortRounds; ++r) {
-        const int i = base + r * kSortThreads + tid;
-        key[r] = i < n ? k_in[i] : 0u;
-        val[r] = i < n ? v_in[i] : 0;
+    for (int w = 0; w < kRadixThreads / 64; ++w) s_cnt[w][tid] = 0u;
+    const uint32_t h = hist[pass * kRadixDigits + tid];
+    __syncthreads();
+    const int tile = s_tile;
+    const int base = tile * kRadixTile + wave * (64 * kRadixRounds);
+    uint32_t key[kRadixRounds], rank[kRadixRounds];
+    int val[kRadixRounds];
+#pragma unroll
+    for (int r = 0; r < kRadixRounds; ++r) {
+        const int i = base + r * 64 + lane;
+        key[r] = i < n ? ki[i] : 0u;
+        val[r] = i < n ? (vi ? vi[i] : i) : 0;
     }
     const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    uint32_t rank[kSortRounds];
 #pragma unroll
-    for (int r = 0; r < kSortRounds; ++r) {
-        const int i = base + r * kSortThreads + tid;
-        const bool valid = i < n;
+    for (int r = 0; r < kRadixRounds; ++r) {
+        const bool valid = base + r * 64 + lane < n;
         const uint32_t d = (key[r] >> shift) & 255u;
-        for (int k = tid; k < (kSortThreads / 64) * kDigits; k += kSortThreads) (&s_wc[0][0])[k] = 0;
-        __syncthreads();
         unsigned long long peers = __ballot(valid);
 #pragma unroll
         for (int bit = 0; bit < 8; ++bit) {
             const unsigned long long m = __ballot(((d >> bit) & 1u) != 0u);
             peers &= ((d >> bit) & 1u) ? m : ~m;
         }
-        if (valid && (peers & lt) == 0ull) s_wc[wave][d] = (uint32_t)__popcll(peers);   // the lowest lane of its digit
-        __syncthreads();
-        uint32_t before = s_run[d];
-        for (int w = 0; w < wave; ++w) before += s_wc[w][d];
-        rank[r] = before + (uint32_t)__popcll(peers & lt);
-        __syncthreads();
-        uint32_t add = 0;
+        // every lane reads its digit's count before the group's lowest lane writes it (one wave: LDS in order)
+        const uint32_t prev = s_cnt[wave][d];
+        rank[r] = prev + (uint32_t)__popcll(peers & lt);
+        if (valid && (peers & lt) == 0ull) s_cnt[wave][d] = prev + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    // digit tid: the waves' counts -> per-wave exclusive prefixes, the tile's count
+    uint32_t cnt = 0;
 #pragma unroll
-        for (int w = 0; w < kSortThreads / 64; ++w) add += s_wc[w][tid];
-        s_run[tid] += add;
-        __syncthreads();
+    for (int w = 0; w < kRadixThreads / 64; ++w) {
+        const uint32_t c = s_cnt[w][tid];
+        s_cnt[w][tid] = cnt;
+        cnt += c;
     }
-    // publish this tile's counts, then the counts of every earlier tile per digit (decoupled look-back)
-    uint32_t* my = state + (size_t)tile * kDigits;
-    const uint32_t cnt = s_run[tid];
-    st_agent(&my[tid], kFlagAgg | cnt);
-    uint32_t excl = 0;
-    for (int p = tile - 1; p >= 0; --p) {
-        uint32_t v;
-        unsigned spins = 0;
-        while (((v = ld_agent(&state[(size_t)p * kDigits + tid])) & ~kCountMask) == 0u) {
-            if (++spins > kLookbackSpinLimit) break;   // bounded: a broken invariant shows as a wrong sort, not a hang
-            __builtin_amdgcn_s_sleep(1);
-        }
-        excl += v & kCountMask;
-        if ((v & ~kCountMask) == kFlagInc) break;
-    }
-    st_agent(&my[tid], kFlagInc | (excl + cnt));
-    s_off[tid] = s_base[tid] + excl;
+    unsigned long long* my = state + (size_t)tile * kRadixDigits + tid;
+    if (tile > 0) lb_store(my, epoch, kLbAgg, cnt);
+    else lb_store(my, epoch, kLbInc, cnt);
+    uint32_t total;
+    const uint32_t digit_base = block_exclusive_scan<kRadixThreads>(h, s_wave, &total);
+    const uint32_t before = lookback_sum(state + tid, tile, kRadixDigits, epoch);
+    if (tile > 0) lb_store(my, epoch, kLbInc, before + cnt);
+    s_off[tid] = digit_base + before;
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kSortRounds; ++r) {
-        const int i = base + r * kSortThreads + tid;
+    for (int r = 0; r < kRadixRounds; ++r) {
+        const int i = base + r * 64 + lane;
         if (i < n) {
-            const uint32_t pos = s_off[(key[r] >> shift) & 255u] + rank[r];
-            k_out[pos] = key[r];
-            v_out[pos] = val[r];
+            const uint32_t d = (key[r] >> shift) & 255u;
+            const uint32_t pos = s_off[d] + s_cnt[wave][d] + rank[r];
+            ko[pos] = key[r];
+            vo[pos] = val[r];
         }
     }
 }
 
 }  // namespace
 
-size_t radix_sort_scratch_words(size_t n) {
-    const size_t tiles = (n + kSortTile - 1) / kSortTile;
-    return (size_t)kPasses * kDigits + kPasses * 16 + (size_t)kPasses * tiles * kDigits;
-}
-
-// Sorts (keys, vals) of n pairs in place (the 4 passes ping-pong through k_tmp / v_tmp and end in keys / vals).
-// scratch: radix_sort_scratch_words(n) uint32 words.
-hipError_t radix_sort_pairs(uint32_t* keys, int* vals, uint32_t* k_tmp, int* v_tmp, int n, uint32_t* scratch,
-                            hipStream_t s) {
+hipError_t launch_radix_passes(uint32_t* ka, int* va, uint32_t* kb, int* vb, const int* v0, int n,
+                               const uint32_t* bound, const RadixScratch& rs, uint32_t epoch, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    const size_t tiles = (size_t)(n + kSortTile - 1) / kSortTile;
-    uint32_t* hist = scratch;                           // [4][256]
-    uint32_t* ctr = scratch + kPasses * kDigits;        // [4] tile counters, 64 B apart
-    uint32_t* state = ctr + kPasses * 16;               // [4][tiles][256]
-    hipError_t e = hipMemsetAsync(scratch, 0, radix_sort_scratch_words((size_t)n) * sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
-    const int hb = (int)std::min<size_t>((n + 4095) / 4096, 1024);
-    hipLaunchKernelGGL(radix_hist_kernel, dim3(hb), dim3(kSortThreads), 0, s, keys, n, hist);
-    uint32_t* ki = keys;
-    int* vi = vals;
-    uint32_t* ko = k_tmp;
-    int* vo = v_tmp;
-    for (int p = 0; p < kPasses; ++p) {
-        hipLaunchKernelGGL(radix_pass_kernel, dim3((unsigned)tiles), dim3(kSortThreads), 0, s, ki, vi, ko, vo, n, 8 * p,
-                           hist + p * kDigits, state + (size_t)p * tiles * kDigits, ctr + p * 16);
-        std::swap(ki, ko);
-        std::swap(vi, vo);
-    }
+    for (int p = 0; p < kRadixPasses; ++p)
+        hipLaunchKernelGGL(radix_pass_kernel, dim3((unsigned)rs.tiles), dim3(kRadixThreads), 0, s, ka, va, kb, vb, v0, n, p,
+                           bound, rs.hist, rs.ctr, rs.state + (size_t)p * rs.tiles * kRadixDigits, epoch);
     return hipGetLastError();
 }
 

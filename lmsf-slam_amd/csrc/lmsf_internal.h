@@ -255,23 +255,22 @@ int align_parts(int n);
 hipError_t launch_align(const GridView& g, const float4* src, int n, const Affine34f& M, double thresh,
                         double* part_sum, unsigned int* part_cnt, double* out2, hipStream_t s);
 
-// Stable radix sort of (key < 2^31, value) pairs in place (k_sort.hip): 6 enqueues; scratch of
-// radix_sort_scratch_words(n) uint32 words; k_tmp / v_tmp hold n pairs.
-size_t radix_sort_scratch_words(size_t n);
-hipError_t radix_sort_pairs(uint32_t* keys, int* vals, uint32_t* k_tmp, int* v_tmp, int n, uint32_t* scratch,
-                            hipStream_t s);
-
 // pcl::VoxelGrid centroid downsampling on the device (k_voxel.hip); workspace grows on demand.
 // run() synchronises the stream (the output count is returned to the host).
+// Sort: k_sort.hip / radix.h (8 launches per filter, no host round trip).
 struct VoxelFilter {
-    uint32_t *keys = nullptr, *keys_sorted = nullptr, *head = nullptr, *seg = nullptr, *sort_scratch = nullptr;
-    int *idx = nullptr, *idx_sorted = nullptr, *start = nullptr, *bbox = nullptr, *nseg = nullptr;
-    void* tmp = nullptr;
-    size_t tmp_bytes = 0, cap = 0;
+    uint32_t *keys = nullptr, *keys_b = nullptr, *scratch = nullptr;
+    int *idx = nullptr, *idx_b = nullptr, *start = nullptr, *part = nullptr, *nseg = nullptr;
+    uint32_t epoch = 0;   // look-back epoch of the last sort
+    size_t cap = 0;
+    static int box_blocks(int n);
     hipError_t reserve(size_t n);
     hipError_t run(const float4* in, int n, float leaf, float4* out, int* n_out, hipStream_t s);
-    // run() without the read-back: the voxel count stays on the device in *nseg (no host wait)
-    hipError_t enqueue(const float4* in, int n, float leaf, float4* out, hipStream_t s);
+    // run() without the read-back: the voxel count stays on the device in *nseg (no host wait).  map_bb
+    // (optional, device): [0..5] = the map-cell box (k_map.hip's rule, sx x-slices per m) of the INPUT
+    // points -- it bounds the centroids' box -- and [6] = the voxel count, the grid stage's read-back.
+    hipError_t enqueue(const float4* in, int n, float leaf, float4* out, hipStream_t s, int* map_bb = nullptr,
+                       int sx = 0);
     void release();
 };
 
@@ -314,6 +313,13 @@ hipError_t stream_wait(hipStream_t s);
 // drained -- finish (n_out = the window's point count)
 lmsf_status ctx_window_stage(lmsf_ctx* c, int kind, const float4* d_pts, size_t n_max, const int* n_dev, hipStream_t s);
 lmsf_status ctx_window_finish(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s, size_t* n_out);
+// The window grid's source buffer (>= n_max points) and its box + count words ([0..5] map-cell box, [6] count),
+// for a producer that fills both on the stage stream (the tracker's voxel filter); then
+// ctx_window_stage(c, kind, nullptr, n_max, nullptr, s) only reads them back.
+lmsf_status ctx_window_target(lmsf_ctx* c, int kind, size_t n_max, float4** orig, int** bb);
+// The window's points in window order (the grid's unsorted source) after a finished commit.
+const float4* ctx_window_points(const lmsf_ctx* c, int kind);
+int grid_slices();
 lmsf_status ctx_slot0_features(lmsf_ctx* c, const float4** d_feat, int64_t* ne, int64_t* ns);
 
 }  // namespace lmsf

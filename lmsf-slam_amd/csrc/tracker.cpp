@@ -124,8 +124,9 @@ struct Window {
     int head = 0, count = 0;
     float4* prior = nullptr;
     size_t prior_n = 0;
-    float4* wcat = nullptr;        // keyframes concatenated (input of the voxel filter)
-    float4* concat = nullptr;      // the downsampled window (its own device grid, behind the prior's)
+    float4* wcat = nullptr;        // keyframes concatenated, input of the voxel filter (leaf > 0)
+    float4* concat = nullptr;      // keyframes concatenated, the window itself (leaf <= 0); a filtered window
+                                   // is written straight into its grid's source (ctx_window_target)
     size_t concat_cap = 0;
     size_t window_n = 0;
     size_t total = 0;              // prior_n + window_n = GetLocalMap size
@@ -227,14 +228,19 @@ lmsf_status commit_stage_kind(lmsf_tracker* t, int kind, hipStream_t ks) {
         TCHK(t, launch_gather_slots(tab, dst + nw, ks));
         nw += (size_t)tab.start[tab.n];
     }
-    const int* n_dev = nullptr;
-    if (w.leaf > 0 && nw) {                                   // VoxelGrid of the window (count stays on the device)
-        TCHK(t, t->voxel[kind].enqueue(w.wcat, (int)nw, (float)w.leaf, w.concat, ks));
-        n_dev = t->voxel[kind].nseg;
-    }
     t->nmax[kind] = nw;
+    if (w.leaf > 0 && nw) {
+        // VoxelGrid of the window straight into the grid's source, with the grid's box and the voxel count
+        // (they stay on the device; the stage only reads them back)
+        float4* orig;
+        int* bb;
+        lmsf_status rc = ctx_window_target(t->ctx, kind, nw, &orig, &bb);
+        if (rc) return rc;
+        TCHK(t, t->voxel[kind].enqueue(w.wcat, (int)nw, (float)w.leaf, orig, ks, bb, grid_slices()));
+        return ctx_window_stage(t->ctx, kind, nullptr, nw, nullptr, ks);
+    }
     // only the window's grid is rebuilt; the prior's grid was built once (set_prior_map)
-    return ctx_window_stage(t->ctx, kind, w.concat, nw, n_dev, ks);
+    return ctx_window_stage(t->ctx, kind, w.concat, nw, nullptr, ks);
 }
 
 // The aux stream of each changed kind (surf first: the larger window and its sort); returns the count.
@@ -431,7 +437,7 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
             if (hipMalloc((void**)&p, (size_t)t->cap * sizeof(float4)) != hipSuccess) { lmsf_tracker_destroy(t); return LMSF_ERR_HIP; }
         w.concat_cap = (size_t)t->cap * cfg->window_frames;
         w.leaf = kind == LMSF_EDGE ? cfg->leaf_edge : cfg->leaf_surf;
-        if (hipMalloc((void**)&w.concat, w.concat_cap * sizeof(float4)) != hipSuccess ||
+        if ((w.leaf <= 0 && hipMalloc((void**)&w.concat, w.concat_cap * sizeof(float4)) != hipSuccess) ||
             (w.leaf > 0 && hipMalloc((void**)&w.wcat, w.concat_cap * sizeof(float4)) != hipSuccess)) {
             lmsf_tracker_destroy(t);
             return LMSF_ERR_HIP;
@@ -686,7 +692,8 @@ lmsf_status lmsf_tracker_local_map(lmsf_tracker* t, int32_t kind, float* out, si
     hipStream_t s = ctx_stream(t->ctx);
     if (w.prior_n) TCHK(t, hipMemcpyAsync(out, w.prior, w.prior_n * sizeof(float4), hipMemcpyDefault, s));
     if (w.window_n)
-        TCHK(t, hipMemcpyAsync(out + 4 * w.prior_n, w.concat, w.window_n * sizeof(float4), hipMemcpyDefault, s));
+        TCHK(t, hipMemcpyAsync(out + 4 * w.prior_n, ctx_window_points(t->ctx, kind), w.window_n * sizeof(float4),
+                               hipMemcpyDefault, s));
     TCHK(t, hipStreamSynchronize(s));
     return LMSF_OK;
 }
