@@ -6,12 +6,12 @@
 // histograms (radix.h), and each 8-bit digit is one launch; digits above the key bound are skipped on the
 // device (a surf window's keys span ~24 bits: 3 passes).
 //
-// A pass block takes a tile of 2048 pairs in block start order (a tile counter, so a block only ever waits
+// A pass block (1024 threads) takes a tile of 8192 pairs in block start order (a tile counter, so a block only ever waits
 // for tiles whose blocks are already running).  Each wave ranks its own 512 consecutive pairs (8 rounds of
 // 64: ballots over the 8 digit bits, running per-digit counts in the wave's LDS row -- no block barrier per
-// round), one barrier turns the 4 rows into per-wave prefixes and the tile's digit counts, the counts are
-// published and the counts of all earlier tiles found by decoupled look-back (radix.h: 8 predecessors per
-// read, agent-scope words, the tiles' blocks run on different XCDs), and the pairs are scattered.  Tile order
+// round), one barrier turns the 16 rows into per-wave prefixes and the tile's digit counts, the counts are
+// published and the counts of all earlier tiles found by decoupled look-back (block_lookback: 32 predecessors
+// per round trip, agent-scope words, the tiles' blocks run on different XCDs), and the pairs are scattered.  Tile order
 // = wave, round, lane = input order, so equal keys keep their input order.
 #include <hip/hip_runtime.h>
 
@@ -21,6 +21,76 @@
 namespace lmsf {
 
 namespace {
+
+constexpr int kLbParts = kRadixThreads / kRadixDigits;   // threads per digit in the look-back (4)
+constexpr int kLbWin = 8;                                 // tiles each of them reads per round trip (16: spills)
+
+// Decoupled look-back of the 256 digit counts by the whole block: per round trip, digit d's kLbParts threads
+// read kLbWin consecutive predecessor tiles each (32 tiles per round trip, nearest first), and the digit's
+// part-0 thread combines the parts in order -- summing up to the first inclusive word, or up to the first
+// unpublished one, where the next round resumes.  Returns, to the part-0 thread of each digit, the count of
+// the digit in all earlier tiles.
+__device__ __forceinline__ uint32_t block_lookback(const unsigned long long* state, int tile, uint32_t epoch) {
+    __shared__ uint32_t s_sum[kLbParts][kRadixDigits];
+    __shared__ int s_stat[kLbParts][kRadixDigits];
+    __shared__ int s_next[kRadixDigits];
+    const int d = threadIdx.x & (kRadixDigits - 1), part = threadIdx.x / kRadixDigits;
+    if (part == 0) s_next[d] = tile - 1;
+    __syncthreads();
+    uint32_t before = 0;
+    unsigned spins = 0;
+    for (;;) {
+        const int pd = s_next[d];   // -1: this digit is done
+        uint32_t sum = 0;
+        int stat = -1;              // -1: all kLbWin ready aggregates; -2: reached an inclusive word or tile 0;
+                                    // >= 0: the first unpublished tile
+        if (pd >= 0) {
+            const int hi = pd - kLbWin * part;
+            unsigned long long v[kLbWin];
+#pragma unroll
+            for (int j = 0; j < kLbWin; ++j) v[j] = hi - j >= 0 ? lb_load(state + (size_t)(hi - j) * kRadixDigits + d) : 0ull;
+#pragma unroll
+            for (int j = 0; j < kLbWin; ++j) {
+                if (stat != -1) continue;
+                if (hi - j < 0) {
+                    stat = -2;
+                    continue;
+                }
+                const uint32_t lo = (uint32_t)v[j], flag = lo & ~kLbCount;
+                if ((uint32_t)(v[j] >> 32) != epoch || flag == 0u) {
+                    stat = hi - j;
+                    continue;
+                }
+                sum += lo & kLbCount;
+                if (flag == kLbInc) stat = -2;
+            }
+        }
+        s_sum[part][d] = sum;
+        s_stat[part][d] = stat;
+        __syncthreads();
+        bool progress = true;
+        if (part == 0 && pd >= 0) {
+            int next = pd - kLbWin * kLbParts;
+            for (int q = 0; q < kLbParts; ++q) {
+                before += s_sum[q][d];
+                const int sq = s_stat[q][d];
+                if (sq == -1) continue;
+                next = sq == -2 ? -1 : sq;
+                progress = sq != pd;
+                break;
+            }
+            if (next < -1) next = -1;
+            s_next[d] = next;
+        }
+        const int pending = __syncthreads_or(part == 0 && s_next[d] >= 0);
+        if (!pending) break;
+        if (__syncthreads_or(!progress)) {   // an unpublished nearest tile: wait a little
+            if (++spins > kLbSpinLimit) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return before;
+}
 
 __global__ __launch_bounds__(kRadixThreads) void radix_pass_kernel(uint32_t* ka, int* va, uint32_t* kb, int* vb, const int* v0, int n,
                                                                    int pass, const uint32_t* bound,
@@ -39,8 +109,8 @@ __global__ __launch_bounds__(kRadixThreads) void radix_pass_kernel(uint32_t* ka,
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0) s_tile = (int)__hip_atomic_fetch_add(&ctr[pass], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-    for (int w = 0; w < kRadixThreads / 64; ++w) s_cnt[w][tid] = 0u;
-    const uint32_t h = hist[pass * kRadixDigits + tid];
+    for (int k = tid; k < (kRadixThreads / 64) * kRadixDigits; k += kRadixThreads) (&s_cnt[0][0])[k] = 0u;
+    const uint32_t h = tid < kRadixDigits ? hist[pass * kRadixDigits + tid] : 0u;
     __syncthreads();
     const int tile = s_tile;
     const int base = tile * kRadixTile + wave * (64 * kRadixRounds);
@@ -71,20 +141,24 @@ __global__ __launch_bounds__(kRadixThreads) void radix_pass_kernel(uint32_t* ka,
     __syncthreads();
     // digit tid: the waves' counts -> per-wave exclusive prefixes, the tile's count
     uint32_t cnt = 0;
-#pragma unroll
-    for (int w = 0; w < kRadixThreads / 64; ++w) {
-        const uint32_t c = s_cnt[w][tid];
-        s_cnt[w][tid] = cnt;
-        cnt += c;
-    }
     unsigned long long* my = state + (size_t)tile * kRadixDigits + tid;
-    if (tile > 0) lb_store(my, epoch, kLbAgg, cnt);
-    else lb_store(my, epoch, kLbInc, cnt);
+    if (tid < kRadixDigits) {
+#pragma unroll
+        for (int w = 0; w < kRadixThreads / 64; ++w) {
+            const uint32_t c = s_cnt[w][tid];
+            s_cnt[w][tid] = cnt;
+            cnt += c;
+        }
+        if (tile > 0) lb_store(my, epoch, kLbAgg, cnt);
+        else lb_store(my, epoch, kLbInc, cnt);
+    }
     uint32_t total;
     const uint32_t digit_base = block_exclusive_scan<kRadixThreads>(h, s_wave, &total);
-    const uint32_t before = lookback_sum(state + tid, tile, kRadixDigits, epoch);
-    if (tile > 0) lb_store(my, epoch, kLbInc, before + cnt);
-    s_off[tid] = digit_base + before;
+    const uint32_t before = block_lookback(state, tile, epoch);
+    if (tid < kRadixDigits) {
+        if (tile > 0) lb_store(my, epoch, kLbInc, before + cnt);
+        s_off[tid] = digit_base + before;
+    }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kRadixRounds; ++r) {

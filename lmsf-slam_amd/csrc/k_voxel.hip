@@ -30,7 +30,7 @@ namespace lmsf {
 // look-back resets on a ~6e5-point surf window) were replaced by k_sort.hip (r03).
 //
 // Launches per filter: box partials, keys + digit histograms, the digit passes (radix.h: only those the key
-// bound needs run), segment starts (one single-pass scan), centroids -- 8 (was ~20).  No atomics on shared
+// bound needs run), segments + centroids in one single pass -- 7 (was ~20).  No atomics on shared
 // words for the box: each box block writes its partial, and every key block reduces the (L2-resident) partials.
 
 constexpr int kVoxBatch = 8;   // points in flight per thread (independent loads: one memory latency per batch)
@@ -178,95 +178,156 @@ __global__ void __launch_bounds__(256) voxel_key_kernel(const float4* pts, int n
     radix_hist_commit(s_h, hist, passes);
 }
 
-// start[s] = first sorted position of voxel s, *nseg = the voxel count (also map_bb[6] for the tracker's
-// grid read-back), start[*nseg] = n: head flags (key differs from its predecessor) scanned in one pass --
-// 8 consecutive keys per thread, a block scan, the tile offset by look-back (radix.h) over a tile counter.
-__global__ void __launch_bounds__(256) voxel_segments_kernel(const uint32_t* ka, const uint32_t* kb, int n,
-                                                             const uint32_t* bound, uint32_t* ctr,
-                                                             unsigned long long* st, uint32_t epoch, int* start,
-                                                             int* nseg, int* map_bb) {
-    __shared__ int s_tile;
-    __shared__ uint32_t s_wave[4], s_before;
-    const uint32_t* keys = radix_pass_count(*bound) & 1 ? kb : ka;
-    if (threadIdx.x == 0) s_tile = (int)__hip_atomic_fetch_add(&ctr[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Segments and centroids in one pass over the sorted pairs (pcl::VoxelGrid's "one output point per run of
+// equal voxel indices").  A block takes a tile of kSegTile sorted positions in start order: each thread flags
+// the voxel heads (key differs from its predecessor) of 8 consecutive positions, the block scans the counts,
+// the tile's first output index comes by look-back (radix.h), and the heads are listed in LDS.  The tile's
+// points -- plus a margin past its end, where its last voxel may run on -- are gathered into LDS once,
+// coalesced.  Then each thread sums whole voxels from LDS, one voxel per thread: the sums are sequential
+// double sums in sorted (= stable input) order, as in the oracle.  A last voxel longer than the margin reads
+// its remaining points from HBM.
+// (r03: a segment scan + one wave per voxel took 19 + 42 us on a C4 surf window -- 65k mostly latency-bound
+// waves for 3e4 voxels; a wave walking its positions in order through readlane, 150-200 us: one point per
+// iteration per wave, and the CU's 16 waves contend for its scalar unit.)
+constexpr int kSegThreads = 512;
+constexpr int kSegPer = kSegTile / kSegThreads;   // 8 positions per thread
+constexpr int kSegMargin = 1024;
+constexpr int kSegStage = kSegTile + kSegMargin;  // 80 KB of points in LDS
+
+__global__ __launch_bounds__(kSegThreads) void voxel_reduce_kernel(const float4* pts, const uint32_t* ka,
+                                                                   const uint32_t* kb, const int* va, const int* vb,
+                                                                   int n, const uint32_t* bound, uint32_t* ctr,
+                                                                   unsigned long long* st, uint32_t epoch,
+                                                                   float4* out, int* nseg, int* map_bb) {
+    __shared__ float4 s_pts[kSegStage];
+    __shared__ uint16_t s_head[kSegTile];
+    __shared__ uint32_t s_wave[kSegThreads / 64];
+    __shared__ int s_tile, s_end;
+    __shared__ uint32_t s_before;
+    const bool odd = radix_pass_count(*bound) & 1;
+    const uint32_t* keys = odd ? kb : ka;
+    const int* idx = odd ? vb : va;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        s_tile = (int)__hip_atomic_fetch_add(&ctr[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_end = INT_MAX;
+    }
     __syncthreads();
     const int tile = s_tile;
-    const int i0 = tile * kRadixTile + threadIdx.x * 8;
-    uint32_t k[8];
-    if (i0 + 8 <= n) {
-        const uint4 a = *reinterpret_cast<const uint4*>(keys + i0), b = *reinterpret_cast<const uint4*>(keys + i0 + 4);
+    const int tbase = tile * kSegTile;
+    const int staged = min(kSegStage, n - tbase);   // positions [tbase, tbase + staged) land in LDS
+    // the stage: indices, then points (all loads of a thread in flight together)
+    int ix[kSegStage / kSegThreads];
+#pragma unroll
+    for (int q = 0; q < kSegStage / kSegThreads; ++q) {
+        const int i = q * kSegThreads + tid;
+        ix[q] = i < staged ? idx[tbase + i] : 0;
+    }
+    // head flags of 8 consecutive positions
+    const int p0 = tbase + tid * kSegPer;
+    uint32_t k[kSegPer];
+    if (p0 + kSegPer <= n) {
+        const uint4 a = *reinterpret_cast<const uint4*>(keys + p0), b = *reinterpret_cast<const uint4*>(keys + p0 + 4);
         k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w; k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
     } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) k[j] = i0 + j < n ? keys[i0 + j] : 0u;
+        for (int j = 0; j < kSegPer; ++j) k[j] = p0 + j < n ? keys[p0 + j] : 0u;
     }
-    uint32_t prev = i0 > 0 && i0 < n ? keys[i0 - 1] : 0u;
+    uint32_t prev = p0 > 0 && p0 < n ? keys[p0 - 1] : 0u;
+    // the first head past the tile, within the margin (the end of the tile's last voxel)
+    uint32_t mk[kSegMargin / kSegThreads], mp[kSegMargin / kSegThreads];
+#pragma unroll
+    for (int q = 0; q < kSegMargin / kSegThreads; ++q) {
+        const int i = tbase + kSegTile + q * kSegThreads + tid;
+        mk[q] = i < n ? keys[i] : 0u;
+        mp[q] = i < n ? keys[i - 1] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < kSegStage / kSegThreads; ++q) {
+        const int i = q * kSegThreads + tid;
+        if (i < staged) s_pts[i] = pts[ix[q]];
+    }
     uint32_t flags = 0, c = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int i = i0 + j;
+    for (int j = 0; j < kSegPer; ++j) {
+        const int i = p0 + j;
         const bool h = i < n && (i == 0 || k[j] != prev);
         prev = k[j];
         flags |= (uint32_t)h << j;
         c += h;
     }
+#pragma unroll
+    for (int q = 0; q < kSegMargin / kSegThreads; ++q) {
+        const int i = tbase + kSegTile + q * kSegThreads + tid;
+        if (i < n && mk[q] != mp[q]) atomicMin(&s_end, i - tbase);
+    }
     uint32_t total;
-    const uint32_t excl = block_exclusive_scan<256>(c, s_wave, &total);
-    if (threadIdx.x == 0) {
+    const uint32_t excl = block_exclusive_scan<kSegThreads>(c, s_wave, &total);
+    uint32_t r = excl;
+#pragma unroll
+    for (int j = 0; j < kSegPer; ++j)
+        if ((flags >> j) & 1u) s_head[r++] = (uint16_t)(p0 + j - tbase);
+    if (tid == 0) {
+        uint32_t before = 0;
         if (tile == 0) {
             lb_store(st, epoch, kLbInc, total);
-            s_before = 0;
         } else {
             lb_store(st + tile, epoch, kLbAgg, total);
-            const uint32_t before = lookback_sum(st, tile, 1, epoch);
+            before = lookback_sum<32>(st, tile, 1, epoch);
             lb_store(st + tile, epoch, kLbInc, before + total);
-            s_before = before;
         }
+        s_before = before;
+        if (tbase + kSegTile >= n) {   // the last tile: the voxel count
+            *nseg = (int)(before + total);
+            if (map_bb) map_bb[6] = (int)(before + total);
+        }
+        if (s_end == INT_MAX && tbase + kSegStage >= n) s_end = n - tbase;   // runs to the end of the cloud
     }
     __syncthreads();
-    uint32_t seg = s_before + excl;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        if ((flags >> j) & 1u) start[seg++] = i0 + j;
-    if (i0 <= n - 1 && n - 1 < i0 + 8) {   // the thread of the last point
-        *nseg = (int)seg;
-        start[seg] = n;
-        if (map_bb) map_bb[6] = (int)seg;
-    }
-}
-
-// One wave per voxel (grid-stride over the voxels): the wave gathers 64 of the voxel's points at a
-// time and every lane adds them in sorted (= input) order through readlane, so the sums are the
-// sequential double sums of the thread-per-voxel form while the gathers run 64 wide.  (One lane per
-// voxel measured 164 us vs 40 us on a C4 surf window: voxels near the sensor hold hundreds of points
-// and a wave waits for its fullest voxel.)
-__global__ __launch_bounds__(256) void voxel_mean_kernel(const float4* pts, const int* va, const int* vb,
-                                                         const uint32_t* bound, const int* start, const int* nseg,
-                                                         float4* out) {
-    const int* idx_sorted = radix_pass_count(*bound) & 1 ? vb : va;
-    const int lane = threadIdx.x & 63;
-    const int nw = (gridDim.x * blockDim.x) >> 6;
-    const int ns = *nseg;
-    for (int s = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; s < ns; s += nw) {
-        const int a = start[s], b = start[s + 1];
+    const uint32_t before = s_before;
+    const int tend = s_end;   // INT_MAX: the last voxel runs past the margin
+    for (uint32_t v = tid; v < total; v += kSegThreads) {
+        const int a = s_head[v];
+        const int b = v + 1 < total ? (int)s_head[v + 1] : tend;
         double sx = 0, sy = 0, sz = 0, sw = 0;
-        for (int c = a; c < b; c += 64) {
-            const int m = min(64, b - c);
-            const float4 p = lane < m ? pts[idx_sorted[c + lane]] : make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int j = 0; j < m; ++j) {
-                sx += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.x), j));
-                sy += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.y), j));
-                sz += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.z), j));
-                sw += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.w), j));
+        int i = a;
+        const int lim = min(b, staged);
+        for (; i + 4 <= lim; i += 4) {   // 4 LDS reads in flight, added in order
+            float4 q[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) q[u] = s_pts[i + u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                sx += (double)q[u].x;
+                sy += (double)q[u].y;
+                sz += (double)q[u].z;
+                sw += (double)q[u].w;
             }
         }
-        const double cnt = (double)(b - a);
-        if (lane == 0) out[s] = make_float4((float)(sx / cnt), (float)(sy / cnt), (float)(sz / cnt), (float)(sw / cnt));
+        for (; i < lim; ++i) {
+            const float4 q = s_pts[i];
+            sx += (double)q.x;
+            sy += (double)q.y;
+            sz += (double)q.z;
+            sw += (double)q.w;
+        }
+        if (b == INT_MAX) {   // past the margin: from HBM until the key changes
+            const uint32_t key = keys[tbase + a];
+            for (; tbase + i < n && keys[tbase + i] == key; ++i) {
+                const float4 q = pts[idx[tbase + i]];
+                sx += (double)q.x;
+                sy += (double)q.y;
+                sz += (double)q.z;
+                sw += (double)q.w;
+            }
+        }
+        const double dc = (double)(i - a);
+        out[before + v] = make_float4((float)(sx / dc), (float)(sy / dc), (float)(sz / dc), (float)(sw / dc));
     }
 }
 
 void VoxelFilter::release() {
-    void* bufs[] = {keys, keys_b, idx, idx_b, start, part, nseg, scratch};
+    void* bufs[] = {keys, keys_b, idx, idx_b, part, nseg, scratch};
     for (void* p : bufs) hipFree(p);
     *this = VoxelFilter();
 }
@@ -283,7 +344,6 @@ hipError_t VoxelFilter::reserve(size_t need) {
     VALLOC(keys_b, n * sizeof(uint32_t));
     VALLOC(idx, n * sizeof(int));
     VALLOC(idx_b, n * sizeof(int));
-    VALLOC(start, (n + 1) * sizeof(int));
     VALLOC(part, (size_t)box_blocks((int)n) * 12 * sizeof(int) + 16 * sizeof(int));
     VALLOC(nseg, sizeof(int));
     VALLOC(scratch, radix_scratch_words(n) * sizeof(uint32_t));
@@ -309,12 +369,8 @@ hipError_t VoxelFilter::enqueue(const float4* in, int n, float leaf, float4* out
     hipLaunchKernelGGL(voxel_key_kernel, dim3(kb), dim3(256), 0, s, in, n, inv, part, nb, keys, bound, rs.hist, map_bb);
     // pass 0 takes the point index as its value
     if ((e = launch_radix_passes(keys, idx, keys_b, idx_b, nullptr, n, bound, rs, epoch, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(voxel_segments_kernel, dim3((unsigned)rs.tiles), dim3(256), 0, s, keys, keys_b, n, bound, rs.ctr,
-                       rs.seg_state, epoch, start, nseg, map_bb);
-    // up to one wave per ~4 points (r02: 4096 blocks, 47 vs 40 us on a C4 surf window; the voxel count is on
-    // the device and idle waves exit at once)
-    hipLaunchKernelGGL(voxel_mean_kernel, dim3(min((n + 15) / 16, 16384)), dim3(256), 0, s, in, idx, idx_b, bound,
-                       start, nseg, out);
+    hipLaunchKernelGGL(voxel_reduce_kernel, dim3((unsigned)seg_tiles((size_t)n)), dim3(kSegThreads), 0, s, in, keys,
+                       keys_b, idx, idx_b, n, bound, rs.ctr, rs.seg_state, epoch, out, nseg, map_bb);
     return hipGetLastError();
 }
 

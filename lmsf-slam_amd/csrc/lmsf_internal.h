@@ -257,10 +257,10 @@ hipError_t launch_align(const GridView& g, const float4* src, int n, const Affin
 
 // pcl::VoxelGrid centroid downsampling on the device (k_voxel.hip); workspace grows on demand.
 // run() synchronises the stream (the output count is returned to the host).
-// Sort: k_sort.hip / radix.h (8 launches per filter, no host round trip).
+// Sort: k_sort.hip / radix.h (7 launches per filter, no host round trip).
 struct VoxelFilter {
     uint32_t *keys = nullptr, *keys_b = nullptr, *scratch = nullptr;
-    int *idx = nullptr, *idx_b = nullptr, *start = nullptr, *part = nullptr, *nseg = nullptr;
+    int *idx = nullptr, *idx_b = nullptr, *part = nullptr, *nseg = nullptr;
     uint32_t epoch = 0;   // look-back epoch of the last sort
     size_t cap = 0;
     static int box_blocks(int n);

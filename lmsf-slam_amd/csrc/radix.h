@@ -11,16 +11,17 @@
 
 namespace lmsf {
 
-constexpr int kRadixThreads = 256;
+constexpr int kRadixThreads = 1024;                      // 16 waves; digit d's counts and look-back: thread d
 constexpr int kRadixRounds = 8;                          // pairs per thread (per wave: 8 rounds of 64)
-constexpr int kRadixTile = kRadixThreads * kRadixRounds;  // 2048 pairs per tile
+constexpr int kRadixTile = kRadixThreads * kRadixRounds;  // 8192 pairs per tile (r03: 2048-pair tiles spent
+                                                          // ~20 us per pass in look-back round trips on 6e5 pairs)
 constexpr int kRadixDigits = 256;
 constexpr int kRadixPasses = 4;                           // 8-bit digits of keys < 2^32
 constexpr uint32_t kLbAgg = 1u << 30, kLbInc = 2u << 30, kLbCount = (1u << 30) - 1u;
 constexpr unsigned kLbSpinLimit = 1u << 24;               // bounded waits: a broken invariant is a wrong result
 
 // Scratch of a sort over up to n pairs (uint32 words): hist[4][256] | ctr[16] | state[4][tiles][256] (u64) |
-// seg_state[tiles] (u64, the voxel segment scan).
+// seg_state[seg tiles] (u64, the voxel segment pass: tiles of kSegTile positions).
 struct RadixScratch {
     uint32_t* hist;
     uint32_t* ctr;                      // [0..3] tile counters of the passes, [4] of the segment scan
@@ -29,11 +30,14 @@ struct RadixScratch {
     int tiles;
 };
 
+constexpr int kSegTile = 4096;
+
 inline int radix_tiles(size_t n) { return (int)((n + kRadixTile - 1) / kRadixTile); }
+inline int seg_tiles(size_t n) { return (int)((n + kSegTile - 1) / kSegTile); }
 
 inline size_t radix_scratch_words(size_t n) {
     const size_t t = (size_t)radix_tiles(n);
-    return (size_t)kRadixPasses * kRadixDigits + 16 + 2 * ((size_t)kRadixPasses * t * kRadixDigits + t);
+    return (size_t)kRadixPasses * kRadixDigits + 16 + 2 * ((size_t)kRadixPasses * t * kRadixDigits + seg_tiles(n));
 }
 
 inline RadixScratch radix_scratch(uint32_t* base, size_t n) {
@@ -60,12 +64,13 @@ __device__ __forceinline__ void lb_store(unsigned long long* p, uint32_t epoch, 
     __hip_atomic_store(p, ((unsigned long long)epoch << 32) | flag | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Sum of the counts of tiles [0, tile) from their look-back words st[p * stride]: 8 predecessors are read at
-// once (independent loads in flight), summed nearest first until an inclusive word; an unpublished word
-// restarts the window there.  The tiles come from a start-order counter, so every waited-on tile's block runs.
+// Sum of the counts of tiles [0, tile) from their look-back words st[p * stride]: W predecessors are read at
+// once (independent loads in flight: one round trip covers W tiles), summed nearest first until an inclusive
+// word; an unpublished word restarts the window there.  The tiles come from a start-order counter, so every
+// waited-on tile's block runs.
+template <int W>
 __device__ __forceinline__ uint32_t lookback_sum(const unsigned long long* st, int tile, size_t stride,
                                                  uint32_t epoch) {
-    constexpr int W = 8;
     uint32_t sum = 0;
     int p = tile - 1;
     unsigned spins = 0;

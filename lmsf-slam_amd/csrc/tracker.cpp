@@ -161,6 +161,7 @@ struct lmsf_tracker {
     int job[2] = {0, 0};          // kind to stage on aux[i] (0: none)
     bool quit = false, staging = false;
     lmsf_status job_rc[2] = {LMSF_OK, LMSF_OK};
+    size_t fin_n[3] = {0, 0, 0};  // per kind: the window size a worker's grid finish found
 };
 
 namespace {
@@ -275,6 +276,19 @@ lmsf_status join_worker(lmsf_tracker* t) {
     return t->job_rc[0] ? t->job_rc[0] : t->job_rc[1];
 }
 
+// One kind's half of commit_finish on its stage stream: wait for the stage's read-back, enqueue the grid
+// build, mark its end for the context stream.
+lmsf_status finish_kind(lmsf_tracker* t, int kind, hipStream_t ks) {
+    TCHK(t, stream_wait(ks));
+    lmsf_status rc = ctx_window_finish(t->ctx, kind, t->nmax[kind], ks, &t->fin_n[kind]);
+    if (rc) return rc;
+    TCHK(t, hipEventRecord(t->ev_join[kind], ks));
+    return LMSF_OK;
+}
+
+// Worker i: stage, then finish, of the kind posted for aux[i].  Both halves run here, so the two kinds' host
+// waits and grid builds proceed side by side (r03 trace: one thread finishing both put the edge grid's
+// ~5 launches behind the surf grid's) and the caller's thread only joins.
 void worker_main(lmsf_tracker* t, int i, int device) {
     hipSetDevice(device);
     std::unique_lock<std::mutex> lk(t->mu);
@@ -283,7 +297,8 @@ void worker_main(lmsf_tracker* t, int i, int device) {
         if (t->quit) return;
         const int kind = t->job[i];
         lk.unlock();
-        const lmsf_status rc = commit_stage_kind(t, kind, t->aux[i]);
+        lmsf_status rc = commit_stage_kind(t, kind, t->aux[i]);
+        if (!rc) rc = finish_kind(t, kind, t->aux[i]);
         lk.lock();
         t->job_rc[i] = rc;
         t->job[i] = 0;
@@ -292,16 +307,23 @@ void worker_main(lmsf_tracker* t, int i, int device) {
 }
 
 lmsf_status commit_finish(lmsf_tracker* t) {
-    {
+    hipStream_t s = ctx_stream(t->ctx);
+    if (t->staging) {   // the workers staged and finished: apply the sizes, join their streams
         lmsf_status rj = join_worker(t);
-        if (rj) {
-            t->pending = false;
-            return rj;
+        t->pending = false;
+        if (rj) return rj;
+        for (int kind : {LMSF_SURF, LMSF_EDGE}) {
+            if (!t->ks[kind]) continue;
+            Window& w = t->win[kind];
+            w.window_n = t->fin_n[kind];
+            w.total = w.prior_n + w.window_n;
+            w.dirty = false;
+            TCHK(t, hipStreamWaitEvent(s, t->ev_join[kind], 0));
         }
+        return LMSF_OK;
     }
     if (!t->pending) return LMSF_OK;
     t->pending = false;
-    hipStream_t s = ctx_stream(t->ctx);
     for (int kind : {LMSF_SURF, LMSF_EDGE})
         if (t->ks[kind]) TCHK(t, stream_wait(t->ks[kind]));
     for (int kind : {LMSF_SURF, LMSF_EDGE}) {
@@ -378,8 +400,12 @@ lmsf_status lmsf_tracker_config_init(lmsf_tracker_config* cfg) {
 void lmsf_tracker_destroy(lmsf_tracker* t) {
     if (!t) return;
     hipSetDevice(ctx_device(t->ctx));
-    if (t->worker[0].joinable()) {   // a posted rebuild is enqueued first (commit_finish joins it)
-        join_worker(t);
+    // A deferred commit is completed first (a posted one joined from the workers): its staging already rewrote
+    // the context's window grids (points, box read-back), so the context must not keep searching the old sizes
+    // and offsets.  If it cannot be completed, the windows are dropped (the context keeps its prior maps).
+    if (commit_finish(t) != LMSF_OK)
+        for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) ctx_set_window_device(t->ctx, kind, nullptr, 0);
+    if (t->worker[0].joinable()) {
         {
             std::lock_guard<std::mutex> lk(t->mu);
             t->quit = true;
@@ -387,11 +413,6 @@ void lmsf_tracker_destroy(lmsf_tracker* t) {
         t->cv.notify_all();
         for (auto& w : t->worker) w.join();
     }
-    // A deferred commit is completed first: its staging already rewrote the context's window grids (points,
-    // box read-back), so the context must not keep searching the old sizes and offsets.  If it cannot be
-    // completed, the windows are dropped (the context keeps its prior maps).
-    if (commit_finish(t) != LMSF_OK)
-        for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) ctx_set_window_device(t->ctx, kind, nullptr, 0);
     ctx_remove_settle(t->ctx, t);
     hipStreamSynchronize(ctx_stream(t->ctx));
     for (auto& w : t->win) {

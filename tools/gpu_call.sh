@@ -1,14 +1,14 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "voxel or tracker or keyframe or dual or local_map" > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "voxel or tracker or keyframe or dual or local_map or common" > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "tests_rc=$rc"; tail -2 gpurun_out/gpu_tests.log; case $rc in 0) ;; *) exit $rc;; esac
-for r in 1 2 3; do
+for r in ${ROUNDS:-1 2}; do
   for cfg in C4 C3; do
-    for v in prev ab; do
+    for v in ${VARIANTS:-prev ab2}; do
       LMSF_LIB=$PWD/lmsf-slam_amd/ab/liblmsf_$v.so LMSF_BENCH_PHASES=1 timeout -k 10 300 python bench.py --config $cfg --no-cpu > gpurun_out/w_${cfg}_${v}_r$r.json 2> gpurun_out/w_${cfg}_${v}_r$r.err
       rc=$?; echo "$cfg $v r$r rc=$rc $(python3 -c "import json; d=json.loads([l for l in open('gpurun_out/w_${cfg}_${v}_r$r.json') if l.startswith('{')][-1]); print(d['value'], d['ms_per_step'])" 2>/dev/null) $(grep phases gpurun_out/w_${cfg}_${v}_r$r.err)"
       case $rc in 0) ;; *) exit $rc;; esac
     done
   done
 done
-cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/r03/trace_C4b" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --config C4 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/r03/trace_C4b.json" 2>&1; echo "trace rc=$?"
+mkdir -p gpurun_out/r03 && cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/r03/trace_C4" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --config C4 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/r03/trace_C4.json" 2>&1; echo "trace rc=$?"
