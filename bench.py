@@ -76,6 +76,9 @@ def parse(argv=None):
     ap.add_argument("--pairs", type=int, default=1000, help="C5: scan pairs in the whole job")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="C3/C4: extract each scan only when its step starts (default: the next scan's extraction "
+                         "runs beside the current registration, lmsf_prefetch_features)")
     ap.add_argument("--no-n27", action="store_true",
                     help="skip the untimed n27-counting step (PMC passes: every dispatch then runs as timed)")
     ap.add_argument("--traffic-json", default=None,
@@ -666,6 +669,8 @@ def run_streams(args, d):
         i = state["i"]
         t = time.perf_counter()
         ctx.extract(scans_dev[i])
+        if not args.no_prefetch and i + 1 < n:
+            ctx.prefetch(scans_dev[i + 1])   # the preprocess thread running one scan ahead
         t = mark("extract", t)
         _, r = tr.solve_extracted(0.1 * i)
         t = mark("solve", t)
@@ -733,7 +738,7 @@ def run_streams(args, d):
              f"C4: one VLP-16 16x{args.cols} stream per GPU (8 m/s, 10 Hz) tracked against a {map_points}-pt "
              f"shared map + stitched keyframe window (10 keyframes, voxel 0.2/0.4 m), {args.outer} outer iters",
              {"streams": world, "map_points": map_points, "outer_iterations": args.outer,
-              "parallelism": f"stream-per-GPU x{world}"}, roof, cpu,
+              "parallelism": f"stream-per-GPU x{world}", "extract_ahead": not args.no_prefetch}, roof, cpu,
              tracking_error_m={"rank0_max": max(state["err"]), "rank0_last": state["err"][-1]},
              keyframes_appended=state["kf"])
     tr.close()
@@ -768,7 +773,8 @@ def run_dual(args, d):
 
     def step():
         i = state["i"]
-        out = system.process(prim_dev[i], sub_dev[i], 0.1 * i)
+        nxt = (prim_dev[i + 1], sub_dev[i + 1]) if not args.no_prefetch and i + 1 < len(prim_dev) else None
+        out = system.process(prim_dev[i], sub_dev[i], 0.1 * i, next_frame=nxt)
         state["i"] += 1
         return out
 
@@ -808,7 +814,8 @@ def run_dual(args, d):
              world * args.steps / elapsed, "frames/s", elapsed, "weak",
              f"C3: two VLP-16 16x{args.cols} LiDARs (~{npts} pts each) at the PS-Calib extrinsic, primary "
              f"tracking (reference decay schedule) + sub-LiDAR refine against the voxelised 10-keyframe local map",
-             {"systems": world, "parallelism": f"system-per-GPU x{world}"}, roof, cpu,
+             {"systems": world, "parallelism": f"system-per-GPU x{world}", "extract_ahead": not args.no_prefetch},
+             roof, cpu,
              extrinsic_error={"m": ext_err[0], "rad": ext_err[1]})
     system.close()
     ctx.close()

@@ -157,6 +157,15 @@ lmsf_status lmsf_solve_trace(lmsf_ctx* ctx, double* trace, int32_t cap, int32_t*
  * stay device-resident and become the current scan target (as SetInputTarget with the
  * processor's output container) without a host round trip.  xyzi: host or device memory. */
 lmsf_status lmsf_extract_features(lmsf_ctx* ctx, const float* xyzi, size_t n, lmsf_feature_counts* counts);
+
+/* The extraction of the NEXT scan, enqueued now on a stream of the context's own so that it runs beside
+ * what the context runs meanwhile (normally the current scan's solve): the next lmsf_extract_features call
+ * with the same xyzi pointer and n adopts its result instead of extracting again (bitwise the same features:
+ * the same kernels on the same input).  The scan must stay unchanged until that call; any other extraction
+ * first waits for the prefetch and discards it.  The pipelining of the reference's preprocess and estimate
+ * threads (apps/src/MultiLidarOdometry/lidar_lidar_odometry.cpp:281-284: features of scan k+1 are extracted
+ * while scan k is registered). */
+lmsf_status lmsf_prefetch_features(lmsf_ctx* ctx, const float* xyzi, size_t n);
 /* PointCloudCommonProcess<P>(output_name = "filtered")::Process (INC/Algorithm/PointClouds/processing/
  * common_processing.hpp:87-112), the preprocessor of the "sparse_point_plane_icp" scan-to-map mode
  * (INC/factory/System/ML_SystemFactory.hpp:141-178): optional removeNaNFromPointCloud, VoxelGrid

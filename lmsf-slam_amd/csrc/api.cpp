@@ -8,8 +8,10 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "lmsf_internal.h"
@@ -37,9 +39,17 @@ struct DevMap {
     unsigned long long* h_occ = nullptr;   // pinned
     hipEvent_t ev_occ = nullptr;
     bool occ_pending = false;
-    // build scratch: d_bb = [box 0..5, count 6, -, occupied u64 at 8..9], read back into pinned h_bb
+    // build scratch: d_bb = [box 0..5, count 6, -, occupied u64 at 8..9, device-build overflow 10, its scan
+    // tile counter 16], read back into pinned h_bb
     int* d_bb = nullptr;
     int* h_bb = nullptr;
+    // device-sized build (tracker windows, grid_build_device): scan look-back words, their epoch, the event
+    // after the read-back of d_bb, and the base of the pending build
+    unsigned long long* scan_state = nullptr;
+    size_t scan_state_tiles = 0;
+    uint32_t scan_epoch = 0;
+    hipEvent_t ev_bb = nullptr;
+    bool dev_pending = false;
 
     GridView view() const {
         GridView g{};   // zeroed padding: views are compared bytewise (SolveGraph key)
@@ -159,7 +169,37 @@ struct lmsf_ctx {
     float4* featp = nullptr;          // [B][F] the features in that order (w = slot)
     int* n_pos = nullptr;
     bool qorder_valid = false;        // the slots' features came from the extraction kernels
-    int* d_error = nullptr;           // [0] extraction capacity flags, [8..10] pack3, [16] LM loop wait gave up
+    int* d_error = nullptr;           // [0] extraction capacity flags, [8..10] pack3, [16] LM loop wait gave up,
+                                      // [24] / [40..42]: the same two of a prefetched extraction
+    // lmsf_prefetch_features: the next scan extracted on pre_stream into a second set of the outputs the
+    // registration reads (swapped in by the lmsf_extract_features call of the same scan); its own scan copy,
+    // the extraction scratch shared (a prefetch runs after the extraction before it, and the next one after it)
+    struct OutSet {
+        float4* feat = nullptr;
+        int* feat_src = nullptr;
+        int* n_edge = nullptr;
+        int* n_surf = nullptr;
+        int* qslot = nullptr;
+        int* fslot = nullptr;
+        float4* featp = nullptr;
+        int* n_pos = nullptr;
+    } alt;
+    float4* pre_raw = nullptr;
+    int* pre_raw_count = nullptr;
+    int64_t* pre_raw_off = nullptr;
+    hipStream_t pre_stream = nullptr;
+    hipEvent_t ev_pre = nullptr, ev_pre_after = nullptr;
+    int* h_pre = nullptr;             // pinned [8]: [0] count in, [2..3] offset in (int64), [4..6] counts + flags out
+    const float* pre_src = nullptr;
+    size_t pre_n = 0;
+    bool pre_pending = false;
+    // the prefetch's enqueues (~12 API calls) are made by a worker thread of the context, so that the caller's
+    // next call (the Solve it overlaps) is enqueued at once instead of behind them
+    std::thread pre_worker;
+    std::mutex pre_mu;
+    std::condition_variable pre_cv;
+    bool pre_job = false, pre_quit = false;
+    lmsf_status pre_rc = LMSF_OK;
     unsigned* d_lmsync = nullptr;     // [2 B] lm_loop_kernel counters
     // streaming ingest (lmsf_batch_load_scans_async): copies on their own stream into the raw slots,
     // ordered after the extraction that last read them (ev_raw_free) and before the next (ev_raw_ready)
@@ -214,6 +254,17 @@ struct lmsf_ctx {
     unsigned int* align_part_cnt = nullptr;
     double* align_out = nullptr;
     size_t align_cap = 0;
+
+    void swap_outputs() {
+        std::swap(feat, alt.feat);
+        std::swap(feat_src, alt.feat_src);
+        std::swap(n_edge, alt.n_edge);
+        std::swap(n_surf, alt.n_surf);
+        std::swap(qslot, alt.qslot);
+        std::swap(fslot, alt.fslot);
+        std::swap(featp, alt.featp);
+        std::swap(n_pos, alt.n_pos);
+    }
 
     lmsf_status fail(lmsf_status code, const char* fmt, ...) {
         char buf[512];
@@ -330,8 +381,9 @@ namespace {
 lmsf_status grid_reserve(lmsf_ctx* c, DevMap& m, size_t n) {
     if (n > (size_t)INT32_MAX) return c->fail(LMSF_ERR_CAPACITY, "map too large (%zu points)", n);
     if (!m.d_bb) {
-        HIPCHK(c, hipMalloc((void**)&m.d_bb, 16 * sizeof(int)));
-        HIPCHK(c, hipHostMalloc((void**)&m.h_bb, 8 * sizeof(int), hipHostMallocDefault));
+        HIPCHK(c, hipMalloc((void**)&m.d_bb, 32 * sizeof(int)));
+        HIPCHK(c, hipMemset(m.d_bb, 0, 32 * sizeof(int)));
+        HIPCHK(c, hipHostMalloc((void**)&m.h_bb, 16 * sizeof(int), hipHostMallocDefault));
     }
     if (n > m.cap) {
         hipFree(m.orig); hipFree(m.pts); hipFree(m.cell);
@@ -360,6 +412,69 @@ lmsf_status grid_stage(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, cons
     return LMSF_OK;
 }
 
+// counts / offsets / fill for at least need cells (grown geometrically)
+lmsf_status grid_cells_reserve(lmsf_ctx* c, DevMap& m, size_t need, hipStream_t s) {
+    if (need <= m.cells_cap) return LMSF_OK;
+    hipFree(m.counts); hipFree(m.off); hipFree(m.fill); hipFree(m.scan_tmp);
+    m.counts = m.off = m.fill = nullptr;
+    m.scan_tmp = nullptr;
+    const size_t cap = std::min(grow_cap(need, m.cells_cap), kMaxCells + 1);
+    m.cells_cap = 0;
+    HIPCHK(c, dalloc(&m.counts, cap));
+    HIPCHK(c, dalloc(&m.off, cap));
+    HIPCHK(c, dalloc(&m.fill, cap));
+    m.scan_tmp_bytes = 0;
+    HIPCHK(c, exclusive_scan_u32(m.counts, m.off, cap, nullptr, m.scan_tmp_bytes, s));
+    HIPCHK(c, hipMalloc(&m.scan_tmp, std::max<size_t>(m.scan_tmp_bytes, 16)));
+    m.cells_cap = cap;
+    return LMSF_OK;
+}
+
+// The grid of points a producer left in m.orig with their box + count in m.d_bb, built on stream s without a
+// host wait (launch_grid_build_dev); grid_finish_device takes the box read-back and sets the view.  Cells
+// are allocated from the last build's size (first build: 2^21, ~8 MB per array): a larger box is rebuilt by
+// the host path at the finish.
+lmsf_status grid_build_device(lmsf_ctx* c, DevMap& m, size_t n_max, int base, hipStream_t s) {
+    lmsf_status rc = grid_cells_reserve(c, m, std::max<size_t>(m.cells_cap, (size_t)1 << 21), s);
+    if (rc) return rc;
+    const size_t tiles = grid_scan_tiles(m.cells_cap);
+    if (tiles > m.scan_state_tiles) {
+        hipFree(m.scan_state);
+        m.scan_state = nullptr;
+        m.scan_state_tiles = 0;
+        HIPCHK(c, hipMalloc((void**)&m.scan_state, tiles * sizeof(unsigned long long)));
+        HIPCHK(c, hipMemsetAsync(m.scan_state, 0, tiles * sizeof(unsigned long long), s));   // epoch 0: unpublished
+        m.scan_state_tiles = tiles;
+    }
+    if (!m.ev_bb) HIPCHK(c, hipEventCreateWithFlags(&m.ev_bb, hipEventDisableTiming));
+    if (++m.scan_epoch == 0) ++m.scan_epoch;
+    HIPCHK(c, launch_grid_build_dev(m.orig, (int)n_max, grid_slices(), m.d_bb, m.counts, m.off, m.fill, m.cells_cap,
+                                    m.cell, m.pts, base, m.scan_state, m.scan_epoch, m.h_bb, m.ev_bb, s));
+    m.dev_pending = true;
+    return LMSF_OK;
+}
+
+lmsf_status grid_finish(lmsf_ctx* c, DevMap& m, int base, hipStream_t s, bool density);
+
+lmsf_status grid_finish_device(lmsf_ctx* c, DevMap& m, int base, hipStream_t s) {
+    m.dev_pending = false;
+    HIPCHK(c, hipEventSynchronize(m.ev_bb));
+    const int* bb = m.h_bb;
+    if (bb[6] == 0) {
+        m.n = 0;
+        m.occ_pending = false;
+        return LMSF_OK;
+    }
+    if (bb[10]) return grid_finish(c, m, base, s, false);   // more cells than allocated: host-sized rebuild
+    m.ox = bb[0]; m.oy = bb[1]; m.oz = bb[2];
+    m.nx = bb[3] - bb[0] + 1; m.ny = bb[4] - bb[1] + 1; m.nz = bb[5] - bb[2] + 1;
+    m.sx = grid_slices();
+    m.lim1 = 1.f;
+    m.n = bb[6];
+    m.occ_pending = false;
+    return LMSF_OK;
+}
+
 // density: also count the occupied slices (lim1 of the pruned one-lane walk); keyframe windows skip it
 // (lim1 stays 1, the plain walk -- speed only, results do not depend on it).
 lmsf_status grid_finish(lmsf_ctx* c, DevMap& m, int base, hipStream_t s, bool density = true) {
@@ -375,20 +490,8 @@ lmsf_status grid_finish(lmsf_ctx* c, DevMap& m, int base, hipStream_t s, bool de
     const size_t cells = (size_t)nx * ny * nz;
     if (nx <= 0 || ny <= 0 || nz <= 0 || cells > kMaxCells)
         return c->fail(LMSF_ERR_CAPACITY, "map extent of %d x %d x %d cells exceeds the dense grid limit", nx, ny, nz);
-    if (cells + 1 > m.cells_cap) {
-        hipFree(m.counts); hipFree(m.off); hipFree(m.fill); hipFree(m.scan_tmp);
-        m.counts = m.off = m.fill = nullptr;
-        m.scan_tmp = nullptr;
-        const size_t cap = std::min(grow_cap(cells + 1, m.cells_cap), kMaxCells + 1);
-        m.cells_cap = 0;
-        HIPCHK(c, dalloc(&m.counts, cap));
-        HIPCHK(c, dalloc(&m.off, cap));
-        HIPCHK(c, dalloc(&m.fill, cap));
-        m.scan_tmp_bytes = 0;
-        HIPCHK(c, exclusive_scan_u32(m.counts, m.off, cap, nullptr, m.scan_tmp_bytes, s));
-        HIPCHK(c, hipMalloc(&m.scan_tmp, std::max<size_t>(m.scan_tmp_bytes, 16)));
-        m.cells_cap = cap;
-    }
+    lmsf_status rc = grid_cells_reserve(c, m, cells + 1, s);
+    if (rc) return rc;
     m.ox = bb[0]; m.oy = bb[1]; m.oz = bb[2];
     m.nx = nx; m.ny = ny; m.nz = nz; m.sx = sx;
     unsigned long long* d_occ = reinterpret_cast<unsigned long long*>(m.d_bb + 8);
@@ -646,9 +749,12 @@ void fill_stats(const SolveState& S, lmsf_solve_stats* st) {
     st->final_cost = S.cost;
 }
 
-lmsf_status collect_timing(lmsf_ctx* c) {
+// The wall-clock stamps of the timed search launches, summed on the host.  Solves and batch waits call it only
+// once the stamp buffer is half full (lazy = true): a read-back and a stream wait per solve would be
+// instrumentation inside a timed loop; lmsf_kernel_stats_get collects the rest.
+lmsf_status collect_timing(lmsf_ctx* c, bool lazy = false) {
     if (!c->timing) return LMSF_OK;
-    if (c->ev_used < 2) return LMSF_OK;
+    if (c->ev_used < 2 || (lazy && c->ev_used < kEventPairs)) return LMSF_OK;
     HIPCHK(c, hipMemcpyAsync(c->h_stamps, c->d_stamps, c->ev_used * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -712,6 +818,8 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
             if (m.h_occ) hipHostFree(m.h_occ);
             if (m.ev_occ) hipEventDestroy(m.ev_occ);
             hipFree(m.d_bb);
+            hipFree(m.scan_state);
+            if (m.ev_bb) hipEventDestroy(m.ev_bb);
             if (m.h_bb) hipHostFree(m.h_bb);
         }
     }
@@ -720,6 +828,22 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->sort_key,
                     c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->featp, c->n_pos, c->d_error, c->d_lmsync};
     for (void* p : bufs) hipFree(p);
+    if (c->pre_worker.joinable()) {
+        {
+            std::lock_guard<std::mutex> lk(c->pre_mu);
+            c->pre_quit = true;
+        }
+        c->pre_cv.notify_all();
+        c->pre_worker.join();
+    }
+    if (c->pre_stream) hipStreamSynchronize(c->pre_stream);
+    void* pre_bufs[] = {c->alt.feat, c->alt.feat_src, c->alt.n_edge, c->alt.n_surf, c->alt.qslot, c->alt.fslot,
+                        c->alt.featp, c->alt.n_pos, c->pre_raw, c->pre_raw_count, c->pre_raw_off};
+    for (void* p : pre_bufs) hipFree(p);
+    if (c->h_pre) hipHostFree(c->h_pre);
+    if (c->ev_pre) hipEventDestroy(c->ev_pre);
+    if (c->ev_pre_after) hipEventDestroy(c->ev_pre_after);
+    if (c->pre_stream) hipStreamDestroy(c->pre_stream);
     hipFree(c->cap_rec);
     hipFree(c->cap_nn);
     hipFree(c->cap_pose);
@@ -822,10 +946,10 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->fslot, B * c->F));
     CHK(dalloc(&c->featp, B * c->F));
     CHK(dalloc(&c->n_pos, B));
-    CHK(dalloc(&c->d_error, 32));
+    CHK(dalloc(&c->d_error, 64));
     CHK(dalloc(&c->d_lmsync, 2 * B));
     CHK(hipMemset(c->d_lmsync, 0, 2 * B * sizeof(unsigned)));
-    CHK(hipMemset(c->d_error, 0, 32 * sizeof(int)));
+    CHK(hipMemset(c->d_error, 0, 64 * sizeof(int)));
     CHK(hipMemset(c->n_edge, 0, B * sizeof(int)));
     CHK(hipMemset(c->n_surf, 0, B * sizeof(int)));
     CHK(hipMemset(c->d_n27, 0, kCounterShards * 16 * sizeof(unsigned long long)));
@@ -931,7 +1055,7 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, stream_wait(c->stream));
-    rc = collect_timing(c);
+    rc = collect_timing(c, true);
     if (rc) return rc;
     if (c->h_pack[3]) return loop_fault(c);
     const SolveState& S = c->h_st[0];
@@ -952,10 +1076,149 @@ lmsf_status lmsf_solve_trace(lmsf_ctx* c, double* trace, int32_t cap, int32_t* n
 
 static lmsf_status load_scans(lmsf_ctx* c, const float* xyzi, const int64_t* counts, int32_t n, bool sync);
 
+// The extraction outcome read back into pinned hc = [n_edge, n_surf, capacity flags]: slot 0's features.
+static lmsf_status adopt_counts(lmsf_ctx* c, const int* hc, lmsf_feature_counts* counts) {
+    if (hc[2]) return c->fail(LMSF_ERR_CAPACITY, "ring or sector larger than the extraction kernel supports (flags %d)", hc[2]);
+    c->slot0_ne = hc[0];
+    c->slot0_ns = hc[1];
+    c->features_on_device = true;
+    c->scan_dirty = false;
+    c->host_scan[LMSF_EDGE].clear();
+    c->host_scan[LMSF_SURF].clear();
+    if (counts) { counts->n_edge = hc[0]; counts->n_surf = hc[1]; }
+    return LMSF_OK;
+}
+
+// The prefetch worker's enqueues, done (their status; the worker thread stays for the next prefetch).
+static lmsf_status join_prefetch(lmsf_ctx* c) {
+    std::unique_lock<std::mutex> lk(c->pre_mu);
+    c->pre_cv.wait(lk, [c] { return !c->pre_job; });
+    const lmsf_status rc = c->pre_rc;
+    c->pre_rc = LMSF_OK;
+    return rc;
+}
+
+// A pending prefetch that will not be adopted: later extractions queue behind it (shared scratch).
+static lmsf_status drop_prefetch(lmsf_ctx* c) {
+    if (!c->pre_pending) return LMSF_OK;
+    c->pre_pending = false;
+    lmsf_status rc = join_prefetch(c);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_pre, 0));
+    return LMSF_OK;
+}
+
+// The extraction of (pre_src, pre_n) on pre_stream into the alternate output set (worker thread).
+static lmsf_status enqueue_prefetch(lmsf_ctx* c) {
+    hipStream_t s = c->pre_stream;
+    const size_t n = c->pre_n;
+    HIPCHK(c, hipStreamWaitEvent(s, c->ev_pre_after, 0));
+    if (n) HIPCHK(c, hipMemcpyAsync(c->pre_raw, c->pre_src, n * sizeof(float4), hipMemcpyDefault, s));
+    HIPCHK(c, hipMemcpyAsync(c->pre_raw_count, c->h_pre, sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->pre_raw_off, c->h_pre + 2, sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemsetAsync(c->d_error + 24, 0, sizeof(int), s));
+    ExtractView e = c->eview(1);
+    e.raw = c->pre_raw;
+    e.raw_count = c->pre_raw_count;
+    e.raw_off = c->pre_raw_off;
+    e.feat = c->alt.feat;
+    e.feat_src = c->alt.feat_src;
+    e.n_edge = c->alt.n_edge;
+    e.n_surf = c->alt.n_surf;
+    e.qslot = c->alt.qslot;
+    e.fslot = c->alt.fslot;
+    e.featp = c->alt.featp;
+    e.n_pos = c->alt.n_pos;
+    e.error = c->d_error + 24;
+    HIPCHK(c, launch_extract(e, s));
+    HIPCHK(c, launch_pack3(c->alt.n_edge, c->alt.n_surf, c->d_error + 24, c->d_error + 40, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_pre + 4, c->d_error + 40, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipEventRecord(c->ev_pre, s));
+    return LMSF_OK;
+}
+
+static void prefetch_worker(lmsf_ctx* c) {
+    hipSetDevice(c->cfg.device);
+    std::unique_lock<std::mutex> lk(c->pre_mu);
+    for (;;) {
+        c->pre_cv.wait(lk, [c] { return c->pre_job || c->pre_quit; });
+        if (c->pre_quit) return;
+        lk.unlock();
+        const lmsf_status rc = enqueue_prefetch(c);
+        lk.lock();
+        c->pre_rc = rc;
+        c->pre_job = false;
+        c->pre_cv.notify_all();
+    }
+}
+
+lmsf_status lmsf_prefetch_features(lmsf_ctx* c, const float* xyzi, size_t n) {
+    if (!c || (n && !xyzi)) return LMSF_ERR_ARG;
+    if (n > (size_t)c->R) return c->fail(LMSF_ERR_CAPACITY, "%zu points exceed max_scan_points %d", n, c->R);
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (c->pre_pending) {   // replaced: its outputs are never adopted
+        c->pre_pending = false;
+        lmsf_status rc = join_prefetch(c);
+        if (rc) return rc;
+        HIPCHK(c, hipStreamSynchronize(c->pre_stream));
+    }
+    if (!c->pre_stream) {
+        const size_t B = c->B, F = c->F;
+        HIPCHK(c, dalloc(&c->alt.feat, B * F));
+        HIPCHK(c, dalloc(&c->alt.feat_src, B * F));
+        HIPCHK(c, dalloc(&c->alt.n_edge, B));
+        HIPCHK(c, dalloc(&c->alt.n_surf, B));
+        HIPCHK(c, dalloc(&c->alt.qslot, B * (size_t)c->R));
+        HIPCHK(c, dalloc(&c->alt.fslot, B * F));
+        HIPCHK(c, dalloc(&c->alt.featp, B * F));
+        HIPCHK(c, dalloc(&c->alt.n_pos, B));
+        HIPCHK(c, dalloc(&c->pre_raw, (size_t)c->R));
+        HIPCHK(c, dalloc(&c->pre_raw_count, 1));
+        HIPCHK(c, dalloc(&c->pre_raw_off, 1));
+        HIPCHK(c, hipHostMalloc((void**)&c->h_pre, 8 * sizeof(int), hipHostMallocDefault));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_pre_after, hipEventDisableTiming));
+        HIPCHK(c, hipStreamCreateWithFlags(&c->pre_stream, hipStreamNonBlocking));
+        c->pre_worker = std::thread(prefetch_worker, c);
+    }
+    // after everything enqueued on the context so far: the last extraction (shared scratch) and the readers of
+    // the output set this one overwrites (a keyframe transform of the features before the last)
+    HIPCHK(c, hipEventRecord(c->ev_pre_after, c->stream));
+    c->h_pre[0] = (int)n;
+    c->h_pre[2] = 0;
+    c->h_pre[3] = 0;
+    c->pre_src = xyzi;
+    c->pre_n = n;
+    c->pre_pending = true;
+    {
+        std::lock_guard<std::mutex> lk(c->pre_mu);
+        c->pre_job = true;
+    }
+    c->pre_cv.notify_all();
+    return LMSF_OK;
+}
+
 lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf_feature_counts* counts) {
     if (!c || (n && !xyzi)) return LMSF_ERR_ARG;
     if (n > (size_t)c->R) return c->fail(LMSF_ERR_CAPACITY, "%zu points exceed max_scan_points %d", n, c->R);
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (c->pre_pending && xyzi == c->pre_src && n == c->pre_n) {   // prefetched: adopt its outputs
+        c->pre_pending = false;
+        lmsf_status rj = join_prefetch(c);
+        if (rj) return rj;
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_pre, 0));
+        HIPCHK(c, hipEventRecord(c->ev_raw_free, c->stream));
+        c->swap_outputs();
+        c->qorder_valid = true;
+        lmsf_status rc = ctx_settle(c);
+        if (rc) return rc;
+        HIPCHK(c, hipEventSynchronize(c->ev_pre));
+        return adopt_counts(c, c->h_pre + 4, counts);
+    }
+    {
+        lmsf_status rd = drop_prefetch(c);
+        if (rd) return rd;
+    }
     const int64_t counts_in[1] = {(int64_t)n};
     lmsf_status rc = load_scans(c, xyzi, counts_in, 1, false);   // synchronised below
     if (rc) return rc;
@@ -971,16 +1234,7 @@ lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf
     HIPCHK(c, launch_pack3(c->n_edge, c->n_surf, c->d_error, c->d_error + 8, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->h_pack, c->d_error + 8, 3 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, stream_wait(c->stream));
-    const int* hc = c->h_pack;
-    if (hc[2]) return c->fail(LMSF_ERR_CAPACITY, "ring or sector larger than the extraction kernel supports (flags %d)", hc[2]);
-    c->slot0_ne = hc[0];
-    c->slot0_ns = hc[1];
-    c->features_on_device = true;
-    c->scan_dirty = false;
-    c->host_scan[LMSF_EDGE].clear();
-    c->host_scan[LMSF_SURF].clear();
-    if (counts) { counts->n_edge = hc[0]; counts->n_surf = hc[1]; }
-    return LMSF_OK;
+    return adopt_counts(c, c->h_pack, counts);
 }
 
 lmsf_status lmsf_common_params_init(lmsf_common_params* p) {
@@ -1279,6 +1533,10 @@ lmsf_status lmsf_batch_launch(lmsf_ctx* c, int32_t n, const double* poses) {
     std::memcpy(c->h_poses, poses, (size_t)n * 7 * sizeof(double));
     HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, (size_t)n * 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_error, 0, sizeof(int), c->stream));   // capacity flags of this batch only
+    {
+        lmsf_status rd = drop_prefetch(c);
+        if (rd) return rd;
+    }
     if (c->raw_pending) {   // streamed scans: extract once their copy has landed
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_raw_ready, 0));
         c->raw_pending = false;
@@ -1302,7 +1560,7 @@ lmsf_status lmsf_batch_wait(lmsf_ctx* c, int32_t n, double* poses, lmsf_solve_st
     HIPCHK(c, hipMemcpyAsync(&herr, c->d_error, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    lmsf_status rc = collect_timing(c);
+    lmsf_status rc = collect_timing(c, true);
     if (rc) return rc;
     if (c->h_pack[3]) return loop_fault(c);
     for (int i = 0; i < n; ++i) {
@@ -1581,6 +1839,10 @@ lmsf_status ctx_window_target(lmsf_ctx* c, int kind, size_t n_max, float4** orig
     return LMSF_OK;
 }
 
+lmsf_status ctx_window_build(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s) {
+    return grid_build_device(c, c->map[kind], n_max, c->prior[kind].n, s);
+}
+
 const float4* ctx_window_points(const lmsf_ctx* c, int kind) { return reinterpret_cast<const float4*>(c->map[kind].orig); }
 
 lmsf_status ctx_window_finish(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s, size_t* n_out) {
@@ -1588,7 +1850,8 @@ lmsf_status ctx_window_finish(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s
     if (n_max == 0) {
         m.n = 0;
     } else {
-        lmsf_status rc = grid_finish(c, m, c->prior[kind].n, s, false);
+        lmsf_status rc = m.dev_pending ? grid_finish_device(c, m, c->prior[kind].n, s)
+                                       : grid_finish(c, m, c->prior[kind].n, s, false);
         if (rc) return rc;
     }
     *n_out = (size_t)m.n;

@@ -14,6 +14,7 @@
 
 #include "bbox.h"
 #include "lmsf_internal.h"
+#include "radix.h"
 
 namespace lmsf {
 
@@ -177,6 +178,142 @@ __global__ void grid_clear_kernel(uint32_t* counts, uint32_t* fill, size_t n, un
 hipError_t launch_grid_clear(uint32_t* counts, uint32_t* fill, size_t n, unsigned long long* occ, hipStream_t s) {
     const size_t blocks = std::min<size_t>(2048, (n + 255) / 256);
     hipLaunchKernelGGL(grid_clear_kernel, dim3((unsigned)std::max<size_t>(blocks, 1)), dim3(256), 0, s, counts, fill, n, occ);
+    return hipGetLastError();
+}
+
+// ---- device-sized builds (tracker windows): the box and count come from a producer on the device (d_bb:
+// box 0..5, count 6), so the grid is built without a host round trip; d_bb[10] = cells + 1 when that exceeds
+// the allocation (the host then rebuilds with room), else 0; d_bb[16] = the scan's tile counter.
+
+__device__ __forceinline__ size_t grid_cells(const int* bb) {
+    const long long nx = (long long)bb[3] - bb[0] + 1, ny = (long long)bb[4] - bb[1] + 1, nz = (long long)bb[5] - bb[2] + 1;
+    if (nx <= 0 || ny <= 0 || nz <= 0) return 0;
+    return (size_t)(nx * ny * nz);
+}
+
+__global__ void grid_clear_dev_kernel(int* bb, uint32_t* counts, uint32_t* fill, size_t cap) {
+    const size_t cells = grid_cells(bb);
+    const bool over = bb[6] > 0 && (cells == 0 || cells + 1 > cap);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        bb[10] = over ? (int)min(cells + 1, (size_t)INT_MAX) : 0;
+        bb[16] = 0;
+    }
+    if (over) return;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells + 1; i += stride) {
+        counts[i] = 0u;
+        fill[i] = 0u;
+    }
+}
+
+__global__ void map_count_dev_kernel(const float4* pts, const int* bb, float sx, int* cell, uint32_t* counts) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= bb[6] || bb[10]) return;
+    const int ox = bb[0], oy = bb[1], oz = bb[2], nx = bb[3] - ox + 1, ny = bb[4] - oy + 1;
+    const float4 p = pts[i];
+    const int cx = (int)fminf(fmaxf(floorf(p.x * sx), -1073741824.f), 1073741824.f) - ox;
+    const int cy = (int)fminf(fmaxf(floorf(p.y), -1073741824.f), 1073741824.f) - oy;
+    const int cz = (int)fminf(fmaxf(floorf(p.z), -1073741824.f), 1073741824.f) - oz;
+    const int c = (cz * ny + cy) * nx + cx;
+    cell[i] = c;
+    atomicAdd(&counts[c], 1u);
+}
+
+__global__ void map_scatter_dev_kernel(const float4* pts, const int* bb, const int* cell, const uint32_t* off,
+                                       uint32_t* fill, float4* sorted, int base) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= bb[6] || bb[10]) return;
+    const int c = cell[i];
+    const uint32_t pos = off[c] + atomicAdd(&fill[c], 1u);
+    const float4 p = pts[i];
+    sorted[pos] = make_float4(p.x, p.y, p.z, __int_as_float(base + i));
+}
+
+// off = exclusive scan of counts[0, cells + 1): tiles of 16 consecutive values per thread, block scan, tile
+// offset by wave look-back (radix.h) over a tile counter; blocks past the device-side length exit.
+constexpr int kScanThreads = 1024, kScanPer = 16, kScanTile = kScanThreads * kScanPer;
+
+__global__ __launch_bounds__(kScanThreads) void scan_dev_kernel(const uint32_t* in, uint32_t* out, int* bb,
+                                                                unsigned long long* st, uint32_t epoch) {
+    __shared__ int s_tile;
+    __shared__ uint32_t s_wave[kScanThreads / 64], s_before;
+    if (bb[10] || bb[6] <= 0) return;
+    const size_t len = grid_cells(bb) + 1;
+    if (threadIdx.x == 0)
+        s_tile = (int)__hip_atomic_fetch_add(reinterpret_cast<unsigned*>(bb + 16), 1u, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int tile = s_tile;
+    const size_t base = (size_t)tile * kScanTile;
+    if (base >= len) return;   // block-uniform
+    const size_t i0 = base + (size_t)threadIdx.x * kScanPer;
+    uint32_t v[kScanPer];
+    if (i0 + kScanPer <= len) {
+#pragma unroll
+        for (int q = 0; q < kScanPer / 4; ++q) {
+            const uint4 a = *reinterpret_cast<const uint4*>(in + i0 + 4 * q);
+            v[4 * q] = a.x; v[4 * q + 1] = a.y; v[4 * q + 2] = a.z; v[4 * q + 3] = a.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kScanPer; ++j) v[j] = i0 + j < len ? in[i0 + j] : 0u;
+    }
+    uint32_t t = 0;
+#pragma unroll
+    for (int j = 0; j < kScanPer; ++j) t += v[j];
+    uint32_t total;
+    uint32_t run = block_exclusive_scan<kScanThreads>(t, s_wave, &total);
+    if (threadIdx.x < 64) {
+        uint32_t before = 0;
+        if (tile == 0) {
+            if (threadIdx.x == 0) lb_store(st, epoch, kLbInc, total);
+        } else {
+            if (threadIdx.x == 0) lb_store(st + tile, epoch, kLbAgg, total);
+            before = wave_lookback(st, tile, epoch);
+            if (threadIdx.x == 0) lb_store(st + tile, epoch, kLbInc, before + total);
+        }
+        if (threadIdx.x == 0) s_before = before;
+    }
+    __syncthreads();
+    run += s_before;
+    if (i0 + kScanPer <= len) {
+#pragma unroll
+        for (int q = 0; q < kScanPer / 4; ++q) {
+            uint4 a;
+            a.x = run; run += v[4 * q];
+            a.y = run; run += v[4 * q + 1];
+            a.z = run; run += v[4 * q + 2];
+            a.w = run; run += v[4 * q + 3];
+            *reinterpret_cast<uint4*>(out + i0 + 4 * q) = a;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kScanPer; ++j)
+            if (i0 + j < len) {
+                out[i0 + j] = run;
+                run += v[j];
+            }
+    }
+}
+
+size_t grid_scan_tiles(size_t cells_cap) { return (cells_cap + kScanTile - 1) / kScanTile; }
+
+hipError_t launch_grid_build_dev(const float4* orig, int n_max, int sx, int* d_bb, uint32_t* counts, uint32_t* off,
+                                 uint32_t* fill, size_t cells_cap, int* cell, float4* sorted, int base,
+                                 unsigned long long* scan_state, uint32_t epoch, int* h_bb, hipEvent_t ev_bb,
+                                 hipStream_t s) {
+    if (n_max <= 0) return hipSuccess;
+    const unsigned cb = (unsigned)std::min<size_t>(2048, (cells_cap + 255) / 256);
+    hipLaunchKernelGGL(grid_clear_dev_kernel, dim3(std::max(cb, 1u)), dim3(256), 0, s, d_bb, counts, fill, cells_cap);
+    // the box, count and overflow flag are final here: the host reads them while the build goes on
+    hipError_t e = hipMemcpyAsync(h_bb, d_bb, 11 * sizeof(int), hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+    if ((e = hipEventRecord(ev_bb, s)) != hipSuccess) return e;
+    const dim3 g((n_max + 255) / 256), b(256);
+    hipLaunchKernelGGL(map_count_dev_kernel, g, b, 0, s, orig, d_bb, (float)sx, cell, counts);
+    hipLaunchKernelGGL(scan_dev_kernel, dim3((unsigned)grid_scan_tiles(cells_cap + 1)), dim3(kScanThreads), 0, s,
+                       counts, off, d_bb, scan_state, epoch);
+    hipLaunchKernelGGL(map_scatter_dev_kernel, g, b, 0, s, orig, d_bb, cell, off, fill, sorted, base);
     return hipGetLastError();
 }
 

@@ -157,6 +157,14 @@ hipError_t launch_map_count(const float4* pts, int n, int sx, int ox, int oy, in
 hipError_t launch_map_scatter(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
                               float4* sorted, int base, hipStream_t s);
 hipError_t launch_count_nonzero(const uint32_t* counts, size_t n, unsigned long long* out, hipStream_t s);
+// Grid of a window whose box + count a producer left in d_bb (box 0..5, count 6), built on stream s without
+// a host round trip (k_map.hip): clear, read-back of d_bb[0..10] into h_bb + ev_bb, count, scan, scatter.
+// d_bb[10] != 0: the cells exceed cells_cap (nothing built; the host rebuilds).
+size_t grid_scan_tiles(size_t cells_cap);
+hipError_t launch_grid_build_dev(const float4* orig, int n_max, int sx, int* d_bb, uint32_t* counts, uint32_t* off,
+                                 uint32_t* fill, size_t cells_cap, int* cell, float4* sorted, int base,
+                                 unsigned long long* scan_state, uint32_t epoch, int* h_bb, hipEvent_t ev_bb,
+                                 hipStream_t s);
 hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, void* tmp, size_t& tmp_bytes, hipStream_t s);
 
 // edge2 / surf2: optional second grid per kind (n = 0: none), searched as if concatenated after
@@ -317,6 +325,9 @@ lmsf_status ctx_window_finish(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s
 // for a producer that fills both on the stage stream (the tracker's voxel filter); then
 // ctx_window_stage(c, kind, nullptr, n_max, nullptr, s) only reads them back.
 lmsf_status ctx_window_target(lmsf_ctx* c, int kind, size_t n_max, float4** orig, int** bb);
+// ... or, instead of that read-back, the whole grid build on s (no host wait; ctx_window_finish then only
+// takes the box read-back and sets the view).
+lmsf_status ctx_window_build(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s);
 // The window's points in window order (the grid's unsorted source) after a finished commit.
 const float4* ctx_window_points(const lmsf_ctx* c, int kind);
 int grid_slices();

@@ -103,6 +103,37 @@ __device__ __forceinline__ uint32_t lookback_sum(const unsigned long long* st, i
     return sum;
 }
 
+// Sum of the counts of tiles [0, tile) by one wave: lane j reads tile p - j (64 tiles per round trip), the
+// nearest inclusive word ends the walk, the nearest unpublished one resumes it; every lane returns the sum.
+__device__ __forceinline__ uint32_t wave_lookback(const unsigned long long* st, int tile, uint32_t epoch) {
+    const int lane = threadIdx.x & 63;
+    uint32_t sum = 0;
+    int p = tile - 1;
+    unsigned spins = 0;
+    while (p >= 0) {
+        const int q = p - lane;
+        const unsigned long long v = q >= 0 ? lb_load(st + q) : 0ull;
+        const uint32_t lo = (uint32_t)v, flag = lo & ~kLbCount;
+        const bool ready = q < 0 || ((uint32_t)(v >> 32) == epoch && flag != 0u);
+        const bool inc = q < 0 || (ready && flag == kLbInc);   // before tile 0: an inclusive zero
+        const unsigned long long notready = __ballot(!ready), incm = __ballot(inc);
+        const unsigned long long stopm = notready | incm;
+        const int stop = stopm ? __ffsll((long long)stopm) - 1 : 64;
+        const bool stop_inc = stop < 64 && ((incm >> stop) & 1ull);
+        uint32_t c = (lane < stop || (lane == stop && stop_inc)) && q >= 0 ? (lo & kLbCount) : 0u;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+        sum += c;
+        if (stop_inc) break;
+        p -= stop;
+        if (stop == 0) {
+            if (++spins > kLbSpinLimit) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return sum;
+}
+
 // Exclusive scan over the block's threads (kBlock = whole waves, <= 1024) of one value each; *total = the sum.
 template <int kBlock>
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t* total) {

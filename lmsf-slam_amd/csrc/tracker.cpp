@@ -238,7 +238,7 @@ lmsf_status commit_stage_kind(lmsf_tracker* t, int kind, hipStream_t ks) {
         lmsf_status rc = ctx_window_target(t->ctx, kind, nw, &orig, &bb);
         if (rc) return rc;
         TCHK(t, t->voxel[kind].enqueue(w.wcat, (int)nw, (float)w.leaf, orig, ks, bb, grid_slices()));
-        return ctx_window_stage(t->ctx, kind, nullptr, nw, nullptr, ks);
+        return ctx_window_build(t->ctx, kind, nw, ks);   // the grid too, without a host round trip
     }
     // only the window's grid is rebuilt; the prior's grid was built once (set_prior_map)
     return ctx_window_stage(t->ctx, kind, w.concat, nw, nullptr, ks);
@@ -279,7 +279,9 @@ lmsf_status join_worker(lmsf_tracker* t) {
 // One kind's half of commit_finish on its stage stream: wait for the stage's read-back, enqueue the grid
 // build, mark its end for the context stream.
 lmsf_status finish_kind(lmsf_tracker* t, int kind, hipStream_t ks) {
-    TCHK(t, stream_wait(ks));
+    // a device-built grid (filtered windows) needs only its box read-back, which the finish waits for itself:
+    // the rest of the build stays queued, and the context stream joins it on the device (ev_join)
+    if (!(t->win[kind].leaf > 0)) TCHK(t, stream_wait(ks));
     lmsf_status rc = ctx_window_finish(t->ctx, kind, t->nmax[kind], ks, &t->fin_n[kind]);
     if (rc) return rc;
     TCHK(t, hipEventRecord(t->ev_join[kind], ks));
@@ -325,7 +327,7 @@ lmsf_status commit_finish(lmsf_tracker* t) {
     if (!t->pending) return LMSF_OK;
     t->pending = false;
     for (int kind : {LMSF_SURF, LMSF_EDGE})
-        if (t->ks[kind]) TCHK(t, stream_wait(t->ks[kind]));
+        if (t->ks[kind] && !(t->win[kind].leaf > 0)) TCHK(t, stream_wait(t->ks[kind]));   // see finish_kind
     for (int kind : {LMSF_SURF, LMSF_EDGE}) {
         Window& w = t->win[kind];
         if (!t->ks[kind]) continue;

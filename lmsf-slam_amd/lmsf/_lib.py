@@ -103,6 +103,7 @@ _SIGS = {
     "lmsf_solve": (C.c_int32, [_P, _P, C.POINTER(SolveStats)]),
     "lmsf_solve_trace": (C.c_int32, [_P, _P, C.c_int32, C.POINTER(C.c_int32)]),
     "lmsf_extract_features": (C.c_int32, [_P, _P, C.c_size_t, C.POINTER(FeatureCounts)]),
+    "lmsf_prefetch_features": (C.c_int32, [_P, _P, C.c_size_t]),
     "lmsf_common_params_init": (C.c_int32, [C.POINTER(CommonParams)]),
     "lmsf_common_process": (C.c_int32, [_P, _P, C.c_size_t, C.POINTER(CommonParams), C.POINTER(FeatureCounts)]),
     "lmsf_copy_features": (C.c_int32, [_P, C.c_int32, _P, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
@@ -266,7 +267,15 @@ class Context:
         p, n, keep = _buf(pts)
         fc = FeatureCounts()
         self._check(load().lmsf_extract_features(self.h, p, n, C.byref(fc)))
+        self._prefetched = None
         return fc.n_edge, fc.n_surf
+
+    def prefetch(self, pts):
+        """lmsf_prefetch_features: extract the next scan beside the current work; the next extract(pts) of
+        the same buffer adopts it (the buffer is kept alive until then)."""
+        p, n, keep = _buf(pts)
+        self._check(load().lmsf_prefetch_features(self.h, p, n))
+        self._prefetched = keep
 
     @staticmethod
     def common_params(**kw):

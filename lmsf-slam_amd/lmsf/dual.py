@@ -58,21 +58,27 @@ class DualLidarSystem:
         self.pose = [np.eye(4), np.eye(4)]       # pose_lidar_cur_
         self.last = {}
 
-    def _track(self, i, scan, timestamp):
-        """LidarTrackerLocalMap::Solve of LiDAR i on its device-extracted features, keyframe included."""
+    def _track(self, i, scan, timestamp, prefetch=None):
+        """LidarTrackerLocalMap::Solve of LiDAR i on its device-extracted features, keyframe included; the
+        scan its context extracts next (prefetch) is extracted beside the Solve."""
         self.ctx[i].extract(scan)
+        if prefetch is not None:
+            self.ctx[i].prefetch(prefetch)
         d, r = self.trackers[i].solve_extracted(timestamp)
         if r.update_type:
             self.trackers[i].add_keyframe_extracted(self.trackers[i].pose())
             self.trackers[i].commit_map()
         return d, r
 
-    def process(self, scan_primary, scan_sub, timestamp):
-        """One synchronized frame; returns (primary pose, sub pose) in the tracker's local frame."""
+    def process(self, scan_primary, scan_sub, timestamp, next_frame=None):
+        """One synchronized frame; returns (primary pose, sub pose) in the tracker's local frame.  next_frame
+        (the next (primary, sub) scans, optional): their extraction starts beside this frame's registrations,
+        as the reference's preprocess thread runs ahead of its estimate thread (the results do not change)."""
+        nxt = next_frame if next_frame is not None else (None, None)
         if self.status == 0:
             deltas = []
             for i, scan in enumerate((scan_primary, scan_sub)):
-                d, r = self._track(i, scan, timestamp)
+                d, r = self._track(i, scan, timestamp, prefetch=nxt[i])
                 self.pose[i] = iso_mul(self.pose[i], d)
                 deltas.append(d)
             if self.handeye.add_pose(deltas[0], deltas[1]):              # :268-281
@@ -83,11 +89,13 @@ class DualLidarSystem:
                     self.status = 1
             return self.pose[0], self.pose[1]
         t0 = self.trackers[0]
-        d, r = self._track(0, scan_primary, timestamp)                    # :296-297
+        d, r = self._track(0, scan_primary, timestamp, prefetch=scan_sub)  # :296-297
         primary = t0.pose()                                               # :299
         sub0 = iso_mul(primary, self.extrinsic)                                   # :301
         self.pose[0] = iso_mul(self.pose[0], d)                                   # :302
         self.ctx[0].extract(scan_sub)
+        if nxt[0] is not None:
+            self.ctx[0].prefetch(nxt[0])
         sub, st = t0.register_extracted(sub0)                             # :304-305
         self.extrinsic = iso_mul(iso_inv(primary), sub)                     # :306
         self.pose[1] = iso_mul(self.pose[0], self.extrinsic)                      # :307

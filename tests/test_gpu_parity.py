@@ -49,6 +49,40 @@ def test_extract_bitexact(lib, oracle_mod, small_workload):
         assert gs.tobytes() == s.tobytes()
 
 
+def test_prefetch_features_bitexact(lib, oracle_mod, small_workload):
+    """lmsf_prefetch_features: the next scan extracted beside a solve and adopted by the extract call of the
+    same buffer gives the oracle's features and source indices; a prefetch of another buffer is discarded
+    and the extract of the buffer asked for is exact; a solve between prefetch and adoption is unchanged."""
+    import torch
+    wl = small_workload
+    scans = [torch.from_numpy(sc).to("cuda:0") for sc in wl.scans]
+    ref = _ctx(lib, max_batch=1)
+    ref.set_map(lib.EDGE, wl.edge_map)
+    ref.set_map(lib.SURF, wl.surf_map)
+    ctx = _ctx(lib, max_batch=1)
+    ctx.set_map(lib.EDGE, wl.edge_map)
+    ctx.set_map(lib.SURF, wl.surf_map)
+    ctx.extract(scans[0])
+    for i in range(1, len(scans)):
+        ctx.prefetch(scans[i])
+        ref.extract(scans[i - 1])
+        assert ctx.solve(wl.guess[i - 1])[0].tobytes() == ref.solve(wl.guess[i - 1])[0].tobytes()   # beside it
+        ne, ns = ctx.extract(scans[i])                                                   # adopted
+        e, s, ei, si = oracle_mod.extract(wl.scans[i])
+        assert (ne, ns) == (len(e), len(s))
+        ge, gei = ctx.copy_features(lib.EDGE)
+        gs, gsi = ctx.copy_features(lib.SURF)
+        np.testing.assert_array_equal(gei, ei)
+        np.testing.assert_array_equal(gsi, si)
+        assert ge.tobytes() == e.tobytes() and gs.tobytes() == s.tobytes()
+    ctx.prefetch(scans[0])                      # not adopted: another buffer is extracted
+    other = scans[1].clone()
+    ctx.extract(other)
+    e, s, _, _ = oracle_mod.extract(wl.scans[1])
+    assert ctx.copy_features(lib.EDGE)[0].tobytes() == e.tobytes()
+    assert ctx.copy_features(lib.SURF)[0].tobytes() == s.tobytes()
+
+
 @pytest.mark.parametrize("n_scans,cols,kw", [
     (32, 2048, {}),
     (64, 1024, {}),
@@ -827,8 +861,9 @@ def test_dual_lidar_refine_parity(lib, oracle_mod, cols):
     sysg = dual.DualLidarSystem(_ctx(lib), extrinsic=X0)
     ot = OT.Tracker()
     ext = X0.copy()
-    for i in range(len(ds.truth)):
-        prim_g, sub_g = sysg.process(ds.primary[i], ds.sub[i], 0.1 * i)
+    for i in range(len(ds.truth)):                   # the next frame's extractions run ahead (prefetch)
+        nxt = (ds.primary[i + 1], ds.sub[i + 1]) if i + 1 < len(ds.truth) else None
+        prim_g, sub_g = sysg.process(ds.primary[i], ds.sub[i], 0.1 * i, next_frame=nxt)
         ep, sp, _, _ = oracle_mod.extract(ds.primary[i])
         es, ss, _, _ = oracle_mod.extract(ds.sub[i])
         _, typ, _ = ot.solve(ep, sp, 0.1 * i)
