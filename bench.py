@@ -83,7 +83,7 @@ def parse(argv=None):
                     help="skip the untimed n27-counting step (PMC passes: every dispatch then runs as timed)")
     ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes of the neighbour-search kernel from rocprofv3 PMC runs")
-    ap.add_argument("--h2d", choices=("auto", "on", "off"), default="auto",
+    ap.add_argument("--h2d", choices=("auto", "on", "off", "shadow"), default="auto",
                     help="C2: also time K steps that stream every step's scans from pinned host memory "
                          "(lmsf_batch_load_scans_async, overlapped with the previous launch) -- reported as "
                          "`h2d_inclusive` beside the HBM-resident headline")
@@ -481,7 +481,7 @@ def run_batch(args, d):
     poses = np.zeros((n_units, 7))
     matches = np.zeros(n_units, np.int64)                    # residual blocks of each unit's last outer iteration
     enqueue_s = []                                           # host time inside lmsf_batch_launch, per step
-    stream_in = {"on": False}
+    stream_in = {"on": False, "shadow": None}
     host_bufs = []
 
     def step():
@@ -493,7 +493,16 @@ def run_batch(args, d):
                 t_enq = time.perf_counter()
                 cx.batch_launch(guesses[a:a + m])
                 enq += time.perf_counter() - t_enq
-                if stream_in["on"]:                          # next step's scans, overlapped with this launch
+                if stream_in["shadow"] is not None:          # diagnostics: the same DMA, nothing waits for it
+                    dst, side, spans = stream_in["shadow"]
+                    with torch.cuda.stream(side):
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e0.record(side)
+                        dst[i].copy_(host_bufs[i][0], non_blocking=True)
+                        e1.record(side)
+                        spans.append((e0, e1))
+                elif stream_in["on"]:                        # next step's scans, overlapped with this launch
                     cx.load_scans_async(*host_bufs[i])
             for i, cx, a, m in parts:
                 poses[a:a + m], st = cx.batch_wait(m)
@@ -520,7 +529,7 @@ def run_batch(args, d):
                         "wall-clock stamps around each search launch of a live untimed pass running one context "
                         "stream at a time", solo=solo)
     h2d = None
-    if cfg == "C2" and (args.h2d == "on" or (args.h2d == "auto" and U == n_units)):
+    if cfg == "C2" and (args.h2d in ("on", "shadow") or (args.h2d == "auto" and U == n_units)):
         # SURVEY 8(d) "including ... H2D of the scan": the same K steps with every step's scans streamed
         # from page-locked host memory (one DMA per context, issued right after that context's launch so
         # it overlaps the registration; the copy waits for the launch's extraction to have read the slots)
@@ -528,8 +537,13 @@ def run_batch(args, d):
             counts = np.array([len(x) for x in sc], np.int64)
             buf = torch.from_numpy(np.concatenate(sc, 0)).pin_memory()
             host_bufs.append((buf, counts))
-        for cx, (buf, counts) in zip(ctxs, host_bufs):
-            cx.load_scans_async(buf, counts)
+        if args.h2d == "shadow":   # diagnostics: uploads into scratch on a side stream, launches on resident scans
+            lo, hi = torch.cuda.Stream.priority_range()
+            stream_in["shadow"] = ([torch.empty_like(b, device=d.dev) for b, _ in host_bufs],
+                                   torch.cuda.Stream(priority=hi), [])
+        else:
+            for cx, (buf, counts) in zip(ctxs, host_bufs):
+                cx.load_scans_async(buf, counts)
         stream_in["on"] = True
         step()
         d.barrier()
@@ -543,9 +557,16 @@ def run_batch(args, d):
         if world > 1:
             el2 = multi.max_over_ranks(el2, d.dev)
         stream_in["on"] = False
+        copy_ms = None
+        if stream_in["shadow"] is not None:   # DMA time of the uploads alone: ms per step (link-bound if ~ step)
+            spans = stream_in["shadow"][2][len(host_bufs):]   # the timed steps (after the untimed one)
+            copy_ms = round(sum(a.elapsed_time(b) for a, b in spans) / max(args.steps, 1), 3)
+        stream_in["shadow"] = None
         up = sum(int(b.numel()) * 4 for b, _ in host_bufs)
         h2d = {"value": round(args.batch * world * args.steps / el2, 2), "unit": "scans/s",
                "ms_per_step": round(el2 / args.steps * 1e3, 3), "upload_bytes_per_step_per_gpu": up,
+               "mode": args.h2d if args.h2d == "shadow" else "streamed",
+               **({"upload_dma_ms_per_step": copy_ms} if copy_ms is not None else {}),
                "note": "every step's raw scans uploaded from pinned host memory inside the timed window "
                        "(lmsf_batch_load_scans_async on each context's copy stream, overlapped with the previous "
                        "launch); the headline `value` keeps the scans HBM-resident"}
@@ -655,7 +676,7 @@ def run_streams(args, d):
     cap = max_pts + 64
     fbuf = torch.zeros((2 * cap, 4), dtype=torch.float32, device=d.dev)       # [edges | surfs] of own scan
     xchg = multi.KeyframeExchange(cap, world, d.dev)
-    state = {"i": 0, "kf": 0, "err": []}
+    state = {"i": 0, "kf": 0, "err": [], "xchg_s": 0.0}
 
     phases = collections.defaultdict(float) if os.environ.get("LMSF_BENCH_PHASES") else None
 
@@ -680,7 +701,9 @@ def run_streams(args, d):
             ne = ctx.copy_features_into(_lib.EDGE, fbuf[:cap])
             ns = ctx.copy_features_into(_lib.SURF, fbuf[cap:])
         t = mark("copy_features", t)
+        tx = time.perf_counter()
         kfs = xchg.exchange(P, r.update_type, ne, ns, fbuf)           # same list, same order everywhere
+        state["xchg_s"] += time.perf_counter() - tx
         t = mark("exchange", t)
         for q, fe, fs, pose in kfs:
             if q == rank:                                             # own keyframe: from the context, no copies
@@ -740,7 +763,9 @@ def run_streams(args, d):
              {"streams": world, "map_points": map_points, "outer_iterations": args.outer,
               "parallelism": f"stream-per-GPU x{world}", "extract_ahead": not args.no_prefetch}, roof, cpu,
              tracking_error_m={"rank0_max": max(state["err"]), "rank0_last": state["err"][-1]},
-             keyframes_appended=state["kf"])
+             keyframes_appended=state["kf"],
+             # host time in the keyframe exchange per scan (the collectives at world > 1), over all steps run
+             keyframe_exchange_ms_per_step=round(1e3 * state["xchg_s"] / max(state["i"], 1), 4))
     tr.close()
     ctx.close()
 
