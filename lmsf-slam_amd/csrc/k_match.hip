@@ -68,6 +68,10 @@ constexpr int kKnnUnroll = LMSF_KNN_UNROLL;   // candidate loads in flight per l
 #define LMSF_KNN_ROWS_FIRST 1
 #endif
 constexpr bool kKnnRowsFirst = LMSF_KNN_ROWS_FIRST != 0;
+#ifndef LMSF_KNN_LB_SKIP
+#define LMSF_KNN_LB_SKIP 1
+#endif
+constexpr bool kLbSkip = LMSF_KNN_LB_SKIP != 0;   // rows-first walk: nearest rows first, rows beyond the kept keys skipped
 
 template <int T>
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
@@ -141,9 +145,10 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
     // the kCullLim margin dwarfs float rounding of the gaps, of sqrt and of d2).  c27 counts the
     // untrimmed 27 cells (SURVEY 8(d) accounting).
     constexpr float kCullLim = 1.0f + 1e-5f;
-    auto resolve_row = [&](int rr, int& rs, int& rl) {
+    auto resolve_row = [&](int rr, int& rs, int& rl, float& rlb) {
         rs = 0;
         rl = 0;
+        rlb = 0.f;
         const GridView gg = pick_grid(TWO && rr >= 9, g2, g);
         const int gn = gg.n, ox = gg.ox, oy = gg.oy, oz = gg.oz, nx = gg.nx, ny = gg.ny, nz = gg.nz, sx = gg.sx;
         const uint32_t* off = gg.off;
@@ -160,6 +165,7 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
         const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
         const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
         const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
+        rlb = gy * gy + gz * gz;
         const float rem = lim - gy * gy - gz * gz;
         if (rem >= 0.f) {
             const double r = (double)sqrtf(rem);
@@ -198,11 +204,18 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
     if constexpr (T == 1 && !PRUNE && kKnnRowsFirst) {
         // all rows resolved first (2 x NR offset loads in one batch, one latency instead of NR), then
         // walked with RU candidate loads in flight
+        // Rows are walked nearest first (own row, faces, corners) and a row whose yz-gap^2 lower bound
+        // exceeds the current NK-th key is skipped: exact, as in the pruned walk below (every point of the
+        // row has fl(d2) >= fl(gy^2 + gz^2) > that key, so it cannot enter the kept NK, ties included).
         int rs_[NR], rl_[NR];
+        float lb_[NR];
 #pragma unroll
-        for (int rr = 0; rr < NR; ++rr) resolve_row(rr, rs_[rr], rl_[rr]);
+        for (int rr = 0; rr < NR; ++rr) resolve_row(rr, rs_[rr], rl_[rr], lb_[rr]);
+        constexpr int kNear[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};
 #pragma unroll
-        for (int rr = 0; rr < NR; ++rr) {
+        for (int i = 0; i < NR; ++i) {
+            const int rr = kLbSkip ? kNear[TWO ? i / 2 : i] + ((TWO && (i & 1)) ? 9 : 0) : i;
+            if (kLbSkip && lb_[rr] > key_d2(k[NK - 1])) continue;
             const float4* rp = (TWO && rr >= 9) ? g2.pts : g.pts;
             const uint32_t tag = (TWO && rr >= 9) ? kGridBit : 0u;
             const int a = rs_[rr], len = rl_[rr];
@@ -225,7 +238,8 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
             const float4* rp = (TWO && rr >= 9) ? g2.pts : g.pts;
             const uint32_t tag = (TWO && rr >= 9) ? kGridBit : 0u;
             int a, len;
-            resolve_row(rr, a, len);
+            float lbr;
+            resolve_row(rr, a, len, lbr);
             int c = 0;
             for (; c + kKnnUnroll <= len; c += kKnnUnroll) {
                 float4 m[kKnnUnroll];
@@ -354,7 +368,8 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
         for (int rep = 0; rep < REPS; ++rep) {
             rs_[rep] = 0;
             rl_[rep] = 0;
-            if (lane + rep * T < NR) resolve_row(lane + rep * T, rs_[rep], rl_[rep]);
+            float lbr;
+            if (lane + rep * T < NR) resolve_row(lane + rep * T, rs_[rep], rl_[rep], lbr);
         }
         int st[NR], pre[NR + 1];
         pre[0] = 0;

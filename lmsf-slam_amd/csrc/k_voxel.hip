@@ -267,16 +267,19 @@ __global__ __launch_bounds__(kSegThreads) void voxel_reduce_kernel(const float4*
 #pragma unroll
     for (int j = 0; j < kSegPer; ++j)
         if ((flags >> j) & 1u) s_head[r++] = (uint16_t)(p0 + j - tbase);
-    if (tid == 0) {
+    if (tid < 64) {   // wave 0: the tile's offset by a 64-wide look-back (64 tiles per round trip)
         uint32_t before = 0;
         if (tile == 0) {
-            lb_store(st, epoch, kLbInc, total);
+            if (tid == 0) lb_store(st, epoch, kLbInc, total);
         } else {
-            lb_store(st + tile, epoch, kLbAgg, total);
-            before = lookback_sum<32>(st, tile, 1, epoch);
-            lb_store(st + tile, epoch, kLbInc, before + total);
+            if (tid == 0) lb_store(st + tile, epoch, kLbAgg, total);
+            before = wave_lookback(st, tile, epoch);
+            if (tid == 0) lb_store(st + tile, epoch, kLbInc, before + total);
         }
-        s_before = before;
+        if (tid == 0) s_before = before;
+    }
+    if (tid == 0) {
+        const uint32_t before = s_before;
         if (tbase + kSegTile >= n) {   // the last tile: the voxel count
             *nseg = (int)(before + total);
             if (map_bb) map_bb[6] = (int)(before + total);
