@@ -218,14 +218,17 @@ lmsf_status lmsf_batch_copy_features(lmsf_ctx* ctx, int32_t slot, int32_t kind, 
 /* ---- context options (not on the reference surface): algorithm switches of the build.
  * Results do not depend on them (the memo switches are exact, DESIGN.md section 4 "Query memo"); they
  * exist so tests can compare the paths in one process and a caller can rule a path out.  Values 0 | 1;
- * defaults 1, LMSF_OPT_GRAPH 0. */
+ * defaults 1 except LMSF_OPT_GRAPH 0. */
 #define LMSF_OPT_QUERY_MEMO 0   /* 1: outer iterations > 0 reuse 5-NN sets that provably did not change */
 #define LMSF_OPT_MEMO_REFIT 1   /* 1: a reused set in a new order is refitted without a walk */
 #define LMSF_OPT_MEMO_EXACT 2   /* 1: keep the set when its farthest point is nearer than s6 - d (0: 2d < s6 - s5) */
 #define LMSF_OPT_MEMO_ORDER 3   /* 1: consecutive-gap test first (no re-keying when every gap exceeds 2d) */
 #define LMSF_OPT_MEMO_BOUND 4   /* 1: memo misses walk min(1 m, s6 + d) instead of 1 m */
 #define LMSF_OPT_GRAPH 5        /* 1: replay state init + registration as a HIP graph (default 0) */
-#define LMSF_OPT_COUNT 6
+#define LMSF_OPT_MEMO_SKIP1 6   /* 1: batch launches search outer iteration 1 in full (no memo pass): the first LM
+                                 *    solve moves the queries past the memo's gaps, so its pass finds ~nothing
+                                 *    (default 1; 0: the memo pass from iteration 1) */
+#define LMSF_OPT_COUNT 7
 lmsf_status lmsf_set_option(lmsf_ctx* ctx, int32_t option, int32_t value);
 
 /* ---- diagnostics used by the parity tests and the roofline report (not on the reference surface) */

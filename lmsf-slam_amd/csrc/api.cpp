@@ -109,7 +109,7 @@ struct lmsf_ctx {
     lmsf_config cfg;
     std::string err;
     std::mutex err_mu;                // a tracker's commit worker may report an error beside the caller
-    int opt[LMSF_OPT_COUNT] = {1, 1, 1, 1, 1, 0};   // lmsf_set_option (defaults: lmsf.h)
+    int opt[LMSF_OPT_COUNT] = {1, 1, 1, 1, 1, 0, 1};   // lmsf_set_option (defaults: lmsf.h)
     // record capture (lmsf_batch_capture): device rows [n_cap][kCaptureIters][F] of the captured slots
     std::vector<int> cap_slots;
     lmsf_record* cap_rec = nullptr;
@@ -603,6 +603,10 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
     hipStream_t s = c->stream;
     const bool gn = c->cfg.solver == LMSF_SOLVER_GN;
     const bool memo_on = c->opt[LMSF_OPT_QUERY_MEMO] != 0;
+    // batch launches: memo pass + listed search in outer iterations > 0 of one solve (from 2 with
+    // LMSF_OPT_MEMO_SKIP1: iteration 1 then searches every query, as iteration 0 does)
+    const int memo_from = c->opt[LMSF_OPT_MEMO_SKIP1] ? 2 : 1;
+    auto batch_memo = [&](int o) { return o >= memo_from && !c->count27 && memo_on; };
     // record capture: every launch of this solve writes nnp (stores only: the same kernels, the same
     // results), so a captured slot's neighbours are readable after each outer iteration
     const bool capture = !c->cap_slots.empty();
@@ -623,7 +627,7 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
         if (fused && t) HIPCHK(c, launch_stamp(st0, s));
         if (fused) {
             BatchView bvo = bv;
-            bvo.memo = o > 0 && !c->count27 && memo_on ? 1 : 0;   // within one solve only
+            bvo.memo = batch_memo(o) ? 1 : 0;
             HIPCHK(c, launch_match_fit(ge, gs, bvo, s));
         }
         else {   // single-scan launches: the 8-lane search, with the slot memo under the Ceres-LM solver
@@ -658,9 +662,12 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
             HIPCHK(c, launch_gn_solve(bv, o, s));
         } else {
             BatchView bvb = bv;
-            if (fused) {   // packets: memo pass [0, ceil(nq / 64)) when it ran, search [part2_base, + ceil(n_search / 64))
+            if (fused && lin_eval_enabled()) {   // packets at x from one pass over the records
+                HIPCHK(c, launch_lin_eval(bv, s));
+                bvb.part_q = kEvalBlock;
+            } else if (fused) {   // packets: memo pass [0, ceil(nq / 64)) when it ran, search [part2_base, + ceil(n_search / 64))
                 bvb.fused_parts = 1;
-                bvb.memo = o > 0 && !c->count27 && memo_on && !match_fit_prune(ge, gs) ? 1 : 0;
+                bvb.memo = batch_memo(o) && !match_fit_prune(ge, gs) ? 1 : 0;
             }
             // single-scan launches: the whole LM of this outer iteration in one launch when its grid is
             // co-resident (lm_loop_kernel; A/B builds: LMSF_LM_LOOP=0 for the 9-launch form)

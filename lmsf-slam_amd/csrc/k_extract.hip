@@ -12,12 +12,16 @@
 //   ring_count   tiles of kTile raw points: ring id per point, per-tile ring histogram
 //   ring_offsets per scan: exclusive scan (ring-major) -> stable ring-ordered positions
 //   ring_scatter stable multisplit (wave ballots) into ring order
-//   sector_sort  one workgroup per (sector, ring): curvature + register-resident bitonic sort
-//   ring_features one workgroup per ring: automaton (wave-ballot walk), then per sector in order
-//                 {wave-ballot greedy pick over the sorted list, block-scan compaction}
-//   concat       per scan: edges (ring order) then surfs (ring order) into the feature array
+//   sector_sort  one workgroup per (sector, ring): curvature + register-resident sort by (c, index)
+//   ring_features one workgroup per ring: bad-point events + automaton, then the greedy edge picks of the
+//                 6 sectors in order on one wave while the other three trail it with the surf compactions;
+//                 each feature position's rank in the ring's search order
+//   concat       per scan: edges (ring order) then surfs (ring order) into the feature array, and the
+//                 fused search's order (fslot / featp)
 #include <hip/hip_runtime.h>
 #include <math.h>
+
+#include <type_traits>
 
 #include "lmsf_internal.h"
 
@@ -182,24 +186,38 @@ __device__ void ring_bad_points(const ExtractView& ev, const float4* pts, int si
     const int tid = threadIdx.x, lane = tid & 63;
     const int jmax = size - 7;  // checkBadEdgePoint visits j in [5, size - 7]
     if (ev.remove_bad) {
-        for (int j = 5 + tid; j <= jmax; j += NT) {
-            const float4 a = pts[j], c = pts[j + 1];
-            const double angle_curr = ref_atan2(a.x, a.y, ev.libm_float);   // atan2(x, y) order (FX:223-224)
-            const double angle_after = ref_atan2(c.x, c.y, ev.libm_float);
-            double delta_angle = fabs(angle_curr - angle_after);
-            if (delta_angle > M_PI) delta_angle = M_PI * 2 - delta_angle;
-            uint8_t e = 0;
-            if (delta_angle > 0.0175) {
-                e = 1;
-            } else {
-                const float sc = a.x * a.x + a.y * a.y + a.z * a.z;
-                const float sa = c.x * c.x + c.y * c.y + c.z * c.z;
-                const double dc = ref_sqrt(sc, ev.libm_float), da = ref_sqrt(sa, ev.libm_float);
-                const double ang = dc < da ? atan2(dc * delta_angle, da - dc) : atan2(da * delta_angle, dc - da);
-                if (ang <= 0.17) e = dc < da ? 2 : 3;
+        // events per point: thread t takes a contiguous run of j, so the azimuth of point j + 1 (its
+        // angle_after) is its next j's angle_curr -- one atan2 per point instead of two
+        const int nj = jmax - 4;
+        const int per = (nj + NT - 1) / NT;
+        const int j0 = 5 + tid * per, j1 = min(j0 + per, jmax + 1);
+#ifndef LMSF_AB_NO_EVENTS   // A/B ablation builds only
+        if (j0 < j1) {
+            float4 a = pts[j0];
+            double angle_curr = ref_atan2(a.x, a.y, ev.libm_float);   // atan2(x, y) order (FX:223-224)
+            for (int j = j0; j < j1; ++j) {
+                const float4 c = pts[j + 1];
+                const double angle_after = ref_atan2(c.x, c.y, ev.libm_float);
+                double delta_angle = fabs(angle_curr - angle_after);
+                if (delta_angle > M_PI) delta_angle = M_PI * 2 - delta_angle;
+                uint8_t e = 0;
+                if (delta_angle > 0.0175) {
+                    e = 1;
+                } else {
+                    const float sc = a.x * a.x + a.y * a.y + a.z * a.z;
+                    const float sa = c.x * c.x + c.y * c.y + c.z * c.z;
+                    const double dc = ref_sqrt(sc, ev.libm_float), da = ref_sqrt(sa, ev.libm_float);
+                    const double ang = dc < da ? atan2(dc * delta_angle, da - dc) : atan2(da * delta_angle, dc - da);
+                    if (ang <= 0.17) e = dc < da ? 2 : 3;
+                }
+                flag[j] = e;
+                a = c;
+                angle_curr = angle_after;
             }
-            flag[j] = e;
         }
+#else
+        for (int j = j0; j < j1; ++j) flag[j] = 0;
+#endif
         __syncthreads();
         // sequential skip automaton (next j = j + 5 after event 1 / 2, else j + 1), 64 at a time
         if (tid < 64) {
@@ -231,27 +249,76 @@ __device__ void ring_bad_points(const ExtractView& ev, const float4* pts, int si
     }
 }
 
-// Bitonic sort of npow (key, index) pairs ascending by (key, index), keys/indices in LDS on entry
-// and exit.  Elements live in registers: wave w owns positions [w * 64E, (w + 1) * 64E), lane l
-// holds w * 64E + e * 64 + l (e < E).  A compare-exchange at distance jj < 64 is a lane shuffle,
-// 64 <= jj < 64E a swap inside the thread, and only jj >= 64E crosses waves (LDS + barrier):
-// 2 of the 55 stages of a 1024-element sort with E = 4, instead of 55 barrier stages.
+// Sort of n (key, index) pairs ascending by (key, index), n <= npow = 64 E * 4: keys (non-negative
+// doubles, compared as their u64 bit patterns, which order alike) and indices in LDS on entry and exit,
+// positions [n, npow) holding pads (key ~0: above every double) on entry.
+//   1. A bitonic network in its ascending-only form: merge step kk opens with a "flip" stage (partner
+//      i ^ (kk - 1)) and continues with half-cleaners (partner i ^ jj); every comparator puts the smaller
+//      key at the lower position, so the pads never leave [n, npow) and a wave whose positions all lie
+//      there has nothing to do (n = 650 of a C2 sector: 3 of 4 waves work).  Keys only: equal keys do not
+//      swap, so they end up adjacent in some order.
+//   2. Runs of equal keys are put in index order (rank by index inside the run), giving the (key, index)
+//      order of a comparison sort with the index as tie-break.
+// Elements live in registers: wave w owns positions [w * 64E, (w + 1) * 64E), lane l holds
+// w * 64E + e * 64 + l (e < E).  A partner that differs in the lane bits only is a shuffle, in the e bits
+// (+ lane bits) a register pick (+ shuffle), and only partners in another wave go through LDS.
 template <int E>
-__device__ void bitonic_sort_regs(double* key, int* kidx, int npow) {
+__device__ void sector_sort_regs(uint64_t* key, int* kidx, int n, int npow) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int chunk = 64 * E;
-    const bool active = w * chunk < npow;
-    double k[E];
+    constexpr int chunk = 64 * E;
+    const bool active = w * chunk < n;
+    uint64_t k[E];
     int id[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int i = w * chunk + e * 64 + lane;
-        k[e] = active ? key[i] : 0.0;
-        id[e] = active ? kidx[i] : 0;
+        k[e] = active ? key[i] : ~0ull;
+        id[e] = active ? kidx[i] : 0x7fffffff;
     }
+    // one stage with partner i ^ m, m < chunk (inside the wave): register e ^ ME of the lane l ^ ml
+    auto stage_wave = [&](auto me_tag, int ml) {
+        constexpr int ME = decltype(me_tag)::value;
+        uint64_t ko[E];
+        int io[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            ko[e] = k[e ^ ME];
+            io[e] = id[e ^ ME];
+        }
+        if (ml) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const uint32_t lo = __shfl_xor((uint32_t)ko[e], ml, 64), hi = __shfl_xor((uint32_t)(ko[e] >> 32), ml, 64);
+                ko[e] = ((uint64_t)hi << 32) | lo;
+                io[e] = __shfl_xor(io[e], ml, 64);
+            }
+        }
+        const int m = (ME << 6) | ml;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = w * chunk + e * 64 + lane;
+            const bool take = ((i ^ m) > i) ? ko[e] < k[e] : ko[e] > k[e];   // lower position keeps the smaller
+            if (take) { k[e] = ko[e]; id[e] = io[e]; }
+        }
+    };
+    auto stage = [&](int m) {
+        const int ml = m & 63, me = (m >> 6) & (E - 1);   // uniform: one branch per stage
+        if (me == 0) stage_wave(std::integral_constant<int, 0>{}, ml);
+        if constexpr (E > 1) if (me == 1) stage_wave(std::integral_constant<int, (E > 1 ? 1 : 0)>{}, ml);
+        if constexpr (E > 2) {
+            if (me == 2) stage_wave(std::integral_constant<int, (E > 2 ? 2 : 0)>{}, ml);
+            if (me == 3) stage_wave(std::integral_constant<int, (E > 2 ? 3 : 0)>{}, ml);
+        }
+        if constexpr (E > 4) {
+            if (me == 4) stage_wave(std::integral_constant<int, (E > 4 ? 4 : 0)>{}, ml);
+            if (me == 5) stage_wave(std::integral_constant<int, (E > 4 ? 5 : 0)>{}, ml);
+            if (me == 6) stage_wave(std::integral_constant<int, (E > 4 ? 6 : 0)>{}, ml);
+            if (me == 7) stage_wave(std::integral_constant<int, (E > 4 ? 7 : 0)>{}, ml);
+        }
+    };
     for (int kk = 2; kk <= npow; kk <<= 1) {
-        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-            if (jj >= chunk) {                         // partner in another wave: through LDS
+        for (int m = kk - 1, jj = kk; jj > 1; jj >>= 1, m = jj >> 1) {   // flip (kk - 1), then kk/4 .. 1
+            if (m >= chunk) {                          // partner in another wave: through LDS
                 __syncthreads();
                 if (active) {
 #pragma unroll
@@ -265,45 +332,15 @@ __device__ void bitonic_sort_regs(double* key, int* kidx, int npow) {
                 if (active) {
 #pragma unroll
                     for (int e = 0; e < E; ++e) {
-                        const int i = w * chunk + e * 64 + lane, ixj = i ^ jj;
-                        const double ko = key[ixj];
-                        const int io = kidx[ixj];
-                        const bool lower = i < ixj;
-                        const double ka = lower ? k[e] : ko, kb = lower ? ko : k[e];
-                        const int ia = lower ? id[e] : io, ib = lower ? io : id[e];
-                        const bool a_gt_b = ka > kb || (ka == kb && ia > ib);
-                        const bool up = (i & kk) == 0;
-                        if (up == a_gt_b) { k[e] = ko; id[e] = io; }
+                        const int i = w * chunk + e * 64 + lane, p = i ^ m;
+                        const uint64_t ko = key[p];
+                        const int io = kidx[p];
+                        const bool take = p > i ? ko < k[e] : ko > k[e];
+                        if (take) { k[e] = ko; id[e] = io; }
                     }
                 }
-            } else if (jj >= 64) {                     // same thread, another register
-                const int ej = jj >> 6;
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const int e2 = e ^ ej;
-                    if (e2 > e) {
-                        const int i = w * chunk + e * 64 + lane;
-                        const bool a_gt_b = k[e] > k[e2] || (k[e] == k[e2] && id[e] > id[e2]);
-                        const bool up = (i & kk) == 0;
-                        if (up == a_gt_b) {
-                            const double tk = k[e]; k[e] = k[e2]; k[e2] = tk;
-                            const int ti = id[e]; id[e] = id[e2]; id[e2] = ti;
-                        }
-                    }
-                }
-            } else {                                   // same register, another lane
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const int i = w * chunk + e * 64 + lane;
-                    const double ko = __shfl_xor(k[e], jj, 64);
-                    const int io = __shfl_xor(id[e], jj, 64);
-                    const bool lower = (lane & jj) == 0;
-                    const double ka = lower ? k[e] : ko, kb = lower ? ko : k[e];
-                    const int ia = lower ? id[e] : io, ib = lower ? io : id[e];
-                    const bool a_gt_b = ka > kb || (ka == kb && ia > ib);
-                    const bool up = (i & kk) == 0;
-                    if (up == a_gt_b) { k[e] = ko; id[e] = io; }
-                }
+            } else if (active) {
+                stage(m);
             }
         }
     }
@@ -316,6 +353,33 @@ __device__ void bitonic_sort_regs(double* key, int* kidx, int npow) {
             kidx[i] = id[e];
         }
     }
+    __syncthreads();
+    // equal keys: rank by index inside the run (positions held in registers until every rank is read)
+    constexpr int kPer = (kSortMax + 255) / 256;
+    int fix_pos[kPer], fix_id[kPer];
+#pragma unroll
+    for (int t = 0; t < kPer; ++t) {
+        const int i = threadIdx.x + 256 * t;
+        fix_pos[t] = -1;
+        fix_id[t] = 0;
+        if (i < n) {
+            const uint64_t kv = key[i];
+            if ((i > 0 && key[i - 1] == kv) || (i + 1 < n && key[i + 1] == kv)) {
+                int s0 = i, e0 = i + 1;
+                while (s0 > 0 && key[s0 - 1] == kv) --s0;
+                while (e0 < n && key[e0] == kv) ++e0;
+                const int mine = kidx[i];
+                int r = 0;
+                for (int j = s0; j < e0; ++j) r += kidx[j] < mine;
+                fix_pos[t] = s0 + r;
+                fix_id[t] = mine;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < kPer; ++t)
+        if (fix_pos[t] >= 0) kidx[fix_pos[t]] = fix_id[t];
     __syncthreads();
 }
 
@@ -332,7 +396,7 @@ __device__ __forceinline__ void sector_bounds(int size, int k, int& s0, int& n) 
 // place in the ring.  The 6 sectors of a ring sort concurrently; only the greedy pick, which
 // carries disable marks across sectors, stays sequential (ring_features_kernel).
 __global__ __launch_bounds__(256) void sector_sort_kernel(ExtractView ev) {
-    __shared__ double key[kSortMax];
+    __shared__ uint64_t key[kSortMax];
     __shared__ int kidx[kSortMax];
     const int r = blockIdx.x / 6, k = blockIdx.x % 6, b = blockIdx.y;
     const int* rs = ev.ring_start + (size_t)b * (kMaxRings + 1);
@@ -355,39 +419,46 @@ __global__ __launch_bounds__(256) void sector_sort_kernel(ExtractView ev) {
             const float fy = m5.y + m4.y + m3.y + m2.y + m1.y - 10 * p0.y + q1.y + q2.y + q3.y + q4.y + q5.y;
             const float fz = m5.z + m4.z + m3.z + m2.z + m1.z - 10 * p0.z + q1.z + q2.z + q3.z + q4.z + q5.z;
             const double dx = fx, dy = fy, dz = fz;
-            key[i] = dx * dx + dy * dy + dz * dz;
+            key[i] = (uint64_t)__double_as_longlong(dx * dx + dy * dy + dz * dz);
             kidx[i] = j;
         } else {
-            key[i] = __builtin_huge_val();
+            key[i] = ~0ull;
             kidx[i] = 0x7fffffff;
         }
     }
     __syncthreads();
-    if (npow <= 256) bitonic_sort_regs<1>(key, kidx, npow);
-    else if (npow <= 512) bitonic_sort_regs<2>(key, kidx, npow);
-    else if (npow <= 1024) bitonic_sort_regs<4>(key, kidx, npow);
-    else bitonic_sort_regs<8>(key, kidx, npow);
+    if (npow <= 256) sector_sort_regs<1>(key, kidx, n, npow);
+    else if (npow <= 512) sector_sort_regs<2>(key, kidx, n, npow);
+    else if (npow <= 1024) sector_sort_regs<4>(key, kidx, n, npow);
+    else sector_sort_regs<8>(key, kidx, n, npow);
     double* okey = ev.sort_key + (size_t)b * ev.raw_stride + start + s0;
     int* oidx = ev.sort_idx + (size_t)b * ev.raw_stride + start + s0;
     for (int i = threadIdx.x; i < n; i += 256) {
-        okey[i] = key[i];
+        okey[i] = __longlong_as_double((long long)key[i]);
         oidx[i] = kidx[i];
     }
 }
 
-// One workgroup per (ring, scan): bad-point automaton, then per sector in order the greedy edge
-// pick over the pre-sorted curvature list and the surf compaction.
+// One workgroup per (ring, scan): bad-point automaton (all waves: events; wave 0: the skip walk), then
+// wave 0 runs the greedy edge picks of the 6 sectors in order (FX:157-195; disable marks leak across
+// sectors) while waves 1-3 trail it with the surf compactions (FX:197-206), sector k on wave 1 + k % 3
+// as soon as wave 0 has published sector k's picks: a sector's surfs are its points not picked in that
+// sector, so its compaction needs nothing from later sectors, and its output offset is the earlier
+// sectors' point counts minus their picks.  The pick reads the top kPickWin entries of the sector's
+// sorted list from an LDS window (the next sector's window is loaded while the current one is picked),
+// deeper entries from global memory; no sector is staged whole, so a block needs ~19 KB of LDS.
+constexpr int kPickWin = 256;
 __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
     __shared__ uint8_t dis[kRingMax];
     __shared__ uint8_t flag[kRingMax];
-    __shared__ double key[kSortMax];
-    __shared__ int kidx[kSortMax];
-    __shared__ int scan_part[256];
+    __shared__ double wkey[kPickWin];
+    __shared__ int widx[kPickWin];
     __shared__ int pick[20];
-    __shared__ int sh_ec, sh_sc, sh_err;
-    constexpr int kSurfPer = 3;   // sector points per thread held in registers by the surf compaction
+    __shared__ int sh_e[6];       // edges picked in sector k
+    __shared__ int sh_done;       // sectors whose picks are published
+    __shared__ int sh_sc[6];      // surfs of sector k (written by its compaction wave)
     const int r = blockIdx.x, b = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int* rs = ev.ring_start + (size_t)b * (kMaxRings + 1);
     const int start = rs[r];
     const int size = rs[r + 1] - start;
@@ -406,44 +477,60 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
     const float4* pts = ev.ring_pts + (size_t)b * ev.raw_stride + start;
     const int* psrc = ev.ring_src + (size_t)b * ev.raw_stride + start;
     for (int j = tid; j < size; j += 256) { dis[j] = 0; flag[j] = 0; qc[j] = -1; }
-    if (tid == 0) { sh_ec = 0; sh_sc = 0; sh_err = 0; }
+    if (tid == 0) sh_done = 0;
     __syncthreads();
-    ring_bad_points<256>(ev, pts, size, dis, flag);
-    const double thresh = (double)ev.edge_thresh;
-    float4* estage = ev.edge_stage + ((size_t)b * kMaxRings + r) * kEdgePerRing;
-    int* estage_src = ev.edge_stage_src + ((size_t)b * kMaxRings + r) * kEdgePerRing;
-    float4* sstage = ev.surf_stage + (size_t)b * ev.raw_stride + start;
-    int* sstage_src = ev.surf_stage_src + (size_t)b * ev.raw_stride + start;
-    for (int k = 0; k < 6; ++k) {
-        int s0, n;
-        sector_bounds(size, k, s0, n);
-        if (n > kSortMax) {
-            if (tid == 0) { atomicOr(ev.error, 2); sh_err = 1; }
-            break;
-        }
-        const double* skey = ev.sort_key + (size_t)b * ev.raw_stride + start + s0;
-        const int* sidx = ev.sort_idx + (size_t)b * ev.raw_stride + start + s0;
-        for (int i = tid; i < n; i += 256) {
-            key[i] = skey[i];
-            kidx[i] = sidx[i];
-        }
-        __syncthreads();
-        // greedy edge pick, largest curvature first (FX:157-195), one wave
-        if (tid < 64) {
-            int pos = n - 1, picked = 0, ec = sh_ec;
+    ring_bad_points<256>(ev, pts, size, dis, flag);   // ends with a barrier; flag cleared (is_edge)
+    const double* skey_ring = ev.sort_key + (size_t)b * ev.raw_stride + start;
+    const int* sidx_ring = ev.sort_idx + (size_t)b * ev.raw_stride + start;
+    int s0_[6], n_[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) sector_bounds(size, k, s0_[k], n_[k]);
+    const bool fits = n_[5] <= kSortMax && n_[0] <= kSortMax;   // uniform: sector_sort_kernel's bound
+    if (wave == 0) {
+        const double thresh = (double)ev.edge_thresh;
+        float4* estage = ev.edge_stage + ((size_t)b * kMaxRings + r) * kEdgePerRing;
+        int* estage_src = ev.edge_stage_src + ((size_t)b * kMaxRings + r) * kEdgePerRing;
+        constexpr int kWin = kPickWin / 64;
+        double pk[kWin];
+        int pi[kWin];
+        auto fetch = [&](int k) {   // sector k's window [n - kPickWin, n) into registers
+#pragma unroll
+            for (int u = 0; u < kWin; ++u) {
+                const int i = n_[k] - kPickWin + u * 64 + lane;
+                pk[u] = i >= 0 ? skey_ring[s0_[k] + i] : 0.0;
+                pi[u] = i >= 0 ? sidx_ring[s0_[k] + i] : 0;
+            }
+        };
+        if (fits) fetch(0);
+        int ec = 0;
+        for (int k = 0; k < 6 && fits; ++k) {
+            const int n = n_[k], wlo = n - kPickWin;   // window: sorted positions [wlo, n)
+#pragma unroll
+            for (int u = 0; u < kWin; ++u) {
+                wkey[u * 64 + lane] = pk[u];
+                widx[u * 64 + lane] = pi[u];
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (k < 5) fetch(k + 1);   // in flight during this sector's pick
+            const double* skey = skey_ring + s0_[k];
+            const int* sidx = sidx_ring + s0_[k];
+            auto idx_at = [&](int i) { return i >= wlo ? widx[i - wlo] : sidx[i]; };
+            auto key_at = [&](int i) { return i >= wlo ? wkey[i - wlo] : skey[i]; };
+            int pos = n - 1, picked = 0;
+            const int ec0 = ec;
             while (pos >= 0) {
                 const int cand = pos - lane;
-                const bool elig = cand >= 0 && dis[kidx[cand]] == 0;
+                const bool elig = cand >= 0 && dis[idx_at(cand)] == 0;
                 const unsigned long long m = __ballot(elig);
                 if (!m) { pos -= 64; continue; }
                 const int f = __ffsll((long long)m) - 1;
-                const double c = key[pos - f];
-                const int ind = kidx[pos - f];
+                const double c = key_at(pos - f);
+                const int ind = idx_at(pos - f);
                 if (c <= thresh) break;
                 ++picked;
                 if (picked > 20) break;
                 if (lane == 0) {
-                    pick[picked - 1] = ind;   // staged after the loop: no load -> store round trip per pick
+                    pick[picked - 1] = ind;
                     flag[ind] = 1;
                     qc[ind] = ec;
                 }
@@ -452,72 +539,91 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
                 ++ec;
                 pos = pos - f - 1;
             }
-            if (lane == 0) sh_ec = ec;
-            const int ec0 = ec - min(picked, 20);
             for (int t = lane; t < ec - ec0; t += 64) {
                 const int ind = pick[t];
                 estage[ec0 + t] = pts[ind];
                 estage_src[ec0 + t] = psrc[ind];
             }
+            if (lane == 0) {
+                sh_e[k] = ec - ec0;
+                __hip_atomic_store(&sh_done, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
-        __syncthreads();
-        // surf: every sector point not picked as edge, ascending curvature (FX:197-206);
-        // contiguous chunk per thread, block prefix from wave scans
-        const int per = (n + 255) / 256;
-        const int lo = tid * per, hi = min(lo + per, n);
-        int cntv = 0;
-        for (int i = lo; i < hi; ++i) cntv += flag[kidx[i]] == 0;
-        int incl = cntv;
+        if (lane == 0 && !fits) {
+            atomicOr(ev.error, 2);
+            __hip_atomic_store(&sh_done, 6, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (lane == 0) ecnt[r] = fits ? ec : 0;
+    } else if (fits) {
+        float4* sstage = ev.surf_stage + (size_t)b * ev.raw_stride + start;
+        int* sstage_src = ev.surf_stage_src + (size_t)b * ev.raw_stride + start;
+        for (int k = wave - 1; k < 6; k += 3) {
+            while (__hip_atomic_load(&sh_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= k)
+                __builtin_amdgcn_s_sleep(2);
+            int o = 0;   // surfs of the earlier sectors
+            for (int k2 = 0; k2 < k; ++k2) o += n_[k2] - sh_e[k2];
+            const int n = n_[k];
+            const int* sidx = sidx_ring + s0_[k];
+            // ascending curvature, 64 positions per step, 4 steps' index loads in flight
+            for (int c0 = 0; c0 < n; c0 += 256) {
+                int ind[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = c0 + u * 64 + lane;
+                    ind[u] = i < n ? sidx[i] : -1;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const bool keep = ind[u] >= 0 && flag[ind[u]] == 0;
+                    const unsigned long long m = __ballot(keep);
+                    if (keep) {
+                        const int dst = o + __popcll(m & lanemask_lt(lane));
+                        sstage[dst] = pts[ind[u]];
+                        sstage_src[dst] = psrc[ind[u]];
+                        qc[ind[u]] = kQSurf | dst;
+                    }
+                    o += __popcll(m);
+                }
+            }
+            if (lane == 0) sh_sc[k] = n - sh_e[k];
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int sc = 0;
+        for (int k = 0; k < 6; ++k) sc += sh_sc[k];
+        scnt[r] = fits ? sc : 0;
+    }
+    if (!fits) return;   // uniform: the ring's counts are 0, concat_kernel ignores its codes
+    // Search order inside the ring: every feature position's rank among the ring's features of its kind in
+    // ring order, packed into its code (bits 13-25) for concat_kernel, which places the position at its kind's
+    // ring base + rank (edges before surfs: the fused search's order).  Positions [5, size - 6] are the
+    // sectors': picked (flag) -> edge, else surf.  Block scan over contiguous chunks, (edge, surf) counts
+    // packed 16 | 16 bits.
+    {
+        __shared__ uint32_t wsum[4];
+        const int per = (size + 255) / 256;
+        const int p0 = min(tid * per, size), p1 = min(p0 + per, size);
+        uint32_t cnt = 0;
+        for (int p = p0; p < p1; ++p) {
+            if (flag[p]) cnt += 1u;
+            else if (p >= 5 && p <= size - 6) cnt += 0x10000u;
+        }
+        uint32_t x = cnt;
 #pragma unroll
         for (int o2 = 1; o2 < 64; o2 <<= 1) {
-            const int t = __shfl_up(incl, o2, 64);
-            if (lane >= o2) incl += t;
+            const uint32_t y = __shfl_up(x, o2, 64);
+            if (lane >= o2) x += y;
         }
-        if (lane == 63) scan_part[tid >> 6] = incl;
+        if (lane == 63) wsum[wave] = x;
         __syncthreads();
-        int wbase = 0;
-        for (int w2 = 0; w2 < (tid >> 6); ++w2) wbase += scan_part[w2];
-        int o = sh_sc + wbase + incl - cntv;
-        if (per <= kSurfPer) {   // every point load in flight before the first store
-            int ind[kSurfPer];
-            float4 sp[kSurfPer];
-            int ss[kSurfPer];
-#pragma unroll
-            for (int u = 0; u < kSurfPer; ++u) {
-                const int i = lo + u;
-                ind[u] = i < hi && flag[kidx[i]] == 0 ? kidx[i] : -1;
-                if (ind[u] >= 0) {
-                    sp[u] = pts[ind[u]];
-                    ss[u] = psrc[ind[u]];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kSurfPer; ++u) {
-                if (ind[u] >= 0) {
-                    sstage[o] = sp[u];
-                    sstage_src[o] = ss[u];
-                    qc[ind[u]] = kQSurf | o;
-                    ++o;
-                }
-            }
-        } else {
-            for (int i = lo; i < hi; ++i) {
-                const int ind1 = kidx[i];
-                if (flag[ind1] == 0) {
-                    sstage[o] = pts[ind1];
-                    sstage_src[o] = psrc[ind1];
-                    qc[ind1] = kQSurf | o;
-                    ++o;
-                }
-            }
+        uint32_t ex = x - cnt;
+        for (int w2 = 0; w2 < wave; ++w2) ex += wsum[w2];
+        uint32_t re = ex & 0xffffu, rsf = ex >> 16;
+        for (int p = p0; p < p1; ++p) {
+            if (flag[p]) qc[p] = qc[p] | (int)(re++ << kQRankShift);
+            else if (p >= 5 && p <= size - 6) qc[p] = qc[p] | (int)(rsf++ << kQRankShift);
         }
-        __syncthreads();
-        if (tid == 255) sh_sc = o;  // thread 255's running offset is the sector's total
-        __syncthreads();
-    }
-    if (tid == 0) {
-        ecnt[r] = sh_err ? 0 : sh_ec;
-        scnt[r] = sh_err ? 0 : sh_sc;
     }
 }
 
@@ -594,105 +700,33 @@ __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
     // (capacity flags) are ignored through the ring counts.
     const int npos = rs[nr];
     if (blockIdx.x == 0 && threadIdx.x == 0) ev.n_pos[b] = npos;
+    // The fused search's order (fslot / featp): edges of ring 0..N-1 then surfs, each ring's in ring order
+    // (ring_features_kernel packed every position's rank among its ring's features of its kind into its code).
     const int* qc = ev.qcode + (size_t)b * ev.raw_stride;
     int* qs = ev.qslot + (size_t)b * ev.raw_stride;
+    int* fs = ev.fslot + (size_t)b * ev.feat_stride;
+    float4* fp = ev.featp + (size_t)b * ev.feat_stride;
+    const float4* rp = ev.ring_pts + (size_t)b * ev.raw_stride;
     for (int p = blockIdx.x * 256 + threadIdx.x; p < npos; p += gridDim.x * 256) {
         int lo = 0, hi = nr - 1;  // last ring with rs[r] <= p
         while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (rs[mid] <= p) lo = mid; else hi = mid - 1; }
         const int code = qc[p];
-        int slot = -1;
+        int slot = -1, o = -1;
         if (code >= 0) {
-            const int l = code & ~kQSurf;
+            const int l = code & kQCodeMask, rank = (code >> kQRankShift) & kQCodeMask;
             if (code & kQSurf) {
-                if (l < spre[lo + 1] - spre[lo]) slot = ne + spre[lo] + l;
+                if (l < spre[lo + 1] - spre[lo]) { slot = ne + spre[lo] + l; o = ne + spre[lo] + rank; }
             } else if (l < epre[lo + 1] - epre[lo]) {
                 slot = epre[lo] + l;
+                o = epre[lo] + rank;
             }
         }
         qs[p] = slot;
-    }
-}
-
-// Stable partition of the search order by kind: fslot = the valid entries of qslot, edge slots
-// (slot < n_edge) first, each kind in ring order (the fused search + fit order: neighbouring lanes
-// search neighbouring ring points, and a wave runs one fit kind).  One block per (ring, slot): a
-// ring's valid positions are exactly its ring_edge_cnt edges and ring_surf_cnt surfs (concat_kernel),
-// so ring r writes edges from epre[r] and surfs from n_edge + spre[r]; inside the ring a block-wide
-// exclusive scan of the packed (edge, surf) counts (16 bits each) of 8 consecutive positions per
-// thread, 2048 positions per chunk.
-__global__ __launch_bounds__(256) void order_kernel(ExtractView ev) {
-    constexpr int E = 8;
-    __shared__ uint32_t wsum[4];
-    __shared__ int pre[2];
-    const int r = blockIdx.x, b = blockIdx.y;
-    const int nr = ev.n_scans;
-    if (threadIdx.x < 64) {   // one wave: ring-count prefixes below r
-        int e = 0, sc = 0;
-        for (int k = threadIdx.x; k < r; k += 64) {
-            e += ev.ring_edge_cnt[(size_t)b * kMaxRings + k];
-            sc += ev.ring_surf_cnt[(size_t)b * kMaxRings + k];
+        if (o >= 0 && o < ev.feat_stride) {
+            const float4 q = rp[p];
+            fs[o] = slot;
+            fp[o] = make_float4(q.x, q.y, q.z, __int_as_float(slot));
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            e += __shfl_xor(e, o, 64);
-            sc += __shfl_xor(sc, o, 64);
-        }
-        if (threadIdx.x == 0) { pre[0] = e; pre[1] = sc; }
-    }
-    __syncthreads();
-    if (r >= nr) return;
-    const int ne = ev.n_edge[b];
-    const int* rs = ev.ring_start + (size_t)b * (kMaxRings + 1);
-    const int p0 = rs[r], p1 = rs[r + 1];
-    const int* qs = ev.qslot + (size_t)b * ev.raw_stride;
-    int* fs = ev.fslot + (size_t)b * ev.feat_stride;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t base_e = (uint32_t)pre[0], base_s = (uint32_t)(ne + pre[1]);
-    for (int c0 = p0; c0 < p1; c0 += 256 * E) {
-        int v[E];
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const int p = c0 + threadIdx.x * E + e;
-            v[e] = p < p1 ? qs[p] : -1;
-            if (v[e] >= 0) cnt += v[e] < ne ? 1u : 0x10000u;
-        }
-        uint32_t x = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) wsum[wave] = x;
-        __syncthreads();
-        uint32_t wpre = 0, tot = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const uint32_t t = wsum[w];
-            wpre += w < wave ? t : 0u;
-            tot += t;
-        }
-        const uint32_t ex = wpre + x - cnt;
-        uint32_t oe = base_e + (ex & 0xffffu), os = base_s + (ex >> 16);
-        // all E feature loads first, then the stores (a load after a store to featp, which the compiler
-        // cannot prove distinct from feat, would wait for it: E serial round trips per chunk)
-        uint32_t o[E];
-        float4 f[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            o[e] = v[e] < 0 ? 0xffffffffu : (v[e] < ne ? oe++ : os++);
-            f[e] = o[e] < (uint32_t)ev.feat_stride ? ev.feat[(size_t)b * ev.feat_stride + v[e]] : make_float4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            if (o[e] < (uint32_t)ev.feat_stride) {
-                fs[o[e]] = v[e];
-                ev.featp[(size_t)b * ev.feat_stride + o[e]] = make_float4(f[e].x, f[e].y, f[e].z, __int_as_float(v[e]));
-            }
-        }
-        base_e += tot & 0xffffu;
-        base_s += tot >> 16;
-        __syncthreads();   // wsum is rewritten by the next chunk
     }
 }
 
@@ -709,7 +743,6 @@ hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
     }();
     const int cblocks = min(cmax, (ev.raw_stride + 255) / 256);
     hipLaunchKernelGGL(concat_kernel, dim3(max(cblocks, 1), ev.B), dim3(256), 0, s, ev);
-    hipLaunchKernelGGL(order_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
     return hipGetLastError();
 }
 

@@ -846,6 +846,15 @@ __device__ __forceinline__ void record_packet(int kind, const float4 p, const d3
     P[30] += kind == LMSF_SURF ? 1.0 : 0.0;
 }
 
+// LMSF_LIN_EVAL (default 1): the batch path's packets at the linearisation pose come from one evaluation
+// pass over all records after the matching (lm_eval_kernel<true>, counts included), so the memo pass and the
+// search kernel only write records -- no residual / Jacobian / Huber packet or wave reduction in them.  0 (A/B
+// builds): the memo pass and the search kernel accumulate the packets themselves, one per wave.
+#ifndef LMSF_LIN_EVAL
+#define LMSF_LIN_EVAL 1
+#endif
+constexpr bool kLinEval = LMSF_LIN_EVAL != 0;
+
 // Entries of one memo block's work list per scan: wcount stride.
 __host__ __device__ __forceinline__ size_t memo_blocks(size_t feat_stride) { return feat_stride / 256 + 1; }
 
@@ -952,14 +961,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_W
                             v1x = -v1x;
                             store_record(bv, slot, p, kind, v0, v1x, 0.0, 0.0);
                         }
-                    } else {
+                    } else if (!kLinEval) {
                         const double2 e = bv.rec_e[slot];
                         v1y = e.x;
                         v1z = e.y;
                     }
                 }
                 if (reuse) {
-                    record_packet(kind, p, v0, v1x, v1y, v1z, Ps, P);
+                    if (!kLinEval) record_packet(kind, p, v0, v1x, v1y, v1z, Ps, P);
                     need = false;
                     refit = false;
                     n_reused = 1;
@@ -967,7 +976,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_W
             }
         }
     }
-    if (bx * 256 + wave * 64 < nq)
+    if (!kLinEval && bx * 256 + wave * 64 < nq)
         wave_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + (size_t)bx * 4 + wave) * kPacket);
     // this block's positions still needing a search, in position order from the front of its segment,
     // and those needing only a refit, in position order from its back (deterministic)
@@ -1206,9 +1215,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         }
 #endif
         store_record(bv, ppos, p, kind, v0, v1x, v1y, v1z);   // records by search position
-        record_packet(kind, p, v0, v1x, v1y, v1z, Ps, P);
+        if (!kLinEval) record_packet(kind, p, v0, v1x, v1y, v1z, Ps, P);
     }
-    if (bx * 256 + wave * 64 < total)
+    if (!kLinEval && bx * 256 + wave * 64 < total)
         wave_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + bv.part2_base + (size_t)bx * 4 + wave) * kPacket);
     if (bv.n27) {   // accounting runs: n27 of the searches (+ the queries when there was no memo pass)
         unsigned int qn = (!LIST && e < total) ? 1u : 0u;
@@ -1238,9 +1247,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
 #ifndef LMSF_EVAL_WAVES   // waves per SIMD lm_eval_kernel is compiled for (A/B)
 #define LMSF_EVAL_WAVES 4
 #endif
+template <bool COUNT = false>
 __device__ __forceinline__ void eval_record(const Pose& Ps, bool valid, const float4 rp, const RecV& v, const double2 e,
                                             double* P) {
     const int kind = __float_as_int(rp.w);
+    if (COUNT) {   // match counts (fit_query's P[29] / P[30])
+        P[29] += valid && kind == LMSF_EDGE ? 1.0 : 0.0;
+        P[30] += valid && kind == LMSF_SURF ? 1.0 : 0.0;
+    }
     if (valid && kind != 0) {
         double J[6], res;
         const d3 pp = mk((double)rp.x, (double)rp.y, (double)rp.z);
@@ -1252,12 +1266,15 @@ __device__ __forceinline__ void eval_record(const Pose& Ps, bool valid, const fl
     }
 }
 
+// LIN: the evaluation at the linearisation pose x of the batch path (after the matching; lm_begin reduces
+// its packets, match counts included); else at the LM candidate xc of slots that need one.
+template <bool LIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_EVAL_WAVES))) void lm_eval_kernel(BatchView bv) {
     const int b = blockIdx.y;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
     if (blockIdx.x * kEvalBlock >= nq) return;
-    if (!bv.st[b].need_eval) return;
-    const Pose Ps = load_pose(bv.st[b].xc);
+    if (!LIN && !bv.st[b].need_eval) return;
+    const Pose Ps = load_pose(LIN ? bv.st[b].x : bv.st[b].xc);
     double P[kPacket];
 #pragma unroll
     for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
@@ -1285,7 +1302,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_EVAL_W
         }
         double2 en = ez;
         if (k + 1 < kEvalPerThread && __float_as_int(p1.w) == LMSF_EDGE) en = bv.rec_e[slot_of(k + 1)];
-        eval_record(Ps, q0 + k * 256 < nq, p0, v0, e0, P);
+        eval_record<LIN>(Ps, q0 + k * 256 < nq, p0, v0, e0, P);
         p0 = p1; v0 = v1; e0 = en;
         p1 = pn; v1 = vn;
     }
@@ -1300,7 +1317,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_EVAL_W
 #pragma unroll
     for (int k = 0; k < kEvalPerThread; ++k) {
         const bool edge = __float_as_int(rp[k].w) == LMSF_EDGE;
-        eval_record(Ps, q0 + k * 256 < nq, rp[k], rv[k], edge ? bv.rec_e[slot_of(k)] : make_double2(0.0, 0.0), P);
+        eval_record<LIN>(Ps, q0 + k * 256 < nq, rp[k], rv[k], edge ? bv.rec_e[slot_of(k)] : make_double2(0.0, 0.0), P);
     }
 #endif
     block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + blockIdx.x) * kPacket);
@@ -1642,10 +1659,18 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
 
 hipError_t launch_lm_eval_step(const BatchView& bv, int outer, int is_last, hipStream_t s) {
     dim3 grid((bv.feat_stride + kEvalBlock - 1) / kEvalBlock, bv.B);
-    hipLaunchKernelGGL(lm_eval_kernel, grid, dim3(256), 0, s, bv);
+    hipLaunchKernelGGL(lm_eval_kernel<false>, grid, dim3(256), 0, s, bv);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_lm_step(bv, outer, is_last, s);
+}
+
+bool lin_eval_enabled() { return kLinEval; }
+
+hipError_t launch_lin_eval(const BatchView& bv, hipStream_t s) {
+    dim3 grid((bv.feat_stride + kEvalBlock - 1) / kEvalBlock, bv.B);
+    hipLaunchKernelGGL(lm_eval_kernel<true>, grid, dim3(256), 0, s, bv);
+    return hipGetLastError();
 }
 
 hipError_t launch_eval_at(const BatchView& bv, const double* pose_dev, double* out_dev, hipStream_t s) {

@@ -29,6 +29,9 @@ constexpr int kSortMax = 2048;       // points per sector (ring / 6 + 5, padded 
 constexpr int kMaxRings = 128;
 constexpr int kEdgePerRing = 120;    // 20 per sector x 6 sectors (FX:172)
 constexpr int kQSurf = 0x40000000;  // ExtractView::qcode tag of a surf feature
+constexpr int kQCodeMask = 0x1fff;  // qcode bits 0-12: ring-local feature index; 13-25: rank in the ring's search order
+constexpr int kQRankShift = 13;
+static_assert(kRingMax <= kQCodeMask + 1, "ring positions fit the 13-bit code fields");
 constexpr int kTile = 2048;          // raw points per ring-split tile
 constexpr int kCounterShards = 64;   // candidate / query counters, 16 u64 (128 B) apart
 constexpr int kMemoWords = 7;        // memo words per search position: 5 neighbour indices, s6, order gap
@@ -177,6 +180,10 @@ hipError_t launch_fit_eval(const GridView& edge, const GridView& surf, const Bat
 hipError_t launch_lm_begin(const BatchView& bv, hipStream_t s);
 // One LM inner iteration: evaluation at the candidate, then the step control.
 hipError_t launch_lm_eval_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
+// batch path: packets at the linearisation pose from one pass over the records (lm_begin then reads
+// ceil(nq / kEvalBlock) packets per slot); false in A/B builds where the matching kernels accumulate them
+bool lin_eval_enabled();
+hipError_t launch_lin_eval(const BatchView& bv, hipStream_t s);
 // lm_begin + the 4 inner iterations of one outer iteration in one launch (k_match.hip, lm_loop_kernel): for
 // launches whose B x lm_loop_blocks blocks are all co-resident (kLoopMaxBlocks).  sync: [2 B] counters
 // (zeroed once), err: set when a bounded wait gave up.
@@ -223,7 +230,7 @@ struct ExtractView {
     int* edge_stage_src;         // [B][kMaxRings * kEdgePerRing]
     int* ring_edge_cnt;          // [B][kMaxRings]
     int* ring_surf_cnt;          // [B][kMaxRings]
-    int* qcode;                  // [B][raw_stride] per ring position: ring-local edge index, kQSurf | surf index, -1
+    int* qcode;                  // [B][raw_stride] per ring position: ring-local edge index, kQSurf | surf index, -1; + rank << 13
     int* qslot;                  // [B][raw_stride] per ring position: its feature slot or -1 (the search order)
     int* fslot;                  // [B][feat_stride] qslot's valid entries, edge slots first (stable)
     float4* featp;               // [B][feat_stride] the features in fslot order: xyz, w = slot (int bits)

@@ -20,7 +20,7 @@ EDGE, SURF = 1, 2
 UPDATE_NONE, UPDATE_MOTION, UPDATE_TIME = 0, 1, 2
 SOLVER_CERES_LM, SOLVER_GN = 0, 1
 SCHEDULE_REFERENCE_DECAY, SCHEDULE_FIXED = 0, 1
-OPT_QUERY_MEMO, OPT_MEMO_REFIT, OPT_MEMO_EXACT, OPT_MEMO_ORDER, OPT_MEMO_BOUND, OPT_GRAPH = range(6)
+OPT_QUERY_MEMO, OPT_MEMO_REFIT, OPT_MEMO_EXACT, OPT_MEMO_ORDER, OPT_MEMO_BOUND, OPT_GRAPH, OPT_MEMO_SKIP1 = range(7)
 TERM_NAMES = {0: "max_iterations", 1: "function_tol", 2: "parameter_tol", 3: "gradient_tol",
               4: "no_residuals", 5: "gn_converged", 6: "gn_too_few"}
 

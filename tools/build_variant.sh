@@ -9,5 +9,5 @@ B=$P/build_ab/$1
 mkdir -p $B $P/ab
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -w -DLMSF_AB -I$R/include -I$P/csrc $2"
 ls $P/csrc/*.cpp $P/csrc/*.hip | grep -v /dist.cpp | xargs -P 8 -I{} sh -c "/opt/rocm/bin/hipcc $FL -x hip -c {} -o $B/\$(basename {}).o"
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $P/ab/liblmsf_$1.so $B/*.o
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $P/ab/.tmp_$1.so $B/*.o && mv $P/ab/.tmp_$1.so $P/ab/liblmsf_$1.so
 echo "built $P/ab/liblmsf_$1.so"
