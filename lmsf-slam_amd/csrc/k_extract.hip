@@ -220,27 +220,35 @@ __device__ void ring_bad_points(const ExtractView& ev, const float4* pts, int si
 #endif
         __syncthreads();
         // sequential skip automaton (next j = j + 5 after event 1 / 2, else j + 1), 64 at a time
+        // one load of 64 events per step; the step's skips are followed in registers (start: the first lane
+        // the walk visits in this step)
         if (tid < 64) {
             int pos = 5;
             while (pos <= jmax) {
                 const int j = pos + lane;
                 const int e = j <= jmax ? (int)flag[j] : 0;
-                const unsigned long long m = __ballot(e == 1 || e == 2);
-                const int f = m ? (__ffsll((long long)m) - 1) : 64;
-                if (lane < f && e == 3) {
+                const unsigned long long ev12 = __ballot(e == 1 || e == 2);
+                int start = 0;
+                while (true) {
+                    const unsigned long long m = ev12 & (~0ull << start);
+                    const int f = m ? (__ffsll((long long)m) - 1) : 64;
+                    if (lane >= start && lane < f && e == 3) {
 #pragma unroll
-                    for (int k = 0; k <= 5; ++k) dis[j - k] = 1;
-                }
-                if (lane == f) {
-                    if (e == 1) {
-#pragma unroll
-                        for (int k = -5; k <= 5; ++k) dis[j + k] = 1;
-                    } else {
-#pragma unroll
-                        for (int k = 1; k <= 5; ++k) dis[j + k] = 1;
+                        for (int k = 0; k <= 5; ++k) dis[j - k] = 1;
                     }
+                    if (lane == f) {
+                        if (e == 1) {
+#pragma unroll
+                            for (int k = -5; k <= 5; ++k) dis[j + k] = 1;
+                        } else {
+#pragma unroll
+                            for (int k = 1; k <= 5; ++k) dis[j + k] = 1;
+                        }
+                    }
+                    if (!m) { pos += 64; break; }
+                    start = f + 5;   // the reference's j += 4 and the loop's ++j (FX:231-260)
+                    if (start >= 64) { pos += start; break; }
                 }
-                pos = m ? pos + f + 5 : pos + 64;
             }
         }
         __syncthreads();
@@ -516,28 +524,36 @@ __global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
             const int* sidx = sidx_ring + s0_[k];
             auto idx_at = [&](int i) { return i >= wlo ? widx[i - wlo] : sidx[i]; };
             auto key_at = [&](int i) { return i >= wlo ? wkey[i - wlo] : skey[i]; };
+            // 64 candidates per step (lane l: sorted position pos - l, descending curvature): one load of
+            // their ring indices, keys and disable marks, then the step's picks in registers -- a pick at ring
+            // index ind disables the candidates within 5 of it (the marks it writes), so the next pick is the
+            // next eligible lane.  Keys at or below the threshold end the sector (sorted: no later candidate
+            // is above it), as the reference's break at the first enabled one does (FX:163-165).
             int pos = n - 1, picked = 0;
             const int ec0 = ec;
-            while (pos >= 0) {
+            while (pos >= 0 && picked < 20) {
                 const int cand = pos - lane;
-                const bool elig = cand >= 0 && dis[idx_at(cand)] == 0;
-                const unsigned long long m = __ballot(elig);
-                if (!m) { pos -= 64; continue; }
-                const int f = __ffsll((long long)m) - 1;
-                const double c = key_at(pos - f);
-                const int ind = idx_at(pos - f);
-                if (c <= thresh) break;
-                ++picked;
-                if (picked > 20) break;
-                if (lane == 0) {
-                    pick[picked - 1] = ind;
-                    flag[ind] = 1;
-                    qc[ind] = ec;
+                const bool valid = cand >= 0;
+                const int idx = valid ? idx_at(cand) : -100;   // -100: more than 5 from every ring index
+                const bool above = valid && key_at(cand) > thresh;
+                unsigned long long m = __ballot(above && dis[idx] == 0);
+                const bool last = pos < 64 || __ballot(valid && !above) != 0;
+                while (m && picked < 20) {
+                    const int f = __ffsll((long long)m) - 1;
+                    const int ind = __builtin_amdgcn_readlane(idx, f);
+                    ++picked;
+                    if (lane == 0) {
+                        pick[picked - 1] = ind;
+                        flag[ind] = 1;
+                        qc[ind] = ec;
+                    }
+                    if (lane >= 1 && lane <= 5) dis[min(ind + lane, size - 1)] = 1;
+                    if (lane >= 6 && lane <= 10) dis[max(ind - (lane - 5), 0)] = 1;
+                    ++ec;
+                    m &= ~__ballot(abs(idx - ind) <= 5);
                 }
-                if (lane >= 1 && lane <= 5) dis[min(ind + lane, size - 1)] = 1;
-                if (lane >= 6 && lane <= 10) dis[max(ind - (lane - 5), 0)] = 1;
-                ++ec;
-                pos = pos - f - 1;
+                if (last) break;
+                pos -= 64;
             }
             for (int t = lane; t < ec - ec0; t += 64) {
                 const int ind = pick[t];
