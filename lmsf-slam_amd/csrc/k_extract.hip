@@ -270,8 +270,110 @@ __device__ void ring_bad_points(const ExtractView& ev, const float4* pts, int si
 // Elements live in registers: wave w owns positions [w * 64E, (w + 1) * 64E), lane l holds
 // w * 64E + e * 64 + l (e < E).  A partner that differs in the lane bits only is a shuffle, in the e bits
 // (+ lane bits) a register pick (+ shuffle), and only partners in another wave go through LDS.
-template <int E>
-__device__ void sector_sort_regs(uint64_t* key, int* kidx, int n, int npow) {
+// Lane exchange x <- x of lane (lane ^ M), M a constant: DPP quad / row permutations where one exists
+// (xor 1, 2, 3 within quads; xor 7 / 15 = the half-row / row mirrors), ds_swizzle's xor mode inside 32
+// lanes, ds_bpermute across the two halves.
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t x) {
+    if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // [2,3,0,1]
+    else if constexpr (M == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x1B, 0xF, 0xF, false);   // [3,2,1,0]
+    else if constexpr (M == 7) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    else if constexpr (M == 15) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false); // row_mirror
+    else if constexpr (M < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (M << 10) | 0x1F);
+    else return (uint32_t)__shfl_xor((int)x, M, 64);
+}
+
+// Stage s of the ascending-only bitonic network of NPOW elements: merge step kk opens with the flip (partner
+// mask kk - 1) and continues with the half-cleaners kk/4 .. 1.
+constexpr int sort_stage_mask(int npow, int s) {
+    for (int kk = 2; kk <= npow; kk <<= 1) {
+        for (int m = kk - 1, jj = kk; jj > 1; jj >>= 1, m = jj >> 1) {
+            if (s == 0) return m;
+            --s;
+        }
+    }
+    return 0;
+}
+constexpr int sort_stage_count(int npow) {
+    int c = 0;
+    for (int kk = 2; kk <= npow; kk <<= 1)
+        for (int jj = kk; jj > 1; jj >>= 1) ++c;
+    return c;
+}
+constexpr int high_bit(int m) {
+    int h = 1;
+    while (h * 2 <= m) h *= 2;
+    return h;
+}
+
+// One compare-exchange stage with the constant partner mask M over the E keys of every lane (positions
+// w * 64E + e * 64 + lane): the lower position of each pair keeps the smaller key.
+template <int M, int E>
+__device__ __forceinline__ void sort_stage(uint64_t (&k)[E], int (&id)[E], uint64_t* key, int* kidx, int w, int lane,
+                                           bool active) {
+    constexpr int chunk = 64 * E, HB = high_bit(M);
+    if constexpr (M >= chunk) {   // partner in another wave: through LDS
+        __syncthreads();
+        if (active) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                key[w * chunk + e * 64 + lane] = k[e];
+                kidx[w * chunk + e * 64 + lane] = id[e];
+            }
+        }
+        __syncthreads();
+        if (active) {
+            const bool lower = ((w * chunk) & HB) == 0;   // HB >= chunk: a wave bit
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int p = (w * chunk + e * 64 + lane) ^ M;
+                const uint64_t ko = key[p];
+                const int io = kidx[p];
+                const bool take = lower ? ko < k[e] : ko > k[e];
+                if (take) { k[e] = ko; id[e] = io; }
+            }
+        }
+    } else if (active) {
+        constexpr int ML = M & 63, ME = (M >> 6) & (E - 1);
+        uint64_t ko[E];
+        int io[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            ko[e] = k[e ^ ME];
+            io[e] = id[e ^ ME];
+            if constexpr (ML != 0) {
+                const uint32_t lo = lane_xor<ML>((uint32_t)ko[e]), hi = lane_xor<ML>((uint32_t)(ko[e] >> 32));
+                ko[e] = ((uint64_t)hi << 32) | lo;
+                io[e] = (int)lane_xor<ML>((uint32_t)io[e]);
+            }
+        }
+        const bool lane_lower = (lane & HB) == 0;   // used when HB is a lane bit (HB < 64)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const bool lower = HB < 64 ? lane_lower : ((e * 64) & HB) == 0;
+            const bool take = lower ? ko[e] < k[e] : ko[e] > k[e];
+            if (take) { k[e] = ko[e]; id[e] = io[e]; }
+        }
+    }
+}
+
+template <int E, int NPOW, int S, int NS = sort_stage_count(NPOW)>
+struct SortStages {
+    static __device__ __forceinline__ void run(uint64_t (&k)[E], int (&id)[E], uint64_t* key, int* kidx, int w, int lane,
+                                               bool active) {
+        sort_stage<sort_stage_mask(NPOW, S), E>(k, id, key, kidx, w, lane, active);
+        SortStages<E, NPOW, S + 1, NS>::run(k, id, key, kidx, w, lane, active);
+    }
+};
+template <int E, int NPOW, int NS>
+struct SortStages<E, NPOW, NS, NS> {
+    static __device__ __forceinline__ void run(uint64_t (&)[E], int (&)[E], uint64_t*, int*, int, int, bool) {}
+};
+
+template <int E, int NPOW>
+__device__ void sector_sort_regs(uint64_t* key, int* kidx, int n) {
+    static_assert(NPOW == 4 * 64 * E, "four waves of E keys per lane");
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     constexpr int chunk = 64 * E;
     const bool active = w * chunk < n;
@@ -283,75 +385,9 @@ __device__ void sector_sort_regs(uint64_t* key, int* kidx, int n, int npow) {
         k[e] = active ? key[i] : ~0ull;
         id[e] = active ? kidx[i] : 0x7fffffff;
     }
-    // one stage with partner i ^ m, m < chunk (inside the wave): register e ^ ME of the lane l ^ ml
-    auto stage_wave = [&](auto me_tag, int ml) {
-        constexpr int ME = decltype(me_tag)::value;
-        uint64_t ko[E];
-        int io[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            ko[e] = k[e ^ ME];
-            io[e] = id[e ^ ME];
-        }
-        if (ml) {
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const uint32_t lo = __shfl_xor((uint32_t)ko[e], ml, 64), hi = __shfl_xor((uint32_t)(ko[e] >> 32), ml, 64);
-                ko[e] = ((uint64_t)hi << 32) | lo;
-                io[e] = __shfl_xor(io[e], ml, 64);
-            }
-        }
-        const int m = (ME << 6) | ml;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const int i = w * chunk + e * 64 + lane;
-            const bool take = ((i ^ m) > i) ? ko[e] < k[e] : ko[e] > k[e];   // lower position keeps the smaller
-            if (take) { k[e] = ko[e]; id[e] = io[e]; }
-        }
-    };
-    auto stage = [&](int m) {
-        const int ml = m & 63, me = (m >> 6) & (E - 1);   // uniform: one branch per stage
-        if (me == 0) stage_wave(std::integral_constant<int, 0>{}, ml);
-        if constexpr (E > 1) if (me == 1) stage_wave(std::integral_constant<int, (E > 1 ? 1 : 0)>{}, ml);
-        if constexpr (E > 2) {
-            if (me == 2) stage_wave(std::integral_constant<int, (E > 2 ? 2 : 0)>{}, ml);
-            if (me == 3) stage_wave(std::integral_constant<int, (E > 2 ? 3 : 0)>{}, ml);
-        }
-        if constexpr (E > 4) {
-            if (me == 4) stage_wave(std::integral_constant<int, (E > 4 ? 4 : 0)>{}, ml);
-            if (me == 5) stage_wave(std::integral_constant<int, (E > 4 ? 5 : 0)>{}, ml);
-            if (me == 6) stage_wave(std::integral_constant<int, (E > 4 ? 6 : 0)>{}, ml);
-            if (me == 7) stage_wave(std::integral_constant<int, (E > 4 ? 7 : 0)>{}, ml);
-        }
-    };
-    for (int kk = 2; kk <= npow; kk <<= 1) {
-        for (int m = kk - 1, jj = kk; jj > 1; jj >>= 1, m = jj >> 1) {   // flip (kk - 1), then kk/4 .. 1
-            if (m >= chunk) {                          // partner in another wave: through LDS
-                __syncthreads();
-                if (active) {
-#pragma unroll
-                    for (int e = 0; e < E; ++e) {
-                        const int i = w * chunk + e * 64 + lane;
-                        key[i] = k[e];
-                        kidx[i] = id[e];
-                    }
-                }
-                __syncthreads();
-                if (active) {
-#pragma unroll
-                    for (int e = 0; e < E; ++e) {
-                        const int i = w * chunk + e * 64 + lane, p = i ^ m;
-                        const uint64_t ko = key[p];
-                        const int io = kidx[p];
-                        const bool take = p > i ? ko < k[e] : ko > k[e];
-                        if (take) { k[e] = ko; id[e] = io; }
-                    }
-                }
-            } else if (active) {
-                stage(m);
-            }
-        }
-    }
+    // every stage's partner mask is a compile-time constant: the in-wave / cross-wave choice, the register
+    // pick and the lane exchange (DPP / swizzle) are fixed at compile time, no address arithmetic
+    SortStages<E, NPOW, 0>::run(k, id, key, kidx, w, lane, active);
     __syncthreads();
     if (active) {
 #pragma unroll
@@ -415,8 +451,7 @@ __global__ __launch_bounds__(256) void sector_sort_kernel(ExtractView ev) {
     sector_bounds(size, k, s0, n);
     if (n > kSortMax) return;
     const float4* pts = ev.ring_pts + (size_t)b * ev.raw_stride + start;
-    int npow = 1;
-    while (npow < n) npow <<= 1;
+    const int npow = n <= 256 ? 256 : n <= 512 ? 512 : n <= 1024 ? 1024 : 2048;   // the network's size
     for (int i = threadIdx.x; i < npow; i += 256) {
         if (i < n) {
             const int j = s0 + i;
@@ -435,10 +470,10 @@ __global__ __launch_bounds__(256) void sector_sort_kernel(ExtractView ev) {
         }
     }
     __syncthreads();
-    if (npow <= 256) sector_sort_regs<1>(key, kidx, n, npow);
-    else if (npow <= 512) sector_sort_regs<2>(key, kidx, n, npow);
-    else if (npow <= 1024) sector_sort_regs<4>(key, kidx, n, npow);
-    else sector_sort_regs<8>(key, kidx, n, npow);
+    if (npow == 256) sector_sort_regs<1, 256>(key, kidx, n);
+    else if (npow == 512) sector_sort_regs<2, 512>(key, kidx, n);
+    else if (npow == 1024) sector_sort_regs<4, 1024>(key, kidx, n);
+    else sector_sort_regs<8, 2048>(key, kidx, n);
     double* okey = ev.sort_key + (size_t)b * ev.raw_stride + start + s0;
     int* oidx = ev.sort_idx + (size_t)b * ev.raw_stride + start + s0;
     for (int i = threadIdx.x; i < n; i += 256) {
@@ -456,7 +491,12 @@ __global__ __launch_bounds__(256) void sector_sort_kernel(ExtractView ev) {
 // sorted list from an LDS window (the next sector's window is loaded while the current one is picked),
 // deeper entries from global memory; no sector is staged whole, so a block needs ~19 KB of LDS.
 constexpr int kPickWin = 256;
-__global__ __launch_bounds__(256) void ring_features_kernel(ExtractView ev) {
+// Waves per SIMD ring_features_kernel is compiled for (A/B builds; C2, one box, two rounds each: 5 waves
+// (82 VGPRs) 26.02k / 26.13k scans/s, 6 (80) 26.08k / 26.09k, 8 (64, 48 B spill) 25.83k / 25.72k).
+#ifndef LMSF_RF_WAVES
+#define LMSF_RF_WAVES 5
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_RF_WAVES))) void ring_features_kernel(ExtractView ev) {
     __shared__ uint8_t dis[kRingMax];
     __shared__ uint8_t flag[kRingMax];
     __shared__ double wkey[kPickWin];
