@@ -186,18 +186,18 @@ __device__ void ring_bad_points(const ExtractView& ev, const float4* pts, int si
     const int tid = threadIdx.x, lane = tid & 63;
     const int jmax = size - 7;  // checkBadEdgePoint visits j in [5, size - 7]
     if (ev.remove_bad) {
-        // events per point: thread t takes a contiguous run of j, so the azimuth of point j + 1 (its
-        // angle_after) is its next j's angle_curr -- one atan2 per point instead of two
-        const int nj = jmax - 4;
-        const int per = (nj + NT - 1) / NT;
-        const int j0 = 5 + tid * per, j1 = min(j0 + per, jmax + 1);
+        // events per point in wave chunks of 63: lane l loads point j = base + l (coalesced) and its azimuth,
+        // and takes point j + 1's (its angle_after) from lane l + 1 -- one atan2 per point (+ 1 in 63);
+        // lane 63 only serves lane 62
 #ifndef LMSF_AB_NO_EVENTS   // A/B ablation builds only
-        if (j0 < j1) {
-            float4 a = pts[j0];
-            double angle_curr = ref_atan2(a.x, a.y, ev.libm_float);   // atan2(x, y) order (FX:223-224)
-            for (int j = j0; j < j1; ++j) {
-                const float4 c = pts[j + 1];
-                const double angle_after = ref_atan2(c.x, c.y, ev.libm_float);
+        const int wave = tid >> 6;
+        for (int base = 5 + 63 * wave; base <= jmax; base += 63 * (NT / 64)) {
+            const int j = base + lane;
+            const float4 a = pts[min(j, jmax + 1)];   // jmax + 1 = size - 6: a ring point
+            const double angle_curr = ref_atan2(a.x, a.y, ev.libm_float);   // atan2(x, y) order (FX:223-224)
+            const double angle_after = __shfl_down(angle_curr, 1, 64);
+            const float4 c = make_float4(__shfl_down(a.x, 1, 64), __shfl_down(a.y, 1, 64), __shfl_down(a.z, 1, 64), 0.f);
+            if (lane < 63 && j <= jmax) {
                 double delta_angle = fabs(angle_curr - angle_after);
                 if (delta_angle > M_PI) delta_angle = M_PI * 2 - delta_angle;
                 uint8_t e = 0;
@@ -211,12 +211,10 @@ __device__ void ring_bad_points(const ExtractView& ev, const float4* pts, int si
                     if (ang <= 0.17) e = dc < da ? 2 : 3;
                 }
                 flag[j] = e;
-                a = c;
-                angle_curr = angle_after;
             }
         }
 #else
-        for (int j = j0; j < j1; ++j) flag[j] = 0;
+        for (int j = 5 + tid; j <= jmax; j += NT) flag[j] = 0;
 #endif
         __syncthreads();
         // sequential skip automaton (next j = j + 5 after event 1 / 2, else j + 1), 64 at a time
