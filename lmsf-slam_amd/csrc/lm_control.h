@@ -124,8 +124,11 @@ __device__ __forceinline__ bool chol_solve6(double* A, const double* b, double* 
 }
 
 // ComputeTrustRegionStep + HandleInvalidStep loop: leaves a candidate awaiting evaluation, or
-// terminates (max iterations / min radius).
-__device__ __forceinline__ void compute_step(SolveState& S) {
+// terminates (max iterations / min radius).  Not inlined: lm_step_apply calls it from two places, and the
+// inlined copies kept lm_step_kernel at 256 VGPRs + 14 AGPRs (one wave per SIMD, only on a SIMD with at most
+// one search wave); as a call it is 84 VGPRs (868 B of stack in the serial lane).  C2 A/B, three rounds on
+// one box: 25.67k / 25.93k / 25.68k vs 25.58k / 25.65k / 25.61k scans/s.
+__device__ __noinline__ void compute_step(SolveState& S) {
     while (true) {
         if (S.iteration >= kMaxInner) { S.done = 1; S.term = LMSF_TERM_MAX_ITERATIONS; return; }
         if (S.radius < 1e-32) { S.done = 1; S.term = LMSF_TERM_PARAMETER_TOL; return; }
