@@ -324,7 +324,8 @@ def test_batch_run_matches_oracle(lib, oracle_mod, small_workload):
     # neighbour-distance gap, and refit (without a walk) those whose set only changed order: same
     # records, packets summed in another grouping (the searching lanes are packed), so the poses
     # agree with re-searching every query (and with searching the reordered ones) to rounding
-    for opt in (lib.OPT_QUERY_MEMO, lib.OPT_MEMO_REFIT, lib.OPT_MEMO_EXACT, lib.OPT_MEMO_ORDER, lib.OPT_MEMO_BOUND):
+    for opt in (lib.OPT_QUERY_MEMO, lib.OPT_MEMO_REFIT, lib.OPT_MEMO_EXACT, lib.OPT_MEMO_ORDER, lib.OPT_MEMO_BOUND,
+                lib.OPT_MEMO_SKIP1):
         ctx.set_option(opt, 0)
         try:
             poses0, _ = ctx.batch_run(np.stack([wl.guess[i % n] for i in range(16)]))
