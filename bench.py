@@ -235,8 +235,8 @@ def shared_map(d, make):
 def kernel_name(ks):
     """The timed neighbour-search launch: the fused search + fit kernels (batch launches) or knn_kernel."""
     if ks.launches and ks.fused_launches == ks.launches:
-        return ("match_memo_kernel + match_fit_kernel (query memo pass, then the fused 5-NN search + line/plane "
-                "fit + first evaluation of the queries it lists; one outer iteration)")
+        return ("match_memo_kernel + match_fit_kernel (query memo pass from outer iteration 2, then the fused 5-NN "
+                "search + line/plane fit + record write of the queries it lists; one outer iteration)")
     return "knn_kernel (8-lane 5-NN search with the slot memo; fit_eval_kernel follows)"
 
 

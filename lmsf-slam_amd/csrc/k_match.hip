@@ -265,12 +265,12 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
         // candidates they save (measured).
         auto scan_range = [&](const float4* rp, uint32_t tag, int a, int len) {
             int c = 0;
-            for (; c + kKnnUnroll <= len; c += kKnnUnroll) {
-                float4 m[kKnnUnroll];
+            for (; c + RU <= len; c += RU) {
+                float4 m[RU];
 #pragma unroll
-                for (int u = 0; u < kKnnUnroll; ++u) m[u] = rp[a + c + u];
+                for (int u = 0; u < RU; ++u) m[u] = rp[a + c + u];
 #pragma unroll
-                for (int u = 0; u < kKnnUnroll; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
+                for (int u = 0; u < RU; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
             }
             for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
         };
@@ -898,25 +898,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_W
         const float4 p = bv.featp[pos];
         const int q = __float_as_int(p.w);
         const float4 pw = bv.prevw[pos];
+        // everything the position may need, in flight together (the pass is latency-bound: one round trip
+        // for the state instead of three dependent ones -- memo words, then the record)
+        int mw[7];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) mw[j] = bv.memo_nbr[((size_t)b * kMemoWords + j) * F + i];
+        const float4 rp = bv.rec_p[pos];
+        const RecV rv = bv.rec_v[pos];
         if (q >= 0 && q < nq && pw.w >= 0.f) {
             const size_t slot = pos;
             const float3 w = associate(Ps, p);
             const double dx = (double)w.x - pw.x, dy = (double)w.y - pw.y, dz = (double)w.z - pw.z;
             const double dd = sqrt(dx * dx + dy * dy + dz * dz);
-            const double s6 = (double)__int_as_float(bv.memo_nbr[((size_t)b * kMemoWords + 5) * F + i]);
+            const double s6 = (double)__int_as_float(mw[5]);
             const double r6 = s6 + dd + 1e-5;
             if (r6 < 1.0 && bv.memo_bound) lim = fminf(kFullLim, (float)(r6 * r6) + 1e-5f);
             // every distance moved by at most dd: with 2 dd + 1e-5 below every gap between consecutive
             // neighbours and below s6 - s5, neither the set nor the order of the 5 nearest changed, and a
             // search would return the stored keys -- no re-keying (r01's test, ahead of the exact one)
-            const double gord = (double)__int_as_float(bv.memo_nbr[((size_t)b * kMemoWords + 6) * F + i]);
+            const double gord = (double)__int_as_float(mw[6]);
             bool same = bv.memo_order && 2.0 * dd + 1e-5 < gord;
             if (!same && (bv.memo_exact || 2.0 * dd + 1e-5 < (double)pw.w)) {
                 const float4* orig = q < ne ? ge.orig : gs.orig;
                 uint32_t idx[5];
                 double k[5];
 #pragma unroll
-                for (int j = 0; j < 5; ++j) idx[j] = (uint32_t)bv.memo_nbr[((size_t)b * kMemoWords + j) * F + i];
+                for (int j = 0; j < 5; ++j) idx[j] = (uint32_t)mw[j];
 #pragma unroll
                 for (int j = 0; j < 5; ++j) k[j] = nn_key(w, orig[idx[j]], idx[j]);
                 // 5-key sorting network (9 compare-exchanges)
@@ -940,12 +947,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_W
                 }
             }
             if (same) {
-                const int kind = __float_as_int(bv.rec_p[slot].w);
+                const int kind = __float_as_int(rp.w);
                 d3 v0 = mk(0, 0, 0);
                 double v1x = 0.0, v1y = 0.0, v1z = 0.0;
                 bool reuse = true;
                 if (kind != 0) {
-                    const RecV v = bv.rec_v[slot];
+                    const RecV v = rv;
                     v0 = mk(v.v[0], v.v[1], v.v[2]);
                     v1x = v.v[3];
                     if (kind == LMSF_SURF) {

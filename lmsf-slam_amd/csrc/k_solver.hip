@@ -63,7 +63,7 @@ __global__ __launch_bounds__(kBeginThreads) LMSF_CTL_ATTR void lm_begin_kernel(B
         const int fb = bv.part_q;
         reduce_parts(bv, b, (nq + fb - 1) / fb, tot);
     }   // (reduce_parts ends with a barrier: sS is in place)
-    if (threadIdx.x == 0) lm_begin_apply(sS, tot);
+    if (threadIdx.x == 0) lm_begin_apply<true>(sS, tot);
     __syncthreads();
     state_copy(bv.st[b], sS);
 }
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kStepThreads) LMSF_CTL_ATTR void lm_step_kernel(Bat
     const int nq = bv.n_edge[b] + bv.n_surf[b];
     __shared__ double tot[kPacket];
     reduce_parts(bv, b, (nq + kEvalBlock - 1) / kEvalBlock, tot);   // ends with a barrier
-    if (threadIdx.x == 0) lm_step_apply(sS, tot, outer, is_last);
+    if (threadIdx.x == 0) lm_step_apply<true>(sS, tot, outer, is_last);
     __syncthreads();
     state_copy(S, sS);
 }

@@ -124,11 +124,8 @@ __device__ __forceinline__ bool chol_solve6(double* A, const double* b, double* 
 }
 
 // ComputeTrustRegionStep + HandleInvalidStep loop: leaves a candidate awaiting evaluation, or
-// terminates (max iterations / min radius).  Not inlined: lm_step_apply calls it from two places, and the
-// inlined copies kept lm_step_kernel at 256 VGPRs + 14 AGPRs (one wave per SIMD, only on a SIMD with at most
-// one search wave); as a call it is 84 VGPRs (868 B of stack in the serial lane).  C2 A/B, three rounds on
-// one box: 25.67k / 25.93k / 25.68k vs 25.58k / 25.65k / 25.61k scans/s.
-__device__ __noinline__ void compute_step(SolveState& S) {
+// terminates (max iterations / min radius).
+__device__ __forceinline__ void compute_step_body(SolveState& S) {
     while (true) {
         if (S.iteration >= kMaxInner) { S.done = 1; S.term = LMSF_TERM_MAX_ITERATIONS; return; }
         if (S.radius < 1e-32) { S.done = 1; S.term = LMSF_TERM_PARAMETER_TOL; return; }
@@ -177,6 +174,20 @@ __device__ __noinline__ void compute_step(SolveState& S) {
     }
 }
 
+// CALL: the step computation as a non-inlined call.  lm_step_apply calls it from two places, and the
+// inlined copies keep lm_step_kernel at 256 VGPRs + 14 AGPRs (one wave per SIMD, only on a SIMD with at most
+// one search wave); as a call it is 84 VGPRs (868 B of stack in the serial lane): 12.4 -> 29 us alone, but
+// C2 +0.5-1% (three alternating rounds: 25.67k / 25.93k / 25.68k vs 25.58k / 25.65k / 25.61k scans/s) --
+// the batch lm_step waits less for room beside the other contexts' search waves.  The batch lm_begin takes
+// the call too (C2 26.14k / 25.88k with it vs 25.85k / 25.84k without); the single-scan lm_loop_kernel keeps
+// the inlined form (C4 1,153 / 1,123 vs 1,073 / 1,100 scans/s with the call there as well).
+__device__ __noinline__ void compute_step_call(SolveState& S) { compute_step_body(S); }
+template <bool CALL>
+__device__ __forceinline__ void compute_step(SolveState& S) {
+    if constexpr (CALL) compute_step_call(S);
+    else compute_step_body(S);
+}
+
 __device__ void finish_outer(SolveState& S, int outer) {
     if (outer < kMaxOuter)
         for (int i = 0; i < 7; ++i) S.trace[outer][i] = S.x[i];
@@ -189,6 +200,7 @@ __device__ void finish_outer(SolveState& S, int outer) {
 // lm_step after the evaluation at the candidate (tot = its reduced packet): step acceptance
 // (ParameterToleranceReached, FunctionToleranceReached, IsStepSuccessful, HandleSuccessfulStep /
 // StepRejected) + next step; one thread.
+template <bool CALL = false>
 __device__ __forceinline__ void lm_step_apply(SolveState& S, const double* tot, int outer, int is_last) {
     S.need_eval = 0;
     ++S.evals;
@@ -222,12 +234,12 @@ __device__ __forceinline__ void lm_step_apply(SolveState& S, const double* tot, 
                     S.done = 1;
                     S.term = LMSF_TERM_GRADIENT_TOL;
                 } else {
-                    compute_step(S);
+                    compute_step<CALL>(S);
                 }
             } else {
                 S.radius = S.radius / S.decrease;
                 S.decrease *= 2.0;
-                compute_step(S);
+                compute_step<CALL>(S);
             }
         }
     }
@@ -235,6 +247,7 @@ __device__ __forceinline__ void lm_step_apply(SolveState& S, const double* tot, 
 }
 
 // IterationZero on the reduced first evaluation (tot) + the first step; one lane, S in LDS.
+template <bool CALL = false>
 __device__ __forceinline__ void lm_begin_apply(SolveState& S, const double* tot) {
     S.iteration = 0;
     S.need_eval = 0;
@@ -261,7 +274,7 @@ __device__ __forceinline__ void lm_begin_apply(SolveState& S, const double* tot)
         S.term = LMSF_TERM_GRADIENT_TOL;
         return;
     }
-    compute_step(S);
+    compute_step<CALL>(S);
 }
 
 }  // namespace
