@@ -226,3 +226,20 @@ def test_set_option_validates(lib):
     L = lib.load()
     assert L.lmsf_set_option(None, lib.OPT_QUERY_MEMO, 1) == lib.ERR_ARG
     assert L.lmsf_batch_capture(None, None, 0) == lib.ERR_ARG
+
+
+def test_python_mirror_constants_match_header(lib):
+    """The Python mirror's option and status numbers (lmsf/_lib.py) are the header's #defines: every
+    LMSF_OPT_* of include/lmsf/lmsf.h has its OPT_* twin with the same value (the count included), and the
+    status codes agree."""
+    import re
+    header = open(os.path.join(REPO, "include", "lmsf", "lmsf.h")).read()
+    defs = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define LMSF_(OPT_[A-Z0-9_]+)\s+(-?\d+)", header)}
+    assert defs and defs["OPT_COUNT"] == len(defs) - 1
+    for name, v in defs.items():
+        if name != "OPT_COUNT":
+            assert getattr(lib, name) == v, name
+    status = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define LMSF_(OK|ERR_[A-Z_]+)\s+\(?(-?\d+)\)?", header)}
+    assert "ERR_ARG" in status and "OK" in status
+    for name, v in status.items():
+        assert getattr(lib, name) == v, name
