@@ -809,7 +809,7 @@ def run_dual(args, d):
                         "one ~63k-query scan per launch (8 lanes per query) against the voxelised local map: "
                         "latency-bound launches")
     ext_err = [float(np.linalg.norm(system.extrinsic[:3, 3] - X[:3, 3])),
-               float(math.acos(max(-1.0, min(1.0, (np.trace(system.extrinsic[:3, :3].T @ X[:3, :3]) - 1) / 2))))]
+               synth.rot_angle_of_matrix(system.extrinsic[:3, :3].T @ X[:3, :3])]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         oracle = cpu_oracle()

@@ -114,6 +114,8 @@ lmsf_status lmsf_config_init(lmsf_config* cfg);
  * (REG/ceres_edgeSurfFeatureRegistration.hpp:45-49) + LOAMFeatureProcessorBase ctor (FX:36-50). */
 lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out);
 void lmsf_ctx_destroy(lmsf_ctx* ctx);
+/* Message of the last error on ctx, copied under the context's error lock; valid until the next call of
+ * lmsf_last_error on the same context from any thread (call it from one thread per context). */
 const char* lmsf_last_error(const lmsf_ctx* ctx);
 
 /* RegistrationBase::SetInputSource (REG/registration_base.hpp:31; ceres_...:56-71): set the local
@@ -218,7 +220,7 @@ lmsf_status lmsf_batch_copy_features(lmsf_ctx* ctx, int32_t slot, int32_t kind, 
 /* ---- context options (not on the reference surface): algorithm switches of the build.
  * Results do not depend on them (the memo switches are exact, DESIGN.md section 4 "Query memo"); they
  * exist so tests can compare the paths in one process and a caller can rule a path out.  Values 0 | 1;
- * defaults 1 except LMSF_OPT_GRAPH 0. */
+ * defaults 1 except LMSF_OPT_GRAPH and LMSF_OPT_LOOP_FAULT_TEST 0. */
 #define LMSF_OPT_QUERY_MEMO 0   /* 1: outer iterations > 0 reuse 5-NN sets that provably did not change */
 #define LMSF_OPT_MEMO_REFIT 1   /* 1: a reused set in a new order is refitted without a walk */
 #define LMSF_OPT_MEMO_EXACT 2   /* 1: keep the set when its farthest point is nearer than s6 - d (0: 2d < s6 - s5) */
@@ -228,7 +230,11 @@ lmsf_status lmsf_batch_copy_features(lmsf_ctx* ctx, int32_t slot, int32_t kind, 
 #define LMSF_OPT_MEMO_SKIP1 6   /* 1: batch launches search outer iteration 1 in full (no memo pass): the first LM
                                  *    solve moves the queries past the memo's gaps, so its pass finds ~nothing
                                  *    (default 1; 0: the memo pass from iteration 1) */
-#define LMSF_OPT_COUNT 7
+#define LMSF_OPT_LM_LOOP 7      /* 1: single-scan launches run each outer iteration's Ceres LM as one launch when its
+                                 *    grid is co-resident (lm_loop_kernel); 0: the 9-launch form (default 1) */
+#define LMSF_OPT_LOOP_FAULT_TEST 8 /* 1 (testing only): lm_loop_kernel's bounded waits give up at once, forcing the
+                                 *    fault and its recovery -- the Solve re-run on the 9-launch form (default 0) */
+#define LMSF_OPT_COUNT 9
 lmsf_status lmsf_set_option(lmsf_ctx* ctx, int32_t option, int32_t value);
 
 /* ---- diagnostics used by the parity tests and the roofline report (not on the reference surface) */
@@ -250,6 +256,13 @@ lmsf_status lmsf_match(lmsf_ctx* ctx, const double pose[7], lmsf_record* out, in
 /* Weighted normal-equation packet of the current records at a pose: cost, H (21 upper, row-major),
  * g (6), count -- the quantities the device LM reduces. */
 lmsf_status lmsf_eval(lmsf_ctx* ctx, const double pose[7], double out[29]);
+/* Device self-test of the restated Eigen 3.3 SelfAdjointEigenSolver the kernels run: n symmetric dim x dim
+ * matrices (row-major, lower triangle read; host or device memory) -> ascending eigenvalues d[n][dim],
+ * eigenvectors v[n][dim][dim] (row-major, eigenvector i in column i), info[n] (0 Success, 1 NoConvergence).
+ * dim 3: the fixed-size Matrix3d path of the edge fit (EdgeFeatureMatch.hpp:63); dim 6: the MatrixXd path
+ * of the GN degeneracy test (edgeSurfFeatureRegistration.hpp:282).  Synchronous on the context stream. */
+lmsf_status lmsf_eigen_selfadjoint(lmsf_ctx* ctx, int32_t dim, const double* a, size_t n, double* d, double* v,
+                                   int32_t* info);
 /* Neighbour-search kernel accounting since the last reset: launches, summed device time (ms,
  * HIP events on the context stream), queries, and sum over queries of n27 (map points in the
  * 3x3x3 block of 1 m cells around each query: the algorithmic-byte figure of DESIGN.md).
@@ -271,6 +284,8 @@ typedef struct {
     int64_t fused_launches;
     int64_t reused_queries;
     int64_t refit_queries;
+    int64_t loop_recoveries;  /* solves whose single-launch LM loop gave up a bounded wait and were re-run on
+                               * the 9-launch form (results as without the fault) */
 } lmsf_kernel_stats;
 lmsf_status lmsf_kernel_stats_get(lmsf_ctx* ctx, lmsf_kernel_stats* out);
 lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* ctx, int32_t mode);

@@ -108,8 +108,12 @@ hipError_t dalloc(T** p, size_t count) {
 struct lmsf_ctx {
     lmsf_config cfg;
     std::string err;
-    std::mutex err_mu;                // a tracker's commit worker may report an error beside the caller
-    int opt[LMSF_OPT_COUNT] = {1, 1, 1, 1, 1, 0, 1};   // lmsf_set_option (defaults: lmsf.h)
+    mutable std::mutex err_mu;        // a tracker's commit worker may report an error beside the caller
+    mutable char err_out[512] = {};   // lmsf_last_error's copy: written only by the caller's thread
+    int opt[LMSF_OPT_COUNT] = {1, 1, 1, 1, 1, 0, 1, 1, 0};   // lmsf_set_option (defaults: lmsf.h)
+    bool loop_off_once = false;       // the re-run of a faulted LM loop (9-launch form, direct launches)
+    int64_t loop_recoveries = 0;
+    int last_launch_iters = 0;        // outer iterations of the last batch launch (its re-run after a loop fault)
     // record capture (lmsf_batch_capture): device rows [n_cap][kCaptureIters][F] of the captured slots
     std::vector<int> cap_slots;
     lmsf_record* cap_rec = nullptr;
@@ -119,6 +123,7 @@ struct lmsf_ctx {
     int cap_iters = 0;                // outer iterations captured by the last launch
     int cap_by_pos = 0;
     int raw_loaded = 0;               // slots of the last (or pending streamed) load
+    bool raw_adopted = false;         // the last extraction adopted a prefetch (raw slot 0 not its scan)
     hipStream_t stream = nullptr;
     int B = 1, R = 0, F = 0, max_parts = 0, n_tiles = 0;
     int optimization_count = 10;
@@ -672,8 +677,10 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
             // single-scan launches: the whole LM of this outer iteration in one launch when its grid is
             // co-resident (lm_loop_kernel; A/B builds: LMSF_LM_LOOP=0 for the 9-launch form)
             static const bool loop_on = ab_int("LMSF_LM_LOOP", 1) != 0;
-            if (!fused && loop_on && nb * lm_loop_blocks(bv) <= kLoopMaxBlocks) {
-                HIPCHK(c, launch_lm_loop(bv, o, c->d_lmsync, c->d_error + 16, s));
+            if (!fused && loop_on && c->opt[LMSF_OPT_LM_LOOP] && !c->loop_off_once &&
+                nb * lm_loop_blocks(bv) <= kLoopMaxBlocks) {
+                HIPCHK(c, launch_lm_loop(bv, o, c->d_lmsync, c->d_error + 16,
+                                         c->opt[LMSF_OPT_LOOP_FAULT_TEST] ? 0u : kLoopSpinDefault, s));
             } else {
                 HIPCHK(c, launch_lm_begin(bvb, s));
                 for (int i = 0; i < 4; ++i) HIPCHK(c, launch_lm_eval_step(bv, o, i == 3 ? 1 : 0, s));
@@ -704,8 +711,9 @@ std::vector<unsigned char> solve_key(lmsf_ctx* c, int nb, int iters) {
             const GridView g = ms[kind].view();
             put(&g, sizeof g);
         }
-    const int flags[] = {nb, iters, c->timing ? 1 : 0, c->count27 ? 1 : 0, c->opt[LMSF_OPT_QUERY_MEMO], c->cfg.solver};
+    const int flags[] = {nb, iters, c->timing ? 1 : 0, c->count27 ? 1 : 0, c->cfg.solver};
     put(flags, sizeof flags);
+    put(c->opt, sizeof c->opt);   // every per-context switch the enqueue reads (SKIP1 changes the memo passes)
     return k;
 }
 
@@ -715,7 +723,7 @@ lmsf_status enqueue_solve(lmsf_ctx* c, int nb, int iters) {
     if (rl) return rl;
     hipStream_t s = c->stream;
     // direct launches: graphs off, timing events not yet collected, or a record capture
-    if (!c->opt[LMSF_OPT_GRAPH] || c->ev_used != 0 || !c->cap_slots.empty()) {
+    if (!c->opt[LMSF_OPT_GRAPH] || c->ev_used != 0 || !c->cap_slots.empty() || c->loop_off_once) {
         HIPCHK(c, launch_state_init(c->bview(nb), c->d_poses, s));
         return enqueue_register(c, nb, iters);
     }
@@ -780,12 +788,27 @@ lmsf_status collect_timing(lmsf_ctx* c, bool lazy = false) {
     return LMSF_OK;
 }
 
-// lm_loop_kernel gave up a bounded wait (its blocks were not all resident): the results are not usable.
-lmsf_status loop_fault(lmsf_ctx* c) {
-    HIPCHK(c, hipMemsetAsync(c->d_error + 16, 0, sizeof(int), c->stream));
+// lm_loop_kernel gave up a bounded wait (its blocks were not all co-resident beside other work on the GPU):
+// that launch's results are not usable, and its arrival counters may be out of step.  Recovery: the counters
+// and the flag are reset, then the whole registration of slots [0, nb) is enqueued again from the same
+// initial poses (d_poses, untouched) on the 9-launch form, which has no cross-block wait.  The Solve is
+// deterministic and both forms run the same LM control on the same packet sums, so the result is the one an
+// unfaulted run gives (tests/test_gpu_parity.py::test_lm_loop_fault_recovery).
+lmsf_status loop_recover(lmsf_ctx* c, int nb, int iters) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_lmsync, 0, 2 * (size_t)c->B * sizeof(unsigned), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_error + 16, 0, sizeof(int), c->stream));
     c->h_pack[3] = 0;
-    return c->fail(LMSF_ERR_HIP, "single-scan LM loop: a block waited past its limit (grid not co-resident)");
+    c->loop_recoveries++;
+    c->loop_off_once = true;
+    const lmsf_status rc = enqueue_solve(c, nb, iters);
+    c->loop_off_once = false;
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, (size_t)nb * sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->h_pack[3]) return c->fail(LMSF_ERR_HIP, "LM loop fault persisted on the 9-launch form");
+    return collect_timing(c, true);
 }
 
 int outer_iterations_for_solve(lmsf_ctx* c) {
@@ -826,6 +849,20 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (!c) return;
     hipSetDevice(c->cfg.device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    // quiesce every producer before any buffer is freed: the prefetch worker may still be enqueueing an
+    // extraction (copies + kernels on pre_stream) that uses the shared scratch, and an upload may be in
+    // flight on the copy stream
+    if (c->pre_worker.joinable()) {
+        {
+            std::lock_guard<std::mutex> lk(c->pre_mu);
+            c->pre_quit = true;
+        }
+        c->pre_cv.notify_all();
+        c->pre_worker.join();
+    }
+    if (c->pre_stream) hipStreamSynchronize(c->pre_stream);
+    if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
+    if (c->raw_pending && c->ev_raw_ready) hipEventSynchronize(c->ev_raw_ready);   // an upload on the shared stream
     if (c->sg.exec) hipGraphExecDestroy(c->sg.exec);
     for (DevMap* ms : {c->map, c->prior}) {
         for (int k = 0; k < 3; ++k) {
@@ -845,15 +882,6 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
                     c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->sort_key,
                     c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->featp, c->n_pos, c->d_error, c->d_lmsync};
     for (void* p : bufs) hipFree(p);
-    if (c->pre_worker.joinable()) {
-        {
-            std::lock_guard<std::mutex> lk(c->pre_mu);
-            c->pre_quit = true;
-        }
-        c->pre_cv.notify_all();
-        c->pre_worker.join();
-    }
-    if (c->pre_stream) hipStreamSynchronize(c->pre_stream);
     void* pre_bufs[] = {c->alt.feat, c->alt.feat_src, c->alt.n_edge, c->alt.n_surf, c->alt.qslot, c->alt.fslot,
                         c->alt.featp, c->alt.n_pos, c->pre_raw, c->pre_raw_count, c->pre_raw_off};
     for (void* p : pre_bufs) hipFree(p);
@@ -879,8 +907,6 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (c->h_raw_counts) hipHostFree(c->h_raw_counts);
     if (c->h_raw_off) hipHostFree(c->h_raw_off);
     if (c->h_off) hipHostFree(c->h_off);
-    if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
-    if (c->raw_pending && c->ev_raw_ready) hipEventSynchronize(c->ev_raw_ready);   // an upload on the shared stream
     if (c->ev_raw_free) hipEventDestroy(c->ev_raw_free);
     if (c->ev_raw_free_alt) hipEventDestroy(c->ev_raw_free_alt);
     hipFree(c->raw_alt);
@@ -1003,7 +1029,12 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     return LMSF_OK;
 }
 
-const char* lmsf_last_error(const lmsf_ctx* c) { return c ? c->err.c_str() : "null context"; }
+const char* lmsf_last_error(const lmsf_ctx* c) {
+    if (!c) return "null context";
+    std::lock_guard<std::mutex> lk(c->err_mu);   // a worker's fail() may be rewriting err
+    std::snprintf(c->err_out, sizeof c->err_out, "%s", c->err.c_str());
+    return c->err_out;
+}
 
 lmsf_status lmsf_set_map(lmsf_ctx* c, int32_t kind, const float* xyzi, size_t n) {
     if (!c || (kind != LMSF_EDGE && kind != LMSF_SURF)) return LMSF_ERR_ARG;
@@ -1080,7 +1111,10 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     HIPCHK(c, stream_wait(c->stream));
     rc = collect_timing(c, true);
     if (rc) return rc;
-    if (c->h_pack[3]) return loop_fault(c);
+    if (c->h_pack[3]) {
+        rc = loop_recover(c, 1, iters);
+        if (rc) return rc;
+    }
     const SolveState& S = c->h_st[0];
     std::memcpy(pose, S.x, 7 * sizeof(double));
     c->last_outer = std::min(S.outer_run, kMaxOuter);
@@ -1233,6 +1267,10 @@ lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf
         HIPCHK(c, hipEventRecord(c->ev_raw_free, c->stream));
         c->swap_outputs();
         c->qorder_valid = true;
+        // the scan was copied into the prefetch buffer, not into raw slot 0: a batch launch would re-extract
+        // whatever slot 0 held before, so it is refused (LMSF_ERR_STATE) until the next scan load
+        c->raw_loaded = 0;
+        c->raw_adopted = true;
         lmsf_status rc = ctx_settle(c);
         if (rc) return rc;
         HIPCHK(c, hipEventSynchronize(c->ev_pre));
@@ -1502,6 +1540,7 @@ static lmsf_status load_scans(lmsf_ctx* c, const float* xyzi, const int64_t* cou
         if (counts[i] < 0 || counts[i] > c->R)
             return c->fail(LMSF_ERR_CAPACITY, "scan %d has %lld points (max_scan_points %d)", i, (long long)counts[i], c->R);
     c->raw_loaded = n;   // replaces any streamed batch: slots >= n hold nothing a launch may extract
+    c->raw_adopted = false;
     for (int i = 0; i < n; ++i) {
         c->h_counts[i] = (int)counts[i];
         c->h_off[i] = (int64_t)off;
@@ -1582,6 +1621,7 @@ lmsf_status lmsf_batch_load_scans_async(lmsf_ctx* c, const float* xyzi, const in
     HIPCHK(c, hipEventRecord(c->ev_raw_ready, c->copy_stream));
     c->raw_pending = true;
     c->raw_loaded = n;
+    c->raw_adopted = false;
     return LMSF_OK;
 }
 
@@ -1591,6 +1631,9 @@ lmsf_status lmsf_batch_launch(lmsf_ctx* c, int32_t n, const double* poses) {
     lmsf_status rs = ctx_settle(c);   // a deferred tracker commit may be the first map of this context
     if (rs) return rs;
     if (!c->map_set[LMSF_EDGE] && !c->map_set[LMSF_SURF]) return c->fail(LMSF_ERR_NO_MAP, "no map set");
+    if (c->raw_loaded == 0 && c->raw_adopted)
+        return c->fail(LMSF_ERR_STATE, "the last extraction adopted a prefetched scan: load the batch's scans "
+                                       "(lmsf_batch_load_scans) before a launch");
     if (n > c->raw_loaded)   // e.g. lmsf_extract_features (one scan into slot 0) after a batch load
         return c->fail(LMSF_ERR_STATE, "launch of %d slots but the last scan load filled %d", n, c->raw_loaded);
     std::memcpy(c->h_poses, poses, (size_t)n * 7 * sizeof(double));
@@ -1612,6 +1655,7 @@ lmsf_status lmsf_batch_launch(lmsf_ctx* c, int32_t n, const double* poses) {
     if (c->cfg.solver == LMSF_SOLVER_CERES_LM && c->cfg.schedule == LMSF_SCHEDULE_REFERENCE_DECAY && iters > 2) --iters;
     iters = std::min(iters, kMaxOuter);
     c->features_on_device = false;
+    c->last_launch_iters = iters;
     return enqueue_solve(c, n, iters);
 }
 
@@ -1625,7 +1669,10 @@ lmsf_status lmsf_batch_wait(lmsf_ctx* c, int32_t n, double* poses, lmsf_solve_st
     HIPCHK(c, hipStreamSynchronize(c->stream));
     lmsf_status rc = collect_timing(c, true);
     if (rc) return rc;
-    if (c->h_pack[3]) return loop_fault(c);
+    if (c->h_pack[3]) {
+        rc = loop_recover(c, n, c->last_launch_iters);
+        if (rc) return rc;
+    }
     for (int i = 0; i < n; ++i) {
         std::memcpy(poses + 7 * i, c->h_st[i].x, 7 * sizeof(double));
         if (stats) fill_stats(c->h_st[i], &stats[i]);
@@ -1785,6 +1832,30 @@ lmsf_status lmsf_eval(lmsf_ctx* c, const double pose[7], double out[29]) {
     return LMSF_OK;
 }
 
+lmsf_status lmsf_eigen_selfadjoint(lmsf_ctx* c, int32_t dim, const double* a, size_t n, double* d, double* v,
+                                   int32_t* info) {
+    if (!c || (dim != 3 && dim != 6) || (n && (!a || !d || !v || !info)) || n > (size_t)INT32_MAX / 64)
+        return LMSF_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (n == 0) return LMSF_OK;
+    const size_t m = (size_t)dim * dim;
+    double *da = nullptr, *dd = nullptr, *dv = nullptr;
+    int* di = nullptr;
+    hipError_t e = dalloc(&da, n * m);
+    if (e == hipSuccess) e = dalloc(&dd, n * dim);
+    if (e == hipSuccess) e = dalloc(&dv, n * m);
+    if (e == hipSuccess) e = dalloc(&di, n);
+    if (e == hipSuccess) e = hipMemcpyAsync(da, a, n * m * sizeof(double), hipMemcpyDefault, c->stream);
+    if (e == hipSuccess) e = launch_eigen_selftest(dim, da, (int)n, dd, dv, di, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d, dd, n * dim * sizeof(double), hipMemcpyDefault, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(v, dv, n * m * sizeof(double), hipMemcpyDefault, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(info, di, n * sizeof(int32_t), hipMemcpyDefault, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(da); (void)hipFree(dd); (void)hipFree(dv); (void)hipFree(di);
+    if (e != hipSuccess) return c->fail(LMSF_ERR_HIP, "eigen self-test: %s", hipGetErrorString(e));
+    return LMSF_OK;
+}
+
 lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* c, int32_t mode) {
     if (!c || (mode & ~(LMSF_STATS_TIMING | LMSF_STATS_N27))) return LMSF_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->cfg.device));
@@ -1805,6 +1876,7 @@ lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* c, int32_t mode) {
     c->knn_launches = 0;
     c->fused_launches = 0;
     c->knn_queries = 0;
+    c->loop_recoveries = 0;
     HIPCHK(c, hipMemset(c->d_n27, 0, kCounterShards * 16 * sizeof(unsigned long long)));
     return LMSF_OK;
 }
@@ -1831,6 +1903,7 @@ lmsf_status lmsf_kernel_stats_get(lmsf_ctx* c, lmsf_kernel_stats* out) {
     out->n27_sum = (int64_t)n27;
     out->reused_queries = (int64_t)r;
     out->refit_queries = (int64_t)rf;
+    out->loop_recoveries = c->loop_recoveries;
     return LMSF_OK;
 }
 

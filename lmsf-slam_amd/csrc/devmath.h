@@ -106,101 +106,281 @@ __device__ inline void pose_plus(const double* x, const double* delta, double* o
     out[4] = tp.x; out[5] = tp.y; out[6] = tp.z;
 }
 
-// ---------------------------------------------------------------- cyclic Jacobi, symmetric NxN
-// (SelfAdjointEigenSolver restated; EdgeFeatureMatch.hpp:63).  Compile-time N keeps every index
-// static so the matrices live in registers.  Output: d ascending (stable on index), v columns.
-template <int N>
-__device__ __forceinline__ void jrot(double* m, int i, int j, int k, int l, double s, double tau) {
-    double g = m[i * N + j], h = m[k * N + l];
-    m[i * N + j] = g - s * (h + g * tau);
-    m[k * N + l] = h + s * (g - h * tau);
+// ---------------------------------------------------------------- SelfAdjointEigenSolver (Eigen 3.3)
+// Eigen's published algorithm (Eigenvalues/SelfAdjointEigenSolver.h, Tridiagonalization.h, Jacobi.h),
+// restated for the two call sites of the reference: the fixed-size Matrix3d edge PCA
+// (EdgeFeatureMatch.hpp:63) and the dynamic MatrixXd degeneracy test of the GN variant
+// (edgeSurfFeatureRegistration.hpp:282).  compute(): lower triangle scaled into [-1, 1] by its largest
+// magnitude, tridiagonalised (3x3: one closed-form Householder step), implicit symmetric QR steps with a
+// Wilkinson shift on the trailing unreduced block (deflation |e| <= 2 eps (|d_i| + |d_i+1|) or
+// |e| <= DBL_MIN, at most 30 n steps), the rotations accumulated into Q on the right, then a selection
+// sort ascending with column swaps (only when converged), eigenvalues scaled back.
+
+// numext::hypot: p = max(|x|, |y|), p sqrt(1 + (min / p)^2)
+__device__ __forceinline__ double eigen_hypot(double x, double y) {
+    const double ax = fabs(x), ay = fabs(y);
+    const double p = ax > ay ? ax : ay;
+    const double qp = (ax > ay ? ay : ax) / p;
+    return p == 0.0 ? 0.0 : p * sqrt(1.0 + qp * qp);
 }
 
-template <int N>
-__device__ inline void jacobi_eig(double* a, double* d, double* v) {
-    double b[N], z[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-#pragma unroll
-        for (int j = 0; j < N; ++j) v[i * N + j] = (i == j) ? 1.0 : 0.0;
-        b[i] = d[i] = a[i * N + i];
-        z[i] = 0.0;
+// JacobiRotation<double>::makeGivens(p, q), real case: G = [c s; -s c], G^T [p; q] = [r; 0]
+__device__ __forceinline__ void make_givens(double p, double q, double& c, double& s) {
+    if (q == 0.0) {
+        c = p < 0.0 ? -1.0 : 1.0;
+        s = 0.0;
+    } else if (p == 0.0) {
+        c = 0.0;
+        s = q < 0.0 ? 1.0 : -1.0;
+    } else if (fabs(p) > fabs(q)) {
+        const double t = q / p;
+        double u = sqrt(1.0 + t * t);
+        if (p < 0.0) u = -u;
+        c = 1.0 / u;
+        s = -t * c;
+    } else {
+        const double t = p / q;
+        double u = sqrt(1.0 + t * t);
+        if (q < 0.0) u = -u;
+        s = -1.0 / u;
+        c = -t * s;
     }
-    for (int sweep = 1; sweep <= 50; ++sweep) {
-        double sm = 0.0;
-#pragma unroll
-        for (int p = 0; p < N - 1; ++p)
-#pragma unroll
-            for (int q = p + 1; q < N; ++q) sm += fabs(a[p * N + q]);
-        if (sm == 0.0) break;
-        double tresh = (sweep < 4) ? 0.2 * sm / (N * N) : 0.0;
-#pragma unroll
-        for (int p = 0; p < N - 1; ++p) {
-#pragma unroll
-            for (int q = p + 1; q < N; ++q) {
-                double apq = a[p * N + q];
-                double g = 100.0 * fabs(apq);
-                if (sweep > 4 && fabs(d[p]) + g == fabs(d[p]) && fabs(d[q]) + g == fabs(d[q])) {
-                    a[p * N + q] = 0.0;
-                } else if (fabs(apq) > tresh) {
-                    double h = d[q] - d[p];
-                    double t;
-                    if (fabs(h) + g == fabs(h)) {
-                        t = apq / h;
-                    } else {
-                        double theta = 0.5 * h / apq;
-                        t = 1.0 / (fabs(theta) + sqrt(1.0 + theta * theta));
-                        if (theta < 0.0) t = -t;
-                    }
-                    double c = 1.0 / sqrt(1 + t * t);
-                    double s = t * c;
-                    double tau = s / (1.0 + c);
-                    h = t * apq;
-                    z[p] -= h; z[q] += h; d[p] -= h; d[q] += h;
-                    a[p * N + q] = 0.0;
-#pragma unroll
-                    for (int j = 0; j < p; ++j) jrot<N>(a, j, p, j, q, s, tau);
-#pragma unroll
-                    for (int j = p + 1; j < q; ++j) jrot<N>(a, p, j, j, q, s, tau);
-#pragma unroll
-                    for (int j = q + 1; j < N; ++j) jrot<N>(a, p, j, q, j, s, tau);
-#pragma unroll
-                    for (int j = 0; j < N; ++j) jrot<N>(v, j, p, j, q, s, tau);
+}
+
+// tridiagonal_qr_step's Wilkinson shift from (diag[end-1], diag[end], sub[end-1])
+__device__ __forceinline__ double wilkinson_shift(double da, double db, double e) {
+    const double td = (da - db) * 0.5;
+    double mu = db;
+    if (td == 0.0) {
+        mu -= fabs(e);
+    } else {
+        const double e2 = e * e;
+        const double h = eigen_hypot(td, e);
+        if (e2 == 0.0)
+            mu -= (e / (td + (td > 0.0 ? 1.0 : -1.0))) * (e / h);
+        else
+            mu -= e2 / (td + (td > 0.0 ? h : -h));
+    }
+    return mu;
+}
+
+// One bulge-chasing rotation of tridiagonal_qr_step at k on (diag[k], diag[k+1], sub[k]): G^T T G.
+__device__ __forceinline__ void qr_rotate(double c, double s, double& dk, double& dk1, double& ek) {
+    const double sdk = s * dk + c * ek;
+    const double dkp1 = s * ek + c * dk1;
+    const double nk = c * (c * dk - s * ek) - s * (c * ek - s * dk1);
+    dk1 = s * sdk + c * dkp1;
+    ek = c * sdk - s * dkp1;
+    dk = nk;
+}
+// Q = Q * G on columns (k, k+1): applyOnTheRight(k, k+1, rot)
+__device__ __forceinline__ void q_rotate(double c, double s, double& a, double& b) {
+    const double xi = a, yi = b;
+    a = c * xi - s * yi;
+    b = s * xi + c * yi;
+}
+__device__ __forceinline__ bool eig_negligible(double e, double da, double db) {
+    return fabs(e) <= (fabs(da) + fabs(db)) * (2.0 * 2.220446049250313e-16) || fabs(e) <= 2.2250738585072014e-308;
+}
+
+// SelfAdjointEigenSolver<Matrix3d>(A).  A row-major (lower triangle read).  Out: d ascending,
+// V row-major with eigenvector i in column i.  Every index static (registers only).  Returns 0
+// (Success) or 1 (NoConvergence: left unsorted, as Eigen does).
+__device__ inline int saes3(const double* A, double d[3], double V[9]) {
+    double m00 = A[0], m10 = A[3], m20 = A[6], m11 = A[4], m21 = A[7], m22 = A[8];
+    double scale = 0.0;
+    scale = fabs(m00) > scale ? fabs(m00) : scale;
+    scale = fabs(m10) > scale ? fabs(m10) : scale;
+    scale = fabs(m20) > scale ? fabs(m20) : scale;
+    scale = fabs(m11) > scale ? fabs(m11) : scale;
+    scale = fabs(m21) > scale ? fabs(m21) : scale;
+    scale = fabs(m22) > scale ? fabs(m22) : scale;
+    if (scale == 0.0) scale = 1.0;
+    m00 /= scale; m10 /= scale; m20 /= scale; m11 /= scale; m21 /= scale; m22 /= scale;
+    // tridiagonalization_inplace_selector<MatrixType, 3, false>
+    double d0 = m00, d1, d2, e0, e1;
+    double q00 = 1.0, q01 = 0.0, q02 = 0.0, q10 = 0.0, q11, q12, q20 = 0.0, q21, q22;
+    const double v1norm2 = m20 * m20;
+    if (v1norm2 <= 2.2250738585072014e-308) {
+        d1 = m11; d2 = m22; e0 = m10; e1 = m21;
+        q11 = 1.0; q12 = 0.0; q21 = 0.0; q22 = 1.0;
+    } else {
+        const double beta = sqrt(m10 * m10 + v1norm2);
+        const double inv_beta = 1.0 / beta;
+        const double m01 = m10 * inv_beta, m02 = m20 * inv_beta;
+        const double q = 2.0 * m01 * m21 + m02 * (m22 - m11);
+        d1 = m11 + m02 * q;
+        d2 = m22 - m02 * q;
+        e0 = beta;
+        e1 = m21 - m01 * q;
+        q11 = m01; q12 = m02; q21 = m02; q22 = -m01;
+    }
+    // computeFromTridiagonal_impl
+    int end = 2, start = 0, iter = 0;
+    while (true) {
+        if (start <= 0 && end > 0 && eig_negligible(e0, d0, d1)) e0 = 0.0;
+        if (start <= 1 && end > 1 && eig_negligible(e1, d1, d2)) e1 = 0.0;
+        if (end == 2 && e1 == 0.0) end = 1;
+        if (end == 1 && e0 == 0.0) end = 0;
+        if (end == 0) break;
+        if (++iter > 90) break;
+        start = (end == 2 && e0 != 0.0) ? 0 : end - 1;
+        const double mu = end == 2 ? wilkinson_shift(d1, d2, e1) : wilkinson_shift(d0, d1, e0);
+        double c, s;
+        if (start == 0) {
+            make_givens(d0 - mu, e0, c, s);
+            qr_rotate(c, s, d0, d1, e0);
+            q_rotate(c, s, q00, q01); q_rotate(c, s, q10, q11); q_rotate(c, s, q20, q21);
+            if (end == 2) {
+                const double z = -s * e1;       // the bulge
+                e1 = c * e1;
+                make_givens(e0, z, c, s);
+                qr_rotate(c, s, d1, d2, e1);
+                e0 = c * e0 - s * z;
+                q_rotate(c, s, q01, q02); q_rotate(c, s, q11, q12); q_rotate(c, s, q21, q22);
+            }
+        } else {   // start == 1, end == 2
+            make_givens(d1 - mu, e1, c, s);
+            qr_rotate(c, s, d1, d2, e1);
+            q_rotate(c, s, q01, q02); q_rotate(c, s, q11, q12); q_rotate(c, s, q21, q22);
+        }
+    }
+    const int info = iter > 90 ? 1 : 0;
+    if (!info) {
+        // i = 0: first index of min(d0, d1, d2); i = 1: min(d1, d2)
+        if (d1 < d0 && !(d2 < d1)) {
+            double t = d0; d0 = d1; d1 = t;
+            t = q00; q00 = q01; q01 = t; t = q10; q10 = q11; q11 = t; t = q20; q20 = q21; q21 = t;
+        } else if (d2 < d0 && d2 < d1) {
+            double t = d0; d0 = d2; d2 = t;
+            t = q00; q00 = q02; q02 = t; t = q10; q10 = q12; q12 = t; t = q20; q20 = q22; q22 = t;
+        }
+        if (d2 < d1) {
+            double t = d1; d1 = d2; d2 = t;
+            t = q01; q01 = q02; q02 = t; t = q11; q11 = q12; q12 = t; t = q21; q21 = q22; q22 = t;
+        }
+    }
+    d[0] = d0 * scale; d[1] = d1 * scale; d[2] = d2 * scale;
+    V[0] = q00; V[1] = q01; V[2] = q02; V[3] = q10; V[4] = q11; V[5] = q12; V[6] = q20; V[7] = q21; V[8] = q22;
+    return info;
+}
+
+// SelfAdjointEigenSolver<MatrixXd>(A), N x N (one lane, runtime loops: the GN degeneracy test runs once
+// per Solve).  Householder tridiagonalisation (makeHouseholderInPlace, SYMV of the lower triangle,
+// rank-2 update) in plain sequential order (Eigen's packet kernels sum in another order: agreement to
+// rounding), Q from the Householder sequence, then the same QR iteration and sort as saes3.
+template <int N>
+__device__ inline int saesx(const double* A, double* d, double* V) {
+    double M[N * N];
+    double scale = 0.0;
+    for (int r = 0; r < N; ++r)
+        for (int c = 0; c < N; ++c) {
+            M[r * N + c] = c <= r ? A[r * N + c] : 0.0;
+            scale = fabs(M[r * N + c]) > scale ? fabs(M[r * N + c]) : scale;
+        }
+    if (scale == 0.0) scale = 1.0;
+    for (int r = 0; r < N; ++r)
+        for (int c = 0; c <= r; ++c) M[r * N + c] /= scale;
+    double hc[N];
+    for (int i = 0; i < N - 1; ++i) {
+        const int rem = N - i - 1;
+        double* col = M + (i + 1) * N + i;
+        const double c0 = col[0];
+        double tail = 0.0;
+        for (int r = 1; r < rem; ++r) tail += col[r * N] * col[r * N];
+        double tau, beta;
+        if (tail <= 2.2250738585072014e-308) {
+            tau = 0.0;
+            beta = c0;
+            for (int r = 1; r < rem; ++r) col[r * N] = 0.0;
+        } else {
+            beta = sqrt(c0 * c0 + tail);
+            if (c0 >= 0.0) beta = -beta;
+            for (int r = 1; r < rem; ++r) col[r * N] = col[r * N] / (c0 - beta);
+            tau = (beta - c0) / beta;
+        }
+        col[0] = 1.0;
+        double w[N], hv[N];
+        for (int r = 0; r < rem; ++r) hv[r] = tau * col[r * N];
+        for (int r = 0; r < rem; ++r) {
+            double s = 0.0;
+            for (int c = 0; c < rem; ++c) {
+                const int R = i + 1 + (r > c ? r : c), Cc = i + 1 + (r > c ? c : r);
+                s += M[R * N + Cc] * hv[c];
+            }
+            w[r] = s;
+        }
+        double dt = 0.0;
+        for (int r = 0; r < rem; ++r) dt += w[r] * col[r * N];
+        const double alpha = tau * -0.5 * dt;
+        for (int r = 0; r < rem; ++r) w[r] += alpha * col[r * N];
+        for (int c = 0; c < rem; ++c)
+            for (int r = c; r < rem; ++r)
+                M[(i + 1 + r) * N + (i + 1 + c)] += (-1.0 * col[c * N]) * w[r] + (-1.0 * w[c]) * col[r * N];
+        col[0] = beta;
+        hc[i] = tau;
+    }
+    double dg[N], sb[N];
+    for (int i = 0; i < N; ++i) dg[i] = M[i * N + i];
+    for (int i = 0; i < N - 1; ++i) sb[i] = M[(i + 1) * N + i];
+    for (int r = 0; r < N; ++r)
+        for (int c = 0; c < N; ++c) V[r * N + c] = r == c ? 1.0 : 0.0;
+    for (int k = N - 2; k >= 0; --k) {
+        const int o = k + 1, cs = N - k - 1;
+        const double tau = hc[k];
+        if (cs == 1) {
+            V[o * N + o] *= (1.0 - tau);
+        } else if (tau != 0.0) {
+            for (int c = o; c < N; ++c) {
+                double tmp = 0.0;
+                for (int r = 1; r < cs; ++r) tmp += M[(o + r) * N + k] * V[(o + r) * N + c];
+                tmp += V[o * N + c];
+                V[o * N + c] -= tau * tmp;
+                for (int r = 1; r < cs; ++r) V[(o + r) * N + c] -= (tau * M[(o + r) * N + k]) * tmp;
+            }
+        }
+    }
+    int end = N - 1, start = 0, iter = 0;
+    while (end > 0) {
+        for (int i = start; i < end; ++i)
+            if (eig_negligible(sb[i], dg[i], dg[i + 1])) sb[i] = 0.0;
+        while (end > 0 && sb[end - 1] == 0.0) end--;
+        if (end <= 0) break;
+        if (++iter > 30 * N) break;
+        start = end - 1;
+        while (start > 0 && sb[start - 1] != 0.0) start--;
+        const double mu = wilkinson_shift(dg[end - 1], dg[end], sb[end - 1]);
+        double x = dg[start] - mu, z = sb[start];
+        for (int k = start; k < end; ++k) {
+            double c, s;
+            make_givens(x, z, c, s);
+            qr_rotate(c, s, dg[k], dg[k + 1], sb[k]);
+            if (k > start) sb[k - 1] = c * sb[k - 1] - s * z;
+            x = sb[k];
+            if (k < end - 1) {
+                z = -s * sb[k + 1];
+                sb[k + 1] = c * sb[k + 1];
+            }
+            for (int r = 0; r < N; ++r) q_rotate(c, s, V[r * N + k], V[r * N + k + 1]);
+        }
+    }
+    const int info = iter > 30 * N ? 1 : 0;
+    if (!info) {
+        for (int i = 0; i < N - 1; ++i) {
+            int k = 0;
+            for (int j = 1; j < N - i; ++j)
+                if (dg[i + j] < dg[i + k]) k = j;
+            if (k > 0) {
+                const double t = dg[i]; dg[i] = dg[i + k]; dg[i + k] = t;
+                for (int r = 0; r < N; ++r) {
+                    const double u = V[r * N + i]; V[r * N + i] = V[r * N + i + k]; V[r * N + i + k] = u;
                 }
             }
         }
-#pragma unroll
-        for (int p = 0; p < N; ++p) { b[p] += z[p]; d[p] = b[p]; z[p] = 0.0; }
     }
+    for (int i = 0; i < N; ++i) d[i] = dg[i] * scale;
+    return info;
 }
-
-// Eigenvalue order of a 3x3 result (ascending, stable on index) without dynamic indexing.
-__device__ __forceinline__ void order3(const double* d, int& i0, int& i1, int& i2) {
-    // insertion sort of (0,1,2) by d, stable; the values ride along (a0 = d[i0], a1 = d[i1]) so no
-    // runtime index touches d (a dynamically indexed array lives in scratch)
-    i0 = 0; i1 = 1; i2 = 2;
-    double a0 = d[0], a1 = d[1];
-    const double a2 = d[2];
-    if (a0 > a1) { int t = i0; i0 = i1; i1 = t; double u = a0; a0 = a1; a1 = u; }
-    // insert element 2
-    if (a1 > a2) {
-        i2 = i1;
-        if (a0 > a2) { i1 = i0; i0 = 2; } else { i1 = 2; }
-    }
-}
-// Middle and largest value of the stable ascending order of d[0..2] and the largest's index
-// (= d[i1], d[i2] of order3), as selects: order3's reference outputs end up in scratch.
-__device__ __forceinline__ void top2_of3(const double* d, double& mid, double& big, int& ibig) {
-    double a0 = d[0], a1 = d[1];
-    int j1 = 1;
-    if (a0 > a1) { const double u = a0; a0 = a1; a1 = u; j1 = 0; }
-    const double a2 = d[2];
-    const bool hi = a1 > a2;   // element 2 inserted below a1
-    ibig = hi ? j1 : 2;
-    big = hi ? a1 : a2;
-    mid = hi ? (a0 > a2 ? a0 : a2) : a1;
-}
-__device__ __forceinline__ double pick3(const double* a, int i) { return i == 0 ? a[0] : (i == 1 ? a[1] : a[2]); }
 
 // ---------------------------------------------------------------- ColPivHouseholderQR solve
 // Eigen computeInPlace + _solve_impl restated (surfFeatureMatch.hpp:52, edgeSurf...:272).

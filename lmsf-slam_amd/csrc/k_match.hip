@@ -597,13 +597,9 @@ __device__ bool edge_fit(const float4* np, d3& a, d3& b) {
             for (int c = 0; c < 3; ++c) cov[r * 3 + c] = cov[r * 3 + c] + ev[r] * ev[c];
     }
     double d[3], v[9];
-    jacobi_eig<3>(cov, d, v);
-    int i2;
-    double l1, l2;
-    top2_of3(d, l1, l2, i2);
-    if (!(l2 > 3 * l1)) return false;
-    const double c0[3] = {v[0], v[3], v[6]}, c1[3] = {v[1], v[4], v[7]}, c2[3] = {v[2], v[5], v[8]};
-    d3 u = i2 == 0 ? mk(c0[0], c0[1], c0[2]) : (i2 == 1 ? mk(c1[0], c1[1], c1[2]) : mk(c2[0], c2[1], c2[2]));
+    saes3(cov, d, v);   // Eigen::SelfAdjointEigenSolver<Matrix3d> (EdgeFeatureMatch.hpp:63)
+    if (!(d[2] > 3 * d[1])) return false;
+    const d3 u = mk(v[2], v[5], v[8]);   // eigenvectors().col(2)
     a = smul(0.1, u) + center;
     b = smul(-0.1, u) + center;
     return true;
@@ -1346,7 +1342,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_EVAL_W
 // err[0] and leaves (the host reports LMSF_ERR_HIP), so no configuration can hang the device.
 // sync[2 b] counts arrivals of slot b across launches; sync[2 b + 1] holds the count at the start of the
 // next launch (written by block 0 after the last wait of this one).
-constexpr unsigned kLoopSpinLimit = 1u << 24;
 
 __device__ __forceinline__ void coherent_store_f64(double* p, double v) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
@@ -1358,7 +1353,7 @@ __device__ __forceinline__ double coherent_load_f64(const double* p) {
 }
 
 // Every block of the slot arrives once; returns when all nblk of this barrier have (count reaches target).
-__device__ __forceinline__ void slot_barrier(unsigned* cnt, unsigned target, int* err) {
+__device__ __forceinline__ void slot_barrier(unsigned* cnt, unsigned target, int* err, unsigned spin_limit) {
     __builtin_amdgcn_s_waitcnt(0);   // this wave's packet stores are complete
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1366,7 +1361,7 @@ __device__ __forceinline__ void slot_barrier(unsigned* cnt, unsigned target, int
         unsigned spins = 0;
         while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > kLoopSpinLimit) {
+            if (++spins > spin_limit) {
                 __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
@@ -1402,7 +1397,8 @@ __device__ void reduce_coherent(const BatchView& bv, int b, int p0, int np, doub
     __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, unsigned* sync, int* err) {
+__global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, unsigned* sync, int* err,
+                                                      unsigned spin_limit) {
     const int b = blockIdx.y, part = blockIdx.x, nblk = gridDim.x;
     __shared__ SolveState sS;
     __shared__ double tot[kPacket];
@@ -1460,14 +1456,14 @@ __global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, u
             }
         }
         ++nbar;
-        slot_barrier(&sync[2 * b], base + nbar * (unsigned)nblk, err);
+        slot_barrier(&sync[2 * b], base + nbar * (unsigned)nblk, err, spin_limit);
         reduce_coherent(bv, b, pbuf + (i & 1) * nblk, nblk, tot);
         if (threadIdx.x == 0) lm_step_apply(sS, tot, outer, last);
         __syncthreads();
     }
     if (nbar == 0) {   // no wait yet: make sure every block has read st before block 0 rewrites it
         ++nbar;
-        slot_barrier(&sync[2 * b], base + nbar * (unsigned)nblk, err);
+        slot_barrier(&sync[2 * b], base + nbar * (unsigned)nblk, err, spin_limit);
     }
     if (part == 0) {
         state_copy(bv.st[b], sS);
@@ -1477,8 +1473,10 @@ __global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, u
 
 int lm_loop_blocks(const BatchView& bv) { return (bv.feat_stride + kEvalBlock - 1) / kEvalBlock; }
 
-hipError_t launch_lm_loop(const BatchView& bv, int outer, unsigned* sync, int* err, hipStream_t s) {
-    hipLaunchKernelGGL(lm_loop_kernel, dim3(lm_loop_blocks(bv), bv.B), dim3(256), 0, s, bv, outer, sync, err);
+hipError_t launch_lm_loop(const BatchView& bv, int outer, unsigned* sync, int* err, unsigned spin_limit,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(lm_loop_kernel, dim3(lm_loop_blocks(bv), bv.B), dim3(256), 0, s, bv, outer, sync, err,
+                       spin_limit);
     return hipGetLastError();
 }
 

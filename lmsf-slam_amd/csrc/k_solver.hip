@@ -133,20 +133,10 @@ __global__ __launch_bounds__(64) void gn_solve_kernel(BatchView bv, int outer) {
     for (int i = 0; i < 6; ++i) nb[i] = -JTR[i];
     colpiv_qr_solve<6, 6>(A, nb, X);
     if (outer == 0) {  // degeneracy check at iterCount == 0 (edgeSurf...:280-304)
-        double a2[36], d[6], V[36];
+        double a2[36], d[6], ds[6], Vs[36], V2[36];
         for (int i = 0; i < 36; ++i) a2[i] = JTJ[i];
-        jacobi_eig<6>(a2, d, V);
-        int ord[6] = {0, 1, 2, 3, 4, 5};
-        for (int i = 1; i < 6; ++i) {
-            int k = ord[i], j = i;
-            while (j > 0 && d[ord[j - 1]] > d[k]) { ord[j] = ord[j - 1]; --j; }
-            ord[j] = k;
-        }
-        double ds[6], Vs[36], V2[36];
-        for (int c = 0; c < 6; ++c) {
-            ds[c] = d[ord[c]];
-            for (int r = 0; r < 6; ++r) Vs[r * 6 + c] = V[r * 6 + ord[c]];
-        }
+        saesx<6>(a2, d, Vs);   // SelfAdjointEigenSolver<MatrixXd> (edgeSurf...:282): ascending, sorted
+        for (int i = 0; i < 6; ++i) ds[i] = d[i];
         for (int i = 0; i < 36; ++i) V2[i] = Vs[i];
         S.gn_degenerate = 0;
         for (int i = 5; i >= 0; i--) {
@@ -298,6 +288,30 @@ hipError_t launch_lm_begin(const BatchView& bv, hipStream_t s) {
 
 hipError_t launch_lm_step(const BatchView& bv, int outer, int is_last, hipStream_t s) {
     hipLaunchKernelGGL(lm_step_kernel, dim3(bv.B), dim3(kStepThreads), 0, s, bv, outer, is_last);
+    return hipGetLastError();
+}
+
+// Device self-test of the restated SelfAdjointEigenSolver (lmsf_eigen_selfadjoint): one lane per matrix,
+// dim 3 = the Matrix3d path of the edge fit, 6 = the MatrixXd path of the GN degeneracy test.
+template <int D>
+__global__ __launch_bounds__(64) void eigen_selftest_kernel(const double* a, int n, double* d, double* v, int* info) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    double A[D * D], dd[D], V[D * D];
+    for (int k = 0; k < D * D; ++k) A[k] = a[(size_t)i * D * D + k];
+    int rc;
+    if constexpr (D == 3) rc = saes3(A, dd, V);
+    else rc = saesx<D>(A, dd, V);
+    for (int k = 0; k < D; ++k) d[(size_t)i * D + k] = dd[k];
+    for (int k = 0; k < D * D; ++k) v[(size_t)i * D * D + k] = V[k];
+    info[i] = rc;
+}
+
+hipError_t launch_eigen_selftest(int dim, const double* a, int n, double* d, double* v, int* info, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((n + 63) / 64);
+    if (dim == 3) hipLaunchKernelGGL(eigen_selftest_kernel<3>, grid, dim3(64), 0, s, a, n, d, v, info);
+    else hipLaunchKernelGGL(eigen_selftest_kernel<6>, grid, dim3(64), 0, s, a, n, d, v, info);
     return hipGetLastError();
 }
 

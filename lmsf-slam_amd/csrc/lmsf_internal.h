@@ -189,9 +189,13 @@ hipError_t launch_lin_eval(const BatchView& bv, hipStream_t s);
 // (zeroed once), err: set when a bounded wait gave up.
 constexpr int kLoopMaxBlocks = 128;   // half the CUs: room for other streams' launches beside it
 int lm_loop_blocks(const BatchView& bv);
-hipError_t launch_lm_loop(const BatchView& bv, int outer, unsigned* sync, int* err, hipStream_t s);
+// spin_limit: sleeps a block waits at a barrier before it flags err and leaves (kLoopSpinDefault; 0 in the
+// fault-recovery test, LMSF_OPT_LOOP_FAULT_TEST)
+constexpr unsigned kLoopSpinDefault = 1u << 24;
+hipError_t launch_lm_loop(const BatchView& bv, int outer, unsigned* sync, int* err, unsigned spin_limit, hipStream_t s);
 hipError_t launch_lm_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
 hipError_t launch_gn_solve(const BatchView& bv, int outer, hipStream_t s);
+hipError_t launch_eigen_selftest(int dim, const double* a, int n, double* d, double* v, int* info, hipStream_t s);
 int fit_per_thread_default();
 int knn_team_for(size_t query_slots);   // lanes per query of a search launch over that many query slots
 // Fused 5-NN search + fit + first evaluation (one lane per query, queries in fslot order); false:

@@ -20,7 +20,8 @@ EDGE, SURF = 1, 2
 UPDATE_NONE, UPDATE_MOTION, UPDATE_TIME = 0, 1, 2
 SOLVER_CERES_LM, SOLVER_GN = 0, 1
 SCHEDULE_REFERENCE_DECAY, SCHEDULE_FIXED = 0, 1
-OPT_QUERY_MEMO, OPT_MEMO_REFIT, OPT_MEMO_EXACT, OPT_MEMO_ORDER, OPT_MEMO_BOUND, OPT_GRAPH, OPT_MEMO_SKIP1 = range(7)
+(OPT_QUERY_MEMO, OPT_MEMO_REFIT, OPT_MEMO_EXACT, OPT_MEMO_ORDER, OPT_MEMO_BOUND, OPT_GRAPH, OPT_MEMO_SKIP1, OPT_LM_LOOP,
+ OPT_LOOP_FAULT_TEST) = range(9)
 TERM_NAMES = {0: "max_iterations", 1: "function_tol", 2: "parameter_tol", 3: "gradient_tol",
               4: "no_residuals", 5: "gn_converged", 6: "gn_too_few"}
 
@@ -51,7 +52,7 @@ class FeatureCounts(C.Structure):
 class KernelStats(C.Structure):
     _fields_ = [("launches", C.c_int64), ("total_ms", C.c_double), ("queries", C.c_int64), ("n27_sum", C.c_int64),
                 ("fused_launches", C.c_int64), ("reused_queries", C.c_int64),
-                ("refit_queries", C.c_int64)]
+                ("refit_queries", C.c_int64), ("loop_recoveries", C.c_int64)]
 
 
 class ExtractParams(C.Structure):
@@ -119,6 +120,7 @@ _SIGS = {
     "lmsf_batch_records": (C.c_int32, [_P, C.c_int32, C.c_int32, _P, _P, C.c_size_t, _P, C.POINTER(C.c_size_t)]),
     "lmsf_match": (C.c_int32, [_P, _P, _P, _P, C.c_size_t]),
     "lmsf_eval": (C.c_int32, [_P, _P, _P]),
+    "lmsf_eigen_selfadjoint": (C.c_int32, [_P, C.c_int32, _P, C.c_size_t, _P, _P, _P]),
     "lmsf_kernel_stats_get": (C.c_int32, [_P, C.POINTER(KernelStats)]),
     "lmsf_kernel_stats_reset": (C.c_int32, [_P, C.c_int32]),
     "lmsf_version": (C.c_char_p, []),
@@ -443,6 +445,18 @@ class Context:
         x = np.ascontiguousarray(pose, dtype=np.float64)
         self._check(load().lmsf_eval(self.h, x.ctypes.data, out.ctypes.data))
         return out
+
+    def eigen_selfadjoint(self, a):
+        """The device's restated SelfAdjointEigenSolver on a stack of 3x3 (Matrix3d path) or 6x6 (MatrixXd
+        path) symmetric matrices -> (eigenvalues ascending, eigenvectors in columns, info)."""
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        n, dim = a.shape[0], a.shape[1]
+        d = np.zeros((n, dim))
+        v = np.zeros((n, dim, dim))
+        info = np.zeros(n, np.int32)
+        self._check(load().lmsf_eigen_selfadjoint(self.h, dim, a.ctypes.data, n, d.ctypes.data, v.ctypes.data,
+                                                  info.ctypes.data))
+        return d, v, info
 
     def kernel_stats_reset(self, timing=True, n27=False):
         """timing: HIP-event time, launches and queries of the neighbour search; n27: the n27

@@ -152,12 +152,32 @@ def perturb(pose, rng, sigma_t=0.1, sigma_r_deg=1.0):
 
 
 def pose_delta(a, b):
-    """(translation error m, rotation error rad) between two (q, t) poses."""
+    """(translation error m, rotation error rad) between two (q, t) poses.  The angle is the log map of the
+    relative rotation, 2 atan2(|v|, |w|) of r = conj(qa) qb: it resolves angles down to ~1e-16 rad, where
+    the acos of a dot product stops at its sqrt(2 eps) ~ 3e-8 floor."""
     dt = float(np.linalg.norm(np.asarray(a[4:]) - np.asarray(b[4:])))
-    qa = np.asarray(a[:4]) / np.linalg.norm(a[:4])
-    qb = np.asarray(b[:4]) / np.linalg.norm(b[:4])
-    d = abs(float(np.dot(qa, qb)))
-    return dt, 2.0 * math.acos(min(1.0, d))
+    return dt, rot_angle_between(a[:4], b[:4])
+
+
+def rot_angle_between(qa, qb):
+    """Angle of conj(qa) * qb (quaternions x, y, z, w; normalised here) by 2 atan2(|vec|, |w|)."""
+    qa = np.asarray(qa, np.float64) / np.linalg.norm(qa)
+    qb = np.asarray(qb, np.float64) / np.linalg.norm(qb)
+    ax, ay, az, aw = -qa[0], -qa[1], -qa[2], qa[3]
+    bx, by, bz, bw = qb
+    w = aw * bw - ax * bx - ay * by - az * bz
+    x = aw * bx + ax * bw + ay * bz - az * by
+    y = aw * by + ay * bw + az * bx - ax * bz
+    z = aw * bz + az * bw + ax * by - ay * bx
+    return 2.0 * math.atan2(math.sqrt(x * x + y * y + z * z), abs(w))
+
+
+def rot_angle_of_matrix(R):
+    """Rotation angle of a 3x3 rotation matrix: atan2(|vee(R - R^T)| / 2, (tr R - 1) / 2), accurate at small
+    angles (no acos)."""
+    R = np.asarray(R, np.float64)
+    v = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]]) * 0.5
+    return float(math.atan2(float(np.linalg.norm(v)), (float(np.trace(R)) - 1.0) * 0.5))
 
 
 # ----------------------------------------------------------------------------- ray casting

@@ -128,6 +128,13 @@ void lmsfo_eval(const lmsfo_record* rec, int64_t n, const double pose[7], double
 /* PoseSE3Parameterization::Plus (INC/Algorithm/Ceres/Parameterization/PoseSE3Parameterization.hpp:32-46). */
 void lmsfo_pose_plus(const double x[7], const double delta[6], double out[7]);
 
+/* Eigen 3.3 SelfAdjointEigenSolver restated (oracle/saes.cpp).  a: n x n row-major symmetric (lower
+ * triangle read); d: ascending eigenvalues; v: row-major, eigenvector i in column i.  lmsfo_saes3 is
+ * the fixed-size Matrix3d path (EdgeFeatureMatch.hpp:63), lmsfo_saesx the dynamic MatrixXd path
+ * (edgeSurfFeatureRegistration.hpp:282), n <= 8.  Returns 0 (Success) or 1 (NoConvergence: unsorted). */
+int lmsfo_saes3(const double a[9], double d[3], double v[9]);
+int lmsfo_saesx(int n, const double* a, double* d, double* v);
+
 void lmsfo_set_num_threads(int n);
 
 #ifdef __cplusplus

@@ -76,6 +76,8 @@ def lib():
         L.lmsfo_ingest.argtypes = [C.c_void_p, C.c_int64, C.c_uint32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                    C.c_float, C.c_float, C.c_float, fp]
         L.lmsfo_voxel_filter.argtypes = [fp, C.c_int64, C.c_float, fp]
+        L.lmsfo_saes3.argtypes = [dp, dp, dp]
+        L.lmsfo_saesx.argtypes = [C.c_int, dp, dp, dp]
         _lib = L
     return _lib
 
@@ -216,6 +218,22 @@ def eval_records(rec, pose):
     r = np.ascontiguousarray(rec)
     lib().lmsfo_eval(r.ctypes.data, len(r), np.ascontiguousarray(pose, np.float64), out)
     return out
+
+
+def saes(a, fixed3=None):
+    """Eigen 3.3 SelfAdjointEigenSolver restated (saes.cpp) -> (eigenvalues ascending, eigenvectors in
+    columns, info).  fixed3 (default: n == 3) selects the Matrix3d path, else the MatrixXd path."""
+    a = np.ascontiguousarray(a, np.float64)
+    n = a.shape[0]
+    d = np.zeros(n)
+    v = np.zeros((n, n))
+    if fixed3 is None:
+        fixed3 = n == 3
+    if fixed3:
+        info = lib().lmsfo_saes3(a.reshape(-1), d, v.reshape(-1))
+    else:
+        info = lib().lmsfo_saesx(n, a.reshape(-1), d, v.reshape(-1))
+    return d, v, info
 
 
 def pose_plus(x, delta):

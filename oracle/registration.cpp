@@ -9,7 +9,7 @@
 //   REG/edgeSurfFeatureRegistration.hpp:113-350        (GN variant)
 // External algorithms restated from their published descriptions (parity unpinned):
 //   Eigen 3 Quaternion::_transformVector / quat_product / toRotationMatrix, ColPivHouseholderQR,
-//   SelfAdjointEigenSolver (restated as cyclic Jacobi), Ceres Solver 1.x TrustRegionMinimizer +
+//   SelfAdjointEigenSolver (saes.cpp), Ceres Solver 1.x TrustRegionMinimizer +
 //   LevenbergMarquardtStrategy (jacobi_scaling, DENSE_QR restated as normal equations), HuberLoss.
 #include <algorithm>
 #include <cfloat>
@@ -111,74 +111,6 @@ void pose_plus(const double* x, const double* delta, double* out) {
     V3 tp = add(rotate(dq, pose_t(x)), dt);
     out[0] = qp.x; out[1] = qp.y; out[2] = qp.z; out[3] = qp.w;
     out[4] = tp.x; out[5] = tp.y; out[6] = tp.z;
-}
-
-// ---------------------------------------------------------------- symmetric eigen (cyclic Jacobi)
-// Ascending eigenvalues; eigenvectors in the columns of v.  n <= 6.
-void jacobi_eig(int n, double* a, double* d, double* v) {
-    double b[6], z[6];
-    for (int i = 0; i < n; ++i) {
-        for (int j = 0; j < n; ++j) v[i * n + j] = (i == j) ? 1.0 : 0.0;
-        b[i] = d[i] = a[i * n + i];
-        z[i] = 0.0;
-    }
-    auto rot = [](double* m, int n_, int i, int j, int k, int l, double s, double tau) {
-        double g = m[i * n_ + j], h = m[k * n_ + l];
-        m[i * n_ + j] = g - s * (h + g * tau);
-        m[k * n_ + l] = h + s * (g - h * tau);
-    };
-    for (int sweep = 1; sweep <= 50; ++sweep) {
-        double sm = 0.0;
-        for (int p = 0; p < n - 1; ++p)
-            for (int q = p + 1; q < n; ++q) sm += std::fabs(a[p * n + q]);
-        if (sm == 0.0) break;
-        double tresh = (sweep < 4) ? 0.2 * sm / (n * n) : 0.0;
-        for (int p = 0; p < n - 1; ++p) {
-            for (int q = p + 1; q < n; ++q) {
-                double apq = a[p * n + q];
-                double g = 100.0 * std::fabs(apq);
-                if (sweep > 4 && std::fabs(d[p]) + g == std::fabs(d[p]) && std::fabs(d[q]) + g == std::fabs(d[q])) {
-                    a[p * n + q] = 0.0;
-                } else if (std::fabs(apq) > tresh) {
-                    double h = d[q] - d[p];
-                    double t;
-                    if (std::fabs(h) + g == std::fabs(h)) {
-                        t = apq / h;
-                    } else {
-                        double theta = 0.5 * h / apq;
-                        t = 1.0 / (std::fabs(theta) + std::sqrt(1.0 + theta * theta));
-                        if (theta < 0.0) t = -t;
-                    }
-                    double c = 1.0 / std::sqrt(1 + t * t);
-                    double s = t * c;
-                    double tau = s / (1.0 + c);
-                    h = t * apq;
-                    z[p] -= h; z[q] += h; d[p] -= h; d[q] += h;
-                    a[p * n + q] = 0.0;
-                    for (int j = 0; j < p; ++j) rot(a, n, j, p, j, q, s, tau);
-                    for (int j = p + 1; j < q; ++j) rot(a, n, p, j, j, q, s, tau);
-                    for (int j = q + 1; j < n; ++j) rot(a, n, p, j, q, j, s, tau);
-                    for (int j = 0; j < n; ++j) rot(v, n, j, p, j, q, s, tau);
-                }
-            }
-        }
-        for (int p = 0; p < n; ++p) { b[p] += z[p]; d[p] = b[p]; z[p] = 0.0; }
-    }
-    // sort ascending (stable on index), as SelfAdjointEigenSolver reports
-    int ord[6];
-    for (int i = 0; i < n; ++i) ord[i] = i;
-    for (int i = 1; i < n; ++i) {
-        int k = ord[i], j = i;
-        while (j > 0 && d[ord[j - 1]] > d[k]) { ord[j] = ord[j - 1]; --j; }
-        ord[j] = k;
-    }
-    double dd[6], vv[36];
-    for (int c = 0; c < n; ++c) {
-        dd[c] = d[ord[c]];
-        for (int r = 0; r < n; ++r) vv[r * n + c] = v[r * n + ord[c]];
-    }
-    for (int c = 0; c < n; ++c) d[c] = dd[c];
-    for (int i = 0; i < n * n; ++i) v[i] = vv[i];
 }
 
 // ---------------------------------------------------------------- ColPivHouseholderQR solve
@@ -320,7 +252,7 @@ bool edge_fit(const float* mp, const int32_t* nn, const float q[3], Match& m) {
             for (int c = 0; c < 3; ++c) cov[r * 3 + c] = cov[r * 3 + c] + ev[r] * ev[c];
     }
     double d[3], v[9];
-    jacobi_eig(3, cov, d, v);
+    lmsfo_saes3(cov, d, v);   // Eigen::SelfAdjointEigenSolver<Matrix3d> (EdgeFeatureMatch.hpp:63, saes.cpp)
     V3 u{v[0 * 3 + 2], v[1 * 3 + 2], v[2 * 3 + 2]};
     if (!(d[2] > 3 * d[1])) return false;
     V3 a = add(mul(0.1, u), center);
@@ -708,7 +640,7 @@ bool gn_step(lmsfo_reg* r, int iterCount, const std::vector<Match>& ms, int64_t 
     if (iterCount == 0) {
         double a2[36], d[6], V[36];
         std::memcpy(a2, JTJ, sizeof a2);
-        jacobi_eig(6, a2, d, V);
+        lmsfo_saesx(6, a2, d, V);   // SelfAdjointEigenSolver<MatrixXd> (edgeSurf...:282, saes.cpp)
         double V2[36];
         std::memcpy(V2, V, sizeof V2);
         r->gn_degenerate = false;

@@ -55,6 +55,29 @@ def sequence_workload():
     return SimpleNamespace(scans=scans, truth=truth, n_scans=64, dt=0.1, edge_map=edge_map, surf_map=surf_map)
 
 
+def saes_cases():
+    """Symmetric 3x3 inputs of the edge fit's eigen-solver: 5-point covariances, near-collinear sets,
+    and the special cases of Eigen's algorithm (diagonal, tridiagonal, underflowing m20, repeated)."""
+    rng = np.random.default_rng(11)
+    out = []
+    for _ in range(3000):                   # 5-point covariances, as the edge fit builds them
+        P = (rng.normal(size=(5, 3)) * rng.uniform(0.001, 1.0, 3)).astype(np.float32).astype(np.float64)
+        c = P.sum(0) / 5.0
+        out.append((P - c).T @ (P - c))
+    for _ in range(300):                    # nearly collinear points: the accepted-edge regime
+        t = rng.uniform(-0.5, 0.5, 5)
+        d = rng.normal(size=3)
+        P = np.outer(t, d) + rng.normal(scale=1e-3, size=(5, 3))
+        c = P.sum(0) / 5.0
+        out.append((P - c).T @ (P - c))
+    out += [np.diag([3.0, 1.0, 2.0]), np.diag([1.0, 1.0, 1.0]), np.zeros((3, 3)),
+            np.array([[2.0, 1.0, 0.0], [1.0, 2.0, 1.0], [0.0, 1.0, 2.0]]),       # already tridiagonal
+            np.array([[1.0, 0.0, 1e-170], [0.0, 1.0, 0.0], [1e-170, 0.0, 1.0]]),  # m20^2 underflows
+            np.array([[4.0, 2.0, 2.0], [2.0, 4.0, 2.0], [2.0, 2.0, 4.0]]),       # repeated eigenvalue
+            np.ones((3, 3)), -np.eye(3), np.diag([1e-300, 1.0, 1e300])]
+    return out
+
+
 def pose_matrix(p):
     from lmsf import synth
     T = np.eye(4)
@@ -77,11 +100,9 @@ def relative_truth(truth):
 
 
 def mat_err(A, B):
-    import math
+    from lmsf import synth
     dt = float(np.linalg.norm(A[:3, 3] - B[:3, 3]))
-    R = A[:3, :3].T @ B[:3, :3]
-    c = max(-1.0, min(1.0, (np.trace(R) - 1) / 2))
-    return dt, math.acos(c)
+    return dt, synth.rot_angle_of_matrix(A[:3, :3].T @ B[:3, :3])
 
 
 def pose_err(a, b):

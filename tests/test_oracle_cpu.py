@@ -1,7 +1,7 @@
 """CPU checks of the oracle (the parity checker) against independent implementations.
 
 The reference has no runnable tests or golden vectors for this path, so
-the CPU restatement is pinned here by: scipy cKDTree (exact k-NN), numpy eigh (PCA line),
+the CPU restatement is pinned here by: scipy cKDTree (exact k-NN), numpy eigh (PCA line; plus an independent transcription of Eigen's SelfAdjointEigenSolver),
 numpy lstsq (plane fit), finite differences (Jacobians / gradient), closed-form SE(3) algebra
 (Plus), the reference's own commented-out known-answer test re-created on synthetic clouds
 (feature_registration_test.cpp:73-112: yaw 5 deg, t = (0.9, 0.4, 0.5)), and the committed
@@ -13,7 +13,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import pose_err
+from conftest import pose_err, saes_cases
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -74,6 +74,191 @@ def test_edge_line_fit_vs_numpy(oracle_mod, tiny):
         d = (a - b) / 0.2
         assert abs(abs(d @ u) - 1.0) < 1e-9                      # same principal direction (sign free)
         assert w[2] > 3 * w[1]                                    # linearity test passed (EdgeFeatureMatch.hpp:68)
+
+
+# ---------------------------------------------------------------- Eigen SelfAdjointEigenSolver
+# A second, independent transcription of Eigen 3.3's published algorithm (pure Python floats: IEEE double,
+# no FMA) -- the C restatement (oracle/saes.cpp) must agree with it bit for bit, which pins the rotation
+# signs, the deflation test and the sort, i.e. the eigenvector sign convention the reference's edge fit
+# inherits (a = c + 0.1 u, b = c - 0.1 u: EdgeFeatureMatch.hpp:65-73).
+_DBL_MIN = 2.2250738585072014e-308
+_EPS = 2.220446049250313e-16
+
+
+def _py_givens(p, q):
+    if q == 0.0:
+        return (-1.0 if p < 0.0 else 1.0), 0.0
+    if p == 0.0:
+        return 0.0, (1.0 if q < 0.0 else -1.0)
+    if abs(p) > abs(q):
+        t = q / p
+        u = math.sqrt(1.0 + t * t)
+        u = -u if p < 0.0 else u
+        c = 1.0 / u
+        return c, -t * c
+    t = p / q
+    u = math.sqrt(1.0 + t * t)
+    u = -u if q < 0.0 else u
+    s = -1.0 / u
+    return -t * s, s
+
+
+def _py_saes3(A):
+    m = [[float(A[r][c]) if c <= r else 0.0 for c in range(3)] for r in range(3)]
+    scale = 0.0
+    for c in range(3):                      # column-major walk; max is order-free
+        for r in range(3):
+            scale = max(scale, abs(m[r][c]))
+    if scale == 0.0:
+        scale = 1.0
+    for r in range(3):
+        for c in range(r + 1):
+            m[r][c] = m[r][c] / scale
+    diag = [m[0][0], 0.0, 0.0]
+    v1 = m[2][0] * m[2][0]
+    if v1 <= _DBL_MIN:
+        diag[1], diag[2] = m[1][1], m[2][2]
+        sub = [m[1][0], m[2][1]]
+        Q = [[1.0, 0.0, 0.0], [0.0, 1.0, 0.0], [0.0, 0.0, 1.0]]
+    else:
+        beta = math.sqrt(m[1][0] * m[1][0] + v1)
+        ib = 1.0 / beta
+        m01, m02 = m[1][0] * ib, m[2][0] * ib
+        q = 2.0 * m01 * m[2][1] + m02 * (m[2][2] - m[1][1])
+        diag[1] = m[1][1] + m02 * q
+        diag[2] = m[2][2] - m02 * q
+        sub = [beta, m[2][1] - m01 * q]
+        Q = [[1.0, 0.0, 0.0], [0.0, m01, m02], [0.0, m02, -m01]]
+    n, end, start, it = 3, 2, 0, 0
+    while end > 0:
+        for i in range(start, end):
+            if abs(sub[i]) <= (abs(diag[i]) + abs(diag[i + 1])) * (2 * _EPS) or abs(sub[i]) <= _DBL_MIN:
+                sub[i] = 0.0
+        while end > 0 and sub[end - 1] == 0.0:
+            end -= 1
+        if end <= 0:
+            break
+        it += 1
+        if it > 30 * n:
+            break
+        start = end - 1
+        while start > 0 and sub[start - 1] != 0.0:
+            start -= 1
+        td = (diag[end - 1] - diag[end]) * 0.5
+        e = sub[end - 1]
+        mu = diag[end]
+        if td == 0.0:
+            mu -= abs(e)
+        else:
+            ax, ay = abs(td), abs(e)
+            p, qp = (ax, ay / ax) if ax > ay else (ay, ax / ay)
+            h = 0.0 if p == 0.0 else p * math.sqrt(1.0 + qp * qp)
+            mu -= (e / (td + (1.0 if td > 0 else -1.0))) * (e / h) if e * e == 0.0 else e * e / (td + (h if td > 0 else -h))
+        x, z = diag[start] - mu, sub[start]
+        for k in range(start, end):
+            c, s = _py_givens(x, z)
+            sdk = s * diag[k] + c * sub[k]
+            dkp1 = s * sub[k] + c * diag[k + 1]
+            diag[k] = c * (c * diag[k] - s * sub[k]) - s * (c * sub[k] - s * diag[k + 1])
+            diag[k + 1] = s * sdk + c * dkp1
+            sub[k] = c * sdk - s * dkp1
+            if k > start:
+                sub[k - 1] = c * sub[k - 1] - s * z
+            x = sub[k]
+            if k < end - 1:
+                z = -s * sub[k + 1]
+                sub[k + 1] = c * sub[k + 1]
+            for r in range(3):
+                a_, b_ = Q[r][k], Q[r][k + 1]
+                Q[r][k], Q[r][k + 1] = c * a_ - s * b_, s * a_ + c * b_
+    if it <= 30 * n:
+        for i in range(n - 1):
+            k = min(range(n - i), key=lambda j: (diag[i + j], j))
+            if k > 0:
+                diag[i], diag[i + k] = diag[i + k], diag[i]
+                for r in range(3):
+                    Q[r][i], Q[r][i + k] = Q[r][i + k], Q[r][i]
+    return np.array([d * scale for d in diag]), np.array(Q)
+
+
+def test_saes3_matches_independent_transcription(oracle_mod):
+    for A in saes_cases():
+        d, V, info = oracle_mod.saes(A)
+        assert info == 0
+        pd, pV = _py_saes3(A)
+        assert d.tobytes() == pd.tobytes() and V.tobytes() == pV.tobytes(), A
+
+
+def test_saes_vs_numpy_eigh_up_to_sign(oracle_mod):
+    rng = np.random.default_rng(3)
+    cases = [(A, True) for A in saes_cases()[:2000]]
+    for _ in range(500):                    # the GN path: 6x6 J^T J, dynamic size
+        J = rng.normal(size=(40, 6)) * rng.uniform(0.01, 10, 6)
+        cases.append((J.T @ J, False))
+    for _ in range(200):                    # the dynamic path on 3x3 too
+        P = rng.normal(size=(5, 3))
+        cases.append(((P - P.mean(0)).T @ (P - P.mean(0)), False))
+    for A, fixed in cases:
+        d, V, info = oracle_mod.saes(A, fixed3=fixed)
+        assert info == 0
+        w, W = np.linalg.eigh(A)
+        sc = max(abs(w).max(), 1e-300)
+        np.testing.assert_allclose(d, w, rtol=0, atol=1e-13 * sc)
+        assert np.all(np.diff(d) >= 0)                                   # ascending (Eigen's sort)
+        np.testing.assert_allclose(V.T @ V, np.eye(len(d)), atol=1e-13)
+        np.testing.assert_allclose(A @ V, V * d, atol=1e-13 * sc)
+        gap = np.diff(w)
+        for i in range(len(d)):              # well-separated eigenvalues: same vector up to sign
+            g = min(gap[i - 1] if i > 0 else np.inf, gap[i] if i < len(gap) else np.inf)
+            if g > 1e-6 * sc:
+                assert abs(abs(V[:, i] @ W[:, i]) - 1.0) < 1e-8
+
+
+def test_saes_sign_convention(oracle_mod):
+    """What the published algorithm implies for the signs: an already-diagonal matrix keeps +unit
+    eigenvectors (only column swaps by the sort); a tridiagonal 3x3 starts from Q = I; otherwise Q
+    starts from the Householder [1 0 0; 0 m01 m02; 0 m02 -m01], so column 0 of the tridiagonal basis
+    stays e0 -- and the QR rotations fix the rest, pinned by the transcription test above."""
+    d, V, _ = oracle_mod.saes(np.diag([3.0, 1.0, 2.0]))
+    assert list(d) == [1.0, 2.0, 3.0]
+    assert V.tolist() == [[0.0, 0.0, 1.0], [1.0, 0.0, 0.0], [0.0, 1.0, 0.0]]
+    d, V, _ = oracle_mod.saes(np.diag([5.0, -1.0, 7.0, 2.0, 0.5, 3.0]), fixed3=False)
+    assert list(d) == [-1.0, 0.5, 2.0, 3.0, 5.0, 7.0]
+    assert sorted(V.reshape(-1).tolist()) == [0.0] * 30 + [1.0] * 6
+    # a 2x2-block rotation: [[2, 1], [1, 2]] (+ an isolated 5): Eigen's QR step gives the eigenvectors
+    # (1, -1)/sqrt2 for 1 and (1, 1)/sqrt2 for 3 with these signs
+    d, V, _ = oracle_mod.saes(np.array([[2.0, 1.0, 0.0], [1.0, 2.0, 0.0], [0.0, 0.0, 5.0]]))
+    pd, pV = _py_saes3([[2.0, 1.0, 0.0], [1.0, 2.0, 0.0], [0.0, 0.0, 5.0]])
+    assert V.tobytes() == pV.tobytes()
+    np.testing.assert_allclose(d, [1.0, 3.0, 5.0], atol=1e-15)
+    r = math.sqrt(0.5)
+    np.testing.assert_allclose(np.abs(V), [[r, r, 0], [r, r, 0], [0, 0, 1]], atol=1e-15)
+
+
+def test_edge_records_carry_saes3_direction(oracle_mod, tiny):
+    """The oracle's edge records are a = 0.1 u + c, b = -0.1 u + c with u = column 2 of the restated
+    SelfAdjointEigenSolver<Matrix3d> of the 5-point covariance, bit for bit (EdgeFeatureMatch.hpp:44-73)."""
+    reg, e, s = _registration(oracle_mod, tiny, 0)
+    rec, nn = reg.match(tiny.guess[0])
+    idx = np.nonzero(rec["kind"] == 1)[0]
+    assert len(idx) > 10
+    for i in idx[:300]:
+        P = [[float(v) for v in tiny.edge_map[j, :3]] for j in nn[i]]
+        c = [0.0, 0.0, 0.0]
+        for p in P:
+            c = [c[k] + p[k] for k in range(3)]
+        c = [v / 5.0 for v in c]
+        cov = [[0.0] * 3 for _ in range(3)]
+        for p in P:
+            ev = [p[k] - c[k] for k in range(3)]
+            for r in range(3):
+                for q in range(3):
+                    cov[r][q] = cov[r][q] + ev[r] * ev[q]
+        d, V = _py_saes3(cov)
+        assert d[2] > 3 * d[1]
+        a = [0.1 * V[k][2] + c[k] for k in range(3)]
+        b = [-0.1 * V[k][2] + c[k] for k in range(3)]
+        assert np.array(a).tobytes() == rec["v0"][i].tobytes() and np.array(b).tobytes() == rec["v1"][i].tobytes()
 
 
 def test_surf_plane_fit_vs_lstsq(oracle_mod, tiny):

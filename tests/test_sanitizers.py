@@ -23,7 +23,7 @@ def test_oracle_and_handeye_under_asan_ubsan(tmp_path):
     synth.to_pointcloud2(org).tofile(tmp_path / "msg.bin")
     exe = tmp_path / "sanitize_driver"
     oracle = os.path.join(REPO, "oracle")
-    srcs = [os.path.join(oracle, f) for f in ("extract.cpp", "kdtree.cpp", "registration.cpp", "voxel.cpp",
+    srcs = [os.path.join(oracle, f) for f in ("extract.cpp", "kdtree.cpp", "registration.cpp", "saes.cpp", "voxel.cpp",
                                               "ingest.cpp")]
     srcs += [os.path.join(REPO, "lmsf-slam_amd", "csrc", "calib.cpp"), os.path.join(REPO, "tests", "cpp",
                                                                                    "sanitize_driver.cpp")]
