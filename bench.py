@@ -102,7 +102,7 @@ def parse(argv=None):
     if a.streams is None:
         a.streams = 1
     if a.unique_scans is None:
-        a.unique_scans = {"C2": a.batch, "C5": 5}.get(a.config, 1)   # C2: one distinct scan per slot
+        a.unique_scans = {"C2": a.batch, "C5": a.batch}.get(a.config, 1)   # one distinct scan per slot of a launch
     if a.traffic_json is None:
         a.traffic_json = os.path.join(REPO, "profiles", f"traffic_{a.config}.json")   # latest PMC summary (tools/traffic.py)
     return a
@@ -481,6 +481,7 @@ def run_batch(args, d):
     poses = np.zeros((n_units, 7))
     matches = np.zeros(n_units, np.int64)                    # residual blocks of each unit's last outer iteration
     enqueue_s = []                                           # host time inside lmsf_batch_launch, per step
+    coll_s = []                                              # host time of the pose all-gather section, per step
     stream_in = {"on": False, "shadow": None}
     host_bufs = []
 
@@ -507,12 +508,16 @@ def run_batch(args, d):
             for i, cx, a, m in parts:
                 poses[a:a + m], st = cx.batch_wait(m)
                 matches[a:a + m] = [s.edge_matches + s.surf_matches for s in st]
+        t_c = time.perf_counter()
         exchange_poses(cfg, poses, gathered, args.pairs, world, d.dev)
+        coll_s.append(time.perf_counter() - t_c)
         enqueue_s.append(enq)
         return poses
 
     elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, ctxs, not args.no_n27)
     enqueue_ms = float(np.median(enqueue_s)) * 1e3
+    timed_coll = coll_s[args.warmup:args.warmup + args.steps]   # timed() runs the warmups first
+    collective_ms = round(1e3 * float(np.mean(timed_coll)), 4) if timed_coll and world > 1 else 0.0
     ks = sum_stats([timed_stats(cx) for cx in ctxs])
     total_units = (args.batch * world if cfg == "C2" else args.pairs) * args.steps
     terr = [synth.pose_delta(poses[i], truth_u[unit_scan[i]]) for i in range(n_units)]
@@ -629,11 +634,13 @@ def run_batch(args, d):
             unit, scaling = "scans/s", "weak"
         else:
             metric = "LiDAR scan pairs/sec re-registered (128-beam 254k-pt scan, 10M-pt map, 1k pairs)"
-            wl = (f"C5: 128x{args.cols} scans (~{npts} pts) vs {map_points}-pt map, {args.pairs} pairs "
-                  f"(i mod {world} per GPU, launches of {chunk}), {args.outer} outer iters x Ceres-LM(4)")
-            extra = {"pairs": args.pairs, "launch_batch": chunk, "map_points": map_points,
+            wl = (f"C5: 128x{args.cols} scans (~{npts} pts, {U} distinct per GPU) vs {map_points}-pt map, "
+                  f"{args.pairs} pairs (i mod {world} per GPU, launches of {chunk}), {args.outer} outer iters x "
+                  f"Ceres-LM(4)")
+            extra = {"pairs": args.pairs, "launch_batch": chunk, "distinct_scans_per_gpu": U, "map_points": map_points,
                      "outer_iterations": args.outer, "parallelism": f"pair-sharded x{world}"}
             unit, scaling = "pairs/s", "strong"
+        extra["collective_ms_per_step"] = collective_ms   # pose all-gather section (0: one rank, no collective)
         line(args, d, metric, total_units / elapsed, unit, elapsed, scaling, wl, extra, roof, cpu,
              h2d_inclusive=h2d, pose_delta_vs_cpu=pose_dv,
              pose_error_vs_truth={"max_m": max(t for t, _ in terr), "max_rad": max(r for _, r in terr)})
@@ -765,7 +772,8 @@ def run_streams(args, d):
              tracking_error_m={"rank0_max": max(state["err"]), "rank0_last": state["err"][-1]},
              keyframes_appended=state["kf"],
              # host time in the keyframe exchange per scan (the collectives at world > 1), over all steps run
-             keyframe_exchange_ms_per_step=round(1e3 * state["xchg_s"] / max(state["i"], 1), 4))
+             keyframe_exchange_ms_per_step=round(1e3 * state["xchg_s"] / max(state["i"], 1), 4),
+             keyframe_payload_bytes_per_step=int(xchg.payload_bytes / max(xchg.steps, 1)))
     tr.close()
     ctx.close()
 

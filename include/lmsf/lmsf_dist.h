@@ -11,8 +11,8 @@
  *   C4       the shared map broadcast from rank 0 once (into device memory, then lmsf_set_map /
  *            lmsf_tracker_set_prior_map from it), and per tracking step an all-gather of every
  *            stream's (pose, keyframe flag, feature counts) followed -- only when some stream
- *            keyframed -- by an all-gather of the padded feature buffers, so every replica appends
- *            the same keyframes in rank order.
+ *            keyframed -- by an all-gather of the feature buffers at the keyframing streams' largest
+ *            counts, so every replica appends the same keyframes in rank order.
  * Every call is collective (all ranks, same order) and returns when its result is usable: host
  * results are written, device results are complete on the device.  Every rank takes the same path
  * through a call: an argument problem only one rank can see (a null buffer, a too-small capacity)
@@ -68,14 +68,18 @@ lmsf_status lmsf_group_broadcast_cloud(lmsf_group* g, int32_t root, float* xyzi,
 
 /* C4 keyframe exchange.  In: this rank's pose (4x4 row-major), update type (0: none), feature counts
  * and feat = [edges (cap rows) | surfs (cap rows)] xyzi (device memory for RCCL groups).  Out: info[rank]
- * [19] = (pose[16], update type, n_edge, n_surf) of every rank (host); *any = 1 when some rank keyframed,
- * and then gathered[rank][2 * cap][4] holds every rank's buffer.  Every replica appends rank r's
- * keyframe (gathered[r] rows [0, n_edge) and [cap, cap + n_surf)) for r = 0, 1, ... with a non-zero
- * update type: the same keyframes in the same order on every rank.  Counts above cap or a null feat /
- * gathered on any rank: LMSF_ERR_ARG on every rank (*any = 0).  g, pose, info and any are required. */
+ * [19] = (pose[16], update type, n_edge, n_surf) of every rank (host); *any = 1 when some rank keyframed.
+ * The feature payload is sized by the keyframing ranks' largest counts, rows[0] = max n_edge and rows[1] =
+ * max n_surf over the ranks with a non-zero update type (not by cap): gathered then holds the edges of
+ * rank r at rows [r rows[0], r rows[0] + n_edge_r) and its surfs at rows [nranks rows[0] + r rows[1], + n_surf_r)
+ * -- (rows[0] + rows[1]) rows per rank on the wire.  gathered must hold nranks (rows[0] + rows[1]) rows;
+ * nranks * 2 * cap always does.  Every replica appends rank r's keyframe for r = 0, 1, ... with a non-zero
+ * update type: the same keyframes in the same order on every rank.  Counts above cap, a null feat /
+ * gathered on any rank, or a maximum count above some rank's cap: LMSF_ERR_ARG on every rank (*any = 0).
+ * g, pose, info, rows and any are required. */
 lmsf_status lmsf_group_exchange_keyframes(lmsf_group* g, const double pose[16], int32_t update_type, int64_t n_edge,
                                           int64_t n_surf, const float* feat, size_t cap, double* info, float* gathered,
-                                          int32_t* any);
+                                          int64_t rows[2], int32_t* any);
 
 /* Max over ranks of a host double (the bench's max-over-ranks timing). */
 lmsf_status lmsf_group_max(lmsf_group* g, double* value);

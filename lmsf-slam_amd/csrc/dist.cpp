@@ -169,33 +169,59 @@ lmsf_status lmsf_group_broadcast_cloud(lmsf_group* g, int32_t root, float* xyzi,
 
 lmsf_status lmsf_group_exchange_keyframes(lmsf_group* g, const double pose[16], int32_t update_type, int64_t n_edge,
                                           int64_t n_surf, const float* feat, size_t cap, double* info, float* gathered,
-                                          int32_t* any) {
-    if (!g || !pose || !info || !any) return LMSF_ERR_ARG;
+                                          int64_t rows[2], int32_t* any) {
+    if (!g || !pose || !info || !any || !rows) return LMSF_ERR_ARG;
     // local argument state travels with the info row, so a bad argument on one rank fails every rank
     const bool args_ok = n_edge >= 0 && n_surf >= 0 && (size_t)n_edge <= cap && (size_t)n_surf <= cap && feat && gathered;
-    constexpr int kRow = 20;   // pose[16], update type, n_edge, n_surf, args ok
+    constexpr int kRow = 21;   // pose[16], update type, n_edge, n_surf, args ok, cap
     double mine[kRow];
     std::memcpy(mine, pose, 16 * sizeof(double));
     mine[16] = (double)update_type;
     mine[17] = (double)n_edge;
     mine[18] = (double)n_surf;
     mine[19] = args_ok ? 1.0 : 0.0;
+    mine[20] = (double)cap;
     std::vector<double> all((size_t)kRow * g->nranks);
     lmsf_status rc = allgather_host(g, mine, kRow, all.data());
     if (rc) return rc;
     bool all_ok = true;
     *any = 0;
+    rows[0] = rows[1] = 0;
+    double min_cap = all[20];
     for (int r = 0; r < g->nranks; ++r) {
-        std::memcpy(info + (size_t)r * 19, &all[(size_t)r * kRow], 19 * sizeof(double));
-        if (all[(size_t)r * kRow + 16] != 0.0) *any = 1;
-        all_ok = all_ok && all[(size_t)r * kRow + 19] != 0.0;
+        const double* row = &all[(size_t)r * kRow];
+        std::memcpy(info + (size_t)r * 19, row, 19 * sizeof(double));
+        all_ok = all_ok && row[19] != 0.0;
+        min_cap = std::min(min_cap, row[20]);
+        if (row[16] != 0.0) {   // the payload is sized by the keyframing ranks' largest counts
+            *any = 1;
+            rows[0] = std::max(rows[0], (int64_t)row[17]);
+            rows[1] = std::max(rows[1], (int64_t)row[18]);
+        }
     }
-    if (!all_ok) {
+    // every rank sends rows[k] rows of its own buffer: they must fit the smallest one
+    if (!all_ok || (double)rows[0] > min_cap || (double)rows[1] > min_cap) {
         *any = 0;
+        rows[0] = rows[1] = 0;
         return LMSF_ERR_ARG;
     }
     if (!*any) return LMSF_OK;
-    return allgather_buffers(g, feat, 2 * cap * 4, gathered);
+    // two gathers at the max counts instead of the padded 2 cap rows: edges [rank][rows[0]], then surfs
+    // [rank][rows[1]] behind them
+    float* g_edge = gathered;
+    float* g_surf = gathered + (size_t)g->nranks * (size_t)rows[0] * 4;
+    if (!g->custom) {
+        LCHK(hipSetDevice(g->device));
+        LCHK(ncclGroupStart());
+        if (rows[0]) LCHK(ncclAllGather(feat, g_edge, (size_t)rows[0] * 4, ncclFloat32, g->comm, g->stream));
+        if (rows[1]) LCHK(ncclAllGather(feat + cap * 4, g_surf, (size_t)rows[1] * 4, ncclFloat32, g->comm, g->stream));
+        LCHK(ncclGroupEnd());
+        LCHK(hipStreamSynchronize(g->stream));
+        return LMSF_OK;
+    }
+    rc = allgather_buffers(g, feat, (size_t)rows[0] * 4, g_edge);
+    if (rc) return rc;
+    return allgather_buffers(g, feat + cap * 4, (size_t)rows[1] * 4, g_surf);
 }
 
 lmsf_status lmsf_group_max(lmsf_group* g, double* value) {

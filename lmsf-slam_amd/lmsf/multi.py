@@ -2,7 +2,8 @@
 C2 batch path: scans sharded across ranks with no data-path collective, then one all-gather of the
 6-DoF poses (7 doubles per scan).  C5: pairs partitioned i mod N, one padded pose all-gather.
 C4: shared map broadcast once from rank 0; per tracking step a pose/keyframe-flag all-gather and,
-when a stream keyframes, an all-gather of its features (KeyframeExchange).
+when a stream keyframes, an all-gather of the features at the keyframing streams' largest counts
+(KeyframeExchange).
 
 The same functions run on CPU tensors with the gloo backend (tests/test_multirank.py).
 """
@@ -84,39 +85,53 @@ def broadcast_map(edge, surf, device=None):
 
 class KeyframeExchange:
     """Per tracking step: all-gather (pose 4x4, update type, edge count, surf count) of every
-    stream, and -- only when some stream keyframed -- the padded feature buffers, so that every
-    replica appends the same keyframes in rank order (`ncclAllGather` of the pose
-    every step, of the transformed-feature payload when a stream emits a keyframe).
+    stream, and -- only when some stream keyframed -- the feature buffers at the keyframing streams'
+    largest counts (max n_edge rows of edges, then max n_surf rows of surfs per rank, not the padded
+    capacity), so that every replica appends the same keyframes in rank order (SURVEY 8(e) C4:
+    `ncclAllGather` of the pose every step, of the transformed-feature payload when a stream emits a
+    keyframe).
 
     feat: (2 * cap, 4) float32 tensor on `device` holding this rank's [edges | surfs] (edges at 0,
     surfs at cap).  Returns [(rank, edge_view, surf_view, pose4x4)] for the keyframed streams (a replica adds
     its own entry from its context, lmsf_tracker_add_keyframe_extracted; with one stream the views are None
-    and feat is not read)."""
+    and feat is not read).  payload_bytes / steps count what went over the wire."""
 
     def __init__(self, cap: int, world: int, device=None):
         import torch
         self.cap, self.world, self.device = cap, world, device
         self.info = torch.zeros((world, 19), dtype=torch.float64, device=device)
         self.own = torch.zeros(19, dtype=torch.float64, device=device)
-        self.gbuf = torch.zeros((world, 2 * cap, 4), dtype=torch.float32, device=device)
+        self.gbuf = torch.zeros(world * 2 * cap * 4, dtype=torch.float32, device=device)
+        self.payload_bytes = 0      # feature bytes this rank received, summed over steps
+        self.steps = 0
 
     def exchange(self, pose, update_type, n_edge, n_surf, feat):
-        import torch
         import torch.distributed as dist
+        import torch
         vec = np.concatenate([np.asarray(pose, dtype=np.float64).ravel(), [update_type, n_edge, n_surf]])
-        if self.world > 1:
-            self.own.copy_(torch.from_numpy(vec))
-            dist.all_gather_into_tensor(self.info, self.own.unsqueeze(0))
-            allinfo = self.info.cpu().numpy()
-            if (allinfo[:, 16] > 0).any():
-                dist.all_gather_into_tensor(self.gbuf, feat.unsqueeze(0))
-        else:   # one stream: nothing to exchange; the caller adds its own keyframe from its context
+        self.steps += 1
+        if self.world <= 1:   # one stream: nothing to exchange; the caller adds its own keyframe from its context
             return [(0, None, None, np.asarray(pose, dtype=np.float64).reshape(4, 4))] if update_type else []
+        self.own.copy_(torch.from_numpy(vec))
+        dist.all_gather_into_tensor(self.info, self.own.unsqueeze(0))
+        allinfo = self.info.cpu().numpy()
+        kf = allinfo[:, 16] > 0
+        if not kf.any():
+            return []
+        me, ms = int(allinfo[kf, 17].max()), int(allinfo[kf, 18].max())
+        W, cap = self.world, self.cap
+        ge = self.gbuf[:W * me * 4].view(W, me, 4)
+        gs = self.gbuf[W * me * 4:W * (me + ms) * 4].view(W, ms, 4)
+        if me:
+            dist.all_gather_into_tensor(ge.view(W * me, 4), feat[:me].contiguous())
+        if ms:
+            dist.all_gather_into_tensor(gs.view(W * ms, 4), feat[cap:cap + ms].contiguous())
+        self.payload_bytes += W * (me + ms) * 16
         out = []
-        for q in range(self.world):
-            if allinfo[q, 16] > 0:
+        for q in range(W):
+            if kf[q]:
                 ne, ns = int(allinfo[q, 17]), int(allinfo[q, 18])
-                out.append((q, self.gbuf[q, :ne], self.gbuf[q, self.cap:self.cap + ns], allinfo[q, :16].reshape(4, 4)))
+                out.append((q, ge[q, :ne], gs[q, :ns], allinfo[q, :16].reshape(4, 4)))
         return out
 
 
@@ -152,15 +167,17 @@ class CGroup:
         L.lmsf_group_allgather_poses.argtypes = [P, P, C.c_int32, P]
         L.lmsf_group_broadcast_cloud.argtypes = [P, C.c_int32, P, C.c_size_t, C.POINTER(C.c_size_t)]
         L.lmsf_group_exchange_keyframes.argtypes = [P, P, C.c_int32, C.c_int64, C.c_int64, P, C.c_size_t, P, P,
-                                                    C.POINTER(C.c_int32)]
+                                                    P, C.POINTER(C.c_int32)]
         L.lmsf_group_max.argtypes = [P, C.POINTER(C.c_double)]
         for f in ("lmsf_group_allgather_poses", "lmsf_group_broadcast_cloud", "lmsf_group_exchange_keyframes",
                   "lmsf_group_max"):
             getattr(L, f).restype = C.c_int32
         self.C, self.L = C, L
         self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.gather_bytes = []      # bytes per rank of every all-gather the library asked for (protocol tests)
 
         def allgather(user, send, recv, nbytes):
+            self.gather_bytes.append(int(nbytes))
             try:
                 import torch
                 src = torch.frombuffer(bytearray(C.string_at(send, nbytes)), dtype=torch.uint8)
@@ -209,16 +226,18 @@ class CGroup:
         return rc, nn.value
 
     def exchange_keyframes(self, pose, update_type, n_edge, n_surf, feat, cap, gathered):
-        """feat: (2 cap, 4) float32 or None; gathered: (world, 2 cap, 4) float32 or None.
-        Returns (status, info (world, 19), any)."""
+        """feat: (2 cap, 4) float32 or None; gathered: float32 of >= world * 2 cap rows or None.
+        Returns (status, info (world, 19), any, (rows_edge, rows_surf)); rank r's edges are then rows
+        [r rows_edge, + n_edge_r) of gathered and its surfs rows [world rows_edge + r rows_surf, + n_surf_r)."""
         info = np.zeros((self.world, 19))
         anyk = self.C.c_int32(-1)
+        rows = np.zeros(2, np.int64)
         P = np.ascontiguousarray(pose, dtype=np.float64)
         rc = self.L.lmsf_group_exchange_keyframes(self.h, P.ctypes.data, int(update_type), int(n_edge), int(n_surf),
                                                   feat.ctypes.data if feat is not None else None, cap, info.ctypes.data,
                                                   gathered.ctypes.data if gathered is not None else None,
-                                                  self.C.byref(anyk))
-        return rc, info, anyk.value
+                                                  rows.ctypes.data, self.C.byref(anyk))
+        return rc, info, anyk.value, (int(rows[0]), int(rows[1]))
 
     def max(self, v):
         d = self.C.c_double(v)

@@ -122,14 +122,21 @@ int main(int argc, char** argv) {
     T[11] = pose[6];
     std::vector<double> info((size_t)nranks * 19);
     int32_t any = 0;
-    if (lmsf_group_exchange_keyframes(g, T, 1, (int64_t)got_e, (int64_t)got_s, d_feat, cap, info.data(), d_gath, &any) !=
-        LMSF_OK)
+    int64_t rows[2] = {0, 0};
+    if (lmsf_group_exchange_keyframes(g, T, 1, (int64_t)got_e, (int64_t)got_s, d_feat, cap, info.data(), d_gath, rows,
+                                      &any) != LMSF_OK)
         DIE("keyframe exchange");
-    std::vector<float> mine(2 * cap * 4), back(2 * cap * 4);
-    HIP(hipMemcpy(mine.data(), d_feat, mine.size() * 4, hipMemcpyDeviceToHost));
-    HIP(hipMemcpy(back.data(), d_gath + (size_t)rank * 2 * cap * 4, back.size() * 4, hipMemcpyDeviceToHost));
-    const int kf_ok = any == 1 && info[(size_t)rank * 19 + 17] == (double)got_e &&
-                      info[(size_t)rank * 19 + 18] == (double)got_s && std::memcmp(mine.data(), back.data(), mine.size() * 4) == 0;
+    // this rank's rows come back at [rank rows[0], + got_e) and [nranks rows[0] + rank rows[1], + got_s)
+    std::vector<float> mine_e(got_e * 4), mine_s(got_s * 4), back_e(got_e * 4), back_s(got_s * 4);
+    HIP(hipMemcpy(mine_e.data(), d_feat, mine_e.size() * 4, hipMemcpyDeviceToHost));
+    HIP(hipMemcpy(mine_s.data(), d_feat + 4 * cap, mine_s.size() * 4, hipMemcpyDeviceToHost));
+    HIP(hipMemcpy(back_e.data(), d_gath + (size_t)rank * rows[0] * 4, back_e.size() * 4, hipMemcpyDeviceToHost));
+    HIP(hipMemcpy(back_s.data(), d_gath + ((size_t)nranks * rows[0] + (size_t)rank * rows[1]) * 4, back_s.size() * 4,
+                  hipMemcpyDeviceToHost));
+    const int kf_ok = any == 1 && rows[0] == (int64_t)got_e && rows[1] == (int64_t)got_s &&
+                      info[(size_t)rank * 19 + 17] == (double)got_e && info[(size_t)rank * 19 + 18] == (double)got_s &&
+                      std::memcmp(mine_e.data(), back_e.data(), mine_e.size() * 4) == 0 &&
+                      std::memcmp(mine_s.data(), back_s.data(), mine_s.size() * 4) == 0;
     double tmax = 1.5 + rank;
     lmsf_group_max(g, &tmax);
     std::printf("%lld %lld %.17g %.17g %.17g %.17g %.17g %.17g %.17g %d %d %.17g\n", (long long)fc.n_edge,

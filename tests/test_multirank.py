@@ -99,7 +99,7 @@ def _worker_c45(rank, world, port, out_q):
         pose[0, 3] = 100 * rank + step
         got = xchg.exchange(pose, typ, ne if typ else 0, ns if typ else 0, feat)
         log.append([(q, fe.numpy().copy(), fs.numpy().copy(), P.copy()) for q, fe, fs, P in got])
-    out_q.put((rank, allp, et.numpy(), st.numpy(), log))
+    out_q.put((rank, allp, et.numpy(), st.numpy(), log, xchg.payload_bytes))
     dist.destroy_process_group()
 
 
@@ -118,7 +118,10 @@ def test_gloo_world2_pairs_map_and_keyframe_exchange():
     rng = np.random.default_rng(0)
     e0 = rng.random((11, 4)).astype(np.float32)
     s0 = rng.random((23, 4)).astype(np.float32)
-    for rank, allp, et, st, log in res:
+    for rank, allp, et, st, log, payload in res:
+        # features gathered at the keyframing ranks' largest counts: step 0 (3 + 3 rows), step 2 (3 + 5 rows),
+        # 2 ranks x 16 B per row -- not 2 x 2 cap rows per exchange
+        assert payload == 2 * (3 + 3) * 16 + 2 * (3 + 5) * 16
         np.testing.assert_array_equal(allp, np.stack([np.full(7, float(i)) for i in range(7)]))
         assert et.tobytes() == e0.tobytes() and st.tobytes() == s0.tobytes()
         assert [q for q, *_ in log[0]] == [0, 1] and log[1] == [] and [q for q, *_ in log[2]] == [1]
@@ -167,21 +170,31 @@ def _worker_cdist(rank, world, port, out_q):
         feat[cap:cap + ns] = -(10 * rank + step)
         pose = np.eye(4)
         pose[0, 3] = 100 * rank + step
-        rc, info, anyk = g.exchange_keyframes(pose, typ, ne if typ else 0, ns if typ else 0, feat, cap, gathered)
-        steps.append((rc, info.copy(), anyk))
+        n_calls = len(g.gather_bytes)
+        rc, info, anyk, rows = g.exchange_keyframes(pose, typ, ne if typ else 0, ns if typ else 0, feat, cap,
+                                                    gathered)
+        steps.append((rc, info.copy(), anyk, rows, g.gather_bytes[n_calls + 1:]))   # the calls after the info row
         if rc == 0 and anyk:
+            flat = gathered.reshape(-1, 4)
             for q in range(world):
                 if info[q, 16] != 0:
                     ne_q, ns_q = int(info[q, 17]), int(info[q, 18])
-                    replica.append((q, gathered[q, :ne_q].copy(), gathered[q, cap:cap + ns_q].copy(),
+                    e0, s0 = q * rows[0], world * rows[0] + q * rows[1]
+                    replica.append((q, flat[e0:e0 + ne_q].copy(), flat[s0:s0 + ns_q].copy(),
                                     info[q, :16].reshape(4, 4).copy()))
     res["steps"] = steps
     res["replica"] = replica
     # rank 1 passes no gathered buffer while rank 0 keyframes: both must return LMSF_ERR_ARG (-1)
     feat = np.zeros((2 * cap, 4), np.float32)
-    rc, _, anyk = g.exchange_keyframes(np.eye(4), 1 if rank == 0 else 0, 1, 1, feat, cap,
-                                       gathered if rank == 0 else None)
+    rc, _, anyk, _ = g.exchange_keyframes(np.eye(4), 1 if rank == 0 else 0, 1, 1, feat, cap,
+                                          gathered if rank == 0 else None)
     res["bad_args"] = (rc, anyk)
+    # rank 0 keyframes 6 rows while rank 1's buffer holds 4 per kind: the max count exceeds a rank's capacity
+    small_cap = 4 if rank == 1 else cap
+    feat = np.zeros((2 * small_cap, 4), np.float32)
+    rc, _, anyk, _ = g.exchange_keyframes(np.eye(4), 1 if rank == 0 else 0, 6 if rank == 0 else 0,
+                                          1 if rank == 0 else 0, feat, small_cap, gathered)
+    res["over_cap"] = (rc, anyk)
     res["max"] = g.max(1.5 + rank)
     g.close()
     out_q.put((rank, res))
@@ -216,10 +229,15 @@ def test_gloo_world2_c_library_protocol():
         assert r["bcast_small"] == (-4, 13)                      # LMSF_ERR_CAPACITY on both ranks
         assert [s[0] for s in r["steps"]] == [0, 0, 0]
         assert [s[2] for s in r["steps"]] == [1, 0, 1]
+        # payload at the keyframing ranks' largest counts, not 2 cap = 16 rows per rank:
+        # step 0 both keyframe (n_edge 2 / 3, n_surf 3 / 3), step 2 only rank 1 (3 edges, 5 surfs)
+        assert [s[3] for s in r["steps"]] == [(3, 3), (0, 0), (3, 5)]
+        assert r["steps"][0][4] == [3 * 16, 3 * 16] and r["steps"][1][4] == [] and r["steps"][2][4] == [3 * 16, 5 * 16]
         assert r["bad_args"] == (-1, 0)
+        assert r["over_cap"] == (-1, 0)
         assert r["max"] == (0, 2.5)
         assert [q2 for q2, *_ in r["replica"]] == [0, 1, 1]
-    for (rc0, i0, _), (rc1, i1, _) in zip(res[0]["steps"], res[1]["steps"]):
+    for (rc0, i0, *_), (rc1, i1, *_) in zip(res[0]["steps"], res[1]["steps"]):
         assert i0.tobytes() == i1.tobytes()                      # the same info table on every rank
     for a, b in zip(res[0]["replica"], res[1]["replica"]):
         assert a[0] == b[0] and all(x.tobytes() == y.tobytes() for x, y in zip(a[1:], b[1:]))
