@@ -160,12 +160,8 @@ struct lmsf_ctx {
     int* ring_start = nullptr;
     float4* ring_pts = nullptr;
     int* ring_src = nullptr;
-    float4* surf_stage = nullptr;
-    int* surf_stage_src = nullptr;
     double* sort_key = nullptr;
     int* sort_idx = nullptr;
-    float4* edge_stage = nullptr;
-    int* edge_stage_src = nullptr;
     int* ring_edge_cnt = nullptr;
     int* ring_surf_cnt = nullptr;
     int* qcode = nullptr;             // ring position -> feature code / slot (knn order, k_extract.hip)
@@ -175,7 +171,8 @@ struct lmsf_ctx {
     int* n_pos = nullptr;
     bool qorder_valid = false;        // the slots' features came from the extraction kernels
     int* d_error = nullptr;           // [0] extraction capacity flags, [8..10] pack3, [16] LM loop wait gave up,
-                                      // [24] / [40..42]: the same two of a prefetched extraction
+                                      // [24] / [40..42]: the same two of a prefetched extraction,
+                                      // [48]: dense-map pass-2 list count (BatchView::p2count)
     // lmsf_prefetch_features: the next scan extracted on pre_stream into a second set of the outputs the
     // registration reads (swapped in by the lmsf_extract_features call of the same scan); its own scan copy,
     // the extraction scratch shared (a prefetch runs after the extraction before it, and the next one after it)
@@ -331,6 +328,7 @@ struct lmsf_ctx {
         v.write_nn = 0;
         v.n_pos = n_pos;
         v.pos_stride = R;
+        v.p2count = reinterpret_cast<unsigned*>(d_error + 48);
         return v;
     }
 
@@ -347,12 +345,8 @@ struct lmsf_ctx {
         e.ring_start = ring_start;
         e.ring_pts = ring_pts;
         e.ring_src = ring_src;
-        e.surf_stage = surf_stage;
-        e.surf_stage_src = surf_stage_src;
         e.sort_key = sort_key;
         e.sort_idx = sort_idx;
-        e.edge_stage = edge_stage;
-        e.edge_stage_src = edge_stage_src;
         e.ring_edge_cnt = ring_edge_cnt;
         e.ring_surf_cnt = ring_surf_cnt;
         e.qcode = qcode;
@@ -879,8 +873,8 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     }
     void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->prevw, c->memo_nbr, c->wl, c->wlim, c->wcount, c->n_search, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
-                    c->ring_start, c->ring_pts, c->ring_src, c->surf_stage, c->surf_stage_src, c->sort_key,
-                    c->sort_idx, c->edge_stage, c->edge_stage_src, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->featp, c->n_pos, c->d_error, c->d_lmsync};
+                    c->ring_start, c->ring_pts, c->ring_src, c->sort_key,
+                    c->sort_idx, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->featp, c->n_pos, c->d_error, c->d_lmsync};
     for (void* p : bufs) hipFree(p);
     void* pre_bufs[] = {c->alt.feat, c->alt.feat_src, c->alt.n_edge, c->alt.n_surf, c->alt.qslot, c->alt.fslot,
                         c->alt.featp, c->alt.n_pos, c->pre_raw, c->pre_raw_count, c->pre_raw_off};
@@ -982,12 +976,8 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->ring_start, B * (kMaxRings + 1)));
     CHK(dalloc(&c->ring_pts, B * R));
     CHK(dalloc(&c->ring_src, B * R));
-    CHK(dalloc(&c->surf_stage, B * R));
-    CHK(dalloc(&c->surf_stage_src, B * R));
     CHK(dalloc(&c->sort_key, B * R));
     CHK(dalloc(&c->sort_idx, B * R));
-    CHK(dalloc(&c->edge_stage, B * kMaxRings * kEdgePerRing));
-    CHK(dalloc(&c->edge_stage_src, B * kMaxRings * kEdgePerRing));
     CHK(dalloc(&c->ring_edge_cnt, B * kMaxRings));
     CHK(dalloc(&c->ring_surf_cnt, B * kMaxRings));
     CHK(dalloc(&c->qcode, B * R));

@@ -16,8 +16,8 @@
 //   ring_features one workgroup per ring: bad-point events + automaton, then the greedy edge picks of the
 //                 6 sectors in order on one wave while the other three trail it with the surf compactions;
 //                 each feature position's rank in the ring's search order
-//   concat       per scan: edges (ring order) then surfs (ring order) into the feature array, and the
-//                 fused search's order (fslot / featp)
+//   concat       per scan, per ring position: the feature slot (edges of ring 0..N-1 then surfs) and the
+//                 fused search's order (fslot / featp), the point written to both
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -499,7 +499,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_RF_WAV
     __shared__ uint8_t flag[kRingMax];
     __shared__ double wkey[kPickWin];
     __shared__ int widx[kPickWin];
-    __shared__ int pick[20];
     __shared__ int sh_e[6];       // edges picked in sector k
     __shared__ int sh_done;       // sectors whose picks are published
     __shared__ int sh_sc[6];      // surfs of sector k (written by its compaction wave)
@@ -521,7 +520,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_RF_WAV
         return;
     }
     const float4* pts = ev.ring_pts + (size_t)b * ev.raw_stride + start;
-    const int* psrc = ev.ring_src + (size_t)b * ev.raw_stride + start;
     for (int j = tid; j < size; j += 256) { dis[j] = 0; flag[j] = 0; qc[j] = -1; }
     if (tid == 0) sh_done = 0;
     __syncthreads();
@@ -534,8 +532,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_RF_WAV
     const bool fits = n_[5] <= kSortMax && n_[0] <= kSortMax;   // uniform: sector_sort_kernel's bound
     if (wave == 0) {
         const double thresh = (double)ev.edge_thresh;
-        float4* estage = ev.edge_stage + ((size_t)b * kMaxRings + r) * kEdgePerRing;
-        int* estage_src = ev.edge_stage_src + ((size_t)b * kMaxRings + r) * kEdgePerRing;
         constexpr int kWin = kPickWin / 64;
         double pk[kWin];
         int pi[kWin];
@@ -581,9 +577,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_RF_WAV
                     const int ind = __builtin_amdgcn_readlane(idx, f);
                     ++picked;
                     if (lane == 0) {
-                        pick[picked - 1] = ind;
                         flag[ind] = 1;
-                        qc[ind] = ec;
+                        qc[ind] = ec;   // ring-local edge index: concat_kernel places the point
                     }
                     if (lane >= 1 && lane <= 5) dis[min(ind + lane, size - 1)] = 1;
                     if (lane >= 6 && lane <= 10) dis[max(ind - (lane - 5), 0)] = 1;
@@ -592,11 +587,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_RF_WAV
                 }
                 if (last) break;
                 pos -= 64;
-            }
-            for (int t = lane; t < ec - ec0; t += 64) {
-                const int ind = pick[t];
-                estage[ec0 + t] = pts[ind];
-                estage_src[ec0 + t] = psrc[ind];
             }
             if (lane == 0) {
                 sh_e[k] = ec - ec0;
@@ -609,8 +599,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_RF_WAV
         }
         if (lane == 0) ecnt[r] = fits ? ec : 0;
     } else if (fits) {
-        float4* sstage = ev.surf_stage + (size_t)b * ev.raw_stride + start;
-        int* sstage_src = ev.surf_stage_src + (size_t)b * ev.raw_stride + start;
         for (int k = wave - 1; k < 6; k += 3) {
             while (__hip_atomic_load(&sh_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= k)
                 __builtin_amdgcn_s_sleep(2);
@@ -630,12 +618,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_RF_WAV
                 for (int u = 0; u < 4; ++u) {
                     const bool keep = ind[u] >= 0 && flag[ind[u]] == 0;
                     const unsigned long long m = __ballot(keep);
-                    if (keep) {
-                        const int dst = o + __popcll(m & lanemask_lt(lane));
-                        sstage[dst] = pts[ind[u]];
-                        sstage_src[dst] = psrc[ind[u]];
-                        qc[ind[u]] = kQSurf | dst;
-                    }
+                    if (keep) qc[ind[u]] = kQSurf | (o + __popcll(m & lanemask_lt(lane)));   // ring-local surf index
                     o += __popcll(m);
                 }
             }
@@ -728,45 +711,30 @@ __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
         }
     }
     __syncthreads();
-    const int ne = epre[nr], ns = spre[nr];
+    const int ne = epre[nr];
     const int* rs = ev.ring_start + (size_t)b * (kMaxRings + 1);
-    float4* feat = ev.feat + (size_t)b * ev.feat_stride;
-    int* fsrc = ev.feat_src + (size_t)b * ev.feat_stride;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < ne + ns; i += gridDim.x * 256) {
-        if (i < ne) {
-            int lo = 0, hi = nr - 1;  // last ring with epre[r] <= i
-            while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (epre[mid] <= i) lo = mid; else hi = mid - 1; }
-            const size_t src = ((size_t)b * kMaxRings + lo) * kEdgePerRing + (i - epre[lo]);
-            feat[i] = ev.edge_stage[src];
-            fsrc[i] = ev.edge_stage_src[src];
-        } else {
-            const int k = i - ne;
-            int lo = 0, hi = nr - 1;
-            while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (spre[mid] <= k) lo = mid; else hi = mid - 1; }
-            const size_t src = (size_t)b * ev.raw_stride + rs[lo] + (k - spre[lo]);
-            feat[i] = ev.surf_stage[src];
-            fsrc[i] = ev.surf_stage_src[src];
-        }
-    }
-    // The neighbour search's order: the feature slot of every ring position, so that neighbouring
-    // lanes search neighbouring points of a ring (slot order puts a sector's surfs in curvature
-    // order, spread over ~60 degrees of the ring).  Codes of a ring whose features were dropped
-    // (capacity flags) are ignored through the ring counts.
+    // Every feature position of the rings, in ring order: its feature slot (edges of ring 0..N-1, then surfs,
+    // each ring's in the reference's emission order -- the ring-local index ring_features_kernel packed into the
+    // position's code) and its place in the fused search's order (edges of ring 0..N-1 then surfs, each ring's in
+    // ring order: the rank packed into the code).  The point goes to both: feat / feat_src at the slot (FX:124-125
+    // order), featp at the search position.  Codes of a ring whose features were dropped (capacity flags) are
+    // ignored through the ring counts.
     const int npos = rs[nr];
     if (blockIdx.x == 0 && threadIdx.x == 0) ev.n_pos[b] = npos;
-    // The fused search's order (fslot / featp): edges of ring 0..N-1 then surfs, each ring's in ring order
-    // (ring_features_kernel packed every position's rank among its ring's features of its kind into its code).
     const int* qc = ev.qcode + (size_t)b * ev.raw_stride;
     int* qs = ev.qslot + (size_t)b * ev.raw_stride;
     int* fs = ev.fslot + (size_t)b * ev.feat_stride;
     float4* fp = ev.featp + (size_t)b * ev.feat_stride;
+    float4* feat = ev.feat + (size_t)b * ev.feat_stride;
+    int* fsrc = ev.feat_src + (size_t)b * ev.feat_stride;
     const float4* rp = ev.ring_pts + (size_t)b * ev.raw_stride;
+    const int* rsrc = ev.ring_src + (size_t)b * ev.raw_stride;
     for (int p = blockIdx.x * 256 + threadIdx.x; p < npos; p += gridDim.x * 256) {
-        int lo = 0, hi = nr - 1;  // last ring with rs[r] <= p
-        while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (rs[mid] <= p) lo = mid; else hi = mid - 1; }
         const int code = qc[p];
         int slot = -1, o = -1;
         if (code >= 0) {
+            int lo = 0, hi = nr - 1;  // last ring with rs[r] <= p
+            while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (rs[mid] <= p) lo = mid; else hi = mid - 1; }
             const int l = code & kQCodeMask, rank = (code >> kQRankShift) & kQCodeMask;
             if (code & kQSurf) {
                 if (l < spre[lo + 1] - spre[lo]) { slot = ne + spre[lo] + l; o = ne + spre[lo] + rank; }
@@ -776,10 +744,14 @@ __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
             }
         }
         qs[p] = slot;
-        if (o >= 0 && o < ev.feat_stride) {
+        if (slot >= 0 && slot < ev.feat_stride) {
             const float4 q = rp[p];
-            fs[o] = slot;
-            fp[o] = make_float4(q.x, q.y, q.z, __int_as_float(slot));
+            feat[slot] = q;
+            fsrc[slot] = rsrc[p];
+            if (o < ev.feat_stride) {
+                fs[o] = slot;
+                fp[o] = make_float4(q.x, q.y, q.z, __int_as_float(slot));
+            }
         }
     }
 }

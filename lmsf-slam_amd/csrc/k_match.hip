@@ -1238,6 +1238,336 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     }
 }
 
+// ---------------------------------------------------------------- dense maps (C5): pass 1 sorted + flattened, pass 2 listed
+// The pruned one-lane walk of match_fit_kernel<true, .> ran at lane utilisation 0.53 on C5 (VALU busy 0.94,
+// profiles/r03/C5): lanes of a wave walk very different candidate counts (C5 surf queries: mean 77, p90 128,
+// tools/c5_walk_model.py), and a loop per row runs each row for its longest lane (loop-level utilisation
+// 0.25 by the model), then pass 2 (10% of the queries) holds every wave it touches.  Here:
+//   dense_pass1_kernel: every query resolves its 9 pass-1 rows (the x-windows of radius sqrt(lim1): offsets
+//     only), the block re-deals its 256 queries to its waves in order of their pass-1 work (a counting sort
+//     on RU-step buckets, rows carried in LDS), and each lane walks its rows as one flattened candidate
+//     stream (RU loads in flight, masked at row ends; a row is entered only while its yz-gap bound is within
+//     the current 5th key).  A query whose 5th key is within lim1 is complete (pass 2 would scan nothing:
+//     its windows lie inside pass 1's) and is fitted here; the others go, with their 5 keys (as map
+//     indices), to a work list.
+//   dense_pass2_kernel: the listed queries (dense, grid-stride) run pass 2 -- the rows within the 5th key,
+//     minus pass 1's windows -- then the fit.
+// Results are the pruned walk's exactly (the same rows, windows and keys; the sets and their order do not
+// depend on which lane walks a query or on the order of a row's candidates), so the records are unchanged.
+#ifndef LMSF_DENSE_SPLIT
+#define LMSF_DENSE_SPLIT 1
+#endif
+#ifndef LMSF_DENSE_SORT
+#define LMSF_DENSE_SORT 1
+#endif
+constexpr int kDenseBuckets = 16;        // pass-1 work classes of the block re-deal (2 RU-steps each)
+constexpr int kDensePay = 31;            // LDS words per query: e, w (3), rows: start (9), len (9), lb (9)
+
+// The line / plane fit of a query's 5 kept keys and its record (match_fit_kernel's tail).
+__device__ __forceinline__ void dense_finish(const GridView& g, const BatchView& bv, size_t ppos, const float4 p, bool is_edge,
+                                             size_t slot, const float3 w, const double (&k)[5]) {
+    float4 np[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const uint64_t kb = key_bits(k[j]);
+        np[j] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+        if (kb < kSentinel) {
+            const uint32_t idx = (uint32_t)kb;
+            const float4 mp = g.orig[idx];
+            np[j] = make_float4(mp.x, mp.y, mp.z, __int_as_float((int)idx));
+        }
+    }
+    if (bv.write_nn) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) bv.nnp[slot * 5 + j] = np[j];
+    }
+    int kind = 0;
+    d3 v0 = mk(0, 0, 0);
+    double v1x = 0.0, v1y = 0.0, v1z = 0.0;
+    if (__float_as_int(np[4].w) >= 0) {
+        if (is_edge) {
+            d3 a, bpt;
+            if (edge_fit(np, a, bpt)) {
+                kind = LMSF_EDGE;
+                v0 = a;
+                v1x = bpt.x; v1y = bpt.y; v1z = bpt.z;
+            }
+        } else {
+            d3 n;
+            double D, gn_res;
+            if (surf_fit(np, w, n, D, gn_res)) {
+                kind = LMSF_SURF;
+                v0 = n;
+                v1x = D;
+            }
+        }
+    }
+    store_record(bv, ppos, p, kind, v0, v1x, v1y, v1z);
+}
+
+// Row rr (0..8: dy, dz in {-1, 0, 1}) of the pruned walk around w: its offsets row, x-slice span [xa, xb], the
+// yz-gap bound lb and the grid's x origin / slices; false outside the grid (knn_walk's row_geo).
+__device__ __forceinline__ bool dense_row(const GridView& gg, const float3 w, int rr, const uint32_t*& row, int& xa, int& xb,
+                                          float& lb) {
+    const float fx = floorf(w.x), fy = floorf(w.y), fz = floorf(w.z);
+    const int dyo = (rr % 3) - 1, dzo = (rr / 3) - 1;
+    const float fxs = fx * (float)gg.sx;
+    const bool inside = gg.n > 0 && fxs >= (float)(gg.ox - 2 * gg.sx) && fxs <= (float)(gg.ox + gg.nx + gg.sx) &&
+                        fy >= (float)(gg.oy - 2) && fy <= (float)(gg.oy + gg.ny + 1) &&
+                        fz >= (float)(gg.oz - 2) && fz <= (float)(gg.oz + gg.nz + 1);
+    if (!inside) return false;
+    const int cxs = (int)fxs - gg.ox, cy = (int)fy - gg.oy + dyo, cz = (int)fz - gg.oz + dzo;
+    xa = max(cxs - gg.sx, 0);
+    xb = min(cxs + 2 * gg.sx - 1, gg.nx - 1);
+    if (cy < 0 || cy >= gg.ny || cz < 0 || cz >= gg.nz || xa > xb) return false;
+    row = gg.off + ((size_t)cz * gg.ny + cy) * gg.nx;
+    const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
+    const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
+    const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
+    lb = gy * gy + gz * gz;
+    return true;
+}
+// slices of [xa, xb] meeting [w.x - r, w.x + r], r = sqrt(lim - lb) (sa > sb: empty) -- knn_walk's window
+__device__ __forceinline__ void dense_window(const GridView& gg, const float3 w, float lim, float lb, int xa, int xb, int& sa,
+                                             int& sb) {
+    const float rem = lim - lb;
+    sa = 1;
+    sb = 0;
+    if (rem < 0.f) return;
+    const double r = (double)sqrtf(rem);
+    sa = max(xa, (int)floor(((double)w.x - r) * gg.sx) - gg.ox);
+    sb = min(xb, (int)floor(((double)w.x + r) * gg.sx) - gg.ox);
+}
+
+__device__ __forceinline__ void key_insert(double (&k)[5], double x) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const double lo = key_min(k[i], x);
+        x = key_max(k[i], x);
+        k[i] = lo;
+    }
+}
+
+constexpr int kDenseRowOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // own row, faces, corners (knn_walk's kOrder)
+constexpr float kDenseCull = 1.0f + 1e-5f;                       // knn_walk's kCullLim
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void dense_pass1_kernel(
+    GridView ge, GridView gs, BatchView bv, int gx, int remap, unsigned* p2count) {
+    __shared__ uint32_t pay[kDensePay][256];
+    __shared__ int bcnt[kDenseBuckets * 4];
+    int bx, b;
+    block_coords(remap, gx, bx, b);
+    const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
+    const size_t F = bv.feat_stride;
+    if (bx == 0 && threadIdx.x == 0) bv.n_search[b] = nq;
+    if (bx * 256 >= nq) return;   // uniform per block, ahead of the barriers
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const Pose Ps = load_pose(bv.st[b].x);
+    unsigned int c27 = 0;
+    // ---- pass-1 rows of this lane's own query
+    int steps = 0;
+    {
+        const int e = bx * 256 + tid;
+        const bool valid = e < nq;
+        float3 w = make_float3(0.f, 0.f, 0.f);
+        uint32_t st_[9], ln_[9];
+        float lb_[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) { st_[i] = 0; ln_[i] = 0; lb_[i] = 3.0e38f; }
+        if (valid) {
+            const float4 p = bv.featp[(size_t)b * F + e];
+            const GridView g = pick_grid(__float_as_int(p.w) < ne, ge, gs);
+            w = associate(Ps, p);
+            const float lim1 = g.lim1 * kDenseCull;
+#pragma unroll
+            for (int i = 0; i < 9; ++i) {
+                const uint32_t* row;
+                int xa, xb, sa, sb;
+                float lb;
+                if (!dense_row(g, w, kDenseRowOrder[i], row, xa, xb, lb)) continue;
+                if (bv.count27) c27 += row[xb + 1] - row[xa];
+                lb_[i] = lb;
+                if (lb > lim1) continue;
+                dense_window(g, w, lim1, lb, xa, xb, sa, sb);
+                if (sa <= sb) {
+                    st_[i] = row[sa];
+                    ln_[i] = row[sb + 1] - st_[i];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 9; ++i) steps += (int)((ln_[i] + (uint32_t)(LMSF_FUSED_UNROLL - 1)) / (uint32_t)LMSF_FUSED_UNROLL);
+        }
+        // ---- re-deal the block's queries to its waves by pass-1 work (bucket-major, wave-minor, lane order)
+        int dest = tid;
+#if LMSF_DENSE_SORT
+        const int bk = valid ? min(steps >> 1, kDenseBuckets - 1) : 0;
+        unsigned long long mine = 0;
+#pragma unroll
+        for (int j = 0; j < kDenseBuckets; ++j) {
+            const unsigned long long m = __ballot(bk == j);
+            if (bk == j) mine = m;
+            if (lane == 0) bcnt[j * 4 + wave] = __popcll(m);
+        }
+        __syncthreads();
+        if (wave == 0) {   // exclusive scan of the 64 (bucket, wave) counts
+            const int c = bcnt[lane];
+            int incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o, 64);
+                incl += lane >= o ? t : 0;
+            }
+            bcnt[lane] = incl - c;
+        }
+        __syncthreads();
+        dest = bcnt[bk * 4 + wave] + __popcll(mine & below);
+#endif
+        pay[0][dest] = valid ? (uint32_t)e : 0xffffffffu;
+        pay[1][dest] = __float_as_uint(w.x);
+        pay[2][dest] = __float_as_uint(w.y);
+        pay[3][dest] = __float_as_uint(w.z);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            pay[4 + i][dest] = st_[i];
+            pay[13 + i][dest] = ln_[i];
+            pay[22 + i][dest] = __float_as_uint(lb_[i]);
+        }
+        __syncthreads();
+    }
+    // ---- the query dealt to this lane: its rows as one flattened candidate stream
+    const uint32_t eu = pay[0][tid];
+    const bool valid = eu != 0xffffffffu;
+    const int e = valid ? (int)eu : 0;
+    const size_t ppos = (size_t)b * F + e;
+    const float4 p = bv.featp[ppos];
+    const int qq = __float_as_int(p.w);
+    const bool is_edge = qq < ne;
+    const GridView g = pick_grid(is_edge, ge, gs);
+    const float3 w = make_float3(__uint_as_float(pay[1][tid]), __uint_as_float(pay[2][tid]), __uint_as_float(pay[3][tid]));
+    const double sentinel = key_as_double(kSentinel);
+    double k[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) k[j] = sentinel;
+    if (valid) {
+        const float4* rp = g.pts;
+        uint32_t cur = 0, end = 0;
+        int r = 0;
+        for (;;) {
+            while (cur >= end && r < 9) {   // enter the next row with candidates within the 5th key
+                const uint32_t ln = pay[13 + r][tid];
+                if (ln && !(__uint_as_float(pay[22 + r][tid]) > key_d2(k[4]))) {
+                    cur = pay[4 + r][tid];
+                    end = cur + ln;
+                }
+                ++r;
+            }
+            if (cur >= end) break;
+            float4 m[LMSF_FUSED_UNROLL];
+#pragma unroll
+            for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) m[u] = rp[cur + u < end ? cur + u : cur];
+#pragma unroll
+            for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) {
+                const float dx = w.x - m[u].x, dy = w.y - m[u].y, dz = w.z - m[u].z;
+                const float d2 = dx * dx + dy * dy + dz * dz;
+                const double x = key_as_double(((uint64_t)(__float_as_uint(d2) + kKeyBias) << 32) |
+                                               (uint32_t)__float_as_int(m[u].w));
+                key_insert(k, cur + u < end ? x : sentinel);   // past the row's end: a key that never enters
+            }
+            cur += LMSF_FUSED_UNROLL;
+        }
+    }
+    // ---- complete (5th key within lim1: pass 2 would scan nothing) -> fit; else -> pass-2 list
+    const bool p2 = valid && key_d2(k[4]) > g.lim1;
+    const unsigned long long m2 = __ballot(p2);
+    int base2 = 0;
+    if (lane == 0 && m2) base2 = (int)atomicAdd(p2count, (unsigned)__popcll(m2));
+    base2 = __shfl(base2, 0, 64);
+    if (p2) {
+        bv.wl[base2 + __popcll(m2 & below)] = (int)((size_t)b * F + e);
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+            bv.memo_nbr[((size_t)b * kMemoWords + j) * F + e] =
+                key_bits(k[j]) < kSentinel ? (int)(uint32_t)key_bits(k[j]) : -1;
+    } else if (valid) {
+        dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);
+    }
+    if (bv.n27) {   // accounting runs: the 27-cell candidates and the queries
+        unsigned int qn = (bx * 256 + tid < nq) ? 1u : 0u;
+        unsigned long long c = c27;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            qn += __shfl_xor(qn, o, 64);
+            c += __shfl_xor(c, o, 64);
+        }
+        if (lane == 0) {
+            unsigned long long* shard = bv.n27 + (size_t)((blockIdx.x * 4 + wave) & (kCounterShards - 1)) * 16;
+            if (c) atomicAdd(shard, c);
+            if (qn) atomicAdd(shard + 1, (unsigned long long)qn);
+        }
+    }
+}
+
+// The listed queries of dense_pass1_kernel: pass 2 (knn_walk's second loop) from their pass-1 keys, then the fit.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void dense_pass2_kernel(
+    GridView ge, GridView gs, BatchView bv, const unsigned* p2count) {
+    const unsigned count = *p2count;
+    const size_t F = bv.feat_stride;
+    for (unsigned li = blockIdx.x * 256 + threadIdx.x; li < count; li += gridDim.x * 256) {
+        const size_t code = (size_t)(unsigned)bv.wl[li];
+        const int b = (int)(code / F), e = (int)(code - (size_t)b * F);
+        const int ne = bv.n_edge[b];
+        const size_t ppos = (size_t)b * F + e;
+        const float4 p = bv.featp[ppos];
+        const int qq = __float_as_int(p.w);
+        const bool is_edge = qq < ne;
+        const GridView g = pick_grid(is_edge, ge, gs);
+        const float3 w = associate(load_pose(bv.st[b].x), p);
+        double k[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int idx = bv.memo_nbr[((size_t)b * kMemoWords + j) * F + e];
+            k[j] = idx >= 0 ? nn_key(w, g.orig[idx], (uint32_t)idx) : key_as_double(kSentinel);
+        }
+        const float lim1 = g.lim1 * kDenseCull;
+        const float4* rp = g.pts;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const float d4 = key_d2(k[4]);
+            const uint32_t* row;
+            int xa, xb, sa, sb, ta = 1, tb = 0;
+            float lb;
+            if (!dense_row(g, w, kDenseRowOrder[i], row, xa, xb, lb)) continue;
+            if (lb > d4) continue;
+            dense_window(g, w, d4 * kDenseCull, lb, xa, xb, sa, sb);
+            if (!(lb > lim1)) dense_window(g, w, lim1, lb, xa, xb, ta, tb);   // pass 1's window of this row
+            int ra[2] = {sa, 1}, rb[2] = {sb, 0};
+            if (ta <= tb) {
+                ra[0] = sa; rb[0] = min(sb, ta - 1);
+                ra[1] = max(sa, tb + 1); rb[1] = sb;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (ra[h] > rb[h]) continue;
+                const uint32_t a = row[ra[h]], len = row[rb[h] + 1] - a;
+                uint32_t c = 0;
+                for (; c + LMSF_FUSED_UNROLL <= len; c += LMSF_FUSED_UNROLL) {
+                    float4 m[LMSF_FUSED_UNROLL];
+#pragma unroll
+                    for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) m[u] = rp[a + c + u];
+#pragma unroll
+                    for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) key_insert(k, nn_key(w, m[u], (uint32_t)__float_as_int(m[u].w)));
+                }
+                for (; c < len; ++c) {
+                    const float4 m = rp[a + c];
+                    key_insert(k, nn_key(w, m, (uint32_t)__float_as_int(m.w)));
+                }
+            }
+        }
+        dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);
+    }
+}
+
 // LM candidate evaluation over the fixed correspondences (Ceres re-evaluates the same residual blocks
 // at every trial point): one packet per block; the step runs in lm_step_kernel (k_solver.hip).
 // kEvalPerThread records per thread.  (Fusing the step into the last block to finish, behind an
@@ -1651,7 +1981,19 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
     const dim3 grid(gx * bv.B);
     const int remap = knn_remap();
     if (match_fit_prune(edge, surf)) {
-        hipLaunchKernelGGL((match_fit_kernel<true, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
+        static const bool split = ab_int("LMSF_DENSE_SPLIT", LMSF_DENSE_SPLIT) != 0;
+        if (split && kLinEval && bv.p2count && (size_t)bv.B * bv.feat_stride < ((size_t)1 << 31)) {
+            hipError_t e = hipMemsetAsync(bv.p2count, 0, sizeof(unsigned), s);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(dense_pass1_kernel, grid, dim3(256), 0, s, edge, surf, bv, gx, remap, bv.p2count);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
+            // grid-stride over the list (~10% of the queries on C5): 8 blocks per CU
+            hipLaunchKernelGGL(dense_pass2_kernel, dim3(2048), dim3(256), 0, s, edge, surf, bv,
+                               (const unsigned*)bv.p2count);
+        } else {
+            hipLaunchKernelGGL((match_fit_kernel<true, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
+        }
     } else if (bv.memo) {
         hipLaunchKernelGGL(match_memo_kernel, grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
         const size_t lds = 2 * (memo_blocks(bv.feat_stride) + 1) * sizeof(int);

@@ -138,6 +138,7 @@ struct BatchView {
     // launches are timed by stamp kernels (enqueue_register).
     unsigned long long* stamp_start;
     unsigned long long* stamp_end;
+    unsigned* p2count;       // dense maps: entries of the pass-2 work list in wl (dense_pass1_kernel)
 };
 
 __device__ __forceinline__ void stamp_if(unsigned long long* at, bool first_block) {
@@ -226,12 +227,8 @@ struct ExtractView {
     int* ring_start;             // [B][kMaxRings + 1]
     float4* ring_pts;            // [B][raw_stride] ring-ordered points
     int* ring_src;               // [B][raw_stride] raw index of each ring-ordered point
-    float4* surf_stage;          // [B][raw_stride]   per ring at ring_start
-    int* surf_stage_src;         // [B][raw_stride]
     double* sort_key;            // [B][raw_stride] per sector at ring_start + sector start: curvature
     int* sort_idx;               //                 ascending (c, index), ring-local indices
-    float4* edge_stage;          // [B][kMaxRings * kEdgePerRing]
-    int* edge_stage_src;         // [B][kMaxRings * kEdgePerRing]
     int* ring_edge_cnt;          // [B][kMaxRings]
     int* ring_surf_cnt;          // [B][kMaxRings]
     int* qcode;                  // [B][raw_stride] per ring position: ring-local edge index, kQSurf | surf index, -1; + rank << 13
