@@ -63,21 +63,33 @@ __device__ __forceinline__ Pose load_pose(const double* x) {
 }
 __device__ __forceinline__ d3 transform(const Pose& P, d3 p) { return rotate(P.q, p) + P.t; }
 
+// x^3 correctly rounded (the value glibc's pow(x, 3) returns; two error-free products, then the double-double
+// sum rounded once): 7 VALU instead of ocml pow's ~300 on the serial LM-control lane
+__device__ __forceinline__ double cube_rn(double x) {
+    const double p = x * x;
+    const double pe = fma(x, x, -p);   // x^2 = p + pe exactly
+    const double h = p * x;
+    const double he = fma(p, x, -h);   // p x = h + he exactly
+    return h + (he + pe * x);
+}
+
 // Math::GetTransformFromSe3 (INC/Math.hpp:29-72) + PoseSE3Parameterization::Plus
-// (INC/Algorithm/Ceres/Parameterization/PoseSE3Parameterization.hpp:32-46)
+// (INC/Algorithm/Ceres/Parameterization/PoseSE3Parameterization.hpp:32-46).  sin / cos of one argument come
+// from one sincos (one range reduction), pow(theta, 3) is cube_rn.
 __device__ inline void pose_plus(const double* x, const double* delta, double* out) {
     d3 om = mk(delta[0], delta[1], delta[2]);
     d3 up = mk(delta[3], delta[4], delta[5]);
     double theta = norm(om);
     double half_theta = 0.5 * theta;
-    double real_factor = cos(half_theta);
+    double sin_half, real_factor;
+    sincos(half_theta, &sin_half, &real_factor);
     double imag_factor;
     if (theta < 1e-10) {
         double tsq = theta * theta;
         double tp4 = tsq * tsq;
         imag_factor = 0.5 - 0.0208333 * tsq + 0.000260417 * tp4;
     } else {
-        imag_factor = sin(half_theta) / theta;
+        imag_factor = sin_half / theta;
     }
     dq d;
     d.x = imag_factor * om.x; d.y = imag_factor * om.y; d.z = imag_factor * om.z; d.w = real_factor;
@@ -86,8 +98,10 @@ __device__ inline void pose_plus(const double* x, const double* delta, double* o
         qmat(d, J);
     } else {
         const double Om[9] = {0., -om.z, om.y, om.z, 0., -om.x, -om.y, om.x, 0.};
-        double c1 = (1 - cos(theta)) / (theta * theta);
-        double c2 = (theta - sin(theta)) / (pow(theta, 3.0));
+        double sin_t, cos_t;
+        sincos(theta, &sin_t, &cos_t);
+        double c1 = (1 - cos_t) / (theta * theta);
+        double c2 = (theta - sin_t) / cube_rn(theta);
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll

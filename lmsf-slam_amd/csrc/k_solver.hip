@@ -51,6 +51,12 @@ __global__ void state_init_kernel(BatchView bv, const double* poses) {
 #else
 #define LMSF_CTL_ATTR
 #endif
+// LMSF_CTL_MODE (A/B): the batch control kernels' step computation -- 2: LDS workspace, rolled loops (no
+// scratch within 64 VGPRs); 1: r03's non-inlined call (868 B of scratch); 0: inlined.
+#ifndef LMSF_CTL_MODE
+#define LMSF_CTL_MODE 2
+#endif
+constexpr int kCtlMode = LMSF_CTL_MODE;
 __global__ __launch_bounds__(kBeginThreads) LMSF_CTL_ATTR void lm_begin_kernel(BatchView bv) {
     const int b = blockIdx.x;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
@@ -63,7 +69,8 @@ __global__ __launch_bounds__(kBeginThreads) LMSF_CTL_ATTR void lm_begin_kernel(B
         const int fb = bv.part_q;
         reduce_parts(bv, b, (nq + fb - 1) / fb, tot);
     }   // (reduce_parts ends with a barrier: sS is in place)
-    if (threadIdx.x == 0) lm_begin_apply<true>(sS, tot);
+    __shared__ double ws[kStepWs];
+    if (threadIdx.x == 0) lm_begin_apply<kCtlMode>(sS, tot, ws);
     __syncthreads();
     state_copy(bv.st[b], sS);
 }
@@ -87,7 +94,8 @@ __global__ __launch_bounds__(kStepThreads) LMSF_CTL_ATTR void lm_step_kernel(Bat
     const int nq = bv.n_edge[b] + bv.n_surf[b];
     __shared__ double tot[kPacket];
     reduce_parts(bv, b, (nq + kEvalBlock - 1) / kEvalBlock, tot);   // ends with a barrier
-    if (threadIdx.x == 0) lm_step_apply<true>(sS, tot, outer, is_last);
+    __shared__ double ws[kStepWs];
+    if (threadIdx.x == 0) lm_step_apply<kCtlMode>(sS, tot, outer, is_last, ws);
     __syncthreads();
     state_copy(S, sS);
 }

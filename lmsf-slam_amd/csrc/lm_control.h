@@ -69,6 +69,19 @@ __device__ double norm7(const double* x) {
     return sqrt(s);
 }
 
+__device__ void pose_plus_lds(const double* x, const double* delta, double* out, double* w);
+// grad_max_norm with its Plus in the LDS workspace (MODE 2): ws[0..5] = -g, ws[6..12] = the Plus, ws[13..] its
+// matrices
+__device__ __forceinline__ double grad_max_norm_lds(const double* x, const double* g, double* ws) {
+#pragma unroll 1
+    for (int i = 0; i < 6; ++i) ws[i] = -g[i];
+    pose_plus_lds(x, ws, ws + 6, ws + 13);
+    double m = 0.0;
+#pragma unroll 1
+    for (int i = 0; i < 7; ++i) m = fmax(m, fabs(x[i] - ws[6 + i]));
+    return m;
+}
+
 __device__ __forceinline__ double grad_max_norm(const double* x, const double* g) {
     double ng[6], xp[7];
 #pragma unroll
@@ -182,9 +195,154 @@ __device__ __forceinline__ void compute_step_body(SolveState& S) {
 // the call too (C2 26.14k / 25.88k with it vs 25.85k / 25.84k without); the single-scan lm_loop_kernel keeps
 // the inlined form (C4 1,153 / 1,123 vs 1,073 / 1,100 scans/s with the call there as well).
 __device__ __noinline__ void compute_step_call(SolveState& S) { compute_step_body(S); }
-template <bool CALL>
-__device__ __forceinline__ void compute_step(SolveState& S) {
-    if constexpr (CALL) compute_step_call(S);
+
+// The same step with its 6x6 system in an LDS workspace (kStepWs doubles) and the loops rolled: the serial
+// lane keeps only a few values in registers, so the control kernels fit 64 VGPRs (they co-reside with four
+// search waves per SIMD) with no scratch stack -- the call form above spends its time in 868 B of scratch
+// round trips (lm_step 29 us alone vs 12.4 us inlined at 256 VGPRs).  Arithmetic and order are
+// compute_step_body's, so the results are bit-identical.
+constexpr int kStepWs = 21 + 4 * 6 + 9 + 9 + 7;
+
+// pose_plus (devmath.h) with its 3x3 matrices in the LDS workspace w (25 doubles) and the loops rolled:
+// the same operations in the same order.
+__device__ void pose_plus_lds(const double* x, const double* delta, double* out, double* w) {
+    double* Om = w;
+    double* J = w + 9;
+    const d3 om = mk(delta[0], delta[1], delta[2]);
+    const double theta = norm(om);
+    const double half_theta = 0.5 * theta;
+    double sin_half, real_factor;
+    sincos(half_theta, &sin_half, &real_factor);
+    double imag_factor;
+    if (theta < 1e-10) {
+        const double tsq = theta * theta;
+        const double tp4 = tsq * tsq;
+        imag_factor = 0.5 - 0.0208333 * tsq + 0.000260417 * tp4;
+    } else {
+        imag_factor = sin_half / theta;
+    }
+    dq d;
+    d.x = imag_factor * om.x; d.y = imag_factor * om.y; d.z = imag_factor * om.z; d.w = real_factor;
+    if (theta < 1e-10) {
+        qmat(d, J);
+    } else {
+        Om[0] = 0.; Om[1] = -om.z; Om[2] = om.y; Om[3] = om.z; Om[4] = 0.; Om[5] = -om.x; Om[6] = -om.y; Om[7] = om.x; Om[8] = 0.;
+        double sin_t, cos_t;
+        sincos(theta, &sin_t, &cos_t);
+        const double c1 = (1 - cos_t) / (theta * theta);
+        const double c2 = (theta - sin_t) / cube_rn(theta);
+#pragma unroll 1
+        for (int i = 0; i < 3; ++i)
+#pragma unroll 1
+            for (int j = 0; j < 3; ++j) {
+                const double o2 = Om[i * 3 + 0] * Om[0 * 3 + j] + Om[i * 3 + 1] * Om[1 * 3 + j] + Om[i * 3 + 2] * Om[2 * 3 + j];
+                J[i * 3 + j] = (i == j ? 1.0 : 0.0) + c1 * Om[i * 3 + j] + c2 * o2;
+            }
+    }
+    const d3 up = mk(delta[3], delta[4], delta[5]);
+    const d3 dt = mk(J[0] * up.x + J[1] * up.y + J[2] * up.z,
+                     J[3] * up.x + J[4] * up.y + J[5] * up.z,
+                     J[6] * up.x + J[7] * up.y + J[8] * up.z);
+    dq q; q.x = x[0]; q.y = x[1]; q.z = x[2]; q.w = x[3];
+    const dq qp = qmul(d, q);
+    const d3 tp = rotate(d, mk(x[4], x[5], x[6])) + dt;
+    out[0] = qp.x; out[1] = qp.y; out[2] = qp.z; out[3] = qp.w;
+    out[4] = tp.x; out[5] = tp.y; out[6] = tp.z;
+}
+__device__ __noinline__ bool chol_solve6_lds(double* A, const double* b, double* y, double* x) {
+#pragma unroll 1
+    for (int j = 0; j < 6; ++j) {
+        double s = A[lidx(j, j)];
+#pragma unroll 1
+        for (int k = 0; k < j; ++k) s -= A[lidx(j, k)] * A[lidx(j, k)];
+        if (!(s > 0.0)) return false;
+        const double ljj = sqrt(s);
+        A[lidx(j, j)] = ljj;
+#pragma unroll 1
+        for (int i = j + 1; i < 6; ++i) {
+            double t = A[lidx(i, j)];
+#pragma unroll 1
+            for (int k = 0; k < j; ++k) t -= A[lidx(i, k)] * A[lidx(j, k)];
+            A[lidx(i, j)] = t / ljj;
+        }
+    }
+#pragma unroll 1
+    for (int i = 0; i < 6; ++i) {
+        double t = b[i];
+#pragma unroll 1
+        for (int k = 0; k < i; ++k) t -= A[lidx(i, k)] * y[k];
+        y[i] = t / A[lidx(i, i)];
+    }
+#pragma unroll 1
+    for (int i = 5; i >= 0; --i) {
+        double t = y[i];
+#pragma unroll 1
+        for (int k = i + 1; k < 6; ++k) t -= A[lidx(k, i)] * x[k];
+        x[i] = t / A[lidx(i, i)];
+    }
+    bool fin = true;
+#pragma unroll 1
+    for (int i = 0; i < 6; ++i) fin = fin && isfinite(x[i]);
+    return fin;
+}
+
+__device__ void compute_step_lds(SolveState& S, double* ws) {
+    double* A = ws;
+    double* gs = ws + 21;
+    double* nb = ws + 27;
+    double* step = ws + 33;
+    double* y = ws + 39;
+    while (true) {
+        if (S.iteration >= kMaxInner) { S.done = 1; S.term = LMSF_TERM_MAX_ITERATIONS; return; }
+        if (S.radius < 1e-32) { S.done = 1; S.term = LMSF_TERM_PARAMETER_TOL; return; }
+        ++S.iteration;
+#pragma unroll 1
+        for (int i = 0; i < 6; ++i) {
+            gs[i] = S.g[i] * S.s[i];
+#pragma unroll 1
+            for (int j = 0; j <= i; ++j) A[lidx(i, j)] = S.H[hidx(j, i)] * S.s[i] * S.s[j];
+        }
+#pragma unroll 1
+        for (int i = 0; i < 6; ++i) {
+            const double hs = S.H[hidx(i, i)] * S.s[i] * S.s[i];
+            const double dg = fmin(fmax(hs, 1e-6), 1e32);
+            A[lidx(i, i)] = hs + dg / S.radius;
+            nb[i] = -gs[i];
+        }
+        const bool ok = chol_solve6_lds(A, nb, y, step);
+        double mcc = 0.0;
+        if (ok) {
+            double sg = 0.0, sHs = 0.0;
+#pragma unroll 1
+            for (int i = 0; i < 6; ++i) {
+                sg += step[i] * gs[i];
+                double t = 0.0;
+#pragma unroll 1
+                for (int j = 0; j < 6; ++j) t += S.H[i <= j ? hidx(i, j) : hidx(j, i)] * S.s[i] * S.s[j] * step[j];
+                sHs += step[i] * t;
+            }
+            mcc = -(sg + 0.5 * sHs);
+        }
+        if (!ok || !(mcc > 0.0)) {  // StepIsInvalid == StepRejected(0)
+            S.radius = S.radius / S.decrease;
+            S.decrease *= 2.0;
+            continue;
+        }
+        double* delta = y;   // y is free after the solve
+#pragma unroll 1
+        for (int i = 0; i < 6; ++i) delta[i] = step[i] * S.s[i];
+        pose_plus_lds(S.x, delta, S.xc, ws + 45);
+        S.mcc = mcc;
+        S.need_eval = 1;
+        return;
+    }
+}
+
+// MODE 0: inlined (registers), 1: non-inlined call, 2: LDS workspace ws (kStepWs doubles), rolled loops
+template <int MODE>
+__device__ __forceinline__ void compute_step(SolveState& S, double* ws) {
+    if constexpr (MODE == 1) compute_step_call(S);
+    else if constexpr (MODE == 2) compute_step_lds(S, ws);
     else compute_step_body(S);
 }
 
@@ -200,8 +358,8 @@ __device__ void finish_outer(SolveState& S, int outer) {
 // lm_step after the evaluation at the candidate (tot = its reduced packet): step acceptance
 // (ParameterToleranceReached, FunctionToleranceReached, IsStepSuccessful, HandleSuccessfulStep /
 // StepRejected) + next step; one thread.
-template <bool CALL = false>
-__device__ __forceinline__ void lm_step_apply(SolveState& S, const double* tot, int outer, int is_last) {
+template <int MODE = 0>
+__device__ __forceinline__ void lm_step_apply(SolveState& S, const double* tot, int outer, int is_last, double* ws = nullptr) {
     S.need_eval = 0;
     ++S.evals;
     const double cost_c = isfinite(tot[0]) ? tot[0] : 1.7976931348623157e308;
@@ -218,7 +376,7 @@ __device__ __forceinline__ void lm_step_apply(SolveState& S, const double* tot, 
         } else {
             const double rel = cost_change / S.mcc;
             if (rel > 1e-3) {
-                const double f = 1.0 - pow(2.0 * rel - 1.0, 3.0);
+                const double f = 1.0 - cube_rn(2.0 * rel - 1.0);   // pow(2 rel - 1, 3), correctly rounded
                 S.radius = S.radius / fmax(1.0 / 3.0, f);
                 S.radius = fmin(1e16, S.radius);
                 S.decrease = 2.0;
@@ -230,16 +388,16 @@ __device__ __forceinline__ void lm_step_apply(SolveState& S, const double* tot, 
                 if (S.iteration >= kMaxInner) {
                     S.done = 1;
                     S.term = LMSF_TERM_MAX_ITERATIONS;
-                } else if (grad_max_norm(S.x, S.g) <= 1e-10) {
+                } else if ((MODE == 2 ? grad_max_norm_lds(S.x, S.g, ws) : grad_max_norm(S.x, S.g)) <= 1e-10) {
                     S.done = 1;
                     S.term = LMSF_TERM_GRADIENT_TOL;
                 } else {
-                    compute_step<CALL>(S);
+                    compute_step<MODE>(S, ws);
                 }
             } else {
                 S.radius = S.radius / S.decrease;
                 S.decrease *= 2.0;
-                compute_step<CALL>(S);
+                compute_step<MODE>(S, ws);
             }
         }
     }
@@ -247,8 +405,8 @@ __device__ __forceinline__ void lm_step_apply(SolveState& S, const double* tot, 
 }
 
 // IterationZero on the reduced first evaluation (tot) + the first step; one lane, S in LDS.
-template <bool CALL = false>
-__device__ __forceinline__ void lm_begin_apply(SolveState& S, const double* tot) {
+template <int MODE = 0>
+__device__ __forceinline__ void lm_begin_apply(SolveState& S, const double* tot, double* ws = nullptr) {
     S.iteration = 0;
     S.need_eval = 0;
     S.done = 0;
@@ -269,12 +427,12 @@ __device__ __forceinline__ void lm_begin_apply(SolveState& S, const double* tot)
     S.radius = 1e4;
     S.decrease = 2.0;
     S.x_norm = norm7(S.x);
-    if (grad_max_norm(S.x, S.g) <= 1e-10) {
+    if ((MODE == 2 ? grad_max_norm_lds(S.x, S.g, ws) : grad_max_norm(S.x, S.g)) <= 1e-10) {
         S.done = 1;
         S.term = LMSF_TERM_GRADIENT_TOL;
         return;
     }
-    compute_step<CALL>(S);
+    compute_step<MODE>(S, ws);
 }
 
 }  // namespace
