@@ -302,6 +302,13 @@ def knn_roofline(ks, mean_n27, tj, elapsed_s, note, solo=None):
                      "frac": round(model_gbs / HBM_PEAK_GBS, 4), "gbs_over_timed_window": round(model_wall_gbs, 1),
                      "exceeds_peak": bool(model_gbs > HBM_PEAK_GBS or model_wall_gbs > HBM_PEAK_GBS)},
            "note": note}
+    # a byte model above the HBM peak cannot be HBM traffic: the walk reads fewer candidates than n27 counts (the
+    # pruned walk) or the reads are cache-served -- the model is then no roofline at all
+    out["model"]["valid"] = not out["model"]["exceeds_peak"]
+    if out["model"]["exceeds_peak"]:
+        out["model"]["frac"] = None
+        out["model"]["invalid_reason"] = ("the 8(d) byte model exceeds the HBM peak: it counts every candidate of the "
+                                          "27 cells as an HBM read; only the PMC traffic is a roofline here")
     if solo is not None:
         span = ks.total_ms / max(int(ks.launches), 1)
         out["concurrent"] = {"avg_launch_ms": round(span, 4), "launches": int(ks.launches),
@@ -311,7 +318,8 @@ def knn_roofline(ks, mean_n27, tj, elapsed_s, note, solo=None):
         mean_us = tj.get("rocprof_mean_us")
         out["rocprof"] = {"profile": tj.get("profile"), "mean_us": mean_us,
                           "frac": round(traffic / (mean_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if mean_us else None,
-                          "model_frac": round(model_bytes / (mean_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if mean_us else None,
+                          "model_frac": round(model_bytes / (mean_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+                          if mean_us and out["model"]["valid"] else None,
                           "live_over_rocprof": round(avg_launch_ms * 1e3 / mean_us, 3) if mean_us else None,
                           "dispatches": tj.get("dispatches")}
     return out

@@ -65,6 +65,7 @@ def test_roofline_measured_and_model():
     r2 = bench.knn_roofline(types.SimpleNamespace(**dict(vars(ks), total_ms=0.01)), 50.0, None, 0.02, "n")
     assert r2["basis"].startswith("unmeasured") and r2["achieved"] is None and r2["frac"] is None
     assert r2["model"]["exceeds_peak"] is True and r2["traffic"] is None
+    assert r2["model"]["valid"] is False and r2["model"]["frac"] is None      # no roofline claim from it
     # a build without search stamps (no launch time): no achieved figure, no division by zero
     r3 = bench.knn_roofline(types.SimpleNamespace(**dict(vars(ks), total_ms=0.0)), 50.0, tj, 0.02, "n")
     assert r3["achieved"] is None and r3["frac"] is None and r3["basis"].startswith("untimed")
