@@ -32,8 +32,11 @@ struct DevMap {
     uint32_t* fill = nullptr;
     void* scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
-    int ox = 0, oy = 0, oz = 0, nx = 0, ny = 0, nz = 0, sx = 1;
+    int ox = 0, oy = 0, oz = 0, nx = 0, ny = 0, nz = 0, sx = 1, sy = 1;
     float lim1 = 1.f;
+    bool orig_borrowed = false;       // a dense map's first-pass grid: orig is its 1 m grid's
+    uint64_t build_id = 0;            // bumped by every build (a first-pass grid records the one it follows)
+    uint64_t src_build = 0;
     // occupied-slice count of the last build, read back without blocking: lim1 (the pruned walk's
     // first radius) is resolved only by a launch that can take the pruned one-lane walk
     unsigned long long* h_occ = nullptr;   // pinned
@@ -54,7 +57,7 @@ struct DevMap {
     GridView view() const {
         GridView g{};   // zeroed padding: views are compared bytewise (SolveGraph key)
         g.ox = ox; g.oy = oy; g.oz = oz; g.nx = nx; g.ny = ny; g.nz = nz; g.sx = sx;
-        g.off = off; g.pts = pts; g.orig = orig; g.n = n; g.lim1 = lim1;
+        g.off = off; g.pts = pts; g.orig = orig; g.n = n; g.lim1 = lim1; g.sy = sy;
         return g;
     }
 };
@@ -129,6 +132,7 @@ struct lmsf_ctx {
     int optimization_count = 10;
     DevMap map[3];                    // map of a kind (or its keyframe window when a prior is set)
     DevMap prior[3];                  // static prior part of a kind's map (tracker shared map)
+    DevMap fine[3];                   // first-pass grid of a dense map of a kind (one-lane batch launches)
     bool map_set[3] = {false, false, false};
     // registration buffers
     float4* feat = nullptr;
@@ -481,6 +485,7 @@ lmsf_status grid_finish_device(lmsf_ctx* c, DevMap& m, int base, hipStream_t s) 
     m.lim1 = 1.f;
     m.n = bb[6];
     m.occ_pending = false;
+    ++m.build_id;
     return LMSF_OK;
 }
 
@@ -489,6 +494,7 @@ lmsf_status grid_finish_device(lmsf_ctx* c, DevMap& m, int base, hipStream_t s) 
 lmsf_status grid_finish(lmsf_ctx* c, DevMap& m, int base, hipStream_t s, bool density = true) {
     const int* bb = m.h_bb;
     const int n = bb[6];
+    ++m.build_id;
     if (n == 0) {
         m.n = 0;
         m.occ_pending = false;
@@ -542,6 +548,60 @@ lmsf_status resolve_lim1(lmsf_ctx* c, DevMap& m) {
     return LMSF_OK;
 }
 
+// First-pass grid of a dense map (lim1 < 1): y / z cells of 0.5 m and 8 x-slices per metre over the same points
+// (C5's 10M-point map: the first pass's 3 x 3 rows then cover ~0.9 m^2 of y-z instead of ~2.1 m^2 and its x-windows
+// trim at 1/8 m -- tools/c5_walk_model.py).  Its 3 x 3 rows cover the first-pass radius sqrt(lim1) only up to
+// 0.5 m (lim1 <= 0.25; dense maps have lim1 <= 1/8).  Built once per map, on the first one-lane launch.
+constexpr int kFineSx = 8, kFineSy = 2;
+lmsf_status build_fine(lmsf_ctx* c, int kind) {
+    DevMap& m = c->map[kind];
+    DevMap& f = c->fine[kind];
+    const bool want = m.n > 0 && c->prior[kind].n == 0 && m.lim1 * 1.00001f <= 0.25f;
+    if (!want) {
+        f.n = 0;
+        return LMSF_OK;
+    }
+    if (f.n > 0 && f.src_build == m.build_id) return LMSF_OK;
+    f.n = 0;
+    hipStream_t s = c->stream;
+    if (!f.d_bb) {
+        HIPCHK(c, hipMalloc((void**)&f.d_bb, 32 * sizeof(int)));
+        HIPCHK(c, hipMemset(f.d_bb, 0, 32 * sizeof(int)));
+        HIPCHK(c, hipHostMalloc((void**)&f.h_bb, 16 * sizeof(int), hipHostMallocDefault));
+    }
+    if ((size_t)m.n > f.cap) {
+        hipFree(f.pts); hipFree(f.cell);
+        f.pts = nullptr; f.cell = nullptr;
+        f.cap = 0;
+        HIPCHK(c, dalloc(&f.pts, (size_t)m.n));
+        HIPCHK(c, dalloc(&f.cell, (size_t)m.n));
+        f.cap = (size_t)m.n;
+    }
+    HIPCHK(c, launch_map_bbox(m.orig, m.n, nullptr, kFineSx, f.d_bb, s, kFineSy));
+    HIPCHK(c, hipMemcpyAsync(f.h_bb, f.d_bb, 7 * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const int* bb = f.h_bb;
+    const int nx = bb[3] - bb[0] + 1, ny = bb[4] - bb[1] + 1, nz = bb[5] - bb[2] + 1;
+    const size_t cells = (size_t)nx * ny * nz;
+    if (nx <= 0 || ny <= 0 || nz <= 0 || cells > kMaxCells) return LMSF_OK;   // no first-pass grid: the 1 m grid serves
+    lmsf_status rc = grid_cells_reserve(c, f, cells + 1, s);
+    if (rc) return rc;
+    f.ox = bb[0]; f.oy = bb[1]; f.oz = bb[2];
+    f.nx = nx; f.ny = ny; f.nz = nz; f.sx = kFineSx; f.sy = kFineSy;
+    unsigned long long* d_occ = reinterpret_cast<unsigned long long*>(f.d_bb + 8);
+    HIPCHK(c, launch_grid_clear(f.counts, f.fill, cells + 1, d_occ, s));
+    HIPCHK(c, launch_map_count(m.orig, m.n, kFineSx, f.ox, f.oy, f.oz, nx, ny, nz, f.cell, f.counts, s, kFineSy));
+    size_t tb = f.scan_tmp_bytes;
+    HIPCHK(c, exclusive_scan_u32(f.counts, f.off, cells + 1, f.scan_tmp, tb, s));
+    HIPCHK(c, launch_map_scatter(m.orig, m.n, f.cell, f.off, f.fill, f.pts, 0, s));
+    f.orig = m.orig;
+    f.orig_borrowed = true;
+    f.lim1 = m.lim1;
+    f.n = m.n;
+    f.src_build = m.build_id;
+    return LMSF_OK;
+}
+
 lmsf_status ctx_settle(lmsf_ctx* c) {
     for (auto& h : c->settle_hooks) {
         lmsf_status rc = h.first(h.second);
@@ -559,6 +619,11 @@ lmsf_status resolve_all_lim1(lmsf_ctx* c, size_t query_slots) {
     for (DevMap* ms : {c->map, c->prior})
         for (int k = 0; k < 3; ++k) {
             lmsf_status rc = resolve_lim1(c, ms[k]);
+            if (rc) return rc;
+        }
+    if (c->cfg.solver == LMSF_SOLVER_CERES_LM)   // the fused batch path's dense first pass
+        for (int k : {LMSF_EDGE, LMSF_SURF}) {
+            lmsf_status rc = build_fine(c, k);
             if (rc) return rc;
         }
     return LMSF_OK;
@@ -599,6 +664,11 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
     BatchView bv = c->bview(nb);
     const GridView ge = c->map[LMSF_EDGE].view(), gs = c->map[LMSF_SURF].view();
     const GridView ge2 = c->prior[LMSF_EDGE].view(), gs2 = c->prior[LMSF_SURF].view();
+    // first-pass grids of dense maps (current with their maps), else none
+    const GridView fe = c->fine[LMSF_EDGE].n > 0 && c->fine[LMSF_EDGE].src_build == c->map[LMSF_EDGE].build_id
+                            ? c->fine[LMSF_EDGE].view() : GridView{};
+    const GridView fs = c->fine[LMSF_SURF].n > 0 && c->fine[LMSF_SURF].src_build == c->map[LMSF_SURF].build_id
+                            ? c->fine[LMSF_SURF].view() : GridView{};
     hipStream_t s = c->stream;
     const bool gn = c->cfg.solver == LMSF_SOLVER_GN;
     const bool memo_on = c->opt[LMSF_OPT_QUERY_MEMO] != 0;
@@ -627,7 +697,7 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
         if (fused) {
             BatchView bvo = bv;
             bvo.memo = batch_memo(o) ? 1 : 0;
-            HIPCHK(c, launch_match_fit(ge, gs, bvo, s));
+            HIPCHK(c, launch_match_fit(ge, gs, bvo, s, fe, fs));
         }
         else {   // single-scan launches: the 8-lane search, with the slot memo under the Ceres-LM solver
             BatchView bvk = bv;
@@ -700,7 +770,7 @@ std::vector<unsigned char> solve_key(lmsf_ctx* c, int nb, int iters) {
     };
     const BatchView bv = c->bview(nb);
     put(&bv, sizeof bv);
-    for (DevMap* ms : {c->map, c->prior})
+    for (DevMap* ms : {c->map, c->prior, c->fine})
         for (int kind = 0; kind < 3; ++kind) {
             const GridView g = ms[kind].view();
             put(&g, sizeof g);
@@ -858,10 +928,11 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
     if (c->raw_pending && c->ev_raw_ready) hipEventSynchronize(c->ev_raw_ready);   // an upload on the shared stream
     if (c->sg.exec) hipGraphExecDestroy(c->sg.exec);
-    for (DevMap* ms : {c->map, c->prior}) {
+    for (DevMap* ms : {c->map, c->prior, c->fine}) {
         for (int k = 0; k < 3; ++k) {
             DevMap& m = ms[k];
-            hipFree(m.orig); hipFree(m.pts); hipFree(m.cell); hipFree(m.counts); hipFree(m.off); hipFree(m.fill);
+            if (!m.orig_borrowed) hipFree(m.orig);
+            hipFree(m.pts); hipFree(m.cell); hipFree(m.counts); hipFree(m.off); hipFree(m.fill);
             hipFree(m.scan_tmp);
             if (m.h_occ) hipHostFree(m.h_occ);
             if (m.ev_occ) hipEventDestroy(m.ev_occ);

@@ -25,13 +25,13 @@ __global__ void map_bbox_init_kernel(int* bbox) {
     else if (threadIdx.x < 6) bbox[threadIdx.x] = INT_MIN;
 }
 
-__global__ void __launch_bounds__(256) map_bbox_kernel(const float4* pts, int n, const int* n_dev, float sx, int* bbox) {
+__global__ void __launch_bounds__(256) map_bbox_kernel(const float4* pts, int n, const int* n_dev, float sx, float sy, int* bbox) {
     if (n_dev) n = min(n, *n_dev);
     if (blockIdx.x == 0 && threadIdx.x == 0) bbox[6] = n;
     int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const float4 p = pts[i];
-        const float c[3] = {floorf(p.x * sx), floorf(p.y), floorf(p.z)};
+        const float c[3] = {floorf(p.x * sx), floorf(p.y * sy), floorf(p.z * sy)};   // sy: 1 (1 m cells) or 2
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             // coordinates beyond +-2^30 m are clamped (they cannot be matched anyway)
@@ -43,14 +43,14 @@ __global__ void __launch_bounds__(256) map_bbox_kernel(const float4* pts, int n,
     block_bbox_commit<256>(lo, hi, bbox);
 }
 
-__global__ void map_count_kernel(const float4* pts, int n, float sx, int ox, int oy, int oz, int nx, int ny, int nz,
-                                 int* cell, uint32_t* counts) {
+__global__ void map_count_kernel(const float4* pts, int n, float sx, float sy, int ox, int oy, int oz, int nx, int ny,
+                                 int nz, int* cell, uint32_t* counts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float4 p = pts[i];
     const int cx = (int)fminf(fmaxf(floorf(p.x * sx), -1073741824.f), 1073741824.f) - ox;
-    const int cy = (int)fminf(fmaxf(floorf(p.y), -1073741824.f), 1073741824.f) - oy;
-    const int cz = (int)fminf(fmaxf(floorf(p.z), -1073741824.f), 1073741824.f) - oz;
+    const int cy = (int)fminf(fmaxf(floorf(p.y * sy), -1073741824.f), 1073741824.f) - oy;
+    const int cz = (int)fminf(fmaxf(floorf(p.z * sy), -1073741824.f), 1073741824.f) - oz;
     const int c = (cz * ny + cy) * nx + cx;
     cell[i] = c;
     atomicAdd(&counts[c], 1u);
@@ -128,19 +128,19 @@ hipError_t launch_gather_slots(const SlotTable& tab, float4* out, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_map_bbox(const float4* pts, int n, const int* n_dev, int sx, int* bbox, hipStream_t s) {
+hipError_t launch_map_bbox(const float4* pts, int n, const int* n_dev, int sx, int* bbox, hipStream_t s, int sy) {
     hipLaunchKernelGGL(map_bbox_init_kernel, dim3(1), dim3(64), 0, s, bbox);
     // >= 16 points per thread, <= 512 blocks: each block commits 6 atomics to the same 6 words (512 blocks
     // serialise ~35 us on them, which only a multi-million-point cloud amortises)
     const int blocks = min((n + 4095) / 4096, 512);
-    hipLaunchKernelGGL(map_bbox_kernel, dim3(max(blocks, 1)), dim3(256), 0, s, pts, n, n_dev, (float)sx, bbox);
+    hipLaunchKernelGGL(map_bbox_kernel, dim3(max(blocks, 1)), dim3(256), 0, s, pts, n, n_dev, (float)sx, (float)sy, bbox);
     return hipGetLastError();
 }
 
 hipError_t launch_map_count(const float4* pts, int n, int sx, int ox, int oy, int oz, int nx, int ny, int nz,
-                            int* cell, uint32_t* counts, hipStream_t s) {
-    hipLaunchKernelGGL(map_count_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pts, n, (float)sx, ox, oy, oz, nx,
-                       ny, nz, cell, counts);
+                            int* cell, uint32_t* counts, hipStream_t s, int sy) {
+    hipLaunchKernelGGL(map_count_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pts, n, (float)sx, (float)sy, ox, oy, oz,
+                       nx, ny, nz, cell, counts);
     return hipGetLastError();
 }
 

@@ -121,6 +121,7 @@ __device__ __forceinline__ GridView pick_grid(bool c, const GridView& a, const G
     r.n = c ? a.n : b.n;
     r.sx = c ? a.sx : b.sx;
     r.lim1 = c ? a.lim1 : b.lim1;
+    r.sy = c ? a.sy : b.sy;
     return r;
 }
 
@@ -1260,6 +1261,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
 #ifndef LMSF_DENSE_SORT
 #define LMSF_DENSE_SORT 1
 #endif
+#ifndef LMSF_DENSE_FLAT   // 1: the rows walked as one flattened candidate stream; 0: one loop per row
+#define LMSF_DENSE_FLAT 0
+#endif
 constexpr int kDenseBuckets = 16;        // pass-1 work classes of the block re-deal (2 RU-steps each)
 constexpr int kDensePay = 31;            // LDS words per query: e, w (3), rows: start (9), len (9), lb (9)
 
@@ -1309,7 +1313,9 @@ __device__ __forceinline__ void dense_finish(const GridView& g, const BatchView&
 // yz-gap bound lb and the grid's x origin / slices; false outside the grid (knn_walk's row_geo).
 __device__ __forceinline__ bool dense_row(const GridView& gg, const float3 w, int rr, const uint32_t*& row, int& xa, int& xb,
                                           float& lb) {
-    const float fx = floorf(w.x), fy = floorf(w.y), fz = floorf(w.z);
+    // y / z cells of 1 / sy m (sy = 1 | 2: products and quotients by sy are exact)
+    const float fsy = (float)gg.sy, h = 1.0f / fsy;
+    const float fx = floorf(w.x), fy = floorf(w.y * fsy), fz = floorf(w.z * fsy);
     const int dyo = (rr % 3) - 1, dzo = (rr / 3) - 1;
     const float fxs = fx * (float)gg.sx;
     const bool inside = gg.n > 0 && fxs >= (float)(gg.ox - 2 * gg.sx) && fxs <= (float)(gg.ox + gg.nx + gg.sx) &&
@@ -1321,9 +1327,9 @@ __device__ __forceinline__ bool dense_row(const GridView& gg, const float3 w, in
     xb = min(cxs + 2 * gg.sx - 1, gg.nx - 1);
     if (cy < 0 || cy >= gg.ny || cz < 0 || cz >= gg.nz || xa > xb) return false;
     row = gg.off + ((size_t)cz * gg.ny + cy) * gg.nx;
-    const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
-    const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
-    const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
+    const float ylo = (fy + (float)dyo) * h, zlo = (fz + (float)dzo) * h;
+    const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + h)));
+    const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + h)));
     lb = gy * gy + gz * gz;
     return true;
 }
@@ -1352,7 +1358,7 @@ constexpr int kDenseRowOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // own row, fac
 constexpr float kDenseCull = 1.0f + 1e-5f;                       // knn_walk's kCullLim
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void dense_pass1_kernel(
-    GridView ge, GridView gs, BatchView bv, int gx, int remap, unsigned* p2count) {
+    GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, int gx, int remap, unsigned* p2count) {
     __shared__ uint32_t pay[kDensePay][256];
     __shared__ int bcnt[kDenseBuckets * 4];
     int bx, b;
@@ -1364,6 +1370,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const unsigned long long below = (1ull << lane) - 1ull;
     const Pose Ps = load_pose(bv.st[b].x);
+    // pass 1 runs on a kind's first-pass grid (0.5 m y / z cells) when the map has one, else on its 1 m grid
+    const GridView pe = pick_grid(fe.n > 0, fe, ge), ps = pick_grid(fs.n > 0, fs, gs);
     unsigned int c27 = 0;
     // ---- pass-1 rows of this lane's own query
     int steps = 0;
@@ -1377,7 +1385,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         for (int i = 0; i < 9; ++i) { st_[i] = 0; ln_[i] = 0; lb_[i] = 3.0e38f; }
         if (valid) {
             const float4 p = bv.featp[(size_t)b * F + e];
-            const GridView g = pick_grid(__float_as_int(p.w) < ne, ge, gs);
+            const GridView g = pick_grid(__float_as_int(p.w) < ne, pe, ps);
             w = associate(Ps, p);
             const float lim1 = g.lim1 * kDenseCull;
 #pragma unroll
@@ -1443,7 +1451,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     const float4 p = bv.featp[ppos];
     const int qq = __float_as_int(p.w);
     const bool is_edge = qq < ne;
-    const GridView g = pick_grid(is_edge, ge, gs);
+    const GridView g = pick_grid(is_edge, pe, ps);
     const float3 w = make_float3(__uint_as_float(pay[1][tid]), __uint_as_float(pay[2][tid]), __uint_as_float(pay[3][tid]));
     const double sentinel = key_as_double(kSentinel);
     double k[5];
@@ -1451,6 +1459,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     for (int j = 0; j < 5; ++j) k[j] = sentinel;
     if (valid) {
         const float4* rp = g.pts;
+#if LMSF_DENSE_FLAT
         uint32_t cur = 0, end = 0;
         int r = 0;
         for (;;) {
@@ -1476,6 +1485,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
             }
             cur += LMSF_FUSED_UNROLL;
         }
+#else
+        // one loop per row (RU loads in flight, the tail one at a time), rows nearest first, a row entered only
+        // while its yz-gap bound is within the current 5th key
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+            const uint32_t ln = pay[13 + r][tid];
+            if (!ln || __uint_as_float(pay[22 + r][tid]) > key_d2(k[4])) continue;
+            const uint32_t a = pay[4 + r][tid];
+            uint32_t c = 0;
+            for (; c + LMSF_FUSED_UNROLL <= ln; c += LMSF_FUSED_UNROLL) {
+                float4 m[LMSF_FUSED_UNROLL];
+#pragma unroll
+                for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) m[u] = rp[a + c + u];
+#pragma unroll
+                for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) key_insert(k, nn_key(w, m[u], (uint32_t)__float_as_int(m[u].w)));
+            }
+            for (; c < ln; ++c) {
+                const float4 m = rp[a + c];
+                key_insert(k, nn_key(w, m, (uint32_t)__float_as_int(m.w)));
+            }
+        }
+#endif
     }
     // ---- complete (5th key within lim1: pass 2 would scan nothing) -> fit; else -> pass-2 list
     const bool p2 = valid && key_d2(k[4]) > g.lim1;
@@ -1483,14 +1514,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     int base2 = 0;
     if (lane == 0 && m2) base2 = (int)atomicAdd(p2count, (unsigned)__popcll(m2));
     base2 = __shfl(base2, 0, 64);
-    if (p2) {
-        bv.wl[base2 + __popcll(m2 & below)] = (int)((size_t)b * F + e);
-#pragma unroll
-        for (int j = 0; j < 5; ++j)
-            bv.memo_nbr[((size_t)b * kMemoWords + j) * F + e] =
-                key_bits(k[j]) < kSentinel ? (int)(uint32_t)key_bits(k[j]) : -1;
+    if (p2) {   // pass 2 from scratch on the 1 m grid, bounded by this 5th key (the 5 nearest lie within it)
+        const int at = base2 + __popcll(m2 & below);
+        bv.wl[at] = (int)((size_t)b * F + e);
+        bv.wlim[at] = key_d2(k[4]);
     } else if (valid) {
-        dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);
+        dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);   // g.orig: the caller-order map either way
     }
     if (bv.n27) {   // accounting runs: the 27-cell candidates and the queries
         unsigned int qn = (bx * 256 + tid < nq) ? 1u : 0u;
@@ -1508,13 +1537,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     }
 }
 
-// The listed queries of dense_pass1_kernel: pass 2 (knn_walk's second loop) from their pass-1 keys, then the fit.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void dense_pass2_kernel(
+// The listed queries of dense_pass1_kernel (their 5th key beyond lim1): a fresh pruned walk on the 1 m grid,
+// rows nearest first, every row and x-window bounded by min(the pass-1 5th key, the current 5th key) -- the 5
+// nearest lie within the pass-1 bound, so the walk is exact whichever grid pass 1 searched -- then the fit.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void dense_pass2_kernel(
     GridView ge, GridView gs, BatchView bv, const unsigned* p2count) {
     const unsigned count = *p2count;
     const size_t F = bv.feat_stride;
     for (unsigned li = blockIdx.x * 256 + threadIdx.x; li < count; li += gridDim.x * 256) {
         const size_t code = (size_t)(unsigned)bv.wl[li];
+        const float bound = bv.wlim[li];
         const int b = (int)(code / F), e = (int)(code - (size_t)b * F);
         const int ne = bv.n_edge[b];
         const size_t ppos = (size_t)b * F + e;
@@ -1525,43 +1557,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         const float3 w = associate(load_pose(bv.st[b].x), p);
         double k[5];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const int idx = bv.memo_nbr[((size_t)b * kMemoWords + j) * F + e];
-            k[j] = idx >= 0 ? nn_key(w, g.orig[idx], (uint32_t)idx) : key_as_double(kSentinel);
-        }
-        const float lim1 = g.lim1 * kDenseCull;
+        for (int j = 0; j < 5; ++j) k[j] = key_as_double(kSentinel);
         const float4* rp = g.pts;
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            const float d4 = key_d2(k[4]);
+            const float d4 = fminf(bound, key_d2(k[4]));
             const uint32_t* row;
-            int xa, xb, sa, sb, ta = 1, tb = 0;
+            int xa, xb, sa, sb;
             float lb;
             if (!dense_row(g, w, kDenseRowOrder[i], row, xa, xb, lb)) continue;
             if (lb > d4) continue;
             dense_window(g, w, d4 * kDenseCull, lb, xa, xb, sa, sb);
-            if (!(lb > lim1)) dense_window(g, w, lim1, lb, xa, xb, ta, tb);   // pass 1's window of this row
-            int ra[2] = {sa, 1}, rb[2] = {sb, 0};
-            if (ta <= tb) {
-                ra[0] = sa; rb[0] = min(sb, ta - 1);
-                ra[1] = max(sa, tb + 1); rb[1] = sb;
+            if (sa > sb) continue;
+            const uint32_t a = row[sa], len = row[sb + 1] - a;
+            uint32_t c = 0;
+            for (; c + LMSF_FUSED_UNROLL <= len; c += LMSF_FUSED_UNROLL) {
+                float4 m[LMSF_FUSED_UNROLL];
+#pragma unroll
+                for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) m[u] = rp[a + c + u];
+#pragma unroll
+                for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) key_insert(k, nn_key(w, m[u], (uint32_t)__float_as_int(m[u].w)));
             }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (ra[h] > rb[h]) continue;
-                const uint32_t a = row[ra[h]], len = row[rb[h] + 1] - a;
-                uint32_t c = 0;
-                for (; c + LMSF_FUSED_UNROLL <= len; c += LMSF_FUSED_UNROLL) {
-                    float4 m[LMSF_FUSED_UNROLL];
-#pragma unroll
-                    for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) m[u] = rp[a + c + u];
-#pragma unroll
-                    for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) key_insert(k, nn_key(w, m[u], (uint32_t)__float_as_int(m[u].w)));
-                }
-                for (; c < len; ++c) {
-                    const float4 m = rp[a + c];
-                    key_insert(k, nn_key(w, m, (uint32_t)__float_as_int(m.w)));
-                }
+            for (; c < len; ++c) {
+                const float4 m = rp[a + c];
+                key_insert(k, nn_key(w, m, (uint32_t)__float_as_int(m.w)));
             }
         }
         dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);
@@ -1976,7 +1995,8 @@ bool match_fit_prune(const GridView& edge, const GridView& surf) {
 }
 
 // bv.memo: run the memo pass first, then search only its work lists (sparse maps only).
-hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const BatchView& bv, hipStream_t s) {
+hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const BatchView& bv, hipStream_t s,
+                            const GridView& fine_edge, const GridView& fine_surf) {
     const int gx = (bv.feat_stride + 255) / 256;
     const dim3 grid(gx * bv.B);
     const int remap = knn_remap();
@@ -1985,7 +2005,8 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
         if (split && kLinEval && bv.p2count && (size_t)bv.B * bv.feat_stride < ((size_t)1 << 31)) {
             hipError_t e = hipMemsetAsync(bv.p2count, 0, sizeof(unsigned), s);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(dense_pass1_kernel, grid, dim3(256), 0, s, edge, surf, bv, gx, remap, bv.p2count);
+            hipLaunchKernelGGL(dense_pass1_kernel, grid, dim3(256), 0, s, edge, surf, fine_edge, fine_surf, bv, gx, remap,
+                               bv.p2count);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
             // grid-stride over the list (~10% of the queries on C5): 8 blocks per CU

@@ -62,6 +62,7 @@ struct GridView {
     const float4* orig;    // points in the caller's order (x, y, z, intensity)
     int n;
     float lim1;            // first-pass radius^2 of the pruned one-lane search (m^2); >= 1: sparse grid, plain walk
+    int sy;                // y / z cells per metre: 1 (the 1 m grid of every search), 2 (a dense map's first-pass grid)
 };
 
 // Per-registration solver state (device resident, one per batch slot).
@@ -154,9 +155,10 @@ __device__ __forceinline__ void stamp_if(unsigned long long* at, bool first_bloc
 // bbox[0..6] = the map box of the first n points (min(n, *n_dev) when n_dev) and that count; resets bbox first.
 hipError_t launch_pack3(const int* a, const int* b, const int* c, int* out, hipStream_t s);
 hipError_t launch_grid_clear(uint32_t* counts, uint32_t* fill, size_t n, unsigned long long* occ, hipStream_t s);
-hipError_t launch_map_bbox(const float4* pts, int n, const int* n_dev, int sx, int* bbox, hipStream_t s);
+// sy: y / z cells per metre (1: the 1 m match-radius grid; 2: the dense maps' first-pass grid)
+hipError_t launch_map_bbox(const float4* pts, int n, const int* n_dev, int sx, int* bbox, hipStream_t s, int sy = 1);
 hipError_t launch_map_count(const float4* pts, int n, int sx, int ox, int oy, int oz, int nx, int ny, int nz,
-                            int* cell, uint32_t* counts, hipStream_t s);
+                            int* cell, uint32_t* counts, hipStream_t s, int sy = 1);
 // sorted[] w = base + original index (base > 0 for a keyframe window behind a prior map)
 hipError_t launch_map_scatter(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
                               float4* sorted, int base, hipStream_t s);
@@ -202,7 +204,9 @@ int knn_team_for(size_t query_slots);   // lanes per query of a search launch ov
 // Fused 5-NN search + fit + first evaluation (one lane per query, queries in fslot order); false:
 // not applicable to this launch (caller runs launch_knn + launch_fit_eval).
 bool match_fit_applies(const GridView& edge2, const GridView& surf2, const BatchView& bv, int solver);
-hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const BatchView& bv, hipStream_t s);
+// fine_*: a dense map's first-pass grid per kind (n = 0: none; pass 1 then runs on the 1 m grid)
+hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const BatchView& bv, hipStream_t s,
+                            const GridView& fine_edge = GridView{}, const GridView& fine_surf = GridView{});
 bool match_fit_prune(const GridView& edge, const GridView& surf);   // dense map: pruned walk, no memo
 // Record capture (lmsf_batch_capture): slot b's records after an outer iteration's matching as lmsf_record
 // rows in slot order, its 5 neighbour indices (nnp w bits, -1: none) and the linearisation pose (7 doubles).
