@@ -552,11 +552,23 @@ lmsf_status resolve_lim1(lmsf_ctx* c, DevMap& m) {
 // (C5's 10M-point map: the first pass's 3 x 3 rows then cover ~0.9 m^2 of y-z instead of ~2.1 m^2 and its x-windows
 // trim at 1/8 m -- tools/c5_walk_model.py).  Its 3 x 3 rows cover the first-pass radius sqrt(lim1) only up to
 // 0.5 m (lim1 <= 0.25; dense maps have lim1 <= 1/8).  Built once per map, on the first one-lane launch.
-constexpr int kFineSx = 8, kFineSy = 2;
+constexpr int kFineSx = 8;
+// y / z cells per metre of the first-pass grid: the largest power of two (<= LMSF_FINE_SY_MAX, A/B) whose cell
+// still holds the first-pass radius, so its 3 x 3 rows cover it (C5: surf lim1 0.052 -> 0.23 m)
+#ifndef LMSF_FINE_SY_MAX
+#define LMSF_FINE_SY_MAX 2
+#endif
+int fine_cells_per_m(float lim1) {
+    static const int sy_max = ab_int("LMSF_FINE_SY_MAX", LMSF_FINE_SY_MAX);
+    int sy = 1;
+    while (sy < sy_max && lim1 * 1.00001f * (float)(4 * sy * sy) <= 1.0f) sy *= 2;
+    return sy;
+}
 lmsf_status build_fine(lmsf_ctx* c, int kind) {
     DevMap& m = c->map[kind];
     DevMap& f = c->fine[kind];
-    const bool want = m.n > 0 && c->prior[kind].n == 0 && m.lim1 * 1.00001f <= 0.25f;
+    const int kFineSy = fine_cells_per_m(m.lim1);
+    const bool want = m.n > 0 && c->prior[kind].n == 0 && m.lim1 < 1.f && kFineSy > 1;
     if (!want) {
         f.n = 0;
         return LMSF_OK;

@@ -1239,33 +1239,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     }
 }
 
-// ---------------------------------------------------------------- dense maps (C5): pass 1 sorted + flattened, pass 2 listed
+// ---------------------------------------------------------------- dense maps (C5): first pass on a fine grid, pass 2 listed
 // The pruned one-lane walk of match_fit_kernel<true, .> ran at lane utilisation 0.53 on C5 (VALU busy 0.94,
-// profiles/r03/C5): lanes of a wave walk very different candidate counts (C5 surf queries: mean 77, p90 128,
-// tools/c5_walk_model.py), and a loop per row runs each row for its longest lane (loop-level utilisation
-// 0.25 by the model), then pass 2 (10% of the queries) holds every wave it touches.  Here:
-//   dense_pass1_kernel: every query resolves its 9 pass-1 rows (the x-windows of radius sqrt(lim1): offsets
-//     only), the block re-deals its 256 queries to its waves in order of their pass-1 work (a counting sort
-//     on RU-step buckets, rows carried in LDS), and each lane walks its rows as one flattened candidate
-//     stream (RU loads in flight, masked at row ends; a row is entered only while its yz-gap bound is within
-//     the current 5th key).  A query whose 5th key is within lim1 is complete (pass 2 would scan nothing:
-//     its windows lie inside pass 1's) and is fitted here; the others go, with their 5 keys (as map
-//     indices), to a work list.
-//   dense_pass2_kernel: the listed queries (dense, grid-stride) run pass 2 -- the rows within the 5th key,
-//     minus pass 1's windows -- then the fit.
-// Results are the pruned walk's exactly (the same rows, windows and keys; the sets and their order do not
-// depend on which lane walks a query or on the order of a row's candidates), so the records are unchanged.
+// profiles/r03/C5) and scanned ~9x the points inside its first-pass sphere: the 1 m y-z rows of the match-radius
+// grid are far wider than the first-pass radius sqrt(lim1) (0.23 m on C5's surf map, tools/c5_walk_model.py).
+//   dense_pass1_kernel: one lane per query, its 9 first-pass rows resolved up front (offsets only, one batch of
+//     loads) on the map's first-pass grid (FineGrid: y-z cells of 1/sy m holding the first-pass radius, 8
+//     x-slices per metre; the 1 m grid when the map has none), then walked one loop per row, nearest rows first,
+//     a row entered only while its yz-gap bound is within the current 5th key.  A query whose 5th key is within
+//     lim1 is complete (every point nearer than its 5th lies in the scanned ball) and is fitted here; the others
+//     go, with their 5th key as the bound, to a work list.
+//   dense_pass2_kernel: the listed queries (dense, grid-stride) run a fresh pruned walk on the 1 m grid bounded
+//     by that key (the 5 nearest lie within it), then the fit.
+// Results are the pruned walk's exactly (keys totally ordered by (d2, index): the kept 5 do not depend on the
+// grid or the visit order).  A/B on C5 (profiles/r04/ab_notes.md): this form 3370 pairs/s vs 2967 for r03's
+// kernel on one box; re-dealing a block's queries to its waves by pass-1 work (LDS counting sort) 3220, and a
+// flattened candidate stream 3261 -- both cost more than the lane balance they bought.
 #ifndef LMSF_DENSE_SPLIT
 #define LMSF_DENSE_SPLIT 1
 #endif
-#ifndef LMSF_DENSE_SORT
-#define LMSF_DENSE_SORT 1
-#endif
-#ifndef LMSF_DENSE_FLAT   // 1: the rows walked as one flattened candidate stream; 0: one loop per row
-#define LMSF_DENSE_FLAT 0
-#endif
-constexpr int kDenseBuckets = 16;        // pass-1 work classes of the block re-deal (2 RU-steps each)
-constexpr int kDensePay = 31;            // LDS words per query: e, w (3), rows: start (9), len (9), lb (9)
 
 // The line / plane fit of a query's 5 kept keys and its record (match_fit_kernel's tail).
 __device__ __forceinline__ void dense_finish(const GridView& g, const BatchView& bv, size_t ppos, const float4 p, bool is_edge,
@@ -1311,12 +1303,11 @@ __device__ __forceinline__ void dense_finish(const GridView& g, const BatchView&
 
 // Row rr (0..8: dy, dz in {-1, 0, 1}) of the pruned walk around w: its offsets row, x-slice span [xa, xb], the
 // yz-gap bound lb and the grid's x origin / slices; false outside the grid (knn_walk's row_geo).
-__device__ __forceinline__ bool dense_row(const GridView& gg, const float3 w, int rr, const uint32_t*& row, int& xa, int& xb,
-                                          float& lb) {
-    // y / z cells of 1 / sy m (sy = 1 | 2: products and quotients by sy are exact)
+__device__ __forceinline__ bool dense_row_at(const GridView& gg, const float3 w, int dyo, int dzo, const uint32_t*& row, int& xa,
+                                             int& xb, float& lb) {
+    // y / z cells of 1 / sy m (sy a power of two: products by sy and 1 / sy are exact)
     const float fsy = (float)gg.sy, h = 1.0f / fsy;
     const float fx = floorf(w.x), fy = floorf(w.y * fsy), fz = floorf(w.z * fsy);
-    const int dyo = (rr % 3) - 1, dzo = (rr / 3) - 1;
     const float fxs = fx * (float)gg.sx;
     const bool inside = gg.n > 0 && fxs >= (float)(gg.ox - 2 * gg.sx) && fxs <= (float)(gg.ox + gg.nx + gg.sx) &&
                         fy >= (float)(gg.oy - 2) && fy <= (float)(gg.oy + gg.ny + 1) &&
@@ -1332,6 +1323,10 @@ __device__ __forceinline__ bool dense_row(const GridView& gg, const float3 w, in
     const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + h)));
     lb = gy * gy + gz * gz;
     return true;
+}
+__device__ __forceinline__ bool dense_row(const GridView& gg, const float3 w, int rr, const uint32_t*& row, int& xa, int& xb,
+                                          float& lb) {
+    return dense_row_at(gg, w, (rr % 3) - 1, (rr / 3) - 1, row, xa, xb, lb);
 }
 // slices of [xa, xb] meeting [w.x - r, w.x + r], r = sqrt(lim - lb) (sa > sb: empty) -- knn_walk's window
 __device__ __forceinline__ void dense_window(const GridView& gg, const float3 w, float lim, float lb, int xa, int xb, int& sa,
@@ -1359,140 +1354,57 @@ constexpr float kDenseCull = 1.0f + 1e-5f;                       // knn_walk's k
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void dense_pass1_kernel(
     GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, int gx, int remap, unsigned* p2count) {
-    __shared__ uint32_t pay[kDensePay][256];
-    __shared__ int bcnt[kDenseBuckets * 4];
     int bx, b;
     block_coords(remap, gx, bx, b);
     const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
     const size_t F = bv.feat_stride;
     if (bx == 0 && threadIdx.x == 0) bv.n_search[b] = nq;
-    if (bx * 256 >= nq) return;   // uniform per block, ahead of the barriers
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+    if (bx * 256 >= nq) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const unsigned long long below = (1ull << lane) - 1ull;
-    const Pose Ps = load_pose(bv.st[b].x);
-    // pass 1 runs on a kind's first-pass grid (0.5 m y / z cells) when the map has one, else on its 1 m grid
-    const GridView pe = pick_grid(fe.n > 0, fe, ge), ps = pick_grid(fs.n > 0, fs, gs);
-    unsigned int c27 = 0;
-    // ---- pass-1 rows of this lane's own query
-    int steps = 0;
-    {
-        const int e = bx * 256 + tid;
-        const bool valid = e < nq;
-        float3 w = make_float3(0.f, 0.f, 0.f);
-        uint32_t st_[9], ln_[9];
-        float lb_[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) { st_[i] = 0; ln_[i] = 0; lb_[i] = 3.0e38f; }
-        if (valid) {
-            const float4 p = bv.featp[(size_t)b * F + e];
-            const GridView g = pick_grid(__float_as_int(p.w) < ne, pe, ps);
-            w = associate(Ps, p);
-            const float lim1 = g.lim1 * kDenseCull;
-#pragma unroll
-            for (int i = 0; i < 9; ++i) {
-                const uint32_t* row;
-                int xa, xb, sa, sb;
-                float lb;
-                if (!dense_row(g, w, kDenseRowOrder[i], row, xa, xb, lb)) continue;
-                if (bv.count27) c27 += row[xb + 1] - row[xa];
-                lb_[i] = lb;
-                if (lb > lim1) continue;
-                dense_window(g, w, lim1, lb, xa, xb, sa, sb);
-                if (sa <= sb) {
-                    st_[i] = row[sa];
-                    ln_[i] = row[sb + 1] - st_[i];
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 9; ++i) steps += (int)((ln_[i] + (uint32_t)(LMSF_FUSED_UNROLL - 1)) / (uint32_t)LMSF_FUSED_UNROLL);
-        }
-        // ---- re-deal the block's queries to its waves by pass-1 work (bucket-major, wave-minor, lane order)
-        int dest = tid;
-#if LMSF_DENSE_SORT
-        const int bk = valid ? min(steps >> 1, kDenseBuckets - 1) : 0;
-        unsigned long long mine = 0;
-#pragma unroll
-        for (int j = 0; j < kDenseBuckets; ++j) {
-            const unsigned long long m = __ballot(bk == j);
-            if (bk == j) mine = m;
-            if (lane == 0) bcnt[j * 4 + wave] = __popcll(m);
-        }
-        __syncthreads();
-        if (wave == 0) {   // exclusive scan of the 64 (bucket, wave) counts
-            const int c = bcnt[lane];
-            int incl = c;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int t = __shfl_up(incl, o, 64);
-                incl += lane >= o ? t : 0;
-            }
-            bcnt[lane] = incl - c;
-        }
-        __syncthreads();
-        dest = bcnt[bk * 4 + wave] + __popcll(mine & below);
-#endif
-        pay[0][dest] = valid ? (uint32_t)e : 0xffffffffu;
-        pay[1][dest] = __float_as_uint(w.x);
-        pay[2][dest] = __float_as_uint(w.y);
-        pay[3][dest] = __float_as_uint(w.z);
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            pay[4 + i][dest] = st_[i];
-            pay[13 + i][dest] = ln_[i];
-            pay[22 + i][dest] = __float_as_uint(lb_[i]);
-        }
-        __syncthreads();
-    }
-    // ---- the query dealt to this lane: its rows as one flattened candidate stream
-    const uint32_t eu = pay[0][tid];
-    const bool valid = eu != 0xffffffffu;
-    const int e = valid ? (int)eu : 0;
-    const size_t ppos = (size_t)b * F + e;
+    const int e = bx * 256 + threadIdx.x;
+    const bool valid = e < nq;
+    const size_t ppos = (size_t)b * F + (valid ? e : 0);
     const float4 p = bv.featp[ppos];
     const int qq = __float_as_int(p.w);
     const bool is_edge = qq < ne;
-    const GridView g = pick_grid(is_edge, pe, ps);
-    const float3 w = make_float3(__uint_as_float(pay[1][tid]), __uint_as_float(pay[2][tid]), __uint_as_float(pay[3][tid]));
+    // the first-pass grid of the query's kind (FineGrid), else its 1 m grid
+    const GridView g = pick_grid(is_edge, pick_grid(fe.n > 0, fe, ge), pick_grid(fs.n > 0, fs, gs));
+    const float3 w = associate(load_pose(bv.st[b].x), p);
     const double sentinel = key_as_double(kSentinel);
     double k[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) k[j] = sentinel;
+    unsigned int c27 = 0;
     if (valid) {
-        const float4* rp = g.pts;
-#if LMSF_DENSE_FLAT
-        uint32_t cur = 0, end = 0;
-        int r = 0;
-        for (;;) {
-            while (cur >= end && r < 9) {   // enter the next row with candidates within the 5th key
-                const uint32_t ln = pay[13 + r][tid];
-                if (ln && !(__uint_as_float(pay[22 + r][tid]) > key_d2(k[4]))) {
-                    cur = pay[4 + r][tid];
-                    end = cur + ln;
-                }
-                ++r;
-            }
-            if (cur >= end) break;
-            float4 m[LMSF_FUSED_UNROLL];
+        // rows resolved up front: the 18 offset loads in flight together
+        uint32_t st_[9], ln_[9];
+        float lb_[9];
+        const float lim1 = g.lim1 * kDenseCull;
 #pragma unroll
-            for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) m[u] = rp[cur + u < end ? cur + u : cur];
-#pragma unroll
-            for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) {
-                const float dx = w.x - m[u].x, dy = w.y - m[u].y, dz = w.z - m[u].z;
-                const float d2 = dx * dx + dy * dy + dz * dz;
-                const double x = key_as_double(((uint64_t)(__float_as_uint(d2) + kKeyBias) << 32) |
-                                               (uint32_t)__float_as_int(m[u].w));
-                key_insert(k, cur + u < end ? x : sentinel);   // past the row's end: a key that never enters
+        for (int i = 0; i < 9; ++i) {
+            st_[i] = 0;
+            ln_[i] = 0;
+            lb_[i] = 3.0e38f;
+            const uint32_t* row;
+            int xa, xb, sa, sb;
+            float lb;
+            if (!dense_row(g, w, kDenseRowOrder[i], row, xa, xb, lb)) continue;
+            if (bv.count27) c27 += row[xb + 1] - row[xa];
+            lb_[i] = lb;
+            if (lb > lim1) continue;
+            dense_window(g, w, lim1, lb, xa, xb, sa, sb);
+            if (sa <= sb) {
+                st_[i] = row[sa];
+                ln_[i] = row[sb + 1] - st_[i];
             }
-            cur += LMSF_FUSED_UNROLL;
         }
-#else
-        // one loop per row (RU loads in flight, the tail one at a time), rows nearest first, a row entered only
-        // while its yz-gap bound is within the current 5th key
+        const float4* rp = g.pts;
 #pragma unroll
-        for (int r = 0; r < 9; ++r) {
-            const uint32_t ln = pay[13 + r][tid];
-            if (!ln || __uint_as_float(pay[22 + r][tid]) > key_d2(k[4])) continue;
-            const uint32_t a = pay[4 + r][tid];
+        for (int i = 0; i < 9; ++i) {
+            const uint32_t ln = ln_[i];
+            if (!ln || lb_[i] > key_d2(k[4])) continue;
+            const uint32_t a = st_[i];
             uint32_t c = 0;
             for (; c + LMSF_FUSED_UNROLL <= ln; c += LMSF_FUSED_UNROLL) {
                 float4 m[LMSF_FUSED_UNROLL];
@@ -1506,9 +1418,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
                 key_insert(k, nn_key(w, m, (uint32_t)__float_as_int(m.w)));
             }
         }
-#endif
     }
-    // ---- complete (5th key within lim1: pass 2 would scan nothing) -> fit; else -> pass-2 list
+    // complete (5th key within lim1: nothing nearer lies outside the scanned ball) -> fit; else -> pass-2 list
     const bool p2 = valid && key_d2(k[4]) > g.lim1;
     const unsigned long long m2 = __ballot(p2);
     int base2 = 0;
@@ -1521,8 +1432,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     } else if (valid) {
         dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);   // g.orig: the caller-order map either way
     }
-    if (bv.n27) {   // accounting runs: the 27-cell candidates and the queries
-        unsigned int qn = (bx * 256 + tid < nq) ? 1u : 0u;
+    if (bv.n27) {   // accounting runs: the 27-cell candidates (of the first-pass grid) and the queries
+        unsigned int qn = valid ? 1u : 0u;
         unsigned long long c = c27;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
@@ -1540,8 +1451,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
 // The listed queries of dense_pass1_kernel (their 5th key beyond lim1): a fresh pruned walk on the 1 m grid,
 // rows nearest first, every row and x-window bounded by min(the pass-1 5th key, the current 5th key) -- the 5
 // nearest lie within the pass-1 bound, so the walk is exact whichever grid pass 1 searched -- then the fit.
+// The 5 x 5 rows of a 0.5 m first-pass grid around the query, nearest ring first: they hold every point within 1 m
+// (a row two cells past them is >= 1 m away in y or z), so pass 2 can run there instead of on the 1 m grid.
+constexpr int kRing5[25][2] = {{0, 0},  {0, -1}, {-1, 0}, {1, 0},  {0, 1},  {-1, -1}, {1, -1}, {-1, 1}, {1, 1},
+                               {0, -2}, {-2, 0}, {2, 0},  {0, 2},  {-1, -2}, {1, -2}, {-2, -1}, {2, -1}, {-2, 1},
+                               {2, 1},  {-1, 2}, {1, 2},  {-2, -2}, {2, -2}, {-2, 2}, {2, 2}};
+#ifndef LMSF_PASS2_FINE
+#define LMSF_PASS2_FINE 1
+#endif
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void dense_pass2_kernel(
-    GridView ge, GridView gs, BatchView bv, const unsigned* p2count) {
+    GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, const unsigned* p2count) {
     const unsigned count = *p2count;
     const size_t F = bv.feat_stride;
     for (unsigned li = blockIdx.x * 256 + threadIdx.x; li < count; li += gridDim.x * 256) {
@@ -1553,19 +1473,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
         const float4 p = bv.featp[ppos];
         const int qq = __float_as_int(p.w);
         const bool is_edge = qq < ne;
-        const GridView g = pick_grid(is_edge, ge, gs);
+        const GridView gf = pick_grid(is_edge, fe, fs);
+        const bool fine = LMSF_PASS2_FINE && gf.n > 0 && gf.sy == 2;
+        const GridView g = pick_grid(fine, gf, pick_grid(is_edge, ge, gs));
         const float3 w = associate(load_pose(bv.st[b].x), p);
         double k[5];
 #pragma unroll
         for (int j = 0; j < 5; ++j) k[j] = key_as_double(kSentinel);
         const float4* rp = g.pts;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
+        const int nrows = fine ? 25 : 9;
+#pragma unroll 1
+        for (int i = 0; i < nrows; ++i) {
             const float d4 = fminf(bound, key_d2(k[4]));
             const uint32_t* row;
             int xa, xb, sa, sb;
             float lb;
-            if (!dense_row(g, w, kDenseRowOrder[i], row, xa, xb, lb)) continue;
+            const int dyo = fine ? kRing5[i][0] : (kDenseRowOrder[i] % 3) - 1;
+            const int dzo = fine ? kRing5[i][1] : (kDenseRowOrder[i] / 3) - 1;
+            if (!dense_row_at(g, w, dyo, dzo, row, xa, xb, lb)) continue;
             if (lb > d4) continue;
             dense_window(g, w, d4 * kDenseCull, lb, xa, xb, sa, sb);
             if (sa > sb) continue;
@@ -2010,7 +1935,7 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
             e = hipGetLastError();
             if (e != hipSuccess) return e;
             // grid-stride over the list (~10% of the queries on C5): 8 blocks per CU
-            hipLaunchKernelGGL(dense_pass2_kernel, dim3(2048), dim3(256), 0, s, edge, surf, bv,
+            hipLaunchKernelGGL(dense_pass2_kernel, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge, fine_surf, bv,
                                (const unsigned*)bv.p2count);
         } else {
             hipLaunchKernelGGL((match_fit_kernel<true, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
