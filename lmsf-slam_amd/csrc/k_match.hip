@@ -1303,31 +1303,55 @@ __device__ __forceinline__ void dense_finish(const GridView& g, const BatchView&
 
 // Row rr (0..8: dy, dz in {-1, 0, 1}) of the pruned walk around w: its offsets row, x-slice span [xa, xb], the
 // yz-gap bound lb and the grid's x origin / slices; false outside the grid (knn_walk's row_geo).
-__device__ __forceinline__ bool dense_row_at(const GridView& gg, const float3 w, int dyo, int dzo, const uint32_t*& row, int& xa,
-                                             int& xb, float& lb) {
-    // y / z cells of 1 / sy m (sy a power of two: products by sy and 1 / sy are exact)
-    const float fsy = (float)gg.sy, h = 1.0f / fsy;
-    const float fx = floorf(w.x), fy = floorf(w.y * fsy), fz = floorf(w.z * fsy);
-    const float fxs = fx * (float)gg.sx;
-    const bool inside = gg.n > 0 && fxs >= (float)(gg.ox - 2 * gg.sx) && fxs <= (float)(gg.ox + gg.nx + gg.sx) &&
-                        fy >= (float)(gg.oy - 2) && fy <= (float)(gg.oy + gg.ny + 1) &&
-                        fz >= (float)(gg.oz - 2) && fz <= (float)(gg.oz + gg.nz + 1);
-    if (!inside) return false;
-    const int cxs = (int)fxs - gg.ox, cy = (int)fy - gg.oy + dyo, cz = (int)fz - gg.oz + dzo;
-    xa = max(cxs - gg.sx, 0);
-    xb = min(cxs + 2 * gg.sx - 1, gg.nx - 1);
-    if (cy < 0 || cy >= gg.ny || cz < 0 || cz >= gg.nz || xa > xb) return false;
-    row = gg.off + ((size_t)cz * gg.ny + cy) * gg.nx;
-    const float ylo = (fy + (float)dyo) * h, zlo = (fz + (float)dzo) * h;
-    const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + h)));
-    const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + h)));
-    lb = gy * gy + gz * gz;
-    return true;
-}
-__device__ __forceinline__ bool dense_row(const GridView& gg, const float3 w, int rr, const uint32_t*& row, int& xa, int& xb,
-                                          float& lb) {
-    return dense_row_at(gg, w, (rr % 3) - 1, (rr / 3) - 1, row, xa, xb, lb);
-}
+// A query's row geometry on a grid, the parts shared by its rows computed once: the x-slice span (3 m of slices
+// around floor(w.x)), its cell (y, z), and the yz gaps to the cells R rows away (gy[R + d] for row offset d; the
+// same float expressions per row as knn_walk's, so each row's bound lb = gy^2 + gz^2 is bit-identical).
+template <int R>
+struct DenseQuery {
+    bool inside;
+    int xa, xb, cy0, cz0;
+    float gy[2 * R + 1], gz[2 * R + 1];
+    __device__ __forceinline__ DenseQuery(const GridView& gg, const float3 w) {
+        // y / z cells of 1 / sy m (sy a power of two: products by sy and 1 / sy are exact)
+        const float fsy = (float)gg.sy, h = 1.0f / fsy;
+        const float fx = floorf(w.x), fy = floorf(w.y * fsy), fz = floorf(w.z * fsy);
+        const float fxs = fx * (float)gg.sx;
+        inside = gg.n > 0 && fxs >= (float)(gg.ox - 2 * gg.sx) && fxs <= (float)(gg.ox + gg.nx + gg.sx) &&
+                 fy >= (float)(gg.oy - R - 1) && fy <= (float)(gg.oy + gg.ny + R) && fz >= (float)(gg.oz - R - 1) &&
+                 fz <= (float)(gg.oz + gg.nz + R);
+        const int cxs = inside ? (int)fxs - gg.ox : 0;
+        xa = max(cxs - gg.sx, 0);
+        xb = min(cxs + 2 * gg.sx - 1, gg.nx - 1);
+        inside = inside && xa <= xb;
+        cy0 = inside ? (int)fy - gg.oy : 0;
+        cz0 = inside ? (int)fz - gg.oz : 0;
+#pragma unroll
+        for (int d = -R; d <= R; ++d) {
+            const float ylo = (fy + (float)d) * h, zlo = (fz + (float)d) * h;
+            gy[R + d] = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + h)));
+            gz[R + d] = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + h)));
+        }
+    }
+    // the gap of offset d as a select chain (a runtime index into gy / gz would put them in scratch)
+    __device__ __forceinline__ static float pick(const float (&a)[2 * R + 1], int d) {
+        float v = a[0];
+#pragma unroll
+        for (int j = 1; j <= 2 * R; ++j) v = d == j - R ? a[j] : v;
+        return v;
+    }
+    // row (dyo, dzo): its bound (always) and, when it lies in the grid, its offsets row
+    __device__ __forceinline__ float lb(int dyo, int dzo) const {
+        const float y = pick(gy, dyo), z = pick(gz, dzo);
+        return y * y + z * z;
+    }
+    __device__ __forceinline__ bool row(const GridView& gg, int dyo, int dzo, const uint32_t*& r) const {
+        const int cy = cy0 + dyo, cz = cz0 + dzo;
+        if (!inside || cy < 0 || cy >= gg.ny || cz < 0 || cz >= gg.nz) return false;
+        r = gg.off + ((size_t)cz * gg.ny + cy) * gg.nx;
+        return true;
+    }
+};
+
 // slices of [xa, xb] meeting [w.x - r, w.x + r], r = sqrt(lim - lb) (sa > sb: empty) -- knn_walk's window
 __device__ __forceinline__ void dense_window(const GridView& gg, const float3 w, float lim, float lb, int xa, int xb, int& sa,
                                              int& sb) {
@@ -1381,17 +1405,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         uint32_t st_[9], ln_[9];
         float lb_[9];
         const float lim1 = g.lim1 * kDenseCull;
+        const DenseQuery<1> dq(g, w);
+        const int xa = dq.xa, xb = dq.xb;
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
             st_[i] = 0;
             ln_[i] = 0;
-            lb_[i] = 3.0e38f;
-            const uint32_t* row;
-            int xa, xb, sa, sb;
-            float lb;
-            if (!dense_row(g, w, kDenseRowOrder[i], row, xa, xb, lb)) continue;
-            if (bv.count27) c27 += row[xb + 1] - row[xa];
+            const int dyo = (kDenseRowOrder[i] % 3) - 1, dzo = (kDenseRowOrder[i] / 3) - 1;
+            const float lb = dq.lb(dyo, dzo);
             lb_[i] = lb;
+            const uint32_t* row;
+            int sa, sb;
+            if (!dq.row(g, dyo, dzo, row)) continue;
+            if (bv.count27) c27 += row[xb + 1] - row[xa];
             if (lb > lim1) continue;
             dense_window(g, w, lim1, lb, xa, xb, sa, sb);
             if (sa <= sb) {
@@ -1482,16 +1508,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
         for (int j = 0; j < 5; ++j) k[j] = key_as_double(kSentinel);
         const float4* rp = g.pts;
         const int nrows = fine ? 25 : 9;
+        const DenseQuery<2> dq(g, w);   // the 1 m grid's 3 x 3 rows are its inner ring
+        const int xa = dq.xa, xb = dq.xb;
 #pragma unroll 1
         for (int i = 0; i < nrows; ++i) {
             const float d4 = fminf(bound, key_d2(k[4]));
             const uint32_t* row;
-            int xa, xb, sa, sb;
-            float lb;
+            int sa, sb;
             const int dyo = fine ? kRing5[i][0] : (kDenseRowOrder[i] % 3) - 1;
             const int dzo = fine ? kRing5[i][1] : (kDenseRowOrder[i] / 3) - 1;
-            if (!dense_row_at(g, w, dyo, dzo, row, xa, xb, lb)) continue;
-            if (lb > d4) continue;
+            const float lb = dq.lb(dyo, dzo);
+            if (lb > d4) continue;   // ahead of the row's address and offsets
+            if (!dq.row(g, dyo, dzo, row)) continue;
             dense_window(g, w, d4 * kDenseCull, lb, xa, xb, sa, sb);
             if (sa > sb) continue;
             const uint32_t a = row[sa], len = row[sb + 1] - a;

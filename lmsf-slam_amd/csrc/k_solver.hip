@@ -60,6 +60,9 @@ constexpr int kCtlMode = LMSF_CTL_MODE;
 __global__ __launch_bounds__(kBeginThreads) LMSF_CTL_ATTR void lm_begin_kernel(BatchView bv) {
     const int b = blockIdx.x;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
+#ifdef LMSF_STEP_PROFILE
+    const unsigned long long t0 = wall_clock64();
+#endif
     __shared__ SolveState sS;
     state_copy(sS, bv.st[b]);
     __shared__ double tot[kPacket];
@@ -69,10 +72,21 @@ __global__ __launch_bounds__(kBeginThreads) LMSF_CTL_ATTR void lm_begin_kernel(B
         const int fb = bv.part_q;
         reduce_parts(bv, b, (nq + fb - 1) / fb, tot);
     }   // (reduce_parts ends with a barrier: sS is in place)
+#ifdef LMSF_STEP_PROFILE
+    const unsigned long long t1 = wall_clock64();
+#endif
     __shared__ double ws[kStepWs];
     if (threadIdx.x == 0) lm_begin_apply<kCtlMode>(sS, tot, ws);
     __syncthreads();
+#ifdef LMSF_STEP_PROFILE
+    const unsigned long long t2 = wall_clock64();
+#endif
     state_copy(bv.st[b], sS);
+#ifdef LMSF_STEP_PROFILE
+    __syncthreads();
+    if (b == 0 && threadIdx.x == 0)
+        printf("lm_begin: copy+reduce %llu apply %llu copy-out %llu (x10 ns)\n", t1 - t0, t2 - t1, wall_clock64() - t2);
+#endif
 }
 
 // After lm_eval_kernel at the candidate: the reduction and lm_step_apply.  kStepThreads: one wave.  Four
@@ -89,15 +103,30 @@ __global__ __launch_bounds__(kStepThreads) LMSF_CTL_ATTR void lm_step_kernel(Bat
         if (is_last && threadIdx.x == 0) finish_outer(S, outer);
         return;
     }
+#ifdef LMSF_STEP_PROFILE   // diagnostics build (tools/build_variant.sh): phase times of slot 0's step
+    const unsigned long long t0 = wall_clock64();
+#endif
     __shared__ SolveState sS;
     state_copy(sS, S);
     const int nq = bv.n_edge[b] + bv.n_surf[b];
     __shared__ double tot[kPacket];
     reduce_parts(bv, b, (nq + kEvalBlock - 1) / kEvalBlock, tot);   // ends with a barrier
+#ifdef LMSF_STEP_PROFILE
+    const unsigned long long t1 = wall_clock64();
+#endif
     __shared__ double ws[kStepWs];
     if (threadIdx.x == 0) lm_step_apply<kCtlMode>(sS, tot, outer, is_last, ws);
     __syncthreads();
+#ifdef LMSF_STEP_PROFILE
+    const unsigned long long t2 = wall_clock64();
+#endif
     state_copy(S, sS);
+#ifdef LMSF_STEP_PROFILE
+    __syncthreads();
+    if (b == 0 && threadIdx.x == 0)
+        printf("lm_step outer %d: copy+reduce %llu apply %llu copy-out %llu (x10 ns)\n", outer, t1 - t0, t2 - t1,
+               wall_clock64() - t2);
+#endif
 }
 
 // ---------------------------------------------------------------- GN (edgeSurfFeatureRegistration)
