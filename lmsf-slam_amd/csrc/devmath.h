@@ -76,7 +76,7 @@ __device__ __forceinline__ double cube_rn(double x) {
 // Math::GetTransformFromSe3 (INC/Math.hpp:29-72) + PoseSE3Parameterization::Plus
 // (INC/Algorithm/Ceres/Parameterization/PoseSE3Parameterization.hpp:32-46).  sin / cos of one argument come
 // from one sincos (one range reduction), pow(theta, 3) is cube_rn.
-__device__ inline void pose_plus(const double* x, const double* delta, double* out) {
+__device__ __forceinline__ void pose_plus_inl(const double* x, const double* delta, double* out) {
     d3 om = mk(delta[0], delta[1], delta[2]);
     d3 up = mk(delta[3], delta[4], delta[5]);
     double theta = norm(om);
@@ -119,6 +119,7 @@ __device__ inline void pose_plus(const double* x, const double* delta, double* o
     out[0] = qp.x; out[1] = qp.y; out[2] = qp.z; out[3] = qp.w;
     out[4] = tp.x; out[5] = tp.y; out[6] = tp.z;
 }
+__device__ inline void pose_plus(const double* x, const double* delta, double* out) { pose_plus_inl(x, delta, out); }
 
 // ---------------------------------------------------------------- SelfAdjointEigenSolver (Eigen 3.3)
 // Eigen's published algorithm (Eigenvalues/SelfAdjointEigenSolver.h, Tridiagonalization.h, Jacobi.h),

@@ -1373,6 +1373,59 @@ __device__ __forceinline__ void key_insert(double (&k)[5], double x) {
     }
 }
 
+// One row's candidates [a, a + len) of pts into the kept 5 keys k.  LMSF_DENSE_DEFER: per chunk of U candidates only
+// those with d2 <= the chunk-start 5th key's d2 enter the network, one per lane per step while any lane has one
+// left (a candidate beyond the 5th key at any time can never be kept: the 5th only decreases, and keys are totally
+// ordered, so the kept 5 are the same).  On C5's first pass most scanned candidates lie outside the query's 5-NN
+// ball, where the network's 9 f64 min / max per candidate are half of the loop's VALU.
+#ifndef LMSF_DENSE_DEFER
+#define LMSF_DENSE_DEFER 0
+#endif
+#ifndef LMSF_DEFER_U
+#define LMSF_DEFER_U 8
+#endif
+__device__ __forceinline__ void dense_run(double (&k)[5], const float4* __restrict__ rp, uint32_t a, uint32_t len, const float3 w) {
+    uint32_t c = 0;
+    if constexpr (LMSF_DENSE_DEFER) {
+        constexpr int U = LMSF_DEFER_U;
+        for (; c + U <= len; c += U) {
+            float4 m[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) m[u] = rp[a + c + u];
+            const uint32_t b4 = (uint32_t)(key_bits(k[4]) >> 32);
+            double kk[U];
+            unsigned hm = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                kk[u] = nn_key(w, m[u], (uint32_t)__float_as_int(m[u].w));
+                if ((uint32_t)(key_bits(kk[u]) >> 32) <= b4) hm |= 1u << u;
+            }
+            while (__ballot(hm != 0u)) {
+                if (hm) {
+                    const int j = __builtin_ctz(hm);
+                    hm &= hm - 1u;
+                    double x = kk[0];
+#pragma unroll
+                    for (int u = 1; u < U; ++u) x = j == u ? kk[u] : x;
+                    key_insert(k, x);
+                }
+            }
+        }
+    } else {
+        for (; c + LMSF_FUSED_UNROLL <= len; c += LMSF_FUSED_UNROLL) {
+            float4 m[LMSF_FUSED_UNROLL];
+#pragma unroll
+            for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) m[u] = rp[a + c + u];
+#pragma unroll
+            for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) key_insert(k, nn_key(w, m[u], (uint32_t)__float_as_int(m[u].w)));
+        }
+    }
+    for (; c < len; ++c) {
+        const float4 m = rp[a + c];
+        key_insert(k, nn_key(w, m, (uint32_t)__float_as_int(m.w)));
+    }
+}
+
 constexpr int kDenseRowOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // own row, faces, corners (knn_walk's kOrder)
 constexpr float kDenseCull = 1.0f + 1e-5f;                       // knn_walk's kCullLim
 
@@ -1430,19 +1483,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         for (int i = 0; i < 9; ++i) {
             const uint32_t ln = ln_[i];
             if (!ln || lb_[i] > key_d2(k[4])) continue;
-            const uint32_t a = st_[i];
-            uint32_t c = 0;
-            for (; c + LMSF_FUSED_UNROLL <= ln; c += LMSF_FUSED_UNROLL) {
-                float4 m[LMSF_FUSED_UNROLL];
-#pragma unroll
-                for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) m[u] = rp[a + c + u];
-#pragma unroll
-                for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) key_insert(k, nn_key(w, m[u], (uint32_t)__float_as_int(m[u].w)));
-            }
-            for (; c < ln; ++c) {
-                const float4 m = rp[a + c];
-                key_insert(k, nn_key(w, m, (uint32_t)__float_as_int(m.w)));
-            }
+            dense_run(k, rp, st_[i], ln, w);
         }
     }
     // complete (5th key within lim1: nothing nearer lies outside the scanned ball) -> fit; else -> pass-2 list
@@ -1522,19 +1563,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
             if (!dq.row(g, dyo, dzo, row)) continue;
             dense_window(g, w, d4 * kDenseCull, lb, xa, xb, sa, sb);
             if (sa > sb) continue;
-            const uint32_t a = row[sa], len = row[sb + 1] - a;
-            uint32_t c = 0;
-            for (; c + LMSF_FUSED_UNROLL <= len; c += LMSF_FUSED_UNROLL) {
-                float4 m[LMSF_FUSED_UNROLL];
-#pragma unroll
-                for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) m[u] = rp[a + c + u];
-#pragma unroll
-                for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) key_insert(k, nn_key(w, m[u], (uint32_t)__float_as_int(m[u].w)));
-            }
-            for (; c < len; ++c) {
-                const float4 m = rp[a + c];
-                key_insert(k, nn_key(w, m, (uint32_t)__float_as_int(m.w)));
-            }
+            const uint32_t a = row[sa];
+            dense_run(k, rp, a, row[sb + 1] - a, w);
         }
         dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);
     }
@@ -1699,6 +1729,12 @@ __device__ void reduce_coherent(const BatchView& bv, int b, int p0, int np, doub
     __syncthreads();
 }
 
+// LMSF_LOOP_CTL_WAVE: the LM control of the single-scan loop on wave 0 (lm_control.h wv::, bit-identical) instead
+// of one lane.
+#ifndef LMSF_LOOP_CTL_WAVE
+#define LMSF_LOOP_CTL_WAVE 1
+#endif
+constexpr bool kLoopCtlWave = LMSF_LOOP_CTL_WAVE != 0;
 __global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, unsigned* sync, int* err,
                                                       unsigned spin_limit) {
     const int b = blockIdx.y, part = blockIdx.x, nblk = gridDim.x;
@@ -1708,7 +1744,11 @@ __global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, u
     const int nq = bv.n_edge[b] + bv.n_surf[b];
     // lm_begin: the first evaluation's packets (fit_eval), IterationZero and the first step
     reduce_parts(bv, b, (nq + bv.part_q - 1) / bv.part_q, tot);   // ends with a barrier: sS is in place
-    if (threadIdx.x == 0) lm_begin_apply(sS, tot);
+    if constexpr (kLoopCtlWave) {
+        if (threadIdx.x < 64) wv::lm_begin(sS, tot);
+    } else if (threadIdx.x == 0) {
+        lm_begin_apply(sS, tot);
+    }
     __syncthreads();
     const unsigned base = sync[2 * b + 1];
     unsigned nbar = 0;
@@ -1760,7 +1800,11 @@ __global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, u
         ++nbar;
         slot_barrier(&sync[2 * b], base + nbar * (unsigned)nblk, err, spin_limit);
         reduce_coherent(bv, b, pbuf + (i & 1) * nblk, nblk, tot);
-        if (threadIdx.x == 0) lm_step_apply(sS, tot, outer, last);
+        if constexpr (kLoopCtlWave) {
+            if (threadIdx.x < 64) wv::lm_step(sS, tot, outer, last);
+        } else if (threadIdx.x == 0) {
+            lm_step_apply(sS, tot, outer, last);
+        }
         __syncthreads();
     }
     if (nbar == 0) {   // no wait yet: make sure every block has read st before block 0 rewrites it

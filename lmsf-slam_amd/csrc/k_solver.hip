@@ -51,10 +51,11 @@ __global__ void state_init_kernel(BatchView bv, const double* poses) {
 #else
 #define LMSF_CTL_ATTR
 #endif
-// LMSF_CTL_MODE (A/B): the batch control kernels' step computation -- 2: LDS workspace, rolled loops (no
-// scratch within 64 VGPRs); 1: r03's non-inlined call (868 B of scratch); 0: inlined.
+// LMSF_CTL_MODE (A/B): the batch control kernels' step computation -- 3: on the whole wave (lm_control.h wv::);
+// 2: one lane, LDS workspace, rolled loops (no scratch within 64 VGPRs); 1: r03's non-inlined call (868 B of
+// scratch); 0: one lane, inlined.
 #ifndef LMSF_CTL_MODE
-#define LMSF_CTL_MODE 2
+#define LMSF_CTL_MODE 3
 #endif
 constexpr int kCtlMode = LMSF_CTL_MODE;
 __global__ __launch_bounds__(kBeginThreads) LMSF_CTL_ATTR void lm_begin_kernel(BatchView bv) {
@@ -76,7 +77,11 @@ __global__ __launch_bounds__(kBeginThreads) LMSF_CTL_ATTR void lm_begin_kernel(B
     const unsigned long long t1 = wall_clock64();
 #endif
     __shared__ double ws[kStepWs];
-    if (threadIdx.x == 0) lm_begin_apply<kCtlMode>(sS, tot, ws);
+    if constexpr (kCtlMode == 3) {
+        if (threadIdx.x < 64) wv::lm_begin(sS, tot);
+    } else if (threadIdx.x == 0) {
+        lm_begin_apply<kCtlMode>(sS, tot, ws);
+    }
     __syncthreads();
 #ifdef LMSF_STEP_PROFILE
     const unsigned long long t2 = wall_clock64();
@@ -99,7 +104,8 @@ constexpr int kStepThreads = LMSF_STEP_THREADS;
 __global__ __launch_bounds__(kStepThreads) LMSF_CTL_ATTR void lm_step_kernel(BatchView bv, int outer, int is_last) {
     const int b = blockIdx.x;
     SolveState& S = bv.st[b];
-    if (!S.need_eval) {
+    const int need = S.need_eval, nq = bv.n_edge[b] + bv.n_surf[b];   // one round trip
+    if (!need) {
         if (is_last && threadIdx.x == 0) finish_outer(S, outer);
         return;
     }
@@ -108,14 +114,17 @@ __global__ __launch_bounds__(kStepThreads) LMSF_CTL_ATTR void lm_step_kernel(Bat
 #endif
     __shared__ SolveState sS;
     state_copy(sS, S);
-    const int nq = bv.n_edge[b] + bv.n_surf[b];
     __shared__ double tot[kPacket];
     reduce_parts(bv, b, (nq + kEvalBlock - 1) / kEvalBlock, tot);   // ends with a barrier
 #ifdef LMSF_STEP_PROFILE
     const unsigned long long t1 = wall_clock64();
 #endif
     __shared__ double ws[kStepWs];
-    if (threadIdx.x == 0) lm_step_apply<kCtlMode>(sS, tot, outer, is_last, ws);
+    if constexpr (kCtlMode == 3) {
+        if (threadIdx.x < 64) wv::lm_step(sS, tot, outer, is_last);
+    } else if (threadIdx.x == 0) {
+        lm_step_apply<kCtlMode>(sS, tot, outer, is_last, ws);
+    }
     __syncthreads();
 #ifdef LMSF_STEP_PROFILE
     const unsigned long long t2 = wall_clock64();

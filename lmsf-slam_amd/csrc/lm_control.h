@@ -354,6 +354,268 @@ __device__ void finish_outer(SolveState& S, int outer) {
     S.outer_run = outer + 1;
 }
 
+// ---------------------------------------------------------------- wave-cooperative LM control (MODE 3)
+// The one-lane control above is a chain of dependent operations: ~20 us per step in LDS mode (every access an
+// LDS round trip), ~6 us inlined in registers (256 VGPRs).  Here the 64 lanes of one wave share it, each lane
+// doing one element's arithmetic in exactly the one-lane order, so the results are bit-identical:
+//   * lanes 0..20 hold the packed lower triangle (i, j), lidx(i, j) == lane, of H / the scaled system / L;
+//     lanes 0..5 the vectors (s, g, the right-hand side);
+//   * Cholesky right-looking: at column k every element (i, j), j > k, subtracts L_ik L_jk -- the same
+//     subtractions in the same (ascending k) order as the left-looking loops of chol_solve6; the forward
+//     substitution column by column (again ascending k per element); the back substitution (descending rows,
+//     ascending k inside a row) on broadcast values;
+//   * the Plus of the gradient check (lanes 0..31, at -g) and of the candidate (lanes 32..63, at the step)
+//     evaluated side by side in one pass of pose_plus.
+// Uniform values are broadcast with readlane (scalar registers), per-lane gathers with ds_bpermute.
+namespace wv {
+__device__ __forceinline__ double bcast(double v, int src) {   // src: wave-uniform lane index
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, src);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), src);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double gather(double v, int src) { return __shfl(v, src & 63, 64); }
+__device__ __forceinline__ int tri_row(int l) { return (l >= 1) + (l >= 3) + (l >= 6) + (l >= 10) + (l >= 15); }
+struct Ctl { double radius, decrease; int iteration; };
+
+// compute_step_body on the wave.  h: this lane's H(i, j) (triangle lanes), sv / gv: s / g of this lane (lanes
+// < 6).  True: a candidate step delta (uniform) with model cost change mcc; false: terminated with term.
+__device__ __forceinline__ bool compute_step(double h, double sv, double gv, Ctl& c, double delta[6], double& mcc,
+                                             int& term) {
+    const int lane = __lane_id();
+    const bool tri = lane < 21, vec = lane < 6;
+    const int ti = tri_row(lane), tj = tri ? lane - ti * (ti + 1) / 2 : 63;
+    const double hs = h * gather(sv, ti) * gather(sv, tj);   // Hs = D H D: (H s_i) s_j
+    const double gs = gv * sv;
+    while (true) {
+        if (c.iteration >= kMaxInner) { term = LMSF_TERM_MAX_ITERATIONS; return false; }
+        if (c.radius < 1e-32) { term = LMSF_TERM_PARAMETER_TOL; return false; }
+        ++c.iteration;
+        double a = hs;
+        if (tri && ti == tj) a = hs + fmin(fmax(hs, 1e-6), 1e32) / c.radius;
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const double piv = bcast(a, lidx(k, k));
+            if (!(piv > 0.0)) { ok = false; break; }
+            const double lkk = sqrt(piv);
+            if (lane == lidx(k, k)) a = lkk;
+            else if (tri && tj == k && ti > k) a = a / lkk;
+            const double lik = gather(a, lidx(ti, k)), ljk = gather(a, tri ? lidx(tj, k) : 0);
+            if (tri && tj > k) a = a - lik * ljk;
+        }
+        double st[6];
+        if (ok) {
+            double t = -gs, y[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                y[k] = bcast(t, k) / bcast(a, lidx(k, k));
+                const double lvk = gather(a, vec ? lidx(lane, k) : 0);
+                if (vec && lane > k) t = t - lvk * y[k];
+            }
+#pragma unroll
+            for (int i = 5; i >= 0; --i) {
+                double u = y[i];
+#pragma unroll
+                for (int k = i + 1; k < 6; ++k) u -= bcast(a, lidx(k, i)) * st[k];
+                st[i] = u / bcast(a, lidx(i, i));
+            }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) ok = ok && isfinite(st[i]);
+        }
+        mcc = 0.0;
+        if (ok) {
+            double t = 0.0;   // lane i: sum_j ((H_ij s_i) s_j) step_j
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int r = lane > j ? lane : j, q = lane > j ? j : lane;
+                t += gather(h, vec ? lidx(r, q) : 0) * sv * bcast(sv, j) * st[j];
+            }
+            double sg = 0.0, sHs = 0.0;   // the products step_i gs_i, step_i t_i on broadcast values, in i order
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                sg += st[i] * bcast(gs, i);
+                sHs += st[i] * bcast(t, i);
+            }
+            mcc = -(sg + 0.5 * sHs);
+        }
+        if (!ok || !(mcc > 0.0)) {   // StepIsInvalid == StepRejected(0)
+            c.radius = c.radius / c.decrease;
+            c.decrease *= 2.0;
+            continue;
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) delta[i] = st[i] * bcast(sv, i);
+        return true;
+    }
+}
+
+// The gradient check (if check_grad: max |x - Plus(x, -g)| <= 1e-10 ends the solve) and, unless it ends it,
+// the next step -- IterationZero's / HandleSuccessfulStep's tail and StepRejected's re-step.  Updates S's
+// control fields from lane 0 (the caller writes nothing else of them afterwards).
+__device__ __forceinline__ void grad_then_step(SolveState& S, bool check_grad, const double x[7], double h, double sv,
+                                               double gv, Ctl c) {
+    const int lane = __lane_id();
+    double delta[6] = {0, 0, 0, 0, 0, 0}, mcc = 0.0;
+    int term = 0;
+    Ctl cs = c;
+    const bool stepped = compute_step(h, sv, gv, cs, delta, mcc, term);
+    double xo[7];
+    double m = 0.0;
+    if (check_grad || stepped) {
+        double d[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) d[i] = lane < 32 ? -bcast(gv, i) : delta[i];
+        pose_plus_inl(x, d, xo);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) m = fmax(m, fabs(x[i] - xo[i]));
+        m = bcast(m, 0);
+    }
+    if (check_grad && m <= 1e-10) {
+        if (lane == 0) { S.done = 1; S.term = LMSF_TERM_GRADIENT_TOL; }
+        return;
+    }
+    if (lane == 0) {
+        S.radius = cs.radius;
+        S.decrease = cs.decrease;
+        S.iteration = cs.iteration;
+        if (!stepped) {
+            S.done = 1;
+            S.term = term;
+        } else {
+            S.mcc = mcc;
+            S.need_eval = 1;
+        }
+    }
+    if (stepped && lane == 32) {
+#pragma unroll
+        for (int i = 0; i < 7; ++i) S.xc[i] = xo[i];
+    }
+}
+
+__device__ __forceinline__ double norm7u(const double* x) {   // norm7 of uniform values
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) s += x[i] * x[i];
+    return sqrt(s);
+}
+
+// lm_step_apply on the wave (S, tot in LDS; all 64 lanes of one wave call it).
+__device__ __forceinline__ void lm_step(SolveState& S, const double* tot, int outer, int is_last) {
+    const int lane = __lane_id();
+    const bool tri = lane < 21, vec = lane < 6;
+    const int ti = tri_row(lane), tj = tri ? lane - ti * (ti + 1) / 2 : 0;
+    double x[7], xc[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) { x[i] = S.x[i]; xc[i] = S.xc[i]; }
+    const double cost = S.cost, mcc = S.mcc, x_norm = S.x_norm;
+    Ctl c{S.radius, S.decrease, S.iteration};
+    const int evals = S.evals + 1;
+    double h = tri ? S.H[hidx(tj, ti)] : 0.0;
+    double sv = vec ? S.s[lane] : 0.0, gv = vec ? S.g[lane] : 0.0;
+    const double tot_h = tri ? tot[1 + hidx(tj, ti)] : 0.0, tot_g = vec ? tot[22 + lane] : 0.0;
+    const double cost_c = isfinite(tot[0]) ? tot[0] : 1.7976931348623157e308;
+    double dx[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) dx[i] = x[i] - xc[i];
+    if (lane == 0) { S.need_eval = 0; S.evals = evals; }
+    bool done = false;
+    int term = 0;
+    if (norm7u(dx) <= 1e-8 * (x_norm + 1e-8)) {
+        done = true;
+        term = LMSF_TERM_PARAMETER_TOL;
+    } else {
+        const double cost_change = cost - cost_c;
+        if (fabs(cost_change) <= 1e-6 * cost) {
+            done = true;
+            term = LMSF_TERM_FUNCTION_TOL;
+        } else {
+            const double rel = cost_change / mcc;
+            if (rel > 1e-3) {
+                const double f = 1.0 - cube_rn(2.0 * rel - 1.0);
+                c.radius = c.radius / fmax(1.0 / 3.0, f);
+                c.radius = fmin(1e16, c.radius);
+                c.decrease = 2.0;
+#pragma unroll
+                for (int i = 0; i < 7; ++i) x[i] = xc[i];
+                h = tot_h;
+                gv = tot_g;
+                if (lane == 0) {
+#pragma unroll
+                    for (int i = 0; i < 7; ++i) S.x[i] = x[i];
+                    S.x_norm = norm7u(x);
+                    S.cost = cost_c;
+                    S.radius = c.radius;
+                    S.decrease = c.decrease;
+                }
+                if (tri) S.H[hidx(tj, ti)] = h;
+                if (vec) S.g[lane] = gv;
+                if (c.iteration >= kMaxInner) {
+                    done = true;
+                    term = LMSF_TERM_MAX_ITERATIONS;
+                } else {
+                    grad_then_step(S, true, x, h, sv, gv, c);
+                }
+            } else {
+                c.radius = c.radius / c.decrease;
+                c.decrease *= 2.0;
+                grad_then_step(S, false, x, h, sv, gv, c);
+            }
+        }
+    }
+    if (lane == 0) {
+        if (done) { S.done = 1; S.term = term; }
+        if (is_last) {
+            const int it = S.iteration;   // lane 0 wrote it in grad_then_step (same lane: program order)
+            if (outer < kMaxOuter)
+#pragma unroll
+                for (int i = 0; i < 7; ++i) S.trace[outer][i] = x[i];
+            S.inner_total += it;
+            S.evals_total += evals;
+            S.outer_run = outer + 1;
+        }
+    }
+}
+
+// lm_begin_apply on the wave.
+__device__ __forceinline__ void lm_begin(SolveState& S, const double* tot) {
+    const int lane = __lane_id();
+    const bool tri = lane < 21, vec = lane < 6;
+    const int ti = tri_row(lane), tj = tri ? lane - ti * (ti + 1) / 2 : 0;
+    const double h = tri ? tot[1 + hidx(tj, ti)] : 0.0, gv = vec ? tot[22 + lane] : 0.0;
+    const double hjj = vec ? tot[1 + hidx(lane, lane)] : 0.0;
+    const int nmatch = (int)tot[28];
+    double x[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) x[i] = S.x[i];
+    if (lane == 0) {
+        S.iteration = 0;
+        S.need_eval = 0;
+        S.done = 0;
+        S.evals = 1;
+        S.nmatch = nmatch;
+        S.edge_matches = (int)tot[29];
+        S.surf_matches = (int)tot[30];
+        S.cost = tot[0];
+        S.initial_cost = tot[0];
+    }
+    if (tri) S.H[hidx(tj, ti)] = h;
+    if (vec) S.g[lane] = gv;
+    if (nmatch == 0) {
+        if (lane == 0) { S.done = 1; S.term = LMSF_TERM_NO_RESIDUALS; }
+        return;
+    }
+    const double sv = vec ? 1.0 / (1.0 + sqrt(hjj)) : 0.0;
+    if (vec) S.s[lane] = sv;
+    if (lane == 0) {
+        S.radius = 1e4;
+        S.decrease = 2.0;
+        S.x_norm = norm7u(x);
+    }
+    grad_then_step(S, true, x, h, sv, gv, Ctl{1e4, 2.0, 0});
+}
+}  // namespace wv
+
 
 // lm_step after the evaluation at the candidate (tot = its reduced packet): step acceptance
 // (ParameterToleranceReached, FunctionToleranceReached, IsStepSuccessful, HandleSuccessfulStep /
