@@ -65,14 +65,13 @@ __global__ __launch_bounds__(kBeginThreads) LMSF_CTL_ATTR void lm_begin_kernel(B
     const unsigned long long t0 = wall_clock64();
 #endif
     __shared__ SolveState sS;
-    state_copy(sS, bv.st[b]);
     __shared__ double tot[kPacket];
     if (bv.fused_parts) {   // fused path: the memo pass's wave packets (when it ran), then the search's
-        reduce_parts(bv, b, bv.memo ? (nq + 63) / 64 : 0, tot, bv.part2_base, (bv.n_search[b] + 63) / 64);
+        reduce_parts(bv, b, bv.memo ? (nq + 63) / 64 : 0, tot, bv.part2_base, (bv.n_search[b] + 63) / 64, &bv.st[b], &sS);
     } else {
         const int fb = bv.part_q;
-        reduce_parts(bv, b, (nq + fb - 1) / fb, tot);
-    }   // (reduce_parts ends with a barrier: sS is in place)
+        reduce_parts(bv, b, (nq + fb - 1) / fb, tot, 0, 0, &bv.st[b], &sS);
+    }   // (reduce_parts stages sS and ends with a barrier)
 #ifdef LMSF_STEP_PROFILE
     const unsigned long long t1 = wall_clock64();
 #endif
@@ -101,7 +100,13 @@ __global__ __launch_bounds__(kBeginThreads) LMSF_CTL_ATTR void lm_begin_kernel(B
 #define LMSF_STEP_THREADS 64
 #endif
 constexpr int kStepThreads = LMSF_STEP_THREADS;
-__global__ __launch_bounds__(kStepThreads) LMSF_CTL_ATTR void lm_step_kernel(BatchView bv, int outer, int is_last) {
+// LMSF_STEP_RED_U: packet loads in flight per lane in lm_step's reduction (one wave: 61 packets per C2 slot, so 16
+// takes two batches where 8 took four)
+#ifndef LMSF_STEP_RED_U
+#define LMSF_STEP_RED_U 16
+#endif
+constexpr int kStepRedU = LMSF_STEP_RED_U;
+__global__ __launch_bounds__(kStepThreads) void lm_step_kernel(BatchView bv, int outer, int is_last) {
     const int b = blockIdx.x;
     SolveState& S = bv.st[b];
     const int need = S.need_eval, nq = bv.n_edge[b] + bv.n_surf[b];   // one round trip
@@ -113,9 +118,9 @@ __global__ __launch_bounds__(kStepThreads) LMSF_CTL_ATTR void lm_step_kernel(Bat
     const unsigned long long t0 = wall_clock64();
 #endif
     __shared__ SolveState sS;
-    state_copy(sS, S);
     __shared__ double tot[kPacket];
-    reduce_parts(bv, b, (nq + kEvalBlock - 1) / kEvalBlock, tot);   // ends with a barrier
+    // the state's copy into LDS rides with the packet loads; ends with a barrier
+    reduce_parts<kStepRedU>(bv, b, (nq + kEvalBlock - 1) / kEvalBlock, tot, 0, 0, &S, &sS);
 #ifdef LMSF_STEP_PROFILE
     const unsigned long long t1 = wall_clock64();
 #endif

@@ -21,25 +21,56 @@ constexpr int kMaxInner = 4;  // options.max_num_iterations (ceres_...:118)
 // loads are coalesced and 8 per lane in flight, the two halves add in one shuffle and the waves'
 // sums in wave order through LDS.  Every wave of the block loads (lm_begin: kBeginThreads, 1.5k
 // packets per slot at C2 -- one wave took 60 us, latency-bound).
-__device__ void reduce_parts(const BatchView& bv, int b, int nparts, double* tot, int base2 = 0, int n2 = 0) {
+// U: loads in flight per lane per batch.  stage_src / stage_dst: the slot's SolveState copied into LDS by the same
+// pass, its loads issued ahead of the packet loads (one round trip for both; valid after the closing barrier).
+template <int U = 8>
+__device__ void reduce_parts(const BatchView& bv, int b, int nparts, double* tot, int base2 = 0, int n2 = 0,
+                             const SolveState* stage_src = nullptr, SolveState* stage_dst = nullptr) {
     static_assert(kPacket == 32, "one packet entry per half-wave lane");
     constexpr int kMaxWaves = 16;
+    constexpr int kWords = (int)(sizeof(SolveState) / 8);
+    constexpr int kStage = 6;   // words per thread (64-thread blocks: sizeof(SolveState) <= 3 KB)
+    static_assert(kWords <= 64 * kStage, "SolveState staged by at least one wave");
     __shared__ double red[kMaxWaves][kPacket];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 31;
+    long long sw[kStage];
+    if (stage_src) {
+        const long long* src = reinterpret_cast<const long long*>(stage_src);
+#pragma unroll
+        for (int j = 0; j < kStage; ++j) {
+            const int i = threadIdx.x + j * (int)blockDim.x;
+            sw[j] = i < kWords ? src[i] : 0;
+        }
+    }
     const int nw = min((int)(blockDim.x >> 6), kMaxWaves);
     const int stride = 2 * nw;   // a wave reads two packets per load (one per half-wave)
-    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = 0.0;
     for (int range = 0; range < 2 && wave < nw; ++range) {   // every thread reaches the barrier
         const int np = range ? n2 : nparts;
         const double* base = bv.partials + ((size_t)b * bv.max_parts + (range ? base2 : 0)) * kPacket;
         int p = 2 * wave + (lane >> 5);
-        for (; p + 7 * stride < np; p += 8 * stride) {   // 8 independent loads in flight per lane
+        for (; p + (U - 1) * stride < np; p += U * stride) {   // U independent loads in flight per lane
 #pragma unroll
-            for (int u = 0; u < 8; ++u) acc[u] += base[(size_t)(p + u * stride) * kPacket + e];
+            for (int u = 0; u < U; ++u) acc[u] += base[(size_t)(p + u * stride) * kPacket + e];
         }
         for (; p < np; p += stride) acc[0] += base[(size_t)p * kPacket + e];
     }
-    double v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    if (stage_src) {
+        long long* dst = reinterpret_cast<long long*>(stage_dst);
+#pragma unroll
+        for (int j = 0; j < kStage; ++j) {
+            const int i = threadIdx.x + j * (int)blockDim.x;
+            if (i < kWords) dst[i] = sw[j];
+        }
+    }
+    // pairwise tree over the U accumulators (U = 8: ((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7)))
+#pragma unroll
+    for (int h = 1; h < U; h *= 2)
+#pragma unroll
+        for (int u = 0; u + h < U; u += 2 * h) acc[u] = acc[u] + acc[u + h];
+    double v = acc[0];
     v += __shfl_xor(v, 32, 64);
     if (lane < 32 && wave < nw) red[wave][e] = v;
     __syncthreads();
