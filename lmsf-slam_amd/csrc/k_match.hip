@@ -1373,52 +1373,15 @@ __device__ __forceinline__ void key_insert(double (&k)[5], double x) {
     }
 }
 
-// One row's candidates [a, a + len) of pts into the kept 5 keys k.  LMSF_DENSE_DEFER: per chunk of U candidates only
-// those with d2 <= the chunk-start 5th key's d2 enter the network, one per lane per step while any lane has one
-// left (a candidate beyond the 5th key at any time can never be kept: the 5th only decreases, and keys are totally
-// ordered, so the kept 5 are the same).  On C5's first pass most scanned candidates lie outside the query's 5-NN
-// ball, where the network's 9 f64 min / max per candidate are half of the loop's VALU.
-#ifndef LMSF_DENSE_DEFER
-#define LMSF_DENSE_DEFER 0
-#endif
-#ifndef LMSF_DEFER_U
-#define LMSF_DEFER_U 8
-#endif
+// One row's candidates [a, a + len) of pts into the kept 5 keys k.
 __device__ __forceinline__ void dense_run(double (&k)[5], const float4* __restrict__ rp, uint32_t a, uint32_t len, const float3 w) {
     uint32_t c = 0;
-    if constexpr (LMSF_DENSE_DEFER) {
-        constexpr int U = LMSF_DEFER_U;
-        for (; c + U <= len; c += U) {
-            float4 m[U];
+    for (; c + LMSF_FUSED_UNROLL <= len; c += LMSF_FUSED_UNROLL) {
+        float4 m[LMSF_FUSED_UNROLL];
 #pragma unroll
-            for (int u = 0; u < U; ++u) m[u] = rp[a + c + u];
-            const uint32_t b4 = (uint32_t)(key_bits(k[4]) >> 32);
-            double kk[U];
-            unsigned hm = 0;
+        for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) m[u] = rp[a + c + u];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                kk[u] = nn_key(w, m[u], (uint32_t)__float_as_int(m[u].w));
-                if ((uint32_t)(key_bits(kk[u]) >> 32) <= b4) hm |= 1u << u;
-            }
-            while (__ballot(hm != 0u)) {
-                if (hm) {
-                    const int j = __builtin_ctz(hm);
-                    hm &= hm - 1u;
-                    double x = kk[0];
-#pragma unroll
-                    for (int u = 1; u < U; ++u) x = j == u ? kk[u] : x;
-                    key_insert(k, x);
-                }
-            }
-        }
-    } else {
-        for (; c + LMSF_FUSED_UNROLL <= len; c += LMSF_FUSED_UNROLL) {
-            float4 m[LMSF_FUSED_UNROLL];
-#pragma unroll
-            for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) m[u] = rp[a + c + u];
-#pragma unroll
-            for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) key_insert(k, nn_key(w, m[u], (uint32_t)__float_as_int(m[u].w)));
-        }
+        for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) key_insert(k, nn_key(w, m[u], (uint32_t)__float_as_int(m[u].w)));
     }
     for (; c < len; ++c) {
         const float4 m = rp[a + c];
@@ -1523,30 +1486,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
 constexpr int kRing5[25][2] = {{0, 0},  {0, -1}, {-1, 0}, {1, 0},  {0, 1},  {-1, -1}, {1, -1}, {-1, 1}, {1, 1},
                                {0, -2}, {-2, 0}, {2, 0},  {0, 2},  {-1, -2}, {1, -2}, {-2, -1}, {2, -1}, {-2, 1},
                                {2, 1},  {-1, 2}, {1, 2},  {-2, -2}, {2, -2}, {-2, 2}, {2, 2}};
-// kRing5 / kDenseRowOrder as nibble-packed literals: a row's (dy, dz) from shifts of wave-uniform constants, not a
-// scalar load and wait per row
-constexpr uint64_t ring5_nib(int which, int half) {
-    uint64_t v = 0;
-    for (int j = 0; j < 16; ++j)
-        if (half * 16 + j < 25) v |= (uint64_t)(kRing5[half * 16 + j][which] + 2) << (4 * j);
-    return v;
-}
-constexpr uint64_t row9_nib(int which) {
-    uint64_t v = 0;
-    for (int j = 0; j < 9; ++j) v |= (uint64_t)(which ? kDenseRowOrder[j] / 3 : kDenseRowOrder[j] % 3) << (4 * j);
-    return v;
-}
-__device__ __forceinline__ int ring5_at(int which, int i) {
-    const uint64_t lo = which ? ring5_nib(1, 0) : ring5_nib(0, 0), hi = which ? ring5_nib(1, 1) : ring5_nib(0, 1);
-    return (int)(((i < 16 ? lo >> (4 * i) : hi >> (4 * (i - 16)))) & 15u) - 2;
-}
-__device__ __forceinline__ int ring5_dy(int i) { return ring5_at(0, i); }
-__device__ __forceinline__ int ring5_dz(int i) { return ring5_at(1, i); }
-__device__ __forceinline__ int row9_dy(int i) { return (int)((row9_nib(0) >> (4 * i)) & 15u) - 1; }
-__device__ __forceinline__ int row9_dz(int i) { return (int)((row9_nib(1) >> (4 * i)) & 15u) - 1; }
-#ifndef LMSF_P2_PIPE
-#define LMSF_P2_PIPE 0
-#endif
 #ifndef LMSF_PASS2_FINE
 #define LMSF_PASS2_FINE 1
 #endif
@@ -1575,48 +1514,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
         const int nrows = fine ? 25 : 9;
         const DenseQuery<2> dq(g, w);   // the 1 m grid's 3 x 3 rows are its inner ring
         const int xa = dq.xa, xb = dq.xb;
-        // the next row (from i) that may hold a point within bound d4: its run [a, a + len) of pts, and its gap lb
-        auto next_row = [&](int& i, float d4, uint32_t& a, uint32_t& len, float& lbr) -> bool {
 #pragma unroll 1
-            for (; i < nrows; ++i) {
-                const uint32_t* row;
-                int sa, sb;
-                const int dyo = fine ? ring5_dy(i) : row9_dy(i), dzo = fine ? ring5_dz(i) : row9_dz(i);
-                const float lb = dq.lb(dyo, dzo);
-                if (lb > d4) continue;   // ahead of the row's address and offsets
-                if (!dq.row(g, dyo, dzo, row)) continue;
-                dense_window(g, w, d4 * kDenseCull, lb, xa, xb, sa, sb);
-                if (sa > sb) continue;
-                a = row[sa];
-                len = row[sb + 1] - a;
-                lbr = lb;
-                ++i;
-                return true;
-            }
-            return false;
-        };
-        int i = 0;
-        uint32_t a = 0, len = 0;
-        float lbr = 0.f;
-        bool have = next_row(i, bound, a, len, lbr);
-        if constexpr (LMSF_P2_PIPE) {
-            // the next row's offsets in flight while this row's candidates are walked (its window, from the bound
-            // before this row, is a superset of the one after it: exact); a row the walk moved past is dropped
-            while (have) {
-                uint32_t a2 = 0, len2 = 0;
-                float lb2 = 0.f;
-                const bool have2 = next_row(i, fminf(bound, key_d2(k[4])), a2, len2, lb2);
-                dense_run(k, rp, a, len, w);
-                a = a2;
-                len = len2;
-                have = have2;
-                while (have && lb2 > fminf(bound, key_d2(k[4]))) have = next_row(i, fminf(bound, key_d2(k[4])), a, len, lb2);
-            }
-        } else {
-            while (have) {
-                dense_run(k, rp, a, len, w);
-                have = next_row(i, fminf(bound, key_d2(k[4])), a, len, lbr);
-            }
+        for (int i = 0; i < nrows; ++i) {
+            const float d4 = fminf(bound, key_d2(k[4]));
+            const uint32_t* row;
+            int sa, sb;
+            const int dyo = fine ? kRing5[i][0] : (kDenseRowOrder[i] % 3) - 1;
+            const int dzo = fine ? kRing5[i][1] : (kDenseRowOrder[i] / 3) - 1;
+            const float lb = dq.lb(dyo, dzo);
+            if (lb > d4) continue;   // ahead of the row's address and offsets
+            if (!dq.row(g, dyo, dzo, row)) continue;
+            dense_window(g, w, d4 * kDenseCull, lb, xa, xb, sa, sb);
+            if (sa > sb) continue;
+            const uint32_t a = row[sa];
+            dense_run(k, rp, a, row[sb + 1] - a, w);
         }
         dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);
     }
