@@ -17,9 +17,10 @@ case $CFG in
   C5) PMC_ARGS="--steps 1 --warmup 1 --streams 1" ;;
   *)  PMC_ARGS="--steps 6 --warmup 2" ;;
 esac
+PMC_ARGS="$PMC_ARGS ${PMC_EXTRA:-}"   # e.g. C3 / C4: --opt LM_LOOP=0 --no-prefetch (the r04 C3 PMC pass faulted with both on)
 for ctr in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES" "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_CVT GRBM_GUI_ACTIVE"; do
   tag=$(echo $ctr | cut -d' ' -f1)
-  timeout -s KILL 300 rocprofv3 --pmc $ctr --kernel-trace -d "$O/pmc_$tag" -o pmc --output-format csv -- python3 "$R/bench.py" --config $CFG --no-cpu --no-n27 --h2d off $PMC_ARGS > "$O/pmc_$tag.json" 2> "$O/pmc_$tag.err"
+  timeout -s KILL ${PMC_TIMEOUT:-300} rocprofv3 --pmc $ctr --kernel-trace -d "$O/pmc_$tag" -o pmc --output-format csv -- python3 "$R/bench.py" --config $CFG --no-cpu --no-n27 --h2d off $PMC_ARGS > "$O/pmc_$tag.json" 2> "$O/pmc_$tag.err"
   rc=$?; echo "pmc $CFG $tag rc=$rc"; case $rc in 0) ;; *) exit $rc;; esac
 done
 echo profiles-done
