@@ -50,12 +50,15 @@ __device__ void reduce_parts(const BatchView& bv, int b, int nparts, double* tot
     for (int range = 0; range < 2 && wave < nw; ++range) {   // every thread reaches the barrier
         const int np = range ? n2 : nparts;
         const double* base = bv.partials + ((size_t)b * bv.max_parts + (range ? base2 : 0)) * kPacket;
-        int p = 2 * wave + (lane >> 5);
-        for (; p + (U - 1) * stride < np; p += U * stride) {   // U independent loads in flight per lane
+        // U independent loads in flight per lane, the last batch predicated (a tail of one load per round trip
+        // took 7 of lm_step's 11 round trips at C2's 61 packets per slot)
+        for (int p = 2 * wave + (lane >> 5); p < np; p += U * stride) {
+            double v[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc[u] += base[(size_t)(p + u * stride) * kPacket + e];
+            for (int u = 0; u < U; ++u) v[u] = p + u * stride < np ? base[(size_t)(p + u * stride) * kPacket + e] : 0.0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u] += v[u];
         }
-        for (; p < np; p += stride) acc[0] += base[(size_t)p * kPacket + e];
     }
     if (stage_src) {
         long long* dst = reinterpret_cast<long long*>(stage_dst);
