@@ -1032,7 +1032,7 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->n_surf, B));
     CHK(dalloc(&c->nnp, B * F * 5));
     CHK(dalloc(&c->prevw, B * F));
-    CHK(dalloc(&c->memo_nbr, B * kMemoWords * F));
+    CHK(dalloc(&c->memo_nbr, B * kMemoStride * F));
     CHK(dalloc(&c->wl, B * F));
     CHK(dalloc(&c->wlim, B * F));
     CHK(dalloc(&c->wcount, B * (F / 256 + 1)));

@@ -105,6 +105,16 @@ __device__ __forceinline__ void block_coords(int remap, int gx, int& x, int& b) 
     x = logical - b * gx;
 }
 
+// LMSF_MEMO_AOS: a search position's 7 memo words in one 32-B record ([B][F][8]) instead of 7 planes ([B][7][F]):
+// the listed search writes one partial line per query instead of seven, the memo pass reads it in two 16-B loads
+#ifndef LMSF_MEMO_AOS
+#define LMSF_MEMO_AOS 1
+#endif
+constexpr bool kMemoAos = LMSF_MEMO_AOS != 0;
+__device__ __forceinline__ size_t memo_idx(size_t b, int j, size_t i, size_t F) {
+    return kMemoAos ? (b * F + i) * kMemoStride + j : (b * kMemoWords + j) * F + i;
+}
+
 // Field-wise select of two grids: a runtime-selected GridView reference (or a select of whole
 // structs) makes the compiler spill the kernel arguments to scratch.
 __device__ __forceinline__ GridView pick_grid(bool c, const GridView& a, const GridView& b) {
@@ -477,7 +487,7 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
             if (pw.w >= 0.f) {
                 const double dx = (double)w.x - pw.x, dy = (double)w.y - pw.y, dz = (double)w.z - pw.z;
                 const double dd = sqrt(dx * dx + dy * dy + dz * dz);
-                const double s6 = (double)__int_as_float(bv.memo_nbr[((size_t)b * kMemoWords + 5) * bv.feat_stride + q]);
+                const double s6 = (double)__int_as_float(bv.memo_nbr[memo_idx(b, 5, q, bv.feat_stride)]);
                 const double r6 = s6 + dd + 1e-5;
                 if (r6 < 1.0 && bv.memo_bound) lim = fminf(kFullLim, (float)(r6 * r6) + 1e-5f);
                 double k5[5];
@@ -553,7 +563,7 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
                 if (key_bits(res[4]) < kSentinel) {
                     const double s6 = sqrt((double)fminf(key_d2(res[NK - 1]), 1.0f));
                     gap = (float)(s6 - sqrt((double)key_d2(res[4])));
-                    bv.memo_nbr[((size_t)b * kMemoWords + 5) * bv.feat_stride + q] = __float_as_int((float)s6);
+                    bv.memo_nbr[memo_idx(b, 5, q, bv.feat_stride)] = __float_as_int((float)s6);
                 }
                 bv.prevw[slot] = make_float4(w.x, w.y, w.z, gap);
             }
@@ -854,6 +864,13 @@ constexpr bool kLinEval = LMSF_LIN_EVAL != 0;
 
 // Entries of one memo block's work list per scan: wcount stride.
 __host__ __device__ __forceinline__ size_t memo_blocks(size_t feat_stride) { return feat_stride / 256 + 1; }
+// LMSF_LIST_ATOMIC: the memo pass lists a scan's searches / refits by wave atomics into one list per scan (needs the
+// linearisation pass: the search kernel then forms no packets, so entry order is free); 0: per-block segments in
+// position order, found by the search kernel through a prefix scan of the block counts (r02-r03).
+#ifndef LMSF_LIST_ATOMIC
+#define LMSF_LIST_ATOMIC 1
+#endif
+constexpr bool kListAtomic = kLinEval && LMSF_LIST_ATOMIC != 0;
 
 #ifndef LMSF_MEMO_WAVES   // waves per SIMD the memo pass is compiled for (A/B)
 #define LMSF_MEMO_WAVES 5
@@ -898,8 +915,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_W
         // everything the position may need, in flight together (the pass is latency-bound: one round trip
         // for the state instead of three dependent ones -- memo words, then the record)
         int mw[7];
+        if constexpr (kMemoAos) {
+            const int4 m0 = *reinterpret_cast<const int4*>(bv.memo_nbr + memo_idx(b, 0, i, F));
+            const int4 m1 = *reinterpret_cast<const int4*>(bv.memo_nbr + memo_idx(b, 4, i, F));
+            mw[0] = m0.x; mw[1] = m0.y; mw[2] = m0.z; mw[3] = m0.w; mw[4] = m1.x; mw[5] = m1.y; mw[6] = m1.z;
+        } else {
 #pragma unroll
-        for (int j = 0; j < 7; ++j) mw[j] = bv.memo_nbr[((size_t)b * kMemoWords + j) * F + i];
+            for (int j = 0; j < 7; ++j) mw[j] = bv.memo_nbr[memo_idx(b, j, i, F)];
+        }
         const float4 rp = bv.rec_p[pos];
         const RecV rv = bv.rec_v[pos];
         if (q >= 0 && q < nq && pw.w >= 0.f) {
@@ -937,8 +960,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_W
                 if (refit) {   // the set's new order is what a search would return: keep it for the fit
 #pragma unroll
                     for (int j = 0; j < 5; ++j)
-                        bv.memo_nbr[((size_t)b * kMemoWords + j) * F + i] = (int)(uint32_t)key_bits(k[j]);
-                    bv.memo_nbr[((size_t)b * kMemoWords + 6) * F + i] = __float_as_int(-1.f);   // gaps are w0's order
+                        bv.memo_nbr[memo_idx(b, j, i, F)] = (int)(uint32_t)key_bits(k[j]);
+                    bv.memo_nbr[memo_idx(b, 6, i, F)] = __float_as_int(-1.f);   // gaps are w0's order
                     need = false;
                     n_refit = 1;
                 }
@@ -982,33 +1005,65 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_W
     }
     if (!kLinEval && bx * 256 + wave * 64 < nq)
         wave_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + (size_t)bx * 4 + wave) * kPacket);
-    // this block's positions still needing a search, in position order from the front of its segment,
-    // and those needing only a refit, in position order from its back (deterministic)
     const unsigned long long m = __ballot(need), mr = __ballot(refit);
-    if (lane == 0) {
-        wcnt[wave] = __popcll(m);
-        wcnt[4 + wave] = __popcll(mr);
-    }
-    __syncthreads();
-    int before = 0, total = 0, before_r = 0, total_r = 0;
-#pragma unroll
-    for (int w4 = 0; w4 < 4; ++w4) {
-        before += w4 < wave ? wcnt[w4] : 0;
-        total += wcnt[w4];
-        before_r += w4 < wave ? wcnt[4 + w4] : 0;
-        total_r += wcnt[4 + w4];
-    }
     const unsigned long long below = (1ull << lane) - 1ull;
-    if (need) {
-        const size_t at = (size_t)b * F + (size_t)bx * 256 + before + __popcll(m & below);
-        bv.wl[at] = i;
-        bv.wlim[at] = lim;
+    if constexpr (kListAtomic) {
+        // the scan's searches from the front of its list and its refits from the back, a block's entries placed by
+        // one atomic each (counters at wcount[b * memo_blocks(F) + 0 / 1], zeroed before the pass): no block counts
+        // for the search kernel to scan, and the entry order does not matter -- no packets downstream.  (One
+        // atomic per wave on the scan's counter serialised ~970 waves per address: memo pass 310 vs 201 us.)
+        __shared__ int wbase[2];
+        if (lane == 0) {
+            wcnt[wave] = __popcll(m);
+            wcnt[4 + wave] = __popcll(mr);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int* cnt = bv.wcount + (size_t)b * memo_blocks(F);
+            const int ts = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3], tr = wcnt[4] + wcnt[5] + wcnt[6] + wcnt[7];
+            wbase[0] = ts ? atomicAdd(cnt, ts) : 0;
+            wbase[1] = tr ? atomicAdd(cnt + 1, tr) : 0;
+        }
+        __syncthreads();
+        int before = wbase[0], before_r = wbase[1];
+#pragma unroll
+        for (int w4 = 0; w4 < 4; ++w4) {
+            before += w4 < wave ? wcnt[w4] : 0;
+            before_r += w4 < wave ? wcnt[4 + w4] : 0;
+        }
+        if (need) {
+            const size_t at = (size_t)b * F + before + __popcll(m & below);
+            bv.wl[at] = i;
+            bv.wlim[at] = lim;
+        }
+        if (refit) bv.wl[(size_t)b * F + F - 1 - (before_r + __popcll(mr & below))] = i;
+    } else {
+        // this block's positions still needing a search, in position order from the front of its segment,
+        // and those needing only a refit, in position order from its back (deterministic)
+        if (lane == 0) {
+            wcnt[wave] = __popcll(m);
+            wcnt[4 + wave] = __popcll(mr);
+        }
+        __syncthreads();
+        int before = 0, total = 0, before_r = 0, total_r = 0;
+#pragma unroll
+        for (int w4 = 0; w4 < 4; ++w4) {
+            before += w4 < wave ? wcnt[w4] : 0;
+            total += wcnt[w4];
+            before_r += w4 < wave ? wcnt[4 + w4] : 0;
+            total_r += wcnt[4 + w4];
+        }
+        if (need) {
+            const size_t at = (size_t)b * F + (size_t)bx * 256 + before + __popcll(m & below);
+            bv.wl[at] = i;
+            bv.wlim[at] = lim;
+        }
+        if (refit) {
+            const int seg = min(256, nq - bx * 256);
+            bv.wl[(size_t)b * F + (size_t)bx * 256 + seg - 1 - (before_r + __popcll(mr & below))] = i;
+        }
+        if (threadIdx.x == 0) bv.wcount[(size_t)b * memo_blocks(F) + bx] = total | (total_r << 16);
     }
-    if (refit) {
-        const int seg = min(256, nq - bx * 256);
-        bv.wl[(size_t)b * F + (size_t)bx * 256 + seg - 1 - (before_r + __popcll(mr & below))] = i;
-    }
-    if (threadIdx.x == 0) bv.wcount[(size_t)b * memo_blocks(F) + bx] = total | (total_r << 16);
 
     if (bv.n27) {   // accounting runs: queries and reused ones
         unsigned int qn = i < nq ? 1u : 0u;
@@ -1061,7 +1116,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int total = nq, nblk = 0, total_s = nq;
     int* roff = soff;
-    if constexpr (LIST) {   // block counts: searches in the low 16 bits, refits in the high 16
+    if constexpr (LIST && kListAtomic) {   // the scan's list lengths (memo pass atomics)
+        const int* cnt = bv.wcount + (size_t)b * memo_blocks(F);
+        total_s = cnt[0];
+        total = total_s + cnt[1];
+    } else if constexpr (LIST) {   // block counts: searches in the low 16 bits, refits in the high 16
         __shared__ int wsum[8];
         nblk = (nq + 255) / 256;
         roff = soff + nblk + 1;
@@ -1121,7 +1180,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         int pos = e;
         float lim = kFullLim;
         bool walk = true;
-        if constexpr (LIST) {   // largest block whose list starts at or before e (empty blocks share offsets)
+        if constexpr (LIST && kListAtomic) {
+            if (e < total_s) {
+                const size_t at = (size_t)b * F + e;
+                pos = bv.wl[at];
+                lim = bv.wlim[at];
+            } else {
+                pos = bv.wl[(size_t)b * F + F - 1 - (e - total_s)];
+                walk = false;
+            }
+        } else if constexpr (LIST) {   // largest block whose list starts at or before e (empty blocks share offsets)
             const bool rf = e >= total_s;   // refit entries follow the searches
             const int er = rf ? e - total_s : e;
             const int* off = rf ? roff : soff;
@@ -1159,7 +1227,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
         } else {   // refit: the memo pass left the 5 neighbours in their order at w (key bits: index only)
 #pragma unroll
             for (int j = 0; j < 5; ++j)
-                k[j] = key_as_double((uint64_t)(uint32_t)bv.memo_nbr[((size_t)b * kMemoWords + j) * F + pos]);
+                k[j] = key_as_double((uint64_t)(uint32_t)bv.memo_nbr[memo_idx(b, j, pos, F)]);
         }
         if (kMemo && walk) {   // anchor for the memo pass: gap between the 5th and the 6th neighbour (capped at 1 m)
             float gap = -1.f;
@@ -1173,10 +1241,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
                     sj = sn;
                 }
                 gap = (float)(s6 - sj);
+                if constexpr (kMemoAos) {   // the position's 32-B memo record in two 16-B stores
+                    int* mp = bv.memo_nbr + memo_idx(b, 0, pos, F);
+                    *reinterpret_cast<int4*>(mp) = make_int4((int)(uint32_t)key_bits(k[0]), (int)(uint32_t)key_bits(k[1]),
+                                                             (int)(uint32_t)key_bits(k[2]), (int)(uint32_t)key_bits(k[3]));
+                    *reinterpret_cast<int4*>(mp + 4) = make_int4((int)(uint32_t)key_bits(k[4]), __float_as_int((float)s6),
+                                                                 __float_as_int((float)fmin(gord, s6 - sj)), 0);
+                } else {
 #pragma unroll
-                for (int j = 0; j < 5; ++j) bv.memo_nbr[((size_t)b * kMemoWords + j) * F + pos] = (int)(uint32_t)key_bits(k[j]);
-                bv.memo_nbr[((size_t)b * kMemoWords + 5) * F + pos] = __float_as_int((float)s6);
-                bv.memo_nbr[((size_t)b * kMemoWords + 6) * F + pos] = __float_as_int((float)fmin(gord, s6 - sj));
+                    for (int j = 0; j < 5; ++j) bv.memo_nbr[memo_idx(b, j, pos, F)] = (int)(uint32_t)key_bits(k[j]);
+                    bv.memo_nbr[memo_idx(b, 5, pos, F)] = __float_as_int((float)s6);
+                    bv.memo_nbr[memo_idx(b, 6, pos, F)] = __float_as_int((float)fmin(gord, s6 - sj));
+                }
             }
             bv.prevw[ppos] = make_float4(w.x, w.y, w.z, gap);
         }
@@ -1976,8 +2052,12 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
             hipLaunchKernelGGL((match_fit_kernel<true, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
         }
     } else if (bv.memo) {
+        if (kListAtomic) {
+            const hipError_t e = hipMemsetAsync(bv.wcount, 0, (size_t)bv.B * memo_blocks(bv.feat_stride) * sizeof(int), s);
+            if (e != hipSuccess) return e;
+        }
         hipLaunchKernelGGL(match_memo_kernel, grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
-        const size_t lds = 2 * (memo_blocks(bv.feat_stride) + 1) * sizeof(int);
+        const size_t lds = kListAtomic ? 0 : 2 * (memo_blocks(bv.feat_stride) + 1) * sizeof(int);
         hipLaunchKernelGGL((match_fit_kernel<false, true>), grid, dim3(256), lds, s, edge, surf, bv, gx, remap);
     } else {
         hipLaunchKernelGGL((match_fit_kernel<false, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);

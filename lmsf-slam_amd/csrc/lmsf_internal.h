@@ -35,6 +35,7 @@ static_assert(kRingMax <= kQCodeMask + 1, "ring positions fit the 13-bit code fi
 constexpr int kTile = 2048;          // raw points per ring-split tile
 constexpr int kCounterShards = 64;   // candidate / query counters, 16 u64 (128 B) apart
 constexpr int kMemoWords = 7;        // memo words per search position: 5 neighbour indices, s6, order gap
+constexpr int kMemoStride = 8;       // memo_nbr allocation per search position (the AoS layout's 32-B record)
 constexpr int kCaptureIters = 10;    // outer iterations kept per captured slot (lmsf_batch_capture)
 
 // Tuning knobs measured by A/B builds.  The shipped library reads no environment:
@@ -116,7 +117,7 @@ struct BatchView {
     float4* prevw;           // [B][feat_stride] anchor of position i's last full search: map-frame query w0
                              //   and gap = s6 - s5 (s = distance of the k-th neighbour, the 6th capped at
                              //   the 1 m radius); w = -1 when fewer than 5 neighbours were found
-    int* memo_nbr;           // [B][kMemoWords][feat_stride] that search's 5 neighbour map indices, nearest
+    int* memo_nbr;           // [B][feat_stride][kMemoStride] (LMSF_MEMO_AOS; else [B][kMemoWords][feat_stride]) that search's 5 neighbour map indices, nearest
                              //   first, then s6 (float bits), then (batch path) the order gap: min(s6 - s5,
                              //   s(j+1) - s(j)) (float bits; -1 once a refit reordered the indices)
     float* wlim;             // [B][feat_stride] the listed positions' search radius^2 (knn_walk lim)

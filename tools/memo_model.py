@@ -1,0 +1,74 @@
+"""C2 query-memo outcome model (CPU only, oracle kd-tree + oracle Ceres-LM trace on one scan): per outer iteration
+>= 2, how many queries the memo pass reuses (consecutive-gap test or re-keyed set in the same order), refits (same
+set, new order) or sends to the bounded search -- and how many of those searches return the stored 5 in the stored
+order (their fit would reproduce the stored record).  python tools/memo_model.py"""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(REPO, "lmsf-slam_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+from lmsf import synth  # noqa: E402
+import oracle  # noqa: E402
+
+wl = synth.make_workload("C2", n_scans=1)
+e, s, _, _ = oracle.extract(np.asarray(wl.scans[0]))
+reg = oracle.Registration()
+reg.set_map(0, wl.edge_map) if False else None
+EDGE, SURF = 1, 2
+reg.set_map(EDGE, wl.edge_map)
+reg.set_map(SURF, wl.surf_map)
+reg.set_scan(EDGE, e)
+reg.set_scan(SURF, s)
+x, tr, st = reg.solve(wl.guess[0])
+poses = [np.asarray(wl.guess[0])] + [tr[i] for i in range(len(tr) - 1)]
+kd = oracle.KdMap(np.asarray(wl.surf_map))
+S = np.asarray(s)[:, :3].astype(np.float64)
+
+
+def associate(p, pose):
+    return synth.transform_points(pose, p).astype(np.float32)
+
+
+def knn6(w):
+    idx, d2 = kd.knn(w, 6)
+    return idx, d2.astype(np.float64)
+
+
+state = None
+for it, pose in enumerate(poses):
+    w = associate(S, pose)
+    idx, d2 = knn6(w)
+    s_all = np.sqrt(np.minimum(d2, 1.0))
+    if it < 2:
+        state = dict(w0=w.astype(np.float64), nbr=idx[:, :5].copy(), s6=s_all[:, 5], gap=s_all[:, 5] - s_all[:, 4],
+                     gord=np.minimum(np.min(np.diff(s_all[:, :5], axis=1), axis=1), s_all[:, 5] - s_all[:, 4]))
+        print(f"iteration {it}: full search")
+        continue
+    dd = np.linalg.norm(w.astype(np.float64) - state["w0"], axis=1)
+    same_gap = 2 * dd + 1e-5 < state["gord"]
+    # re-key the stored 5 at w (float d2 as the kernel computes it)
+    P = np.asarray(wl.surf_map)[:, :3].astype(np.float32)
+    nb = state["nbr"]
+    dv = (w[:, None, :] - P[nb]).astype(np.float32)
+    rk = (dv[..., 0] * dv[..., 0] + dv[..., 1] * dv[..., 1] + dv[..., 2] * dv[..., 2]).astype(np.float32)
+    order = np.lexsort((nb, rk), axis=1) if False else np.array([np.lexsort((nb[i], rk[i])) for i in range(len(nb))])
+    k4 = np.sqrt(rk[np.arange(len(nb)), order[:, 4]].astype(np.float64))
+    inside = k4 + dd + 1e-5 < state["s6"]
+    in_order = (order == np.arange(5)).all(axis=1)
+    reuse = same_gap | (inside & in_order)
+    refit = ~same_gap & inside & ~in_order
+    search = ~reuse & ~refit
+    unchanged = search & (idx[:, :5] == nb).all(axis=1)
+    n = len(w)
+    print(f"iteration {it}: reuse {reuse.mean():.3f} (gap test {same_gap.mean():.3f}), refit {refit.mean():.3f}, "
+          f"search {search.mean():.3f}, of which same 5 in the stored order {unchanged.sum() / max(search.sum(), 1):.3f}")
+    # the kernel's state updates: refits reorder the stored set (anchor kept), searches re-anchor
+    state["nbr"][refit] = nb[refit][np.arange(refit.sum())[:, None], order[refit]]
+    state["gord"][refit] = -1.0
+    for key, val in (("w0", w.astype(np.float64)), ("s6", s_all[:, 5]), ("gap", s_all[:, 5] - s_all[:, 4])):
+        state[key][search] = val[search]
+    state["nbr"][search] = idx[search, :5]
+    state["gord"][search] = np.minimum(np.min(np.diff(s_all[search, :5], axis=1), axis=1), s_all[search, 5] - s_all[search, 4])
