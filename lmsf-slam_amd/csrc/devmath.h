@@ -483,7 +483,8 @@ __device__ inline void colpiv_qr_solve(double* A, const double* b, double* x) {
                 double temp = fabs(A[k * N + j]) / cn_upd[j];
                 temp = (1.0 + temp) * (1.0 - temp);
                 temp = temp < 0.0 ? 0.0 : temp;
-                double r = cn_upd[j] / cn_dir[j];
+                // at k = 0 both norms are still the one computed value (swapped together): x / x = 1 exactly
+                double r = k == 0 ? 1.0 : cn_upd[j] / cn_dir[j];
                 double temp2 = temp * r * r;
                 if (temp2 <= downdate_thr) {
                     double s = 0.0;

@@ -72,3 +72,15 @@ for it, pose in enumerate(poses):
         state[key][search] = val[search]
     state["nbr"][search] = idx[search, :5]
     state["gord"][search] = np.minimum(np.min(np.diff(s_all[search, :5], axis=1), axis=1), s_all[search, 5] - s_all[search, 4])
+
+# Full searches: how many queries' ordered 5-NN equal those of the previous outer iteration's match (a full search
+# whose fit could be skipped when the record is kept by position)
+prev = None
+for it, pose in enumerate(poses[:5]):
+    w = associate(S, pose)
+    idx, d2 = knn6(w)
+    ok = d2[:, 4] < 1.0
+    if prev is not None:
+        same = (idx[:, :5] == prev).all(axis=1) & ok
+        print(f"iteration {it}: ordered 5-NN unchanged from iteration {it - 1}: {same.mean():.3f} (matched {ok.mean():.3f})")
+    prev = idx[:, :5]
