@@ -648,6 +648,20 @@ lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t) {
     // by its worker on its aux stream
     TCHK(t, hipEventRecord(t->ev_fork, ctx_stream(t->ctx)));
     if (assign_streams(t) == 0) return LMSF_OK;
+    // A/B builds (diagnostics): the rebuild enqueued on the caller's thread instead of the two workers
+    static const bool inline_commit = ab_int("LMSF_COMMIT_INLINE", 0) != 0;
+    if (inline_commit) {
+        for (int i = 0; i < 2; ++i) {
+            const int kind = t->ks[LMSF_SURF] == t->aux[i] ? LMSF_SURF : t->ks[LMSF_EDGE] == t->aux[i] ? LMSF_EDGE : 0;
+            lmsf_status r = kind ? commit_stage_kind(t, kind, t->aux[i]) : LMSF_OK;
+            if (!r && kind) r = finish_kind(t, kind, t->aux[i]);
+            t->job_rc[i] = r;
+            t->job[i] = 0;
+        }
+        t->staging = true;
+        t->pending = true;
+        return LMSF_OK;
+    }
     if (!t->worker[0].joinable())
         for (int i = 0; i < 2; ++i) t->worker[i] = std::thread(worker_main, t, i, ctx_device(t->ctx));
     {
