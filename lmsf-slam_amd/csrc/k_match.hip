@@ -871,10 +871,6 @@ __host__ __device__ __forceinline__ size_t memo_blocks(size_t feat_stride) { ret
 #define LMSF_LIST_ATOMIC 1
 #endif
 constexpr bool kListAtomic = kLinEval && LMSF_LIST_ATOMIC != 0;
-#ifndef LMSF_LIST_DIV
-#define LMSF_LIST_DIV 4
-#endif
-constexpr int kListDiv = LMSF_LIST_DIV;
 
 #ifndef LMSF_MEMO_WAVES   // waves per SIMD the memo pass is compiled for (A/B)
 #define LMSF_MEMO_WAVES 5
@@ -1175,12 +1171,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     if (bx == 0 && threadIdx.x == 0) bv.n_search[b] = total;   // listed entries (packets), refits included
     if (bx * 256 >= total) return;   // uniform per block, after the last barrier
     const Pose Ps = load_pose(bv.st[b].x);
-    const int e0 = bx * 256 + threadIdx.x;
+    const int e = bx * 256 + threadIdx.x;
     unsigned int c27 = 0;
     double P[kPacket];
 #pragma unroll
     for (int j = 0; j < kPacket; ++j) P[j] = 0.0;
-    auto entry = [&](const int e) {
+    if (e < total) {
         int pos = e;
         float lim = kFullLim;
         bool walk = true;
@@ -1300,17 +1296,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
 #endif
         store_record(bv, ppos, p, kind, v0, v1x, v1y, v1z);   // records by search position
         if (!kLinEval) record_packet(kind, p, v0, v1x, v1y, v1z, Ps, P);
-    };
-    if constexpr (LIST && kListAtomic) {
-        // a listed launch of 1 / kListDiv of the blocks (no packets): each block strides over its scan's list
-        for (int e = e0; e < total; e += gx * 256) entry(e);
-    } else if (e0 < total) {
-        entry(e0);
     }
     if (!kLinEval && bx * 256 + wave * 64 < total)
         wave_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + bv.part2_base + (size_t)bx * 4 + wave) * kPacket);
     if (bv.n27) {   // accounting runs: n27 of the searches (+ the queries when there was no memo pass)
-        unsigned int qn = (!LIST && e0 < total) ? 1u : 0u;
+        unsigned int qn = (!LIST && e < total) ? 1u : 0u;
         unsigned long long c = c27;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
@@ -1475,11 +1465,6 @@ __device__ __forceinline__ void dense_run(double (&k)[5], const float4* __restri
     }
 }
 
-// LMSF_P2_SPLIT: pass-2 queries whose bound exceeds this multiple of lim1 listed apart (0: one list)
-#ifndef LMSF_P2_SPLIT
-#define LMSF_P2_SPLIT 4
-#endif
-constexpr float kP2Split = (float)LMSF_P2_SPLIT;
 constexpr int kDenseRowOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // own row, faces, corners (knn_walk's kOrder)
 constexpr float kDenseCull = 1.0f + 1e-5f;                       // knn_walk's kCullLim
 
@@ -1540,21 +1525,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
             dense_run(k, rp, st_[i], ln, w);
         }
     }
-    // complete (5th key within lim1: nothing nearer lies outside the scanned ball) -> fit; else -> pass-2 list, the
-    // queries whose bound exceeds kP2Split x lim1 from its back (pass 2's waves then walk balls of similar size)
+    // complete (5th key within lim1: nothing nearer lies outside the scanned ball) -> fit; else -> pass-2 list
     const bool p2 = valid && key_d2(k[4]) > g.lim1;
-    const bool p2big = p2 && kP2Split > 0.f && key_d2(k[4]) > kP2Split * g.lim1;
-    const unsigned long long m2 = __ballot(p2 && !p2big), m3 = __ballot(p2big);
-    int base2 = 0, base3 = 0;
-    if (lane == 0) {
-        if (m2) base2 = (int)atomicAdd(p2count, (unsigned)__popcll(m2));
-        if (m3) base3 = (int)atomicAdd(p2count + 1, (unsigned)__popcll(m3));
-    }
+    const unsigned long long m2 = __ballot(p2);
+    int base2 = 0;
+    if (lane == 0 && m2) base2 = (int)atomicAdd(p2count, (unsigned)__popcll(m2));
     base2 = __shfl(base2, 0, 64);
-    base3 = __shfl(base3, 0, 64);
-    if (p2) {   // pass 2 from scratch, bounded by this 5th key (the 5 nearest lie within it)
-        const size_t at = p2big ? (size_t)bv.B * F - 1 - (size_t)(base3 + __popcll(m3 & below))
-                                : (size_t)(base2 + __popcll(m2 & below));
+    if (p2) {   // pass 2 from scratch on the 1 m grid, bounded by this 5th key (the 5 nearest lie within it)
+        const int at = base2 + __popcll(m2 & below);
         bv.wl[at] = (int)((size_t)b * F + e);
         bv.wlim[at] = key_d2(k[4]);
     } else if (valid) {
@@ -1590,12 +1568,11 @@ constexpr int kRing5[25][2] = {{0, 0},  {0, -1}, {-1, 0}, {1, 0},  {0, 1},  {-1,
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void dense_pass2_kernel(
     GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, const unsigned* p2count) {
-    const unsigned count_small = p2count[0], count = count_small + p2count[1];
+    const unsigned count = *p2count;
     const size_t F = bv.feat_stride;
     for (unsigned li = blockIdx.x * 256 + threadIdx.x; li < count; li += gridDim.x * 256) {
-        const size_t at = li < count_small ? (size_t)li : (size_t)bv.B * F - 1 - (li - count_small);
-        const size_t code = (size_t)(unsigned)bv.wl[at];
-        const float bound = bv.wlim[at];
+        const size_t code = (size_t)(unsigned)bv.wl[li];
+        const float bound = bv.wlim[li];
         const int b = (int)(code / F), e = (int)(code - (size_t)b * F);
         const int ne = bv.n_edge[b];
         const size_t ppos = (size_t)b * F + e;
@@ -2062,7 +2039,7 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
     if (match_fit_prune(edge, surf)) {
         static const bool split = ab_int("LMSF_DENSE_SPLIT", LMSF_DENSE_SPLIT) != 0;
         if (split && kLinEval && bv.p2count && (size_t)bv.B * bv.feat_stride < ((size_t)1 << 31)) {
-            hipError_t e = hipMemsetAsync(bv.p2count, 0, 2 * sizeof(unsigned), s);
+            hipError_t e = hipMemsetAsync(bv.p2count, 0, sizeof(unsigned), s);
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(dense_pass1_kernel, grid, dim3(256), 0, s, edge, surf, fine_edge, fine_surf, bv, gx, remap,
                                bv.p2count);
@@ -2081,10 +2058,7 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
         }
         hipLaunchKernelGGL(match_memo_kernel, grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
         const size_t lds = kListAtomic ? 0 : 2 * (memo_blocks(bv.feat_stride) + 1) * sizeof(int);
-        // the listed search on 1 / kListDiv of the full grid, each block striding over its scan's list (after
-        // outer iteration 2 most of a full grid's blocks would find nothing to do)
-        const int gl = kListAtomic ? std::max(1, (gx + kListDiv - 1) / kListDiv) : gx;
-        hipLaunchKernelGGL((match_fit_kernel<false, true>), dim3(gl * bv.B), dim3(256), lds, s, edge, surf, bv, gl, remap);
+        hipLaunchKernelGGL((match_fit_kernel<false, true>), grid, dim3(256), lds, s, edge, surf, bv, gx, remap);
     } else {
         hipLaunchKernelGGL((match_fit_kernel<false, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
     }
