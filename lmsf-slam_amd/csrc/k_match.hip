@@ -1566,7 +1566,16 @@ constexpr int kRing5[25][2] = {{0, 0},  {0, -1}, {-1, 0}, {1, 0},  {0, 1},  {-1,
 #define LMSF_PASS2_FINE 1
 #endif
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void dense_pass2_kernel(
+// LMSF_P2_SPLITFIT: pass 2 as a walk kernel (no fit: few registers, more waves to hide its row-by-row offset
+// latency; the kept 5 indices left in the position's memo record) and a fit kernel over the same list.
+#ifndef LMSF_P2_SPLITFIT
+#define LMSF_P2_SPLITFIT 1
+#endif
+#ifndef LMSF_P2_WALK_WAVES
+#define LMSF_P2_WALK_WAVES 6
+#endif
+template <bool FIT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FIT ? 3 : LMSF_P2_WALK_WAVES))) void dense_pass2_kernel(
     GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, const unsigned* p2count) {
     const unsigned count = *p2count;
     const size_t F = bv.feat_stride;
@@ -1605,6 +1614,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
             const uint32_t a = row[sa];
             dense_run(k, rp, a, row[sb + 1] - a, w);
         }
+        if constexpr (FIT) {
+            dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);
+        } else {   // the kept indices (-1: none) for dense_fit2_kernel, in key order
+            int kid[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) kid[j] = key_bits(k[j]) < kSentinel ? (int)(uint32_t)key_bits(k[j]) : -1;
+            int* mp = bv.memo_nbr + memo_idx(b, 0, e, F);
+            *reinterpret_cast<int4*>(mp) = make_int4(kid[0], kid[1], kid[2], kid[3]);
+            mp[4] = kid[4];
+        }
+    }
+}
+
+// The fit of dense_pass2_kernel<false>'s queries (same list, same order): the kept 5 from the memo record.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void dense_fit2_kernel(
+    GridView ge, GridView gs, BatchView bv, const unsigned* p2count) {
+    const unsigned count = *p2count;
+    const size_t F = bv.feat_stride;
+    for (unsigned li = blockIdx.x * 256 + threadIdx.x; li < count; li += gridDim.x * 256) {
+        const size_t code = (size_t)(unsigned)bv.wl[li];
+        const int b = (int)(code / F), e = (int)(code - (size_t)b * F);
+        const int ne = bv.n_edge[b];
+        const size_t ppos = (size_t)b * F + e;
+        const float4 p = bv.featp[ppos];
+        const int qq = __float_as_int(p.w);
+        const bool is_edge = qq < ne;
+        const GridView g = pick_grid(is_edge, ge, gs);   // orig: the caller-order map either way
+        const float3 w = associate(load_pose(bv.st[b].x), p);
+        const int* mp = bv.memo_nbr + memo_idx(b, 0, e, F);
+        const int4 m0 = *reinterpret_cast<const int4*>(mp);
+        const int kid[5] = {m0.x, m0.y, m0.z, m0.w, mp[4]};
+        double k[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) k[j] = kid[j] >= 0 ? key_as_double((uint64_t)(uint32_t)kid[j]) : key_as_double(kSentinel);
         dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);
     }
 }
@@ -2046,8 +2089,16 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
             e = hipGetLastError();
             if (e != hipSuccess) return e;
             // grid-stride over the list (~10% of the queries on C5): 8 blocks per CU
-            hipLaunchKernelGGL(dense_pass2_kernel, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge, fine_surf, bv,
-                               (const unsigned*)bv.p2count);
+            if (LMSF_P2_SPLITFIT) {
+                hipLaunchKernelGGL(dense_pass2_kernel<false>, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge, fine_surf,
+                                   bv, (const unsigned*)bv.p2count);
+                e = hipGetLastError();
+                if (e != hipSuccess) return e;
+                hipLaunchKernelGGL(dense_fit2_kernel, dim3(2048), dim3(256), 0, s, edge, surf, bv, (const unsigned*)bv.p2count);
+            } else {
+                hipLaunchKernelGGL(dense_pass2_kernel<true>, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge, fine_surf,
+                                   bv, (const unsigned*)bv.p2count);
+            }
         } else {
             hipLaunchKernelGGL((match_fit_kernel<true, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
         }
