@@ -397,8 +397,13 @@ lmsf_status grid_reserve(lmsf_ctx* c, DevMap& m, size_t n) {
         HIPCHK(c, hipMalloc((void**)&m.d_bb, 32 * sizeof(int)));
         HIPCHK(c, hipMemset(m.d_bb, 0, 32 * sizeof(int)));
         HIPCHK(c, hipHostMalloc((void**)&m.h_bb, 16 * sizeof(int), hipHostMallocDefault));
+        // a null-stream memset is not ordered before the context's non-blocking streams: complete it here
+        HIPCHK(c, hipDeviceSynchronize());
     }
     if (n > m.cap) {
+        // growth (rare; a tracker window's grid is grown by a commit worker): kernels of the last build or
+        // search may still read these on another stream -- the device drains before they are freed
+        if (m.cap) HIPCHK(c, hipDeviceSynchronize());
         hipFree(m.orig); hipFree(m.pts); hipFree(m.cell);
         m.orig = nullptr; m.pts = nullptr; m.cell = nullptr;
         const size_t cap = std::min(grow_cap(n, m.cap), (size_t)INT32_MAX);
@@ -428,6 +433,7 @@ lmsf_status grid_stage(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, cons
 // counts / offsets / fill for at least need cells (grown geometrically)
 lmsf_status grid_cells_reserve(lmsf_ctx* c, DevMap& m, size_t need, hipStream_t s) {
     if (need <= m.cells_cap) return LMSF_OK;
+    if (m.cells_cap) HIPCHK(c, hipDeviceSynchronize());   // growth: the last build / search may still read them
     hipFree(m.counts); hipFree(m.off); hipFree(m.fill); hipFree(m.scan_tmp);
     m.counts = m.off = m.fill = nullptr;
     m.scan_tmp = nullptr;
@@ -452,6 +458,7 @@ lmsf_status grid_build_device(lmsf_ctx* c, DevMap& m, size_t n_max, int base, hi
     if (rc) return rc;
     const size_t tiles = grid_scan_tiles(m.cells_cap);
     if (tiles > m.scan_state_tiles) {
+        if (m.scan_state_tiles) HIPCHK(c, hipDeviceSynchronize());   // growth: the last build may still read it
         hipFree(m.scan_state);
         m.scan_state = nullptr;
         m.scan_state_tiles = 0;
@@ -580,8 +587,10 @@ lmsf_status build_fine(lmsf_ctx* c, int kind) {
         HIPCHK(c, hipMalloc((void**)&f.d_bb, 32 * sizeof(int)));
         HIPCHK(c, hipMemset(f.d_bb, 0, 32 * sizeof(int)));
         HIPCHK(c, hipHostMalloc((void**)&f.h_bb, 16 * sizeof(int), hipHostMallocDefault));
+        HIPCHK(c, hipDeviceSynchronize());
     }
     if ((size_t)m.n > f.cap) {
+        if (f.cap) HIPCHK(c, hipDeviceSynchronize());
         hipFree(f.pts); hipFree(f.cell);
         f.pts = nullptr; f.cell = nullptr;
         f.cap = 0;
@@ -1075,6 +1084,7 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(hipMemset(c->n_edge, 0, B * sizeof(int)));
     CHK(hipMemset(c->n_surf, 0, B * sizeof(int)));
     CHK(hipMemset(c->d_n27, 0, kCounterShards * 16 * sizeof(unsigned long long)));
+    CHK(hipDeviceSynchronize());   // the null-stream memsets above complete before the non-blocking streams' work
     CHK(hipHostMalloc((void**)&c->h_poses, B * 7 * sizeof(double), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_st, B * sizeof(SolveState), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_counts, 2 * B * sizeof(int), hipHostMallocDefault));

@@ -1468,6 +1468,14 @@ __device__ __forceinline__ void dense_run(double (&k)[5], const float4* __restri
 constexpr int kDenseRowOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // own row, faces, corners (knn_walk's kOrder)
 constexpr float kDenseCull = 1.0f + 1e-5f;                       // knn_walk's kCullLim
 
+__device__ __forceinline__ void store_kept(const BatchView& bv, int b, int e, size_t F, const double (&k)[5]) {
+    int kid[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) kid[j] = key_bits(k[j]) < kSentinel ? (int)(uint32_t)key_bits(k[j]) : -1;
+    int* mp = bv.memo_nbr + memo_idx(b, 0, e, F);
+    *reinterpret_cast<int4*>(mp) = make_int4(kid[0], kid[1], kid[2], kid[3]);
+    mp[4] = kid[4];
+}
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void dense_pass1_kernel(
     GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, int gx, int remap, unsigned* p2count) {
     int bx, b;
@@ -1616,13 +1624,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FIT ? 3 : L
         }
         if constexpr (FIT) {
             dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);
-        } else {   // the kept indices (-1: none) for dense_fit2_kernel, in key order
-            int kid[5];
-#pragma unroll
-            for (int j = 0; j < 5; ++j) kid[j] = key_bits(k[j]) < kSentinel ? (int)(uint32_t)key_bits(k[j]) : -1;
-            int* mp = bv.memo_nbr + memo_idx(b, 0, e, F);
-            *reinterpret_cast<int4*>(mp) = make_int4(kid[0], kid[1], kid[2], kid[3]);
-            mp[4] = kid[4];
+        } else {   // the kept indices (-1: none) for the fit kernel, in key order
+            store_kept(bv, b, e, F, k);
         }
     }
 }

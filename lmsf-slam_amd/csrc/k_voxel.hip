@@ -337,11 +337,14 @@ void VoxelFilter::release() {
 
 int VoxelFilter::box_blocks(int n) { return std::max(std::min((n + 256 * kVoxBatch - 1) / (256 * kVoxBatch), 1024), 1); }
 
-hipError_t VoxelFilter::reserve(size_t need) {
+hipError_t VoxelFilter::reserve(size_t need, hipStream_t s) {
     if (need <= cap) return hipSuccess;
     const size_t n = std::min(grow_cap(need, cap), (size_t)INT32_MAX);
+    // growth (rare): the old buffers may still be read by this filter's last enqueue, on whichever stream it ran
+    // (a tracker kind's rebuild takes either aux stream), so the device drains before they are freed
+    hipError_t e = cap ? hipDeviceSynchronize() : hipSuccess;
+    if (e != hipSuccess) return e;
     release();
-    hipError_t e;
 #define VALLOC(p, bytes) if ((e = hipMalloc((void**)&(p), (bytes))) != hipSuccess) return e
     VALLOC(keys, n * sizeof(uint32_t));
     VALLOC(keys_b, n * sizeof(uint32_t));
@@ -351,15 +354,16 @@ hipError_t VoxelFilter::reserve(size_t need) {
     VALLOC(nseg, sizeof(int));
     VALLOC(scratch, radix_scratch_words(n) * sizeof(uint32_t));
 #undef VALLOC
-    // look-back words of epoch 0 never match a sort (epochs start at 1)
-    if ((e = hipMemset(scratch, 0, radix_scratch_words(n) * sizeof(uint32_t))) != hipSuccess) return e;
+    // look-back words of epoch 0 never match a sort (epochs start at 1, and restart with the new buffers): zeroed on
+    // the stream whose kernels read them (a null-stream memset is not ordered before a non-blocking stream's work)
+    if ((e = hipMemsetAsync(scratch, 0, radix_scratch_words(n) * sizeof(uint32_t), s)) != hipSuccess) return e;
     cap = n;
     return hipSuccess;
 }
 
 hipError_t VoxelFilter::enqueue(const float4* in, int n, float leaf, float4* out, hipStream_t s, int* map_bb, int sx) {
     if (n <= 0) return hipErrorInvalidValue;
-    hipError_t e = reserve((size_t)n);
+    hipError_t e = reserve((size_t)n, s);
     if (e != hipSuccess) return e;
     if (++epoch == 0) ++epoch;
     const float inv = 1.0f / leaf;

@@ -285,7 +285,7 @@ struct VoxelFilter {
     uint32_t epoch = 0;   // look-back epoch of the last sort
     size_t cap = 0;
     static int box_blocks(int n);
-    hipError_t reserve(size_t n);
+    hipError_t reserve(size_t n, hipStream_t s);   // grows on s (the device drained first when it had buffers)
     hipError_t run(const float4* in, int n, float leaf, float4* out, int* n_out, hipStream_t s);
     // run() without the read-back: the voxel count stays on the device in *nseg (no host wait).  map_bb
     // (optional, device): [0..5] = the map-cell box (k_map.hip's rule, sx x-slices per m) of the INPUT
