@@ -42,6 +42,12 @@ __device__ __forceinline__ float key_d2(double k) { return __uint_as_float((uint
 #ifndef LMSF_KEY_PK
 #define LMSF_KEY_PK 0
 #endif
+// LMSF_TAIL_PAIRS: a row's tail of fewer than RU candidates as straight-line code (a pair, then a last one)
+// instead of a one-candidate loop (A/B)
+#ifndef LMSF_TAIL_PAIRS
+#define LMSF_TAIL_PAIRS 1
+#endif
+constexpr bool kTailPairs = LMSF_TAIL_PAIRS != 0;
 __device__ __forceinline__ double key_min(double a, double b) {
 #if LMSF_KEY_ASM
     double r;
@@ -238,7 +244,17 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
 #pragma unroll
                 for (int u = 0; u < RU; ++u) consider(m[u], (uint32_t)(a + c + u) | tag);
             }
-            for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
+            if constexpr (kTailPairs) {   // the row's tail (< RU) straight-line: a pair, then a last one
+                if (c + 2 <= len) {
+                    const float4 m0 = rp[a + c], m1 = rp[a + c + 1];
+                    consider(m0, (uint32_t)(a + c) | tag);
+                    consider(m1, (uint32_t)(a + c + 1) | tag);
+                    c += 2;
+                }
+                if (c < len) consider(rp[a + c], (uint32_t)(a + c) | tag);
+            } else {
+                for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
+            }
         }
     } else if constexpr (T == 1 && !PRUNE) {
         // one lane walks its rows; kKnnUnroll loads in flight per step (a row is contiguous: 8 points per
@@ -1459,9 +1475,22 @@ __device__ __forceinline__ void dense_run(double (&k)[5], const float4* __restri
 #pragma unroll
         for (int u = 0; u < LMSF_FUSED_UNROLL; ++u) key_insert(k, nn_key(w, m[u], (uint32_t)__float_as_int(m[u].w)));
     }
-    for (; c < len; ++c) {
-        const float4 m = rp[a + c];
-        key_insert(k, nn_key(w, m, (uint32_t)__float_as_int(m.w)));
+    if constexpr (kTailPairs) {
+        if (c + 2 <= len) {
+            const float4 m0 = rp[a + c], m1 = rp[a + c + 1];
+            key_insert(k, nn_key(w, m0, (uint32_t)__float_as_int(m0.w)));
+            key_insert(k, nn_key(w, m1, (uint32_t)__float_as_int(m1.w)));
+            c += 2;
+        }
+        if (c < len) {
+            const float4 m = rp[a + c];
+            key_insert(k, nn_key(w, m, (uint32_t)__float_as_int(m.w)));
+        }
+    } else {
+        for (; c < len; ++c) {
+            const float4 m = rp[a + c];
+            key_insert(k, nn_key(w, m, (uint32_t)__float_as_int(m.w)));
+        }
     }
 }
 
