@@ -70,6 +70,10 @@ def parse(argv=None):
                     help="C2/C5: contexts per GPU (one HIP stream each) sharing a launch batch; their kernels "
                          "run concurrently, so the small solver / extraction launches of one fill the chip "
                          "beside the other's")
+    ap.add_argument("--pipeline", type=int, default=None,
+                    help="C5: contexts per GPU taking whole launches of the pass in turn (launch j on context j mod "
+                         "P, its previous launch waited for first), so one launch's solver phases overlap the "
+                         "next one's search")
     ap.add_argument("--map-points", type=int, default=None)
     ap.add_argument("--cols", type=int, default=None)
     ap.add_argument("--outer", type=int, default=5)
@@ -91,7 +95,10 @@ def parse(argv=None):
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=V",
                     help="context option (lmsf_set_option, e.g. MEMO_BOUND=2 or QUERY_MEMO=0) for A/B runs; the "
                          "line records it under config.options")
-    ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend of the ranks (nccl = RCCL)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo", "gloo-gpu"),
+                    help="torch.distributed backend of the ranks (nccl = RCCL); gloo: CPU rehearsal of the launcher; "
+                         "gloo-gpu: rehearsal of the N-rank GPU path on a box with fewer GPUs (rank r on GPU r mod "
+                         "the device count, gloo collectives on the GPU tensors; the line is marked as a rehearsal)")
     ap.add_argument("--launch-check", action="store_true",
                     help="no GPU work: ranks join the process group, run the C2 pose all-gather on CPU tensors and "
                          "print the line skeleton (CPU test of the --gpus launcher)")
@@ -101,6 +108,8 @@ def parse(argv=None):
             setattr(a, k, v)
     if a.streams is None:
         a.streams = 1
+    if a.pipeline is None:
+        a.pipeline = 1
     if a.unique_scans is None:
         a.unique_scans = {"C2": a.batch, "C5": a.batch}.get(a.config, 1)   # one distinct scan per slot of a launch
     if a.traffic_json is None:
@@ -129,6 +138,7 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.gpu = self.local                             # the device this rank registers on
         self.backend = backend
         self.torch = self.dist = self.dev = None
 
@@ -137,6 +147,14 @@ class Dist:
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
+        if self.backend == "gloo-gpu":                    # N ranks sharing the box's GPUs, gloo collectives
+            self.gpu = self.local % max(torch.cuda.device_count(), 1)
+            torch.cuda.set_device(self.gpu)
+            self.dev = torch.device("cuda", self.gpu)
+            if self.world > 1:
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                dist.init_process_group("gloo")
+            return self
         if self.backend != "nccl":                        # CPU rehearsal (gloo)
             self.dev = torch.device("cpu")
             if self.world > 1:
@@ -352,6 +370,8 @@ def apply_options(args, ctxs):
 def line(args, d, metric, value, unit, elapsed, scaling, workload, extra_cfg, roofline, cpu, **extra):
     if args.opt:
         extra_cfg = dict(extra_cfg, options=list(args.opt))
+    if d.backend == "gloo-gpu":   # ranks share GPUs: a correctness rehearsal, not a scaling measurement
+        extra_cfg = dict(extra_cfg, rehearsal=f"{d.world} ranks on {d.torch.cuda.device_count()} GPU(s), gloo")
     out = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": d.world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
            "scaling": scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
@@ -473,13 +493,16 @@ def run_batch(args, d):
         guesses = np.stack([synth.perturb(truth_u[unit_scan[j]], np.random.default_rng(3000 + k + 7919 * i))
                             for j, i in enumerate(mine)])
     chunk = min(args.batch, n_units)
-    S = max(1, min(args.streams, chunk))
+    P = max(1, args.pipeline) if cfg == "C5" and n_units > chunk else 1   # contexts taking launches in turn
+    S = 1 if P > 1 else max(1, min(args.streams, chunk))    # contexts sharing one launch
     sub_b = -(-chunk // S)                                   # slots per context
     max_pts = max(len(s) for s in scans_u)
-    ctxs = [_lib.Context(device=d.local, max_batch=sub_b, max_scan_points=max_pts + 64, max_features=max_pts + 64,
-                         schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer, **c["extract"]) for _ in range(S)]
+    ctxs = [_lib.Context(device=d.gpu, max_batch=sub_b, max_scan_points=max_pts + 64, max_features=max_pts + 64,
+                         schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer, **c["extract"])
+            for _ in range(max(S, P))]
     apply_options(args, ctxs)
     ctx_scans = [[scans_u[j % U] for j in range(i * sub_b, min((i + 1) * sub_b, chunk))] for i in range(S)]
+    ctx_scans += [ctx_scans[0]] * (len(ctxs) - S)            # pipelined contexts: every launch holds the same slots
     for cx, sc in zip(ctxs, ctx_scans):
         cx.set_map(_lib.EDGE, em_t)
         cx.set_map(_lib.SURF, sm_t)
@@ -493,7 +516,34 @@ def run_batch(args, d):
     stream_in = {"on": False, "shadow": None}
     host_bufs = []
 
+    def pipelined_step():
+        enq = 0.0
+        busy = [None] * P                                    # per context: its launch in flight (first unit, count)
+        order = []
+        for j, c0 in enumerate(range(0, n_units, chunk)):
+            ci, nb = j % P, min(chunk, n_units - c0)
+            if busy[ci] is not None:
+                a, m = busy[ci]
+                poses[a:a + m], st = ctxs[ci].batch_wait(m)
+                matches[a:a + m] = [s.edge_matches + s.surf_matches for s in st]
+            t_enq = time.perf_counter()
+            ctxs[ci].batch_launch(guesses[c0:c0 + nb])
+            enq += time.perf_counter() - t_enq
+            busy[ci] = (c0, nb)
+            order = [x for x in order if x != ci] + [ci]
+        for ci in order:
+            a, m = busy[ci]
+            poses[a:a + m], st = ctxs[ci].batch_wait(m)
+            matches[a:a + m] = [s.edge_matches + s.surf_matches for s in st]
+        t_c = time.perf_counter()
+        exchange_poses(cfg, poses, gathered, args.pairs, world, d.dev)
+        coll_s.append(time.perf_counter() - t_c)
+        enqueue_s.append(enq)
+        return poses
+
     def step():
+        if P > 1:
+            return pipelined_step()
         enq = 0.0
         for c0 in range(0, n_units, chunk):
             nb = min(chunk, n_units - c0)
@@ -532,7 +582,7 @@ def run_batch(args, d):
     tj = load_traffic(args.traffic_json, config=cfg, batch=sub_b, streams=1, map_points=map_points,
                       unique_scans=min(U, sub_b))
     solo = None
-    if S > 1:   # kernel time alone on the chip (the profile's condition), live, after the timed region
+    if S > 1 or P > 1:   # kernel time alone on the chip (the profile's condition), live, after the timed region
         c0 = 0
         solo = solo_launches(ctxs, lambda i: guesses[c0 + i * sub_b:c0 + min((i + 1) * sub_b, chunk)]
                              if i * sub_b < chunk else None)
@@ -643,9 +693,11 @@ def run_batch(args, d):
         else:
             metric = "LiDAR scan pairs/sec re-registered (128-beam 254k-pt scan, 10M-pt map, 1k pairs)"
             wl = (f"C5: 128x{args.cols} scans (~{npts} pts, {U} distinct per GPU) vs {map_points}-pt map, "
-                  f"{args.pairs} pairs (i mod {world} per GPU, launches of {chunk}), {args.outer} outer iters x "
+                  f"{args.pairs} pairs (i mod {world} per GPU, launches of {chunk}"
+                  + (f", {P} contexts taking them in turn" if P > 1 else "") + f"), {args.outer} outer iters x "
                   f"Ceres-LM(4)")
-            extra = {"pairs": args.pairs, "launch_batch": chunk, "distinct_scans_per_gpu": U, "map_points": map_points,
+            extra = {"pairs": args.pairs, "launch_batch": chunk, "pipelined_contexts": P,
+                     "distinct_scans_per_gpu": U, "map_points": map_points,
                      "outer_iterations": args.outer, "parallelism": f"pair-sharded x{world}"}
             unit, scaling = "pairs/s", "strong"
         extra["collective_ms_per_step"] = collective_ms   # pose all-gather section (0: one rank, no collective)
@@ -677,7 +729,7 @@ def run_streams(args, d):
     em_t, sm_t = shared_map(d, lambda: synth.make_map(scene, args.map_points, 1000 + k + 7, center_x=(0.0, 80.0),
                                                       radius=c["radius"]))
     max_pts = max(len(s) for s in scans)
-    ctx = _lib.Context(device=d.local, max_batch=1, max_scan_points=max_pts + 64, max_features=max_pts + 64,
+    ctx = _lib.Context(device=d.gpu, max_batch=1, max_scan_points=max_pts + 64, max_features=max_pts + 64,
                        schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer)
     apply_options(args, [ctx])
     tr = _lib.Tracker(ctx, manual_map_update=True)
@@ -807,7 +859,7 @@ def run_dual(args, d):
     prim_dev = [torch.from_numpy(s).to(d.dev) for s in ds.primary]
     sub_dev = [torch.from_numpy(s).to(d.dev) for s in ds.sub]
     max_pts = max(max(len(s) for s in ds.primary), max(len(s) for s in ds.sub))
-    ctx = _lib.Context(device=d.local, max_batch=1, max_scan_points=max_pts + 64, max_features=max_pts + 64)
+    ctx = _lib.Context(device=d.gpu, max_batch=1, max_scan_points=max_pts + 64, max_features=max_pts + 64)
     apply_options(args, [ctx])
     system = dual.DualLidarSystem(ctx, extrinsic=X0)
     state = {"i": 0}
