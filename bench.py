@@ -54,7 +54,9 @@ DEFAULTS = {   # per configuration: batch (scans per launch), map points, column
     "C2": dict(batch=512, map_points=1_000_000, cols=4096, steps=40, warmup=2, streams=4),
     "C3": dict(batch=1, map_points=0, cols=4096, steps=20, warmup=3),
     "C4": dict(batch=1, map_points=5_000_000, cols=4096, steps=20, warmup=3),
-    "C5": dict(batch=125, map_points=10_000_000, cols=2048, steps=2, warmup=1),
+    # C5: launches of 125 taken in turn by 3 contexts (r04 A/B, two rounds each: 1 context 3,836 pairs/s, 2 4,104,
+    # 3 4,114-4,169, 4 4,138-4,149, 8 4,083-4,108): a launch's LM-control phases overlap the next one's search
+    "C5": dict(batch=125, map_points=10_000_000, cols=2048, steps=2, warmup=1, pipeline=3),
 }
 
 

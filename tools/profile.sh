@@ -14,7 +14,7 @@ rc=$?; echo "trace $CFG rc=$rc"; case $rc in 0) ;; *) exit $rc;; esac
 fi
 case $CFG in
   C2) PMC_ARGS="--steps 2 --warmup 1 --streams 1 --batch 128" ;;
-  C5) PMC_ARGS="--steps 1 --warmup 1 --streams 1" ;;
+  C5) PMC_ARGS="--steps 1 --warmup 1 --streams 1 --pipeline 1" ;;
   *)  PMC_ARGS="--steps 6 --warmup 2" ;;
 esac
 PMC_ARGS="$PMC_ARGS ${PMC_EXTRA:-}"   # e.g. C3 / C4: --opt LM_LOOP=0 --no-prefetch (the r04 C3 PMC pass faulted with both on)
