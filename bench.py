@@ -76,6 +76,9 @@ def parse(argv=None):
                     help="C5: contexts per GPU taking whole launches of the pass in turn (launch j on context j mod "
                          "P, its previous launch waited for first), so one launch's solver phases overlap the "
                          "next one's search")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="C2: at most this many of the --streams contexts' launches in flight (the next one "
+                         "launched when the oldest finishes; default: all)")
     ap.add_argument("--map-points", type=int, default=None)
     ap.add_argument("--cols", type=int, default=None)
     ap.add_argument("--outer", type=int, default=5)
@@ -550,6 +553,20 @@ def run_batch(args, d):
         for c0 in range(0, n_units, chunk):
             nb = min(chunk, n_units - c0)
             parts = [(i, cx, c0 + i * sub_b, min(sub_b, nb - i * sub_b)) for i, cx in enumerate(ctxs) if nb > i * sub_b]
+            W = len(parts) if not args.inflight else max(1, min(args.inflight, len(parts)))
+            if W < len(parts):                               # a window of W launches in flight, oldest waited first
+                for k2, (i, cx, a, m) in enumerate(parts):
+                    if k2 >= W:
+                        _, cw, aw, mw = parts[k2 - W]
+                        poses[aw:aw + mw], st = cw.batch_wait(mw)
+                        matches[aw:aw + mw] = [s.edge_matches + s.surf_matches for s in st]
+                    t_enq = time.perf_counter()
+                    cx.batch_launch(guesses[a:a + m])
+                    enq += time.perf_counter() - t_enq
+                for i, cx, a, m in parts[len(parts) - W:]:
+                    poses[a:a + m], st = cx.batch_wait(m)
+                    matches[a:a + m] = [s.edge_matches + s.surf_matches for s in st]
+                continue
             for i, cx, a, m in parts:                        # every context's batch enqueued before any wait
                 t_enq = time.perf_counter()
                 cx.batch_launch(guesses[a:a + m])
