@@ -363,6 +363,21 @@ def solo_launches(ctxs, guesses_of):
     return sum_stats(stats) if stats else None
 
 
+def in_turn(n_units, chunk, P):
+    """Launch / wait schedule of a pass whose launches of `chunk` units are taken in turn by P contexts (launch j
+    on context j mod P, that context's previous launch waited for first; the rest waited oldest first at the
+    end): a list of ("launch" | "wait", context, first unit, count)."""
+    ev, busy, order = [], [None] * P, []
+    for j, c0 in enumerate(range(0, n_units, chunk)):
+        ci, nb = j % P, min(chunk, n_units - c0)
+        if busy[ci] is not None:
+            ev.append(("wait", ci) + busy[ci])
+        ev.append(("launch", ci, c0, nb))
+        busy[ci] = (c0, nb)
+        order = [x for x in order if x != ci] + [ci]
+    return ev + [("wait", ci) + busy[ci] for ci in order]
+
+
 def apply_options(args, ctxs):
     """--opt NAME=V on every context (lmsf_set_option)."""
     from lmsf import _lib
@@ -523,23 +538,14 @@ def run_batch(args, d):
 
     def pipelined_step():
         enq = 0.0
-        busy = [None] * P                                    # per context: its launch in flight (first unit, count)
-        order = []
-        for j, c0 in enumerate(range(0, n_units, chunk)):
-            ci, nb = j % P, min(chunk, n_units - c0)
-            if busy[ci] is not None:
-                a, m = busy[ci]
+        for kind, ci, a, m in in_turn(n_units, chunk, P):
+            if kind == "wait":
                 poses[a:a + m], st = ctxs[ci].batch_wait(m)
                 matches[a:a + m] = [s.edge_matches + s.surf_matches for s in st]
-            t_enq = time.perf_counter()
-            ctxs[ci].batch_launch(guesses[c0:c0 + nb])
-            enq += time.perf_counter() - t_enq
-            busy[ci] = (c0, nb)
-            order = [x for x in order if x != ci] + [ci]
-        for ci in order:
-            a, m = busy[ci]
-            poses[a:a + m], st = ctxs[ci].batch_wait(m)
-            matches[a:a + m] = [s.edge_matches + s.surf_matches for s in st]
+            else:
+                t_enq = time.perf_counter()
+                ctxs[ci].batch_launch(guesses[a:a + m])
+                enq += time.perf_counter() - t_enq
         t_c = time.perf_counter()
         exchange_poses(cfg, poses, gathered, args.pairs, world, d.dev)
         coll_s.append(time.perf_counter() - t_c)

@@ -6,6 +6,8 @@ import subprocess
 import sys
 import types
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.path.join(REPO, "bench.py")
 
@@ -78,3 +80,24 @@ def test_load_traffic_matches_workload(tmp_path):
     assert bench.load_traffic(str(p), config="C2", batch=128, map_points=10)["hbm_bytes_per_launch"] == 5
     assert bench.load_traffic(str(p), config="C2", batch=64, map_points=10) is None
     assert bench.load_traffic(str(tmp_path / "missing.json"), config="C2") is None
+
+
+@pytest.mark.parametrize("n_units,chunk,P", [(1000, 125, 1), (1000, 125, 3), (1000, 125, 8), (1000, 125, 9),
+                                              (7, 3, 2), (0, 125, 3)])
+def test_in_turn_schedule(n_units, chunk, P):
+    """C5's pipelined pass (bench.py --pipeline): every unit launched once, a context's launch waited for
+    before it is reused and before the pass ends, at most P launches in flight."""
+    ev = _bench_module().in_turn(n_units, chunk, P)
+    launched, inflight = [], {}
+    for kind, ci, a, m in ev:
+        assert 0 <= ci < P
+        if kind == "launch":
+            assert ci not in inflight
+            inflight[ci] = (a, m)
+            launched.append((a, m))
+            assert len(inflight) <= P
+        else:
+            assert inflight.pop(ci) == (a, m)
+    assert not inflight
+    covered = sorted(u for a, m in launched for u in range(a, a + m))
+    assert covered == list(range(n_units))
