@@ -220,7 +220,8 @@ lmsf_status lmsf_batch_copy_features(lmsf_ctx* ctx, int32_t slot, int32_t kind, 
 /* ---- context options (not on the reference surface): algorithm switches of the build.
  * Results do not depend on them (the memo switches are exact, DESIGN.md section 4 "Query memo"); they
  * exist so tests can compare the paths in one process and a caller can rule a path out.  Values 0 | 1;
- * defaults 1 except LMSF_OPT_GRAPH and LMSF_OPT_LOOP_FAULT_TEST 0. */
+ * defaults 1 except LMSF_OPT_GRAPH and the testing options (LOOP_FAULT_TEST, GROWTH_TEST, FAULT_INJECT) 0;
+ * FAULT_INJECT also takes 2. */
 #define LMSF_OPT_QUERY_MEMO 0   /* 1: outer iterations > 0 reuse 5-NN sets that provably did not change */
 #define LMSF_OPT_MEMO_REFIT 1   /* 1: a reused set in a new order is refitted without a walk */
 #define LMSF_OPT_MEMO_EXACT 2   /* 1: keep the set when its farthest point is nearer than s6 - d (0: 2d < s6 - s5) */
@@ -234,7 +235,14 @@ lmsf_status lmsf_batch_copy_features(lmsf_ctx* ctx, int32_t slot, int32_t kind, 
                                  *    grid is co-resident (lm_loop_kernel); 0: the 9-launch form (default 1) */
 #define LMSF_OPT_LOOP_FAULT_TEST 8 /* 1 (testing only): lm_loop_kernel's bounded waits give up at once, forcing the
                                  *    fault and its recovery -- the Solve re-run on the 9-launch form (default 0) */
-#define LMSF_OPT_COUNT 9
+#define LMSF_OPT_GROWTH_TEST 9  /* 1 (testing only): map grids and voxel-filter workspaces grow to each request exactly
+                                 *    and window grids start at 2^10 cells, so a tracker's buffers are regrown at
+                                 *    nearly every keyframe commit (on the commit streams) (default 0) */
+#define LMSF_OPT_FAULT_INJECT 10 /* 1 | 2 (testing only): the next voxel filters' first radix pass takes a stale
+                                 *    prefix (1: an out-of-range scatter) or meets a foreign look-back word (2); the
+                                 *    device checks flag it and the next Solve / batch wait fails with LMSF_ERR_HIP
+                                 *    "device look-back fault" (default 0) */
+#define LMSF_OPT_COUNT 11
 lmsf_status lmsf_set_option(lmsf_ctx* ctx, int32_t option, int32_t value);
 
 /* ---- diagnostics used by the parity tests and the roofline report (not on the reference surface) */
@@ -286,6 +294,8 @@ typedef struct {
     int64_t refit_queries;
     int64_t loop_recoveries;  /* solves whose single-launch LM loop gave up a bounded wait and were re-run on
                                * the 9-launch form (results as without the fault) */
+    int64_t buffer_growths;   /* map-grid buffer growths since the context was created (not reset: the
+                               * growth test checks that a tracker's window grids were regrown) */
 } lmsf_kernel_stats;
 lmsf_status lmsf_kernel_stats_get(lmsf_ctx* ctx, lmsf_kernel_stats* out);
 lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* ctx, int32_t mode);

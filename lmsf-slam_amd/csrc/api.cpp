@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cstdarg>
 #include <cstdlib>
@@ -36,6 +37,8 @@ struct DevMap {
     float lim1 = 1.f;
     bool orig_borrowed = false;       // a dense map's first-pass grid: orig is its 1 m grid's
     uint64_t build_id = 0;            // bumped by every build (a first-pass grid records the one it follows)
+    int64_t growths = 0;              // buffer growths (lmsf_kernel_stats: the growth test checks they happened)
+    uint64_t skipped_build = 0;       // first-pass grid: the map build it was refused for (not retried)
     uint64_t src_build = 0;
     // occupied-slice count of the last build, read back without blocking: lim1 (the pruned walk's
     // first radius) is resolved only by a launch that can take the pruned one-lane walk
@@ -84,6 +87,13 @@ float knn_first_radius2(size_t n, unsigned long long occupied) {
 
 }  // namespace
 
+uint32_t lmsf::next_lookback_epoch() {
+    static std::atomic<uint32_t> counter{0};
+    uint32_t e;
+    while ((e = counter.fetch_add(1u, std::memory_order_relaxed) + 1u) == 0u) {}
+    return e;
+}
+
 // Host wait on a stream of the latency-bound single-scan paths (extraction read-back, solve, tracker
 // commit).  A/B builds: LMSF_SPIN_SYNC=1 polls hipStreamQuery instead of hipStreamSynchronize: on one box (C4
 // / C3 ms per scan, two runs each: 1.55, 1.74 / 1.50, 1.73 spinning vs 1.63, 1.71 / 1.52, 1.50 blocking)
@@ -113,10 +123,11 @@ struct lmsf_ctx {
     std::string err;
     mutable std::mutex err_mu;        // a tracker's commit worker may report an error beside the caller
     mutable char err_out[512] = {};   // lmsf_last_error's copy: written only by the caller's thread
-    int opt[LMSF_OPT_COUNT] = {1, 1, 1, 1, 1, 0, 1, 1, 0};   // lmsf_set_option (defaults: lmsf.h)
+    int opt[LMSF_OPT_COUNT] = {1, 1, 1, 1, 1, 0, 1, 1, 0, 0, 0};   // lmsf_set_option (defaults: lmsf.h)
     bool loop_off_once = false;       // the re-run of a faulted LM loop (9-launch form, direct launches)
     int64_t loop_recoveries = 0;
     int last_launch_iters = 0;        // outer iterations of the last batch launch (its re-run after a loop fault)
+    int last_launch_n = 0;            // and its slots
     // record capture (lmsf_batch_capture): device rows [n_cap][kCaptureIters][F] of the captured slots
     std::vector<int> cap_slots;
     lmsf_record* cap_rec = nullptr;
@@ -175,6 +186,7 @@ struct lmsf_ctx {
     int* n_pos = nullptr;
     bool qorder_valid = false;        // the slots' features came from the extraction kernels
     int* d_error = nullptr;           // [0] extraction capacity flags, [8..10] pack3, [16] LM loop wait gave up,
+                                      // [17] device fault word (look-back / scatter checks, lmsf_internal.h),
                                       // [24] / [40..42]: the same two of a prefetched extraction,
                                       // [48]: dense-map pass-2 list count (BatchView::p2count)
     // lmsf_prefetch_features: the next scan extracted on pre_stream into a second set of the outputs the
@@ -230,7 +242,7 @@ struct lmsf_ctx {
     double* h_poses = nullptr;        // pinned [B*7]
     SolveState* h_st = nullptr;       // pinned [B]
     int* h_counts = nullptr;          // pinned [2*B]
-    int* h_pack = nullptr;            // pinned [4]: packed single-scan read-back (counts, error flag)
+    int* h_pack = nullptr;            // pinned [8]: packed single-scan read-back (counts, error flag; [3..4] = d_error[16..17])
     std::vector<float> host_scan[3];  // SetInputTarget copies (slot 0)
     bool scan_dirty = false;
     bool features_on_device = false;  // slot 0 features came from lmsf_extract_features
@@ -391,27 +403,32 @@ namespace {
 // once the stream has drained that, grid_finish sizes the grid and sorts the points into cells.
 // n bounds the count, n_dev (device) gives it when the producer's size is still on the device.
 // Sorted points carry w = base + original index.
-lmsf_status grid_reserve(lmsf_ctx* c, DevMap& m, size_t n) {
+//
+// Growth is stream-ordered (galloc / gfree, lmsf_internal.h) on the stream s of the build: every earlier reader
+// of a map's buffers is ordered before s -- searches run on the context stream, a tracker's window build runs on
+// an aux stream that waited for the context stream (ev_fork) after the previous build was joined into it
+// (ev_join), and set_map / the prior grid / the first-pass grid are built on the context stream itself.
+size_t grow_to(const lmsf_ctx* c, size_t need, size_t cap) {
+    return c->opt[LMSF_OPT_GROWTH_TEST] ? need : grow_cap(need, cap);
+}
+
+lmsf_status grid_reserve(lmsf_ctx* c, DevMap& m, size_t n, hipStream_t s) {
     if (n > (size_t)INT32_MAX) return c->fail(LMSF_ERR_CAPACITY, "map too large (%zu points)", n);
     if (!m.d_bb) {
         HIPCHK(c, hipMalloc((void**)&m.d_bb, 32 * sizeof(int)));
-        HIPCHK(c, hipMemset(m.d_bb, 0, 32 * sizeof(int)));
+        HIPCHK(c, hipMemsetAsync(m.d_bb, 0, 32 * sizeof(int), s));   // on the stream of its readers
         HIPCHK(c, hipHostMalloc((void**)&m.h_bb, 16 * sizeof(int), hipHostMallocDefault));
-        // a null-stream memset is not ordered before the context's non-blocking streams: complete it here
-        HIPCHK(c, hipDeviceSynchronize());
     }
     if (n > m.cap) {
-        // growth (rare; a tracker window's grid is grown by a commit worker): kernels of the last build or
-        // search may still read these on another stream -- the device drains before they are freed
-        if (m.cap) HIPCHK(c, hipDeviceSynchronize());
-        hipFree(m.orig); hipFree(m.pts); hipFree(m.cell);
+        gfree(m.orig, s); gfree(m.pts, s); gfree(m.cell, s);
         m.orig = nullptr; m.pts = nullptr; m.cell = nullptr;
-        const size_t cap = std::min(grow_cap(n, m.cap), (size_t)INT32_MAX);
+        const size_t cap = std::min(grow_to(c, n, m.cap), (size_t)INT32_MAX);
         m.cap = 0;
-        HIPCHK(c, dalloc(&m.orig, cap));
-        HIPCHK(c, dalloc(&m.pts, cap));
-        HIPCHK(c, dalloc(&m.cell, cap));
+        HIPCHK(c, galloc(&m.orig, cap, s));
+        HIPCHK(c, galloc(&m.pts, cap, s));
+        HIPCHK(c, galloc(&m.cell, cap, s));
         m.cap = cap;
+        ++m.growths;
     }
     return LMSF_OK;
 }
@@ -419,7 +436,7 @@ lmsf_status grid_reserve(lmsf_ctx* c, DevMap& m, size_t n) {
 // xyzi == nullptr: a producer already wrote the points into m.orig and their box + count into m.d_bb
 // (ctx_window_target), only the read-back is left.
 lmsf_status grid_stage(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, const int* n_dev, hipStream_t s) {
-    lmsf_status rc = grid_reserve(c, m, n);
+    lmsf_status rc = grid_reserve(c, m, n, s);
     if (rc) return rc;
     if (xyzi) {
         // host or device source (unified addressing): the tracker rebuilds from device-resident maps
@@ -433,43 +450,47 @@ lmsf_status grid_stage(lmsf_ctx* c, DevMap& m, const float* xyzi, size_t n, cons
 // counts / offsets / fill for at least need cells (grown geometrically)
 lmsf_status grid_cells_reserve(lmsf_ctx* c, DevMap& m, size_t need, hipStream_t s) {
     if (need <= m.cells_cap) return LMSF_OK;
-    if (m.cells_cap) HIPCHK(c, hipDeviceSynchronize());   // growth: the last build / search may still read them
-    hipFree(m.counts); hipFree(m.off); hipFree(m.fill); hipFree(m.scan_tmp);
+    gfree(m.counts, s); gfree(m.off, s); gfree(m.fill, s); gfree(m.scan_tmp, s);
     m.counts = m.off = m.fill = nullptr;
     m.scan_tmp = nullptr;
-    const size_t cap = std::min(grow_cap(need, m.cells_cap), kMaxCells + 1);
+    const size_t cap = std::min(grow_to(c, need, m.cells_cap), kMaxCells + 1);
     m.cells_cap = 0;
-    HIPCHK(c, dalloc(&m.counts, cap));
-    HIPCHK(c, dalloc(&m.off, cap));
-    HIPCHK(c, dalloc(&m.fill, cap));
+    HIPCHK(c, galloc(&m.counts, cap, s));
+    HIPCHK(c, galloc(&m.off, cap, s));
+    HIPCHK(c, galloc(&m.fill, cap, s));
     m.scan_tmp_bytes = 0;
     HIPCHK(c, exclusive_scan_u32(m.counts, m.off, cap, nullptr, m.scan_tmp_bytes, s));
-    HIPCHK(c, hipMalloc(&m.scan_tmp, std::max<size_t>(m.scan_tmp_bytes, 16)));
+    unsigned char* tmp = nullptr;
+    HIPCHK(c, galloc(&tmp, std::max<size_t>(m.scan_tmp_bytes, 16), s));
+    m.scan_tmp = tmp;
     m.cells_cap = cap;
+    ++m.growths;
     return LMSF_OK;
 }
 
 // The grid of points a producer left in m.orig with their box + count in m.d_bb, built on stream s without a
 // host wait (launch_grid_build_dev); grid_finish_device takes the box read-back and sets the view.  Cells
-// are allocated from the last build's size (first build: 2^21, ~8 MB per array): a larger box is rebuilt by
-// the host path at the finish.
+// are allocated from the last build's size (first build: 2^21, ~8 MB per array; 2^10 under
+// LMSF_OPT_GROWTH_TEST): a larger box is rebuilt by the host path at the finish.
 lmsf_status grid_build_device(lmsf_ctx* c, DevMap& m, size_t n_max, int base, hipStream_t s) {
-    lmsf_status rc = grid_cells_reserve(c, m, std::max<size_t>(m.cells_cap, (size_t)1 << 21), s);
+    const size_t first = c->opt[LMSF_OPT_GROWTH_TEST] ? (size_t)1 << 10 : (size_t)1 << 21;
+    lmsf_status rc = grid_cells_reserve(c, m, std::max<size_t>(m.cells_cap, first), s);
     if (rc) return rc;
     const size_t tiles = grid_scan_tiles(m.cells_cap);
     if (tiles > m.scan_state_tiles) {
-        if (m.scan_state_tiles) HIPCHK(c, hipDeviceSynchronize());   // growth: the last build may still read it
-        hipFree(m.scan_state);
+        gfree(m.scan_state, s);
         m.scan_state = nullptr;
         m.scan_state_tiles = 0;
-        HIPCHK(c, hipMalloc((void**)&m.scan_state, tiles * sizeof(unsigned long long)));
-        HIPCHK(c, hipMemsetAsync(m.scan_state, 0, tiles * sizeof(unsigned long long), s));   // epoch 0: unpublished
+        HIPCHK(c, galloc(&m.scan_state, tiles, s));
+        HIPCHK(c, hipMemsetAsync(m.scan_state, 0, tiles * sizeof(unsigned long long), s));   // epoch 0: older than any
         m.scan_state_tiles = tiles;
+        ++m.growths;
     }
     if (!m.ev_bb) HIPCHK(c, hipEventCreateWithFlags(&m.ev_bb, hipEventDisableTiming));
-    if (++m.scan_epoch == 0) ++m.scan_epoch;
+    m.scan_epoch = next_lookback_epoch();
     HIPCHK(c, launch_grid_build_dev(m.orig, (int)n_max, grid_slices(), m.d_bb, m.counts, m.off, m.fill, m.cells_cap,
-                                    m.cell, m.pts, base, m.scan_state, m.scan_epoch, m.h_bb, m.ev_bb, s));
+                                    m.cell, m.pts, base, m.scan_state, m.scan_epoch, m.h_bb, m.ev_bb,
+                                    c->d_error + 17, s));
     m.dev_pending = true;
     return LMSF_OK;
 }
@@ -521,7 +542,7 @@ lmsf_status grid_finish(lmsf_ctx* c, DevMap& m, int base, hipStream_t s, bool de
     HIPCHK(c, launch_map_count(m.orig, n, sx, m.ox, m.oy, m.oz, nx, ny, nz, m.cell, m.counts, s));
     size_t tb = m.scan_tmp_bytes;
     HIPCHK(c, exclusive_scan_u32(m.counts, m.off, cells + 1, m.scan_tmp, tb, s));
-    HIPCHK(c, launch_map_scatter(m.orig, n, m.cell, m.off, m.fill, m.pts, base, s));
+    HIPCHK(c, launch_map_scatter(m.orig, n, m.cell, m.off, m.fill, m.pts, base, c->d_error + 17, s));
     m.lim1 = 1.f;   // provisional (plain walk) until resolve_lim1
     m.n = n;
     if (!density) {
@@ -571,6 +592,14 @@ int fine_cells_per_m(float lim1) {
     while (sy < sy_max && lim1 * 1.00001f * (float)(4 * sy * sy) <= 1.0f) sy *= 2;
     return sy;
 }
+// The first-pass grid has 8 x 2 x 2 = 32 cells per cubic metre against the 1 m grid's 4: it may take at most
+// kFineBudget times the 1 m grid's cells (plus a floor for small maps).  A grid over that budget, or one whose
+// allocation fails, is not built -- the 1 m grid serves the first pass, results unchanged (a wide
+// map extent could ask for ~12 GB per kind and failed the launch) -- and the refusal is recorded against the map
+// build, so the box pass and its host wait are not repeated at every launch.
+constexpr size_t kFineBudget = 8;
+constexpr size_t kFineFloorCells = (size_t)1 << 22;
+
 lmsf_status build_fine(lmsf_ctx* c, int kind) {
     DevMap& m = c->map[kind];
     DevMap& f = c->fine[kind];
@@ -581,40 +610,55 @@ lmsf_status build_fine(lmsf_ctx* c, int kind) {
         return LMSF_OK;
     }
     if (f.n > 0 && f.src_build == m.build_id) return LMSF_OK;
+    if (f.skipped_build == m.build_id) return LMSF_OK;   // refused for this map build already
     f.n = 0;
     hipStream_t s = c->stream;
+    auto refuse = [&]() {
+        f.skipped_build = m.build_id;
+        f.n = 0;
+        (void)hipGetLastError();   // a failed allocation leaves its error behind
+        return LMSF_OK;
+    };
     if (!f.d_bb) {
         HIPCHK(c, hipMalloc((void**)&f.d_bb, 32 * sizeof(int)));
-        HIPCHK(c, hipMemset(f.d_bb, 0, 32 * sizeof(int)));
+        HIPCHK(c, hipMemsetAsync(f.d_bb, 0, 32 * sizeof(int), s));
         HIPCHK(c, hipHostMalloc((void**)&f.h_bb, 16 * sizeof(int), hipHostMallocDefault));
-        HIPCHK(c, hipDeviceSynchronize());
-    }
-    if ((size_t)m.n > f.cap) {
-        if (f.cap) HIPCHK(c, hipDeviceSynchronize());
-        hipFree(f.pts); hipFree(f.cell);
-        f.pts = nullptr; f.cell = nullptr;
-        f.cap = 0;
-        HIPCHK(c, dalloc(&f.pts, (size_t)m.n));
-        HIPCHK(c, dalloc(&f.cell, (size_t)m.n));
-        f.cap = (size_t)m.n;
     }
     HIPCHK(c, launch_map_bbox(m.orig, m.n, nullptr, kFineSx, f.d_bb, s, kFineSy));
     HIPCHK(c, hipMemcpyAsync(f.h_bb, f.d_bb, 7 * sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     const int* bb = f.h_bb;
-    const int nx = bb[3] - bb[0] + 1, ny = bb[4] - bb[1] + 1, nz = bb[5] - bb[2] + 1;
-    const size_t cells = (size_t)nx * ny * nz;
-    if (nx <= 0 || ny <= 0 || nz <= 0 || cells > kMaxCells) return LMSF_OK;   // no first-pass grid: the 1 m grid serves
-    lmsf_status rc = grid_cells_reserve(c, f, cells + 1, s);
-    if (rc) return rc;
+    const long long nx = (long long)bb[3] - bb[0] + 1, ny = (long long)bb[4] - bb[1] + 1, nz = (long long)bb[5] - bb[2] + 1;
+    if (nx <= 0 || ny <= 0 || nz <= 0) return refuse();
+    const size_t cells = (size_t)nx * (size_t)ny * (size_t)nz;
+    const size_t coarse = (size_t)m.nx * (size_t)m.ny * (size_t)m.nz;
+    if (cells > kMaxCells || cells > std::max(kFineBudget * coarse, kFineFloorCells)) return refuse();
+    if ((size_t)m.n > f.cap) {
+        gfree(f.pts, s); gfree(f.cell, s);
+        f.pts = nullptr; f.cell = nullptr;
+        f.cap = 0;
+        if (galloc(&f.pts, (size_t)m.n, s) != hipSuccess || galloc(&f.cell, (size_t)m.n, s) != hipSuccess) {
+            gfree(f.pts, s); gfree(f.cell, s);
+            f.pts = nullptr; f.cell = nullptr;
+            return refuse();
+        }
+        f.cap = (size_t)m.n;
+    }
+    if (grid_cells_reserve(c, f, cells + 1, s) != LMSF_OK) {
+        gfree(f.counts, s); gfree(f.off, s); gfree(f.fill, s); gfree(f.scan_tmp, s);
+        f.counts = f.off = f.fill = nullptr;
+        f.scan_tmp = nullptr;
+        f.cells_cap = 0;
+        return refuse();
+    }
     f.ox = bb[0]; f.oy = bb[1]; f.oz = bb[2];
-    f.nx = nx; f.ny = ny; f.nz = nz; f.sx = kFineSx; f.sy = kFineSy;
+    f.nx = (int)nx; f.ny = (int)ny; f.nz = (int)nz; f.sx = kFineSx; f.sy = kFineSy;
     unsigned long long* d_occ = reinterpret_cast<unsigned long long*>(f.d_bb + 8);
     HIPCHK(c, launch_grid_clear(f.counts, f.fill, cells + 1, d_occ, s));
-    HIPCHK(c, launch_map_count(m.orig, m.n, kFineSx, f.ox, f.oy, f.oz, nx, ny, nz, f.cell, f.counts, s, kFineSy));
+    HIPCHK(c, launch_map_count(m.orig, m.n, kFineSx, f.ox, f.oy, f.oz, f.nx, f.ny, f.nz, f.cell, f.counts, s, kFineSy));
     size_t tb = f.scan_tmp_bytes;
     HIPCHK(c, exclusive_scan_u32(f.counts, f.off, cells + 1, f.scan_tmp, tb, s));
-    HIPCHK(c, launch_map_scatter(m.orig, m.n, f.cell, f.off, f.fill, f.pts, 0, s));
+    HIPCHK(c, launch_map_scatter(m.orig, m.n, f.cell, f.off, f.fill, f.pts, 0, c->d_error + 17, s));
     f.orig = m.orig;
     f.orig_borrowed = true;
     f.lim1 = m.lim1;
@@ -679,9 +723,9 @@ lmsf_status sync_slot0_features(lmsf_ctx* c) {
 }
 
 // Enqueue the registration of slots [0, nb): outer iterations of match + solver control.
+// Called by enqueue_solve only, after the maps were resolved there (never inside a stream capture: the first-pass
+// grid build and lim1 read back to the host).
 lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
-    lmsf_status rl = resolve_all_lim1(c, (size_t)c->F * nb);
-    if (rl) return rl;
     BatchView bv = c->bview(nb);
     const GridView ge = c->map[LMSF_EDGE].view(), gs = c->map[LMSF_SURF].view();
     const GridView ge2 = c->prior[LMSF_EDGE].view(), gs2 = c->prior[LMSF_SURF].view();
@@ -803,9 +847,12 @@ std::vector<unsigned char> solve_key(lmsf_ctx* c, int nb, int iters) {
 }
 
 // State init from d_poses + the registration of slots [0, nb) on c->stream.
-lmsf_status enqueue_solve(lmsf_ctx* c, int nb, int iters) {
-    lmsf_status rl = resolve_all_lim1(c, (size_t)c->F * nb);   // host read-back: never inside a capture
-    if (rl) return rl;
+// recover: the re-run of a faulted LM loop on the maps of the launch it repeats (no settle, no map resolution).
+lmsf_status enqueue_solve(lmsf_ctx* c, int nb, int iters, bool recover = false) {
+    if (!recover) {
+        lmsf_status rl = resolve_all_lim1(c, (size_t)c->F * nb);   // host read-back: never inside a capture
+        if (rl) return rl;
+    }
     hipStream_t s = c->stream;
     // direct launches: graphs off, timing events not yet collected, or a record capture
     if (!c->opt[LMSF_OPT_GRAPH] || c->ev_used != 0 || !c->cap_slots.empty() || c->loop_off_once) {
@@ -886,7 +933,7 @@ lmsf_status loop_recover(lmsf_ctx* c, int nb, int iters) {
     c->h_pack[3] = 0;
     c->loop_recoveries++;
     c->loop_off_once = true;
-    const lmsf_status rc = enqueue_solve(c, nb, iters);
+    const lmsf_status rc = enqueue_solve(c, nb, iters, true);
     c->loop_off_once = false;
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, (size_t)nb * sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
@@ -894,6 +941,25 @@ lmsf_status loop_recover(lmsf_ctx* c, int nb, int iters) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->h_pack[3]) return c->fail(LMSF_ERR_HIP, "LM loop fault persisted on the 9-launch form");
     return collect_timing(c, true);
+}
+
+// The device fault word (d_error[17], read back beside the LM-loop flag): a look-back or scatter check failed in a
+// map build or a voxel filter since the last report (radix.h).  The word is cleared and the call fails.
+// bits < 0: not read back yet.
+lmsf_status report_fault(lmsf_ctx* c, int bits) {
+    if (bits < 0) {
+        HIPCHK(c, hipMemcpyAsync(&c->h_pack[4], c->d_error + 17, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        bits = c->h_pack[4];
+    }
+    HIPCHK(c, hipMemsetAsync(c->d_error + 17, 0, sizeof(int), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return c->fail(LMSF_ERR_HIP, "device look-back fault (flags 0x%x:%s%s%s%s%s)", bits,
+                   bits & kFaultRadixScatter ? " radix scatter out of range" : "",
+                   bits & kFaultLookbackWait ? " look-back wait exhausted" : "",
+                   bits & kFaultForeignEpoch ? " foreign look-back epoch" : "",
+                   bits & kFaultSegment ? " voxel segments out of range" : "",
+                   bits & kFaultGridScatter ? " grid scatter out of range" : "");
 }
 
 int outer_iterations_for_solve(lmsf_ctx* c) {
@@ -949,16 +1015,16 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
     if (c->raw_pending && c->ev_raw_ready) hipEventSynchronize(c->ev_raw_ready);   // an upload on the shared stream
     if (c->sg.exec) hipGraphExecDestroy(c->sg.exec);
+    if (c->stream) hipStreamSynchronize(c->stream);
     for (DevMap* ms : {c->map, c->prior, c->fine}) {
         for (int k = 0; k < 3; ++k) {
-            DevMap& m = ms[k];
-            if (!m.orig_borrowed) hipFree(m.orig);
-            hipFree(m.pts); hipFree(m.cell); hipFree(m.counts); hipFree(m.off); hipFree(m.fill);
-            hipFree(m.scan_tmp);
+            DevMap& m = ms[k];   // stream-ordered allocations (galloc): freed on the context stream
+            if (!m.orig_borrowed) gfree(m.orig, c->stream);
+            gfree(m.pts, c->stream); gfree(m.cell, c->stream); gfree(m.counts, c->stream); gfree(m.off, c->stream);
+            gfree(m.fill, c->stream); gfree(m.scan_tmp, c->stream); gfree(m.scan_state, c->stream);
             if (m.h_occ) hipHostFree(m.h_occ);
             if (m.ev_occ) hipEventDestroy(m.ev_occ);
             hipFree(m.d_bb);
-            hipFree(m.scan_state);
             if (m.ev_bb) hipEventDestroy(m.ev_bb);
             if (m.h_bb) hipHostFree(m.h_bb);
         }
@@ -975,6 +1041,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (c->ev_pre) hipEventDestroy(c->ev_pre);
     if (c->ev_pre_after) hipEventDestroy(c->ev_pre_after);
     if (c->pre_stream) hipStreamDestroy(c->pre_stream);
+    if (c->stream) hipStreamSynchronize(c->stream);   // the stream-ordered frees above
     hipFree(c->cap_rec);
     hipFree(c->cap_nn);
     hipFree(c->cap_pose);
@@ -1088,7 +1155,7 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(hipHostMalloc((void**)&c->h_poses, B * 7 * sizeof(double), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_st, B * sizeof(SolveState), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_counts, 2 * B * sizeof(int), hipHostMallocDefault));
-    CHK(hipHostMalloc((void**)&c->h_pack, 4 * sizeof(int), hipHostMallocDefault));
+    CHK(hipHostMalloc((void**)&c->h_pack, 8 * sizeof(int), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_raw_counts, B * sizeof(int), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_raw_off, B * sizeof(int64_t), hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&c->h_off, B * sizeof(int64_t), hipHostMallocDefault));
@@ -1190,8 +1257,9 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     rc = enqueue_solve(c, 1, iters);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, stream_wait(c->stream));
+    if (c->h_pack[4]) return report_fault(c, c->h_pack[4]);
     rc = collect_timing(c, true);
     if (rc) return rc;
     if (c->h_pack[3]) {
@@ -1415,7 +1483,9 @@ lmsf_status lmsf_common_process(lmsf_ctx* c, const float* xyzi, size_t n, const 
     }
     if (p->voxel_leaf > 0.f && m > 0) {                              // :104
         int nv = 0;
-        HIPCHK(c, c->voxel.run(cur, m, p->voxel_leaf, other, &nv, s));
+        const hipError_t ve = c->voxel.run(cur, m, p->voxel_leaf, other, &nv, c->d_error + 17, s);
+        if (ve == hipErrorIllegalState) return report_fault(c, -1);
+        HIPCHK(c, ve);
         m = nv;
         std::swap(cur, other);
     }
@@ -1480,7 +1550,9 @@ lmsf_status lmsf_voxel_filter(lmsf_ctx* c, const float* xyzi, size_t n, float le
     }
     HIPCHK(c, hipMemcpyAsync(c->vox_in, xyzi, n * sizeof(float4), hipMemcpyDefault, c->stream));
     int nv = 0;
-    HIPCHK(c, c->voxel.run(c->vox_in, (int)n, leaf, c->vox_out, &nv, c->stream));
+    const hipError_t ve = c->voxel.run(c->vox_in, (int)n, leaf, c->vox_out, &nv, c->d_error + 17, c->stream);
+    if (ve == hipErrorIllegalState) return report_fault(c, -1);
+    HIPCHK(c, ve);
     if (n_out) *n_out = (size_t)nv;
     if ((size_t)nv > cap) return c->fail(LMSF_ERR_CAPACITY, "output capacity %zu < %d voxels", cap, nv);
     HIPCHK(c, hipMemcpyAsync(out, c->vox_out, (size_t)nv * sizeof(float4), hipMemcpyDefault, c->stream));
@@ -1739,6 +1811,7 @@ lmsf_status lmsf_batch_launch(lmsf_ctx* c, int32_t n, const double* poses) {
     iters = std::min(iters, kMaxOuter);
     c->features_on_device = false;
     c->last_launch_iters = iters;
+    c->last_launch_n = n;
     return enqueue_solve(c, n, iters);
 }
 
@@ -1748,12 +1821,13 @@ lmsf_status lmsf_batch_wait(lmsf_ctx* c, int32_t n, double* poses, lmsf_solve_st
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, (size_t)n * sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
     int herr = 0;
     HIPCHK(c, hipMemcpyAsync(&herr, c->d_error, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->h_pack[4]) return report_fault(c, c->h_pack[4]);
     lmsf_status rc = collect_timing(c, true);
     if (rc) return rc;
-    if (c->h_pack[3]) {
-        rc = loop_recover(c, n, c->last_launch_iters);
+    if (c->h_pack[3]) {   // the launched slots are re-run (n may be fewer: ADVICE r04)
+        rc = loop_recover(c, std::max(n, c->last_launch_n), c->last_launch_iters);
         if (rc) return rc;
     }
     for (int i = 0; i < n; ++i) {
@@ -1782,7 +1856,8 @@ lmsf_status lmsf_batch_run(lmsf_ctx* c, int32_t n, double* poses, lmsf_solve_sta
 }
 
 lmsf_status lmsf_set_option(lmsf_ctx* c, int32_t option, int32_t value) {
-    if (!c || option < 0 || option >= LMSF_OPT_COUNT || (value != 0 && value != 1)) return LMSF_ERR_ARG;
+    if (!c || option < 0 || option >= LMSF_OPT_COUNT) return LMSF_ERR_ARG;
+    if (value != 0 && value != 1 && !(option == LMSF_OPT_FAULT_INJECT && value == 2)) return LMSF_ERR_ARG;
     c->opt[option] = value;
     return LMSF_OK;
 }
@@ -1987,6 +2062,10 @@ lmsf_status lmsf_kernel_stats_get(lmsf_ctx* c, lmsf_kernel_stats* out) {
     out->reused_queries = (int64_t)r;
     out->refit_queries = (int64_t)rf;
     out->loop_recoveries = c->loop_recoveries;
+    int64_t g = 0;
+    for (DevMap* ms : {c->map, c->prior, c->fine})
+        for (int k = 0; k < 3; ++k) g += ms[k].growths;
+    out->buffer_growths = g;
     return LMSF_OK;
 }
 
@@ -2005,6 +2084,8 @@ int grid_slices() {
 }
 
 hipStream_t ctx_stream(lmsf_ctx* c) { return c->stream; }
+int* ctx_fault_word(lmsf_ctx* c) { return c->d_error + 17; }
+int ctx_option(const lmsf_ctx* c, int option) { return c->opt[option]; }
 int ctx_device(const lmsf_ctx* c) { return c->cfg.device; }
 int ctx_feature_capacity(const lmsf_ctx* c) { return c->F; }
 bool ctx_features_on_device(const lmsf_ctx* c) { return c->features_on_device; }
@@ -2049,9 +2130,9 @@ lmsf_status ctx_window_stage(lmsf_ctx* c, int kind, const float4* d_pts, size_t 
     return grid_stage(c, c->map[kind], reinterpret_cast<const float*>(d_pts), n_max, n_dev, s);
 }
 
-lmsf_status ctx_window_target(lmsf_ctx* c, int kind, size_t n_max, float4** orig, int** bb) {
+lmsf_status ctx_window_target(lmsf_ctx* c, int kind, size_t n_max, float4** orig, int** bb, hipStream_t s) {
     DevMap& m = c->map[kind];
-    lmsf_status rc = grid_reserve(c, m, n_max);
+    lmsf_status rc = grid_reserve(c, m, n_max, s);
     if (rc) return rc;
     *orig = reinterpret_cast<float4*>(m.orig);
     *bb = m.d_bb;

@@ -78,11 +78,15 @@ hipError_t launch_count_nonzero(const uint32_t* counts, size_t n, unsigned long 
 // Scatter into cell order.  Order inside a cell is arbitrary: the search ranks candidates by the
 // total order (d2, original index), so results do not depend on it.
 __global__ void map_scatter_kernel(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
-                                   float4* sorted, int base) {
+                                   float4* sorted, int base, int* err) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int c = cell[i];
     const uint32_t pos = off[c] + atomicAdd(&fill[c], 1u);
+    if (pos >= (uint32_t)n) {   // never written outside the points (radix.h fault checks)
+        lb_fault(err, kFaultGridScatter);
+        return;
+    }
     const float4 p = pts[i];
     sorted[pos] = make_float4(p.x, p.y, p.z, __int_as_float(base + i));
 }
@@ -145,9 +149,9 @@ hipError_t launch_map_count(const float4* pts, int n, int sx, int ox, int oy, in
 }
 
 hipError_t launch_map_scatter(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
-                              float4* sorted, int base, hipStream_t s) {
+                              float4* sorted, int base, int* err, hipStream_t s) {
     hipLaunchKernelGGL(map_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pts, n, cell, off, fill, sorted,
-                       base);
+                       base, err);
     return hipGetLastError();
 }
 
@@ -220,11 +224,15 @@ __global__ void map_count_dev_kernel(const float4* pts, const int* bb, float sx,
 }
 
 __global__ void map_scatter_dev_kernel(const float4* pts, const int* bb, const int* cell, const uint32_t* off,
-                                       uint32_t* fill, float4* sorted, int base) {
+                                       uint32_t* fill, float4* sorted, int base, int* err) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= bb[6] || bb[10]) return;
     const int c = cell[i];
     const uint32_t pos = off[c] + atomicAdd(&fill[c], 1u);
+    if (pos >= (uint32_t)bb[6]) {   // the offsets came from the look-back scan: checked (radix.h)
+        lb_fault(err, kFaultGridScatter);
+        return;
+    }
     const float4 p = pts[i];
     sorted[pos] = make_float4(p.x, p.y, p.z, __int_as_float(base + i));
 }
@@ -234,7 +242,7 @@ __global__ void map_scatter_dev_kernel(const float4* pts, const int* bb, const i
 constexpr int kScanThreads = 1024, kScanPer = 16, kScanTile = kScanThreads * kScanPer;
 
 __global__ __launch_bounds__(kScanThreads) void scan_dev_kernel(const uint32_t* in, uint32_t* out, int* bb,
-                                                                unsigned long long* st, uint32_t epoch) {
+                                                                unsigned long long* st, uint32_t epoch, int* err) {
     __shared__ int s_tile;
     __shared__ uint32_t s_wave[kScanThreads / 64], s_before;
     if (bb[10] || bb[6] <= 0) return;
@@ -269,7 +277,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_dev_kernel(const uint32_t* 
             if (threadIdx.x == 0) lb_store(st, epoch, kLbInc, total);
         } else {
             if (threadIdx.x == 0) lb_store(st + tile, epoch, kLbAgg, total);
-            before = wave_lookback(st, tile, epoch);
+            before = wave_lookback(st, tile, epoch, err);
             if (threadIdx.x == 0) lb_store(st + tile, epoch, kLbInc, before + total);
         }
         if (threadIdx.x == 0) s_before = before;
@@ -301,7 +309,7 @@ size_t grid_scan_tiles(size_t cells_cap) { return (cells_cap + kScanTile - 1) / 
 hipError_t launch_grid_build_dev(const float4* orig, int n_max, int sx, int* d_bb, uint32_t* counts, uint32_t* off,
                                  uint32_t* fill, size_t cells_cap, int* cell, float4* sorted, int base,
                                  unsigned long long* scan_state, uint32_t epoch, int* h_bb, hipEvent_t ev_bb,
-                                 hipStream_t s) {
+                                 int* err, hipStream_t s) {
     if (n_max <= 0) return hipSuccess;
     const unsigned cb = (unsigned)std::min<size_t>(2048, (cells_cap + 255) / 256);
     hipLaunchKernelGGL(grid_clear_dev_kernel, dim3(std::max(cb, 1u)), dim3(256), 0, s, d_bb, counts, fill, cells_cap);
@@ -312,8 +320,8 @@ hipError_t launch_grid_build_dev(const float4* orig, int n_max, int sx, int* d_b
     const dim3 g((n_max + 255) / 256), b(256);
     hipLaunchKernelGGL(map_count_dev_kernel, g, b, 0, s, orig, d_bb, (float)sx, cell, counts);
     hipLaunchKernelGGL(scan_dev_kernel, dim3((unsigned)grid_scan_tiles(cells_cap + 1)), dim3(kScanThreads), 0, s,
-                       counts, off, d_bb, scan_state, epoch);
-    hipLaunchKernelGGL(map_scatter_dev_kernel, g, b, 0, s, orig, d_bb, cell, off, fill, sorted, base);
+                       counts, off, d_bb, scan_state, epoch, err);
+    hipLaunchKernelGGL(map_scatter_dev_kernel, g, b, 0, s, orig, d_bb, cell, off, fill, sorted, base, err);
     return hipGetLastError();
 }
 

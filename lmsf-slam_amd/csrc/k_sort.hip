@@ -29,8 +29,9 @@ constexpr int kLbWin = 8;                                 // tiles each of them 
 // read kLbWin consecutive predecessor tiles each (32 tiles per round trip, nearest first), and the digit's
 // part-0 thread combines the parts in order -- summing up to the first inclusive word, or up to the first
 // unpublished one, where the next round resumes.  Returns, to the part-0 thread of each digit, the count of
-// the digit in all earlier tiles.
-__device__ __forceinline__ uint32_t block_lookback(const unsigned long long* state, int tile, uint32_t epoch) {
+// the digit in all earlier tiles.  A foreign word (radix.h) ends the digit's walk and an exhausted wait ends all
+// of them, both flagged in *err.
+__device__ __forceinline__ uint32_t block_lookback(const unsigned long long* state, int tile, uint32_t epoch, int* err) {
     __shared__ uint32_t s_sum[kLbParts][kRadixDigits];
     __shared__ int s_stat[kLbParts][kRadixDigits];
     __shared__ int s_next[kRadixDigits];
@@ -53,6 +54,11 @@ __device__ __forceinline__ uint32_t block_lookback(const unsigned long long* sta
             for (int j = 0; j < kLbWin; ++j) {
                 if (stat != -1) continue;
                 if (hi - j < 0) {
+                    stat = -2;
+                    continue;
+                }
+                if (lb_foreign(v[j], epoch)) {
+                    lb_fault(err, kFaultForeignEpoch);
                     stat = -2;
                     continue;
                 }
@@ -85,7 +91,10 @@ __device__ __forceinline__ uint32_t block_lookback(const unsigned long long* sta
         const int pending = __syncthreads_or(part == 0 && s_next[d] >= 0);
         if (!pending) break;
         if (__syncthreads_or(!progress)) {   // an unpublished nearest tile: wait a little
-            if (++spins > kLbSpinLimit) break;
+            if (++spins > kLbSpinLimit) {
+                if (threadIdx.x == 0) lb_fault(err, kFaultLookbackWait);
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -95,7 +104,8 @@ __device__ __forceinline__ uint32_t block_lookback(const unsigned long long* sta
 __global__ __launch_bounds__(kRadixThreads) void radix_pass_kernel(uint32_t* ka, int* va, uint32_t* kb, int* vb, const int* v0, int n,
                                                                    int pass, const uint32_t* bound,
                                                                    const uint32_t* hist, uint32_t* ctr,
-                                                                   unsigned long long* state, uint32_t epoch) {
+                                                                   unsigned long long* state, uint32_t epoch,
+                                                                   int* err, int inject) {
     if (pass >= radix_pass_count(*bound)) return;   // keys < 2^(8 pass): this digit is 0 for all of them
     const uint32_t* ki = pass & 1 ? kb : ka;
     const int* vi = pass & 1 ? vb : (pass == 0 ? v0 : va);
@@ -149,12 +159,15 @@ __global__ __launch_bounds__(kRadixThreads) void radix_pass_kernel(uint32_t* ka,
             s_cnt[w][tid] = cnt;
             cnt += c;
         }
+        // inject 2 (tests): tile 0 publishes a word of a newer epoch, as memory of another allocation would hold
+        const uint32_t e0 = inject == 2 && pass == 0 && tile == 0 ? epoch + 0x40000000u : epoch;   // never reached by a real sort
         if (tile > 0) lb_store(my, epoch, kLbAgg, cnt);
-        else lb_store(my, epoch, kLbInc, cnt);
+        else lb_store(my, e0, kLbInc, cnt);
     }
     uint32_t total;
     const uint32_t digit_base = block_exclusive_scan<kRadixThreads>(h, s_wave, &total);
-    const uint32_t before = block_lookback(state, tile, epoch);
+    uint32_t before = block_lookback(state, tile, epoch, err);
+    if (inject == 1 && pass == 0 && tile == 1) before += 1u << 28;   // tests: a stale prefix
     if (tid < kRadixDigits) {
         if (tile > 0) lb_store(my, epoch, kLbInc, before + cnt);
         s_off[tid] = digit_base + before;
@@ -166,6 +179,10 @@ __global__ __launch_bounds__(kRadixThreads) void radix_pass_kernel(uint32_t* ka,
         if (i < n) {
             const uint32_t d = (key[r] >> shift) & 255u;
             const uint32_t pos = s_off[d] + s_cnt[wave][d] + rank[r];
+            if (pos >= (uint32_t)n) {   // only after a look-back fault: never write outside the pairs
+                lb_fault(err, kFaultRadixScatter);
+                continue;
+            }
             ko[pos] = key[r];
             vo[pos] = val[r];
         }
@@ -175,11 +192,12 @@ __global__ __launch_bounds__(kRadixThreads) void radix_pass_kernel(uint32_t* ka,
 }  // namespace
 
 hipError_t launch_radix_passes(uint32_t* ka, int* va, uint32_t* kb, int* vb, const int* v0, int n,
-                               const uint32_t* bound, const RadixScratch& rs, uint32_t epoch, hipStream_t s) {
+                               const uint32_t* bound, const RadixScratch& rs, uint32_t epoch, int* err, int inject,
+                               hipStream_t s) {
     if (n <= 0) return hipSuccess;
     for (int p = 0; p < kRadixPasses; ++p)
         hipLaunchKernelGGL(radix_pass_kernel, dim3((unsigned)rs.tiles), dim3(kRadixThreads), 0, s, ka, va, kb, vb, v0, n, p,
-                           bound, rs.hist, rs.ctr, rs.state + (size_t)p * rs.tiles * kRadixDigits, epoch);
+                           bound, rs.hist, rs.ctr, rs.state + (size_t)p * rs.tiles * kRadixDigits, epoch, err, inject);
     return hipGetLastError();
 }
 

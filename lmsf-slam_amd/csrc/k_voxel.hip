@@ -198,7 +198,7 @@ __global__ __launch_bounds__(kSegThreads) void voxel_reduce_kernel(const float4*
                                                                    const uint32_t* kb, const int* va, const int* vb,
                                                                    int n, const uint32_t* bound, uint32_t* ctr,
                                                                    unsigned long long* st, uint32_t epoch,
-                                                                   float4* out, int* nseg, int* map_bb) {
+                                                                   float4* out, int* nseg, int* map_bb, int* err) {
     __shared__ float4 s_pts[kSegStage];
     __shared__ uint16_t s_head[kSegTile];
     __shared__ uint32_t s_wave[kSegThreads / 64];
@@ -245,7 +245,8 @@ __global__ __launch_bounds__(kSegThreads) void voxel_reduce_kernel(const float4*
 #pragma unroll
     for (int q = 0; q < kSegStage / kSegThreads; ++q) {
         const int i = q * kSegThreads + tid;
-        if (i < staged) s_pts[i] = pts[ix[q]];
+        // a sorted index outside the cloud exists only after a look-back fault upstream: never read with it
+        if (i < staged) s_pts[i] = pts[(unsigned)ix[q] < (unsigned)n ? ix[q] : 0];
     }
     uint32_t flags = 0, c = 0;
 #pragma unroll
@@ -273,22 +274,27 @@ __global__ __launch_bounds__(kSegThreads) void voxel_reduce_kernel(const float4*
             if (tid == 0) lb_store(st, epoch, kLbInc, total);
         } else {
             if (tid == 0) lb_store(st + tile, epoch, kLbAgg, total);
-            before = wave_lookback(st, tile, epoch);
+            before = wave_lookback(st, tile, epoch, err);
             if (tid == 0) lb_store(st + tile, epoch, kLbInc, before + total);
         }
         if (tid == 0) s_before = before;
     }
     if (tid == 0) {
         const uint32_t before = s_before;
-        if (tbase + kSegTile >= n) {   // the last tile: the voxel count
-            *nseg = (int)(before + total);
-            if (map_bb) map_bb[6] = (int)(before + total);
+        if (tbase + kSegTile >= n) {   // the last tile: the voxel count (0 after a fault: nothing downstream reads)
+            const bool ok = (uint64_t)before + total <= (uint64_t)n;
+            *nseg = ok ? (int)(before + total) : 0;
+            if (map_bb) map_bb[6] = ok ? (int)(before + total) : 0;
         }
         if (s_end == INT_MAX && tbase + kSegStage >= n) s_end = n - tbase;   // runs to the end of the cloud
     }
     __syncthreads();
     const uint32_t before = s_before;
     const int tend = s_end;   // INT_MAX: the last voxel runs past the margin
+    if ((uint64_t)before + total > (uint64_t)n) {   // more voxels than points: only after a look-back fault
+        if (tid == 0) lb_fault(err, kFaultSegment);
+        return;
+    }
     for (uint32_t v = tid; v < total; v += kSegThreads) {
         const int a = s_head[v];
         const int b = v + 1 < total ? (int)s_head[v + 1] : tend;
@@ -317,7 +323,8 @@ __global__ __launch_bounds__(kSegThreads) void voxel_reduce_kernel(const float4*
         if (b == INT_MAX) {   // past the margin: from HBM until the key changes
             const uint32_t key = keys[tbase + a];
             for (; tbase + i < n && keys[tbase + i] == key; ++i) {
-                const float4 q = pts[idx[tbase + i]];
+                const int j = idx[tbase + i];
+                const float4 q = pts[(unsigned)j < (unsigned)n ? j : 0];
                 sx += (double)q.x;
                 sy += (double)q.y;
                 sz += (double)q.z;
@@ -330,8 +337,10 @@ __global__ __launch_bounds__(kSegThreads) void voxel_reduce_kernel(const float4*
 }
 
 void VoxelFilter::release() {
+    if (last) (void)hipStreamSynchronize(last);
     void* bufs[] = {keys, keys_b, idx, idx_b, part, nseg, scratch};
-    for (void* p : bufs) hipFree(p);
+    for (void* p : bufs) gfree(p, last);
+    if (last) (void)hipStreamSynchronize(last);
     *this = VoxelFilter();
 }
 
@@ -339,33 +348,59 @@ int VoxelFilter::box_blocks(int n) { return std::max(std::min((n + 256 * kVoxBat
 
 hipError_t VoxelFilter::reserve(size_t need, hipStream_t s) {
     if (need <= cap) return hipSuccess;
-    const size_t n = std::min(grow_cap(need, cap), (size_t)INT32_MAX);
-    // growth (rare): the old buffers may still be read by this filter's last enqueue, on whichever stream it ran
-    // (a tracker kind's rebuild takes either aux stream), so the device drains before they are freed
-    hipError_t e = cap ? hipDeviceSynchronize() : hipSuccess;
-    if (e != hipSuccess) return e;
-    release();
-#define VALLOC(p, bytes) if ((e = hipMalloc((void**)&(p), (bytes))) != hipSuccess) return e
-    VALLOC(keys, n * sizeof(uint32_t));
-    VALLOC(keys_b, n * sizeof(uint32_t));
-    VALLOC(idx, n * sizeof(int));
-    VALLOC(idx_b, n * sizeof(int));
-    VALLOC(part, (size_t)box_blocks((int)n) * 12 * sizeof(int) + 16 * sizeof(int));
-    VALLOC(nseg, sizeof(int));
-    VALLOC(scratch, radix_scratch_words(n) * sizeof(uint32_t));
+    const size_t n = std::min(exact ? need : grow_cap(need, cap), (size_t)INT32_MAX);
+    // growth: the old buffers may still be read by this filter's last enqueue on another stream (a tracker
+    // kind's rebuild takes either aux stream) -- s waits for that stream's work so far, then frees them in order
+    hipError_t e = hipSuccess;
+    if (cap && last && last != s) {
+        hipEvent_t ev;
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+        e = hipEventRecord(ev, last);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, ev, 0);
+        (void)hipEventDestroy(ev);   // released once the wait completes
+        if (e != hipSuccess) return e;
+    }
+    void* old[] = {keys, keys_b, idx, idx_b, part, nseg, scratch};
+    for (void* p : old) gfree(p, s);
+    const bool ex = exact;
+    *this = VoxelFilter();
+    exact = ex;
+    last = s;
+#define VALLOC(p, count) if ((e = galloc(&(p), (count), s)) != hipSuccess) return e
+    VALLOC(keys, n);
+    VALLOC(keys_b, n);
+    VALLOC(idx, n);
+    VALLOC(idx_b, n);
+    VALLOC(part, (size_t)box_blocks((int)n) * 12 + 16);
+    VALLOC(nseg, 1);
+    VALLOC(scratch, radix_scratch_words(n));
 #undef VALLOC
-    // look-back words of epoch 0 never match a sort (epochs start at 1, and restart with the new buffers): zeroed on
-    // the stream whose kernels read them (a null-stream memset is not ordered before a non-blocking stream's work)
+    // look-back words of epoch 0 are older than every sort (radix.h): zeroed on the stream whose kernels read
+    // them (a null-stream memset is not ordered before a non-blocking stream's work -- the r04 fault)
     if ((e = hipMemsetAsync(scratch, 0, radix_scratch_words(n) * sizeof(uint32_t), s)) != hipSuccess) return e;
     cap = n;
     return hipSuccess;
 }
 
-hipError_t VoxelFilter::enqueue(const float4* in, int n, float leaf, float4* out, hipStream_t s, int* map_bb, int sx) {
-    if (n <= 0) return hipErrorInvalidValue;
+hipError_t VoxelFilter::enqueue(const float4* in, int n, float leaf, float4* out, int* err, hipStream_t s, int* map_bb,
+                                int sx, int inject) {
+    if (n <= 0) return hipSuccess;
     hipError_t e = reserve((size_t)n, s);
     if (e != hipSuccess) return e;
-    if (++epoch == 0) ++epoch;
+    if (last && last != s) {   // the last enqueue ran on another stream: this one follows it (shared workspace)
+        hipEvent_t ev;
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+        e = hipEventRecord(ev, last);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, ev, 0);
+        (void)hipEventDestroy(ev);
+        if (e != hipSuccess) return e;
+    }
+    last = s;
+    if (poisoned) {   // an injected fault left foreign look-back words behind
+        if ((e = hipMemsetAsync(scratch, 0, radix_scratch_words(cap) * sizeof(uint32_t), s)) != hipSuccess) return e;
+        poisoned = false;
+    }
+    epoch = next_lookback_epoch();
     const float inv = 1.0f / leaf;
     const RadixScratch rs = radix_scratch(scratch, (size_t)n);
     uint32_t* bound = reinterpret_cast<uint32_t*>(part) + (size_t)box_blocks(cap) * 12;
@@ -375,19 +410,26 @@ hipError_t VoxelFilter::enqueue(const float4* in, int n, float leaf, float4* out
     const int kb = std::max(std::min((n + 256 * kVoxBatch - 1) / (256 * kVoxBatch), 128), 1);
     hipLaunchKernelGGL(voxel_key_kernel, dim3(kb), dim3(256), 0, s, in, n, inv, part, nb, keys, bound, rs.hist, map_bb);
     // pass 0 takes the point index as its value
-    if ((e = launch_radix_passes(keys, idx, keys_b, idx_b, nullptr, n, bound, rs, epoch, s)) != hipSuccess) return e;
+    if ((e = launch_radix_passes(keys, idx, keys_b, idx_b, nullptr, n, bound, rs, epoch, err, inject, s)) != hipSuccess)
+        return e;
+    if (inject) poisoned = true;
     hipLaunchKernelGGL(voxel_reduce_kernel, dim3((unsigned)seg_tiles((size_t)n)), dim3(kSegThreads), 0, s, in, keys,
-                       keys_b, idx, idx_b, n, bound, rs.ctr, rs.seg_state, epoch, out, nseg, map_bb);
+                       keys_b, idx, idx_b, n, bound, rs.ctr, rs.seg_state, epoch, out, nseg, map_bb, err);
     return hipGetLastError();
 }
 
-hipError_t VoxelFilter::run(const float4* in, int n, float leaf, float4* out, int* n_out, hipStream_t s) {
+hipError_t VoxelFilter::run(const float4* in, int n, float leaf, float4* out, int* n_out, int* err, hipStream_t s) {
     *n_out = 0;
     if (n <= 0) return hipSuccess;
-    hipError_t e = enqueue(in, n, leaf, out, s);
+    hipError_t e = enqueue(in, n, leaf, out, err, s);
     if (e != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(n_out, nseg, sizeof(int), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    return hipStreamSynchronize(s);
+    int h[2] = {0, 0};
+    if ((e = hipMemcpyAsync(&h[0], nseg, sizeof(int), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(&h[1], err, sizeof(int), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    if (h[1]) return hipErrorIllegalState;   // the caller reads and clears the fault word
+    *n_out = h[0];
+    return hipSuccess;
 }
 
 }  // namespace lmsf

@@ -24,6 +24,30 @@ constexpr int kEvalBlock = 256 * kEvalPerThread;
 // request -- the keyframe window, a varying scan size -- then reallocates rarely: hipFree
 // synchronises the device and costs ~0.5 ms on the tracking path).
 inline size_t grow_cap(size_t need, size_t cap) { return need > cap + cap / 2 ? need : cap + cap / 2; }
+
+// Buffers that grow while other streams may still read the old ones (map grids, the voxel filter's workspace)
+// are stream-ordered allocations: a growth allocates the new buffers and frees the old ones on the stream that
+// uses them next, which every earlier user is ordered before ("growth"), so no device
+// drain and no host wait (r04 drained the whole device -- every context's streams -- per growth).
+template <typename T>
+hipError_t galloc(T** p, size_t count, hipStream_t s) {
+    *p = nullptr;
+    return hipMallocAsync((void**)p, (count ? count : 1) * sizeof(T), s);
+}
+inline void gfree(void* p, hipStream_t s) {
+    if (p) (void)hipFreeAsync(p, s);
+}
+
+// Device fault word (lmsf_ctx d_error[17]): bits set by the look-back checks (radix.h) and the scatters whose
+// index comes from a look-back sum; read back with the LM-loop flag at every Solve / batch wait and reported as
+// LMSF_ERR_HIP ("device look-back fault").
+constexpr int kFaultRadixScatter = 1;   // a radix digit pass computed a position outside [0, n)
+constexpr int kFaultLookbackWait = 2;   // a look-back wait exceeded its bound
+constexpr int kFaultForeignEpoch = 4;   // a look-back word newer than the running sort (memory of another allocation)
+constexpr int kFaultSegment = 8;        // the voxel segment pass counted more voxels than points
+constexpr int kFaultGridScatter = 16;   // a grid scatter computed a position outside [0, n)
+// Look-back epochs: one process-wide counter (never restarts, never 0), shared by every sort and scan.
+uint32_t next_lookback_epoch();
 constexpr int kRingMax = 8192;       // points per ring handled by the extraction kernel
 constexpr int kSortMax = 2048;       // points per sector (ring / 6 + 5, padded to a power of two)
 constexpr int kMaxRings = 128;
@@ -162,7 +186,7 @@ hipError_t launch_map_count(const float4* pts, int n, int sx, int ox, int oy, in
                             int* cell, uint32_t* counts, hipStream_t s, int sy = 1);
 // sorted[] w = base + original index (base > 0 for a keyframe window behind a prior map)
 hipError_t launch_map_scatter(const float4* pts, int n, const int* cell, const uint32_t* off, uint32_t* fill,
-                              float4* sorted, int base, hipStream_t s);
+                              float4* sorted, int base, int* err, hipStream_t s);
 hipError_t launch_count_nonzero(const uint32_t* counts, size_t n, unsigned long long* out, hipStream_t s);
 // Grid of a window whose box + count a producer left in d_bb (box 0..5, count 6), built on stream s without
 // a host round trip (k_map.hip): clear, read-back of d_bb[0..10] into h_bb + ev_bb, count, scan, scatter.
@@ -171,7 +195,7 @@ size_t grid_scan_tiles(size_t cells_cap);
 hipError_t launch_grid_build_dev(const float4* orig, int n_max, int sx, int* d_bb, uint32_t* counts, uint32_t* off,
                                  uint32_t* fill, size_t cells_cap, int* cell, float4* sorted, int base,
                                  unsigned long long* scan_state, uint32_t epoch, int* h_bb, hipEvent_t ev_bb,
-                                 hipStream_t s);
+                                 int* err, hipStream_t s);
 hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, void* tmp, size_t& tmp_bytes, hipStream_t s);
 
 // edge2 / surf2: optional second grid per kind (n = 0: none), searched as if concatenated after
@@ -284,15 +308,21 @@ struct VoxelFilter {
     int *idx = nullptr, *idx_b = nullptr, *part = nullptr, *nseg = nullptr;
     uint32_t epoch = 0;   // look-back epoch of the last sort
     size_t cap = 0;
+    hipStream_t last = nullptr;    // stream of the last enqueue (the workspace's release is ordered after it)
+    bool exact = false;            // grow to the request exactly (LMSF_OPT_GROWTH_TEST: a growth at every increase)
+    bool poisoned = false;         // an injected fault (tests) left foreign look-back words: re-zeroed next time
     static int box_blocks(int n);
-    hipError_t reserve(size_t n, hipStream_t s);   // grows on s (the device drained first when it had buffers)
-    hipError_t run(const float4* in, int n, float leaf, float4* out, int* n_out, hipStream_t s);
+    // grows on s: new buffers allocated and the old ones freed on s, after the last enqueue's stream (no drain)
+    hipError_t reserve(size_t n, hipStream_t s);
+    // err: the device fault word (radix.h); run() also returns hipErrorIllegalState when the sort flagged one
+    hipError_t run(const float4* in, int n, float leaf, float4* out, int* n_out, int* err, hipStream_t s);
     // run() without the read-back: the voxel count stays on the device in *nseg (no host wait).  map_bb
     // (optional, device): [0..5] = the map-cell box (k_map.hip's rule, sx x-slices per m) of the INPUT
     // points -- it bounds the centroids' box -- and [6] = the voxel count, the grid stage's read-back.
-    hipError_t enqueue(const float4* in, int n, float leaf, float4* out, hipStream_t s, int* map_bb = nullptr,
-                       int sx = 0);
-    void release();
+    // inject: LMSF_OPT_FAULT_INJECT (launch_radix_passes)
+    hipError_t enqueue(const float4* in, int n, float leaf, float4* out, int* err, hipStream_t s,
+                       int* map_bb = nullptr, int sx = 0, int inject = 0);
+    void release();                // waits for the last enqueue's stream
 };
 
 // PointCloud2 decode + removeNaN + rotary relative time + distance filter (k_ingest.hip).
@@ -337,13 +367,15 @@ lmsf_status ctx_window_finish(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s
 // The window grid's source buffer (>= n_max points) and its box + count words ([0..5] map-cell box, [6] count),
 // for a producer that fills both on the stage stream (the tracker's voxel filter); then
 // ctx_window_stage(c, kind, nullptr, n_max, nullptr, s) only reads them back.
-lmsf_status ctx_window_target(lmsf_ctx* c, int kind, size_t n_max, float4** orig, int** bb);
+lmsf_status ctx_window_target(lmsf_ctx* c, int kind, size_t n_max, float4** orig, int** bb, hipStream_t s);
 // ... or, instead of that read-back, the whole grid build on s (no host wait; ctx_window_finish then only
 // takes the box read-back and sets the view).
 lmsf_status ctx_window_build(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s);
 // The window's points in window order (the grid's unsorted source) after a finished commit.
 const float4* ctx_window_points(const lmsf_ctx* c, int kind);
 int grid_slices();
+int* ctx_fault_word(lmsf_ctx* c);       // the context's device fault word (d_error[17])
+int ctx_option(const lmsf_ctx* c, int option);
 lmsf_status ctx_slot0_features(lmsf_ctx* c, const float4** d_feat, int64_t* ne, int64_t* ns);
 
 }  // namespace lmsf

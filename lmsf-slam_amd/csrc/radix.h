@@ -2,7 +2,14 @@
 // scratch layout, the key-bound -> pass-count rule, the block histogram and the decoupled look-back.
 //
 // Look-back words are 64-bit: the sort's epoch (high 32 bits) | flag (2 bits) | count (30 bits).  A word of an
-// older sort reads as "not published", so the state arrays are never cleared (one memset at allocation).
+// older sort reads as "not published", so the state arrays are never cleared (one memset at allocation, on the
+// stream that reads them).  Epochs come from one process-wide counter (next_lookback_epoch), so they never
+// restart: a word whose epoch is NEWER than the running sort's was not written by any earlier sort on this
+// memory -- it is left over from another allocation (the r04 fault: a null-stream memset not yet done when
+// the sort ran) -- and the walk flags kFaultForeignEpoch instead of waiting on it.  A wait that exceeds its
+// bound flags kFaultLookbackWait.  Every scatter whose index comes from a look-back sum is bounds-checked by its
+// kernel (kFaultRadixScatter / kFaultSegment / kFaultGridScatter).  The flags go to a device word the host reads
+// back at the next Solve / batch wait and reports as LMSF_ERR_HIP.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -60,52 +67,23 @@ __device__ __forceinline__ int radix_pass_count(uint32_t bound) {
 __device__ __forceinline__ unsigned long long lb_load(const unsigned long long* p) {
     return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a word of a newer sort than this one (signed distance: the counter may wrap)
+__device__ __forceinline__ bool lb_foreign(unsigned long long v, uint32_t epoch) {
+    return (int32_t)((uint32_t)(v >> 32) - epoch) > 0;
+}
+
+__device__ __forceinline__ void lb_fault(int* err, int bit) {
+    if (err) atomicOr(err, bit);
+}
+
 __device__ __forceinline__ void lb_store(unsigned long long* p, uint32_t epoch, uint32_t flag, uint32_t count) {
     __hip_atomic_store(p, ((unsigned long long)epoch << 32) | flag | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Sum of the counts of tiles [0, tile) from their look-back words st[p * stride]: W predecessors are read at
-// once (independent loads in flight: one round trip covers W tiles), summed nearest first until an inclusive
-// word; an unpublished word restarts the window there.  The tiles come from a start-order counter, so every
-// waited-on tile's block runs.
-template <int W>
-__device__ __forceinline__ uint32_t lookback_sum(const unsigned long long* st, int tile, size_t stride,
-                                                 uint32_t epoch) {
-    uint32_t sum = 0;
-    int p = tile - 1;
-    unsigned spins = 0;
-    while (p >= 0) {
-        unsigned long long v[W];
-#pragma unroll
-        for (int j = 0; j < W; ++j) v[j] = p - j >= 0 ? lb_load(st + (size_t)(p - j) * stride) : 0ull;
-        int adv = 0;
-        bool done = false;
-#pragma unroll
-        for (int j = 0; j < W; ++j) {
-            if (done || adv != j) continue;
-            if (p - j < 0) {
-                done = true;
-                continue;
-            }
-            const uint32_t lo = (uint32_t)v[j], flag = lo & ~kLbCount;
-            if ((uint32_t)(v[j] >> 32) != epoch || flag == 0u) continue;   // not yet published: wait here
-            sum += lo & kLbCount;
-            adv = j + 1;
-            done = flag == kLbInc;
-        }
-        if (done) break;
-        p -= adv;
-        if (adv == 0) {
-            if (++spins > kLbSpinLimit) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    return sum;
-}
-
 // Sum of the counts of tiles [0, tile) by one wave: lane j reads tile p - j (64 tiles per round trip), the
 // nearest inclusive word ends the walk, the nearest unpublished one resumes it; every lane returns the sum.
-__device__ __forceinline__ uint32_t wave_lookback(const unsigned long long* st, int tile, uint32_t epoch) {
+// A foreign word or an exhausted wait ends the walk with the fault flagged in *err (the sum is then unusable).
+__device__ __forceinline__ uint32_t wave_lookback(const unsigned long long* st, int tile, uint32_t epoch, int* err) {
     const int lane = threadIdx.x & 63;
     uint32_t sum = 0;
     int p = tile - 1;
@@ -113,6 +91,10 @@ __device__ __forceinline__ uint32_t wave_lookback(const unsigned long long* st, 
     while (p >= 0) {
         const int q = p - lane;
         const unsigned long long v = q >= 0 ? lb_load(st + q) : 0ull;
+        if (__ballot(q >= 0 && lb_foreign(v, epoch))) {
+            if (lane == 0) lb_fault(err, kFaultForeignEpoch);
+            break;
+        }
         const uint32_t lo = (uint32_t)v, flag = lo & ~kLbCount;
         const bool ready = q < 0 || ((uint32_t)(v >> 32) == epoch && flag != 0u);
         const bool inc = q < 0 || (ready && flag == kLbInc);   // before tile 0: an inclusive zero
@@ -127,7 +109,10 @@ __device__ __forceinline__ uint32_t wave_lookback(const unsigned long long* st, 
         if (stop_inc) break;
         p -= stop;
         if (stop == 0) {
-            if (++spins > kLbSpinLimit) break;
+            if (++spins > kLbSpinLimit) {
+                if (lane == 0) lb_fault(err, kFaultLookbackWait);
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -175,8 +160,11 @@ __device__ __forceinline__ void radix_hist_commit(uint32_t (*h)[kRadixDigits], u
 
 // The digit passes over (ka, va) <-> (kb, vb) of n pairs whose keys are < *bound (device word), with the
 // global histogram of every needed pass already in rs.hist and rs.ctr[0..3] zeroed: kRadixPasses launches.
-// Pass 0 takes its values from v0 (nullptr: the pair's index) instead of va.  epoch: non-zero, new per sort.
+// Pass 0 takes its values from v0 (nullptr: the pair's index) instead of va.  epoch: next_lookback_epoch(), new
+// per sort.  err: the fault word (radix.h header).  inject (LMSF_OPT_FAULT_INJECT, tests only): 1 = pass 0's tile
+// 1 takes a prefix 2^28 too large (an out-of-range scatter), 2 = pass 0's tile 0 publishes a foreign epoch.
 hipError_t launch_radix_passes(uint32_t* ka, int* va, uint32_t* kb, int* vb, const int* v0, int n,
-                               const uint32_t* bound, const RadixScratch& rs, uint32_t epoch, hipStream_t s);
+                               const uint32_t* bound, const RadixScratch& rs, uint32_t epoch, int* err, int inject,
+                               hipStream_t s);
 
 }  // namespace lmsf

@@ -235,9 +235,12 @@ lmsf_status commit_stage_kind(lmsf_tracker* t, int kind, hipStream_t ks) {
         // (they stay on the device; the stage only reads them back)
         float4* orig;
         int* bb;
-        lmsf_status rc = ctx_window_target(t->ctx, kind, nw, &orig, &bb);
+        lmsf_status rc = ctx_window_target(t->ctx, kind, nw, &orig, &bb, ks);
         if (rc) return rc;
-        TCHK(t, t->voxel[kind].enqueue(w.wcat, (int)nw, (float)w.leaf, orig, ks, bb, grid_slices()));
+        VoxelFilter& vf = t->voxel[kind];
+        vf.exact = ctx_option(t->ctx, LMSF_OPT_GROWTH_TEST) != 0;
+        TCHK(t, vf.enqueue(w.wcat, (int)nw, (float)w.leaf, orig, ctx_fault_word(t->ctx), ks, bb, grid_slices(),
+                           ctx_option(t->ctx, LMSF_OPT_FAULT_INJECT)));
         return ctx_window_build(t->ctx, kind, nw, ks);   // the grid too, without a host round trip
     }
     // only the window's grid is rebuilt; the prior's grid was built once (set_prior_map)

@@ -21,7 +21,7 @@ UPDATE_NONE, UPDATE_MOTION, UPDATE_TIME = 0, 1, 2
 SOLVER_CERES_LM, SOLVER_GN = 0, 1
 SCHEDULE_REFERENCE_DECAY, SCHEDULE_FIXED = 0, 1
 (OPT_QUERY_MEMO, OPT_MEMO_REFIT, OPT_MEMO_EXACT, OPT_MEMO_ORDER, OPT_MEMO_BOUND, OPT_GRAPH, OPT_MEMO_SKIP1, OPT_LM_LOOP,
- OPT_LOOP_FAULT_TEST) = range(9)
+ OPT_LOOP_FAULT_TEST, OPT_GROWTH_TEST, OPT_FAULT_INJECT) = range(11)
 TERM_NAMES = {0: "max_iterations", 1: "function_tol", 2: "parameter_tol", 3: "gradient_tol",
               4: "no_residuals", 5: "gn_converged", 6: "gn_too_few"}
 
@@ -52,7 +52,8 @@ class FeatureCounts(C.Structure):
 class KernelStats(C.Structure):
     _fields_ = [("launches", C.c_int64), ("total_ms", C.c_double), ("queries", C.c_int64), ("n27_sum", C.c_int64),
                 ("fused_launches", C.c_int64), ("reused_queries", C.c_int64),
-                ("refit_queries", C.c_int64), ("loop_recoveries", C.c_int64)]
+                ("refit_queries", C.c_int64), ("loop_recoveries", C.c_int64),
+                ("buffer_growths", C.c_int64)]
 
 
 class ExtractParams(C.Structure):
@@ -412,7 +413,7 @@ class Context:
         return out[:min(n.value, cap)].copy()
 
     def set_option(self, option, value):
-        """lmsf_set_option (OPT_* switches, 0 | 1)."""
+        """lmsf_set_option (OPT_* switches, 0 | 1; OPT_FAULT_INJECT also 2)."""
         self._check(load().lmsf_set_option(self.h, int(option), int(value)))
 
     # ---- diagnostics

@@ -869,6 +869,92 @@ def test_deferred_commit_settles(lib, oracle_mod, sequence_workload):
         x.close()
 
 
+@pytest.mark.parametrize("workers", [True, False], ids=["commit_workers", "inline_commit"])
+def test_tracker_growth_on_commit_streams(lib, oracle_mod, sequence_workload, workers):
+    """a tracker whose window buffers -- the voxel filter's workspace and look-back words, the window
+    grid's points, cells and scan look-back words -- are regrown at nearly every keyframe commit
+    (LMSF_OPT_GROWTH_TEST: exact growth, 2^10 first cells) on the commit streams (workers: manual keyframes +
+    lmsf_tracker_commit_map, the rebuild enqueued by the two worker threads on the aux streams and finished beside
+    the next extraction; inline: the automatic updateLocalMap) equals the oracle tracker: same update decisions,
+    poses <= 1e-4 at every scan, same windows.  The growths happened (buffer_growths), and no device look-back
+    fault was flagged (a set fault word fails the next Solve)."""
+    import tracker as OT
+    from conftest import mat_err
+    wl = sequence_workload
+    ctx = _ctx(lib, n_scans=wl.n_scans)
+    ctx.set_option(lib.OPT_GROWTH_TEST, 1)
+    gt = lib.Tracker(ctx, window_frames=4, manual_map_update=workers)
+    ot = OT.Tracker(window_frames=4, manual_map_update=workers)
+    g0 = ctx.kernel_stats().buffer_growths
+    keyframes = 0
+    for i, scan in enumerate(wl.scans):
+        e, s, _, _ = oracle_mod.extract(scan, n_scans=wl.n_scans)
+        ctx.extract(scan)                        # a deferred commit completes beside this extraction
+        _, r = gt.solve_extracted(wl.dt * i)
+        _, otyp, _ = ot.solve(e, s, wl.dt * i)
+        assert r.update_type == otyp, i
+        dt, dr = mat_err(gt.pose(), ot.curr)
+        assert dt <= POSE_TOL and dr <= POSE_TOL, (i, dt, dr)
+        if otyp:
+            keyframes += 1
+            if workers:
+                gt.add_keyframe_extracted(gt.pose())
+                ot.add_keyframe(e, s, ot.curr.copy())
+                gt.commit_map()
+                ot.commit()
+    assert keyframes >= 5
+    for kind in (lib.EDGE, lib.SURF):
+        np.testing.assert_allclose(gt.local_map(kind), ot.local_map(kind), atol=1e-4)
+    growths = ctx.kernel_stats().buffer_growths - g0
+    assert growths >= 6, growths
+    gt.close()
+
+
+@pytest.mark.parametrize("inject", [1, 2], ids=["stale_prefix", "foreign_epoch"])
+def test_lookback_fault_flagged(lib, oracle_mod, sequence_workload, inject):
+    """The device look-back checks (radix.h) catch what r04's null-stream memset race produced, injected into the
+    window voxel filter's first radix pass (LMSF_OPT_FAULT_INJECT): a stale prefix that puts a tile's scatter outside
+    the pairs (1) and a look-back word of another allocation (2).  Nothing is written or read outside the buffers,
+    the next Solve fails with LMSF_ERR_HIP "device look-back fault", the fault word is cleared by that report, and
+    the next commit (look-back words re-zeroed) tracks exactly as a tracker that never faulted."""
+    from conftest import pose_matrix
+    wl = sequence_workload
+    e, s, _, _ = oracle_mod.extract(wl.scans[0], n_scans=wl.n_scans)
+    T0 = pose_matrix(wl.truth[0])
+    guess = wl.truth[1]
+
+    def tracker(ctx):
+        t = lib.Tracker(ctx, window_frames=4, manual_map_update=True)
+        for _ in range(2):                        # >= 2 radix tiles of 8192 pairs in the surf window
+            t.add_keyframe(e, s, T0)
+        return t
+
+    assert 2 * len(s) > 8192
+    ref_ctx = _ctx(lib, n_scans=wl.n_scans)
+    ref_t = tracker(ref_ctx)
+    ref_t.add_keyframe(e, s, T0)
+    ref_t.commit_map()
+    ref_ctx.extract(wl.scans[1])
+    ref_pose, _ = ref_ctx.solve(guess)
+
+    ctx = _ctx(lib, n_scans=wl.n_scans)
+    t = tracker(ctx)
+    ctx.set_option(lib.OPT_FAULT_INJECT, inject)
+    t.commit_map()
+    ctx.extract(wl.scans[1])                      # completes the faulted commit
+    ctx.set_option(lib.OPT_FAULT_INJECT, 0)
+    with pytest.raises(lib.LmsfError, match="device look-back fault") as ei:
+        ctx.solve(guess)
+    assert ei.value.code == lib.ERR_HIP
+    t.add_keyframe(e, s, T0)                      # window = 3 copies, as the reference tracker's
+    t.commit_map()
+    ctx.extract(wl.scans[1])
+    pose, _ = ctx.solve(guess)
+    assert np.array_equal(pose, ref_pose)
+    for x in (t, ref_t):
+        x.close()
+
+
 def test_lm_loop_fault_recovery(lib, oracle_mod, small_workload):
     """A single-scan Solve whose one-launch LM loop gives up its bounded waits (forced: LMSF_OPT_LOOP_FAULT_TEST)
     is re-run on the 9-launch form in the same call: it returns a pose, no error, bit-identical to a Solve on
