@@ -255,8 +255,13 @@ def shared_map(d, make):
     return multi.broadcast_map(e, s, d.dev)
 
 
-def kernel_name(ks):
-    """The timed neighbour-search launch: the fused search + fit kernels (batch launches) or knn_kernel."""
+def kernel_name(ks, dense=False):
+    """The timed neighbour-search launch: the fused search + fit kernels (batch launches; on a dense map the two
+    passes on the first-pass grid and the pass-2 fit) or the single-scan search."""
+    if ks.launches and ks.fused_launches == ks.launches and dense:
+        return ("dense_pass1_kernel + dense_pass2_kernel + dense_fit2_kernel (dense map: first pass on the 0.5 m "
+                "first-pass grid with the fit of the queries it completes, bounded pass-2 walk of the listed rest, "
+                "their fit; one outer iteration)")
     if ks.launches and ks.fused_launches == ks.launches:
         return ("match_memo_kernel + match_fit_kernel (query memo pass from outer iteration 2, then the fused 5-NN "
                 "search + line/plane fit + record write of the queries it lists; one outer iteration)")
@@ -277,7 +282,7 @@ def load_traffic(traffic_json, **match):
     return tj
 
 
-def knn_roofline(ks, mean_n27, tj, elapsed_s, note, solo=None):
+def knn_roofline(ks, mean_n27, tj, elapsed_s, note, solo=None, dense=False):
     """Roofline of the dominant (neighbour-search) kernel.
 
     The launch time is `solo` when given: the HIP-stamped span of each search launch (memo pass + fused
@@ -315,7 +320,7 @@ def knn_roofline(ks, mean_n27, tj, elapsed_s, note, solo=None):
     out = {"bound": "hbm", "achieved": round(achieved, 1) if achieved is not None else None, "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved is not None else None,
            "traffic": traffic, "basis": basis,
-           "kernel": kernel_name(ks), "avg_launch_ms": round(avg_launch_ms, 4), "launches": int(t.launches),
+           "kernel": kernel_name(ks, dense), "avg_launch_ms": round(avg_launch_ms, 4), "launches": int(t.launches),
            "queries_per_launch": int(t.queries / launches),
            "reused_query_frac": round(reused / max(int(t.queries), 1), 4),
            "refit_query_frac": round(refit / max(int(t.queries), 1), 4),
@@ -405,6 +410,22 @@ def cpu_oracle():
     import oracle
     oracle.set_threads(1)
     return oracle
+
+
+def cpu_share(usable):
+    """Host cores one GPU's CPU baseline may use: the job's per-GPU CPU share when the machine states one
+    (OMP_NUM_THREADS, set to the per-GPU share on the GPU pool: 16), else the usable cores over the node's 8 GPUs."""
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        return max(1, min(int(omp), usable)), f"OMP_NUM_THREADS={omp}: the job's per-GPU CPU share"
+    return max(1, usable // 8), f"{usable} usable host CPUs / 8 GPUs per node"
+
+
+def mat_delta(A, B):
+    """(translation m, rotation rad) between two 4x4 poses."""
+    import numpy as np
+    from lmsf import synth
+    return float(np.linalg.norm(A[:3, 3] - B[:3, 3])), synth.rot_angle_of_matrix(A[:3, :3].T @ B[:3, :3])
 
 
 def host_cpu():
@@ -615,7 +636,7 @@ def run_batch(args, d):
                         "traffic: PMC bytes per outer iteration (memo pass + search) from a one-stream rocprofv3 run "
                         "of the same per-context batch (device-wide counters, profiles/); avg_launch_ms: device "
                         "wall-clock stamps around each search launch of a live untimed pass running one context "
-                        "stream at a time", solo=solo)
+                        "stream at a time", solo=solo, dense=cfg == "C5")
     h2d = None
     if cfg == "C2" and (args.h2d in ("on", "shadow") or (args.h2d == "auto" and U == n_units)):
         # SURVEY 8(d) "including ... H2D of the scan": the same K steps with every step's scans streamed
@@ -685,9 +706,9 @@ def run_batch(args, d):
                          f"excluded), {cpu_el:.1f} s on 1 thread of a {model} ({os.cpu_count()} host CPUs, "
                          f"{usable} usable)"}
         pose_dv = {"scans": n_done, "max_m": worst_t, "max_rad": worst_r}
-        # the same restatement with OpenMP over queries on the host cores this job
-        # may use (the GPU box grants 16 per GPU), reported beside the single-thread baseline
-        nt = max(1, min(16, usable))
+        # the same restatement with OpenMP over queries on one GPU's share of the host cores,
+        # reported beside the single-thread baseline (cpu_share: the share and where it comes from)
+        nt, share_basis = cpu_share(usable)
         oracle.set_threads(nt)
         m_done = 0
         t2 = time.perf_counter()
@@ -699,7 +720,8 @@ def run_batch(args, d):
             m_done += 1
         mt_el = time.perf_counter() - t2
         oracle.set_threads(1)
-        cpu["multi_thread"] = {"value": round(m_done / mt_el, 3), "cores": nt,
+        cpu["multi_thread"] = {"value": round(m_done / mt_el, 3), "cores": nt, "cores_basis": share_basis,
+                               "host_cpus": os.cpu_count(), "usable_cpus": usable,
                                "sample": f"{m_done} {'scans' if cfg == 'C2' else 'pairs'}, {mt_el:.1f} s, OpenMP "
                                          f"over queries"}
     if rank == 0:
@@ -768,7 +790,7 @@ def run_streams(args, d):
     cap = max_pts + 64
     fbuf = torch.zeros((2 * cap, 4), dtype=torch.float32, device=d.dev)       # [edges | surfs] of own scan
     xchg = multi.KeyframeExchange(cap, world, d.dev)
-    state = {"i": 0, "kf": 0, "err": [], "xchg_s": 0.0}
+    state = {"i": 0, "kf": 0, "err": [], "xchg_s": 0.0, "poses": []}
 
     phases = collections.defaultdict(float) if os.environ.get("LMSF_BENCH_PHASES") else None
 
@@ -811,6 +833,7 @@ def run_streams(args, d):
         Tt[:3, :3] = synth.quat_to_mat(truth[i][:4])
         Tt[:3, 3] = truth[i][4:]
         state["err"].append(float(np.linalg.norm(P[:3, 3] - Tt[:3, 3])))
+        state["poses"].append(P.copy())
         state["i"] += 1
         return P
 
@@ -819,6 +842,7 @@ def run_streams(args, d):
         nst = state["i"]
         print("phases ms/step: " + "  ".join(f"{k} {1e3 * v / nst:.3f}" for k, v in phases.items()), file=sys.stderr)
     ks = timed_stats(ctx)
+    pose_dv = None
     roof = knn_roofline(ks, mean_n27, load_traffic(args.traffic_json, config="C4", batch=1, map_points=map_points),
                         elapsed, "one 63k-query scan per launch (8 lanes per query): latency-bound launches")
     cpu = None
@@ -833,6 +857,7 @@ def run_streams(args, d):
         ot.set_prior_map(1, em_t.cpu().numpy())      # the same broadcast map
         ot.set_prior_map(2, sm_t.cpu().numpy())
         n_done = 0
+        worst = [0.0, 0.0]
         t1 = time.perf_counter()
         while n_done < n and (n_done == 0 or time.perf_counter() - t1 < args.cpu_seconds):
             e, s, _, _ = oracle.extract(scans[n_done])
@@ -840,8 +865,11 @@ def run_streams(args, d):
             if typ:
                 ot.add_keyframe(e, s, ot.curr)
                 ot.commit()
+            dt, dr = mat_delta(state["poses"][n_done], ot.curr)   # the GPU tracker's pose of the same scan
+            worst = [max(worst[0], dt), max(worst[1], dr)]
             n_done += 1
         cpu_el = time.perf_counter() - t1
+        pose_dv = {"scans": n_done, "max_m": worst[0], "max_rad": worst[1]}
         cpu = {"value": round(n_done / cpu_el, 3), "unit": "scans/s", "cores": 1, "kind": "port",
                "cpu_model": host_cpu()[0],
                "sample": f"first {n_done} scans of the rank-0 stream (extract + tracker Solve with "
@@ -858,7 +886,8 @@ def run_streams(args, d):
              keyframes_appended=state["kf"],
              # host time in the keyframe exchange per scan (the collectives at world > 1), over all steps run
              keyframe_exchange_ms_per_step=round(1e3 * state["xchg_s"] / max(state["i"], 1), 4),
-             keyframe_payload_bytes_per_step=int(xchg.payload_bytes / max(xchg.steps, 1)))
+             keyframe_payload_bytes_per_step=int(xchg.payload_bytes / max(xchg.steps, 1)),
+             **({"pose_delta_vs_cpu": pose_dv} if cpu is not None else {}))
     tr.close()
     ctx.close()
 
@@ -887,17 +916,19 @@ def run_dual(args, d):
     ctx = _lib.Context(device=d.gpu, max_batch=1, max_scan_points=max_pts + 64, max_features=max_pts + 64)
     apply_options(args, [ctx])
     system = dual.DualLidarSystem(ctx, extrinsic=X0)
-    state = {"i": 0}
+    state = {"i": 0, "poses": []}
 
     def step():
         i = state["i"]
         nxt = (prim_dev[i + 1], sub_dev[i + 1]) if not args.no_prefetch and i + 1 < len(prim_dev) else None
         out = system.process(prim_dev[i], sub_dev[i], 0.1 * i, next_frame=nxt)
+        state["poses"].append((out[0].copy(), out[1].copy()))
         state["i"] += 1
         return out
 
     elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx], not args.no_n27)
     ks = timed_stats(ctx)
+    pose_dv = None
     roof = knn_roofline(ks, mean_n27, load_traffic(args.traffic_json, config="C3", batch=1), elapsed,
                         "one ~63k-query scan per launch (8 lanes per query) against the voxelised local map: "
                         "latency-bound launches")
@@ -911,6 +942,7 @@ def run_dual(args, d):
         ot = OT.Tracker()
         ext = X0.copy()
         n_done = 0
+        worst = [0.0, 0.0]
         t1 = time.perf_counter()
         while n_done < n and (n_done == 0 or time.perf_counter() - t1 < args.cpu_seconds):
             ep, sp, _, _ = oracle.extract(ds.primary[n_done])
@@ -919,8 +951,12 @@ def run_dual(args, d):
             prim = ot.curr.copy()
             sub, _ = ot._register({1: es, 2: ss}, dual.iso_mul(prim, ext))
             ext = dual.iso_mul(dual.iso_inv(prim), sub)
+            for g, o in zip(state["poses"][n_done], (prim, sub)):   # the GPU's primary and refined sub poses
+                dt, dr = mat_delta(g, o)
+                worst = [max(worst[0], dt), max(worst[1], dr)]
             n_done += 1
         cpu_el = time.perf_counter() - t1
+        pose_dv = {"frames": n_done, "max_m": worst[0], "max_rad": worst[1]}
         cpu = {"value": round(n_done / cpu_el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
                "cpu_model": host_cpu()[0],
                "sample": f"first {n_done} frames of the same dual-LiDAR sequence (2 extractions, tracker Solve, "
@@ -934,7 +970,8 @@ def run_dual(args, d):
              f"tracking (reference decay schedule) + sub-LiDAR refine against the voxelised 10-keyframe local map",
              {"systems": world, "parallelism": f"system-per-GPU x{world}", "extract_ahead": not args.no_prefetch},
              roof, cpu,
-             extrinsic_error={"m": ext_err[0], "rad": ext_err[1]})
+             extrinsic_error={"m": ext_err[0], "rad": ext_err[1]},
+             **({"pose_delta_vs_cpu": pose_dv} if cpu is not None else {}))
     system.close()
     ctx.close()
 

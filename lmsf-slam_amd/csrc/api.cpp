@@ -94,6 +94,26 @@ uint32_t lmsf::next_lookback_epoch() {
     return e;
 }
 
+hipMemPool_t lmsf::growth_pool() {
+    static std::mutex mu;
+    static hipMemPool_t pools[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!pools[dev]) {
+        hipMemPoolProps props{};
+        props.allocType = hipMemAllocationTypePinned;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        hipMemPool_t p = nullptr;
+        if (hipMemPoolCreate(&p, &props) != hipSuccess) return nullptr;
+        uint64_t keep = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
+        pools[dev] = p;
+    }
+    return pools[dev];
+}
+
 // Host wait on a stream of the latency-bound single-scan paths (extraction read-back, solve, tracker
 // commit).  A/B builds: LMSF_SPIN_SYNC=1 polls hipStreamQuery instead of hipStreamSynchronize: on one box (C4
 // / C3 ms per scan, two runs each: 1.55, 1.74 / 1.50, 1.73 spinning vs 1.63, 1.71 / 1.52, 1.50 blocking)

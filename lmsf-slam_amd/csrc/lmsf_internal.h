@@ -29,10 +29,23 @@ inline size_t grow_cap(size_t need, size_t cap) { return need > cap + cap / 2 ? 
 // are stream-ordered allocations: a growth allocates the new buffers and frees the old ones on the stream that
 // uses them next, which every earlier user is ordered before ("growth"), so no device
 // drain and no host wait (r04 drained the whole device -- every context's streams -- per growth).
+// The pool of these allocations on the current device (created once, never trims: a freed block stays cached for
+// the next growth instead of going back to the driver at every synchronisation).
+hipMemPool_t growth_pool();
+#ifndef LMSF_GROW_POOL
+#define LMSF_GROW_POOL 1   // A/B builds: 0 = the device's default pool
+#endif
 template <typename T>
 hipError_t galloc(T** p, size_t count, hipStream_t s) {
     *p = nullptr;
-    return hipMallocAsync((void**)p, (count ? count : 1) * sizeof(T), s);
+    const size_t bytes = (count ? count : 1) * sizeof(T);
+#if LMSF_GROW_POOL
+    hipMemPool_t pool = growth_pool();
+    if (!pool) return hipErrorOutOfMemory;
+    return hipMallocFromPoolAsync((void**)p, bytes, pool, s);
+#else
+    return hipMallocAsync((void**)p, bytes, s);
+#endif
 }
 inline void gfree(void* p, hipStream_t s) {
     if (p) (void)hipFreeAsync(p, s);

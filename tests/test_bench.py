@@ -101,3 +101,41 @@ def test_in_turn_schedule(n_units, chunk, P):
     assert not inflight
     covered = sorted(u for a, m in launched for u in range(a, a + m))
     assert covered == list(range(n_units))
+
+
+def test_kernel_labels_and_cpu_share(monkeypatch):
+    """the roofline names the kernels it timed (dense maps: the two first-pass-grid passes and the
+    pass-2 fit; sparse batch maps: the memo pass + fused search; tracking: the single-scan search), and the
+    multi-thread CPU baseline runs on a stated per-GPU share of the host cores."""
+    bench = _bench_module()
+    ks = types.SimpleNamespace(launches=10, total_ms=10.0, queries=1000, reused_queries=0, fused_launches=10, n27_sum=0)
+    dense = bench.knn_roofline(ks, 50.0, None, 0.02, "n", dense=True)["kernel"]
+    assert dense.startswith("dense_pass1_kernel + dense_pass2_kernel + dense_fit2_kernel")
+    assert bench.knn_roofline(ks, 50.0, None, 0.02, "n")["kernel"].startswith("match_memo_kernel + match_fit_kernel")
+    single = types.SimpleNamespace(**dict(vars(ks), fused_launches=0))
+    assert "match_" not in bench.knn_roofline(single, 50.0, None, 0.02, "n")["kernel"]
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    assert bench.cpu_share(256) == (16, "OMP_NUM_THREADS=16: the job's per-GPU CPU share")
+    assert bench.cpu_share(8)[0] == 8
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    n, basis = bench.cpu_share(256)
+    assert n == 32 and "/ 8 GPUs" in basis
+
+
+def test_tracking_lines_carry_pose_delta():
+    """The C3 / C4 lines report the GPU-vs-CPU pose difference over the frames the CPU baseline tracked
+    (pose_delta_vs_cpu), as the C2 / C5 lines do; mat_delta is the 4x4 form of synth.pose_delta."""
+    import numpy as np
+    bench = _bench_module()
+    src = open(BENCH).read()
+    for fn in ("def run_streams", "def run_dual"):
+        body = src[src.index(fn):]
+        body = body[:body.index("\ndef ", 1)]
+        assert '"pose_delta_vs_cpu": pose_dv' in body and "mat_delta(" in body, fn
+    A = np.eye(4)
+    B = np.eye(4)
+    B[:3, 3] = (0.0, 3e-5, 4e-5)
+    c, s = np.cos(1e-6), np.sin(1e-6)
+    B[:2, :2] = [[c, -s], [s, c]]
+    dt, dr = bench.mat_delta(A, B)
+    assert abs(dt - 5e-5) < 1e-12 and abs(dr - 1e-6) < 1e-12
