@@ -239,6 +239,7 @@ struct lmsf_ctx {
     bool pre_job = false, pre_quit = false;
     lmsf_status pre_rc = LMSF_OK;
     unsigned* d_lmsync = nullptr;     // [2 B] lm_loop_kernel counters
+    unsigned* d_ticket = nullptr;     // [B][track_ticket_words(F)] track_match_kernel group tickets (self re-arming)
     // streaming ingest (lmsf_batch_load_scans_async): copies on their own stream into the raw slots,
     // ordered after the extraction that last read them (ev_raw_free) and before the next (ev_raw_ready)
     hipStream_t copy_stream = nullptr;
@@ -772,6 +773,10 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
         unsigned long long* st1 = t ? st0 + 1 : nullptr;
         // batch launches: one fused search + fit kernel (it is then the timed neighbour-search launch)
         const bool fused = match_fit_applies(ge2, gs2, bv, c->cfg.solver);
+        // single-scan Ceres-LM launches with the slot memo: the search + fit kernel (the timed launch ends when the
+        // LM kernel after it starts: its entry stamp)
+        const bool track = !fused && !gn && memo_on && track_fused_enabled() &&
+                           knn_team_for((size_t)c->F * nb) == 8 && bv.fit_per_thread == 1;
         // Stamps: batch (fused) launches are timed by a one-lane stamp kernel on each side, single-scan
         // launches in-kernel (knn_kernel's first block at entry, fit_eval's at entry).  Measured r02: the
         // stamp kernels cost ~2.5% of a C4 scan (2 x ~4.5 us of serialised dispatch per outer iteration)
@@ -788,14 +793,19 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
             BatchView bvk = bv;
             bvk.stamp_start = st0;
             bvk.memo = !gn && o > 0 && !c->count27 && memo_on ? 1 : 0;
-            HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{},
-                                 bvk, gn ? 1 : 0, s, !gn && memo_on));
+            if (track) {   // search + fit + first evaluation in one launch (k_match.hip track_match_kernel)
+                HIPCHK(c, launch_track_match(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{},
+                                             gs2.n ? gs : GridView{}, bvk, c->d_ticket, s));
+            } else {
+                HIPCHK(c, launch_knn(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{}, gs2.n ? gs : GridView{},
+                                     bvk, gn ? 1 : 0, s, !gn && memo_on));
+            }
         }
         if (fused && t) HIPCHK(c, launch_stamp(st1, s));
         if (t) c->ev_used += 2;
         c->knn_launches++;
         if (fused) c->fused_launches++;
-        if (!fused) {
+        if (!fused && !track) {
             BatchView bvf = bv;
             bvf.stamp_end = st1;   // fit_eval starts when the search has drained
             HIPCHK(c, launch_fit_eval(ge, gs, bvf, c->cfg.solver, s));
@@ -826,9 +836,10 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
             // single-scan launches: the whole LM of this outer iteration in one launch when its grid is
             // co-resident (lm_loop_kernel; A/B builds: LMSF_LM_LOOP=0 for the 9-launch form)
             static const bool loop_on = ab_int("LMSF_LM_LOOP", 1) != 0;
+            if (track) bvb.stamp_end = st1;
             if (!fused && loop_on && c->opt[LMSF_OPT_LM_LOOP] && !c->loop_off_once &&
                 nb * lm_loop_blocks(bv) <= kLoopMaxBlocks) {
-                HIPCHK(c, launch_lm_loop(bv, o, c->d_lmsync, c->d_error + 16,
+                HIPCHK(c, launch_lm_loop(bvb, o, c->d_lmsync, c->d_error + 16,
                                          c->opt[LMSF_OPT_LOOP_FAULT_TEST] ? 0u : kLoopSpinDefault, s));
             } else {
                 HIPCHK(c, launch_lm_begin(bvb, s));
@@ -1052,7 +1063,8 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     void* bufs[] = {c->feat, c->feat_src, c->n_edge, c->n_surf, c->nnp, c->prevw, c->memo_nbr, c->wl, c->wlim, c->wcount, c->n_search, c->rec_p, c->rec_v, c->rec_e, c->partials, c->partials_gn,
                     c->gn_rows, c->st, c->d_poses, c->d_n27, c->raw, c->raw_count, c->ring_id, c->tile_counts,
                     c->ring_start, c->ring_pts, c->ring_src, c->sort_key,
-                    c->sort_idx, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->featp, c->n_pos, c->d_error, c->d_lmsync};
+                    c->sort_idx, c->ring_edge_cnt, c->ring_surf_cnt, c->qcode, c->qslot, c->fslot, c->featp, c->n_pos, c->d_error, c->d_lmsync,
+                    c->d_ticket};
     for (void* p : bufs) hipFree(p);
     void* pre_bufs[] = {c->alt.feat, c->alt.feat_src, c->alt.n_edge, c->alt.n_surf, c->alt.qslot, c->alt.fslot,
                         c->alt.featp, c->alt.n_pos, c->pre_raw, c->pre_raw_count, c->pre_raw_off};
@@ -1167,6 +1179,8 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     CHK(dalloc(&c->d_error, 64));
     CHK(dalloc(&c->d_lmsync, 2 * B));
     CHK(hipMemset(c->d_lmsync, 0, 2 * B * sizeof(unsigned)));
+    CHK(dalloc(&c->d_ticket, B * track_ticket_words(F)));
+    CHK(hipMemset(c->d_ticket, 0, B * track_ticket_words(F) * sizeof(unsigned)));
     CHK(hipMemset(c->d_error, 0, 64 * sizeof(int)));
     CHK(hipMemset(c->n_edge, 0, B * sizeof(int)));
     CHK(hipMemset(c->n_surf, 0, B * sizeof(int)));

@@ -832,6 +832,258 @@ __global__ __launch_bounds__(256) void fit_eval_kernel(BatchView bv, int solver)
     block_reduce_packet(P, bv.partials + ((size_t)b * bv.max_parts + blockIdx.x) * kPacket);
 }
 
+// Write-through / L2-bypassing accesses for packets other blocks read inside the same launch (per-XCD L2s are not
+// coherent, MI355X_MICROARCH.md): agent-scope atomic stores and loads.
+__device__ __forceinline__ void coherent_store_f64(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double coherent_load_f64(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<double*>(p)),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// ---------------------------------------------------------------- single-scan search + fit (tracking, Ceres-LM)
+// Single-scan launches (C3 / C4 tracking: one ~63k-query scan) run the 8-lane search, the line / plane fit, the
+// record write and the first evaluation in ONE launch (r04: knn_kernel<8> then fit_eval_kernel<1>, the 5
+// neighbours handed over through nnp, knn lane utilisation 0.50: the teams of memo-reused queries idled beside
+// the walking ones).  A block of 8 waves takes 64 consecutive search positions (featp order: edges then surfs,
+// each in ring order; slot order for host features):
+//   1. wave 0, one lane per position: its query and the slot memo test (knn_kernel<., MEMO>'s rule); the
+//      positions that must walk are listed in LDS by ballot compaction;
+//   2. the block's 64 8-lane teams take the listed positions in order (a wave with no entry goes straight to the
+//      barrier), walk (knn_walk<8>, 6 keys), merge, and leave the 5 neighbours in LDS and nnp and the anchor;
+//   3. waves 1-7 exit (their SIMD slots go to other blocks' walks); wave 0 fits its 64 positions -- neighbours
+//      from registers (memo reuse) or LDS (walked) -- writes the records and its packet at the linearisation pose
+//      (write-through); the last block of each group of 4 (agent-scope ticket) sums the group's packets in block
+//      order into the group packet, so lm_begin / lm_loop read one packet per 256 positions (fit_eval_kernel<1>'s
+//      count) and the sums do not depend on which block came last.
+// Records and the memo state stay by slot (the single-scan layout lmsf_match / capture read).
+#ifndef LMSF_TRACK_FUSED
+#define LMSF_TRACK_FUSED 1
+#endif
+constexpr int kTrackPos = 64;     // search positions per block (one 8-lane team each)
+constexpr int kTrackGroup = 4;    // blocks per packet: 256 positions
+__host__ __device__ size_t track_ticket_words(size_t feat_stride) { return (feat_stride + kTrackPos * kTrackGroup - 1) / (kTrackPos * kTrackGroup); }
+
+template <bool TWO>
+__global__ __launch_bounds__(512) void track_match_kernel(GridView ge, GridView gs, GridView ge2, GridView gs2,
+                                                          BatchView bv, unsigned* ticket) {
+    constexpr int T = 8, NK = 6;
+    __shared__ float4 s_nb[kTrackPos][5];
+    __shared__ float4 s_q[kTrackPos];     // listed entries: query (xyz), search radius^2 (w)
+    __shared__ int s_pos[kTrackPos];      // listed entries: block lane | is_edge << 8
+    __shared__ int s_slot[kTrackPos];     // listed entries: the feature slot
+    __shared__ int s_nwalk;
+    __shared__ unsigned long long s_n27;
+    stamp_if(bv.stamp_start, blockIdx.x == 0 && blockIdx.y == 0);
+    const int b = blockIdx.y;
+    const int ne = bv.n_edge[b], nq = ne + bv.n_surf[b];
+    const int pos0 = blockIdx.x * kTrackPos;
+    if (pos0 >= nq) return;   // block-uniform
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t F = bv.feat_stride;
+    const Pose P = load_pose(bv.st[b].x);
+    // ---- 1. wave 0: the queries, the memo test, the walk list
+    bool valid = false, is_edge = false, reuse = false;
+    int q = 0;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    float3 w = make_float3(0.f, 0.f, 0.f);
+    float4 mo[5];   // a reused position's 5 neighbours in this search's order
+    if (wave == 0) {
+        const int i = pos0 + lane;
+        valid = i < nq;
+        if (valid) {
+            if (bv.fslot) {
+                p = bv.featp[(size_t)b * F + i];
+                q = __float_as_int(p.w);
+            } else {
+                q = i;
+                p = bv.feat[(size_t)b * F + i];
+            }
+            is_edge = q < ne;
+            w = associate(P, p);
+        }
+        const size_t slot = (size_t)b * F + q;
+        float lim = kFullLim;
+        if (valid && bv.memo) {
+            const float4 pw = bv.prevw[slot];
+            if (pw.w >= 0.f) {
+                const double dx = (double)w.x - pw.x, dy = (double)w.y - pw.y, dz = (double)w.z - pw.z;
+                const double dd = sqrt(dx * dx + dy * dy + dz * dz);
+                const double s6 = (double)__int_as_float(bv.memo_nbr[memo_idx(b, 5, q, F)]);
+                const double r6 = s6 + dd + 1e-5;
+                if (r6 < 1.0 && bv.memo_bound) lim = fminf(kFullLim, (float)(r6 * r6) + 1e-5f);
+                const float4* nn_in = bv.nnp + slot * 5;
+                double k5[5];
+                float4 m[5];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    m[j] = nn_in[j];
+                    k5[j] = nn_key(w, m[j], (uint32_t)__float_as_int(m[j].w));
+                }
+                key_cswap(k5[0], k5[1]); key_cswap(k5[3], k5[4]); key_cswap(k5[2], k5[4]);
+                key_cswap(k5[2], k5[3]); key_cswap(k5[0], k5[3]); key_cswap(k5[0], k5[2]);
+                key_cswap(k5[1], k5[4]); key_cswap(k5[1], k5[3]); key_cswap(k5[1], k5[2]);
+                bool same = true;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) same = same && (uint32_t)key_bits(k5[j]) == (uint32_t)__float_as_int(m[j].w);
+                reuse = key_bits(k5[4]) < kSentinel &&
+                        (bv.memo_exact ? sqrt((double)key_d2(k5[4])) + dd + 1e-5 < s6
+                                       : same && 2.0 * dd + 1e-5 < (double)pw.w);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {   // the set in key order: what the walk would return
+                    float4 o = m[0];
+#pragma unroll
+                    for (int t = 1; t < 5; ++t)
+                        if ((uint32_t)__float_as_int(m[t].w) == (uint32_t)key_bits(k5[j])) o = m[t];
+                    mo[j] = o;
+                }
+                if (reuse && !same) {
+                    float4* nn_out = bv.nnp + slot * 5;
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) nn_out[j] = mo[j];
+                }
+            }
+        }
+        const bool walk = valid && !reuse;
+        const unsigned long long todo = __ballot(walk);
+        const int rank = __popcll(todo & ((1ull << lane) - 1ull));
+        if (walk) {
+            s_q[rank] = make_float4(w.x, w.y, w.z, lim);
+            s_pos[rank] = lane | (is_edge ? 256 : 0);
+            s_slot[rank] = q;
+        }
+        if (lane == 0) {
+            s_nwalk = __popcll(todo);
+            s_n27 = 0ull;
+        }
+        if (bv.n27) {
+            const unsigned long long vm = __ballot(valid), rm = __ballot(reuse);
+            if (lane == 0) {
+                unsigned long long* shard = bv.n27 + (size_t)((blockIdx.x + blockIdx.y) & (kCounterShards - 1)) * 16;
+                atomicAdd(shard + 1, (unsigned long long)__popcll(vm));
+                if (rm) atomicAdd(shard + 2, (unsigned long long)__popcll(rm));
+            }
+        }
+    }
+    __syncthreads();
+    // ---- 2. the listed positions, one 8-lane team each
+    const int nwalk = s_nwalk;
+    if (wave * (64 / T) < nwalk) {   // wave-uniform: the wave's first team has an entry
+        const int team = threadIdx.x / T, tl = threadIdx.x % T;
+        if (team < nwalk) {          // team-uniform
+            const float4 qe = s_q[team];
+            const int pe = s_pos[team];
+            const bool edge_q = (pe & 256) != 0;
+            const GridView g = pick_grid(edge_q, ge, gs);
+            const GridView g2 = pick_grid(edge_q, ge2, gs2);
+            const double sentinel = key_as_double(kSentinel);
+            double k[NK];
+#pragma unroll
+            for (int j = 0; j < NK; ++j) k[j] = sentinel;
+            unsigned int c27 = 0;
+            knn_walk<T, TWO, false, kKnnUnroll, NK>(g, g2, make_float3(qe.x, qe.y, qe.z), tl, bv.count27, k, c27, qe.w);
+            double res[NK];
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                double mn = k[0];
+#pragma unroll
+                for (int o = T / 2; o >= 1; o >>= 1) mn = key_min(mn, __shfl_xor(mn, o, T));
+                res[i] = mn;
+                if (key_bits(k[0]) == key_bits(mn)) {
+#pragma unroll
+                    for (int j = 0; j + 1 < NK; ++j) k[j] = k[j + 1];
+                    k[NK - 1] = sentinel;
+                }
+            }
+            const int pl = pe & 255;
+            const int qs = s_slot[team];
+            const size_t slot = (size_t)b * F + qs;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                if (i == tl) {
+                    float4 o = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+                    const uint64_t kb = key_bits(res[i]);
+                    if (kb < kSentinel) {
+                        const uint32_t idx = (uint32_t)kb;
+                        const bool second = TWO && idx >= (uint32_t)g.n;
+                        const float4 m = second ? g2.orig[idx - (uint32_t)g.n] : g.orig[idx];
+                        o = make_float4(m.x, m.y, m.z, __int_as_float((int)idx));
+                    }
+                    bv.nnp[slot * 5 + i] = o;
+                    s_nb[pl][i] = o;
+                }
+            }
+            if (tl == 0) {   // the anchor of this full search
+                float gap = -1.f;
+                if (key_bits(res[4]) < kSentinel) {
+                    const double s6 = sqrt((double)fminf(key_d2(res[NK - 1]), 1.0f));
+                    gap = (float)(s6 - sqrt((double)key_d2(res[4])));
+                    bv.memo_nbr[memo_idx(b, 5, qs, F)] = __float_as_int((float)s6);
+                }
+                bv.prevw[slot] = make_float4(qe.x, qe.y, qe.z, gap);
+            }
+            if (bv.count27 && c27) atomicAdd(&s_n27, (unsigned long long)c27);
+        }
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    if (bv.n27 && lane == 0 && s_n27)
+        atomicAdd(bv.n27 + (size_t)((blockIdx.x + blockIdx.y) & (kCounterShards - 1)) * 16, s_n27);
+    // ---- 3. wave 0: the fits, the records, the packet
+    double Pk[kPacket];
+#pragma unroll
+    for (int i = 0; i < kPacket; ++i) Pk[i] = 0.0;
+    if (valid) {
+        if (!reuse)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) mo[j] = s_nb[lane][j];
+        fit_query(bv, LMSF_SOLVER_CERES_LM, (size_t)b * F + q, is_edge, p, w, mo, P, Pk);
+    }
+    // the block's packet (wave butterfly: entry e in lane 2e), stored write-through above the group packets
+    butterfly_step<16>(Pk, lane);
+    butterfly_step<8>(Pk, lane);
+    butterfly_step<4>(Pk, lane);
+    butterfly_step<2>(Pk, lane);
+    butterfly_step<1>(Pk, lane);
+    const double v = Pk[0] + __shfl_xor(Pk[0], 1, 64);
+    double* blk = bv.partials + ((size_t)b * bv.max_parts + bv.max_parts / 2) * kPacket;   // [ceil(F / 64)] packets
+    if ((lane & 1) == 0) coherent_store_f64(blk + (size_t)blockIdx.x * kPacket + (lane >> 1), v);
+    __builtin_amdgcn_s_waitcnt(0);   // this wave's packet stores are complete before its ticket
+    const int grp = blockIdx.x / kTrackGroup;
+    const int nblk = (nq + kTrackPos - 1) / kTrackPos;
+    const int members = min(kTrackGroup, nblk - grp * kTrackGroup);
+    unsigned* tk = ticket + (size_t)b * track_ticket_words(F) + grp;
+    unsigned mine = 0;
+    if (lane == 0) mine = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mine = __shfl(mine, 0, 64);
+    if ((int)mine + 1 != members) return;
+    // the group's last block: its packets summed in block order into the group packet, the ticket re-armed
+    if (lane < kPacket) {
+        double t = 0.0;
+        for (int j = 0; j < members; ++j)
+            t += coherent_load_f64(blk + (size_t)(grp * kTrackGroup + j) * kPacket + lane);
+        bv.partials[((size_t)b * bv.max_parts + grp) * kPacket + lane] = t;
+    }
+    if (lane == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+bool track_fused_enabled() {
+    static const bool v = ab_int("LMSF_TRACK_FUSED", LMSF_TRACK_FUSED) != 0;
+    return v;
+}
+
+hipError_t launch_track_match(const GridView& edge, const GridView& surf, const GridView& edge2, const GridView& surf2,
+                              const BatchView& bv, unsigned* ticket, hipStream_t s) {
+    const dim3 grid((bv.feat_stride + kTrackPos - 1) / kTrackPos, bv.B);
+    if (edge2.n > 0 || surf2.n > 0)
+        hipLaunchKernelGGL(track_match_kernel<true>, grid, dim3(512), 0, s, edge, surf, edge2, surf2, bv, ticket);
+    else
+        hipLaunchKernelGGL(track_match_kernel<false>, grid, dim3(512), 0, s, edge, surf, edge2, surf2, bv, ticket);
+    return hipGetLastError();
+}
+
 // Fused search + fit for batch launches (one lane per query, Ceres-LM solver): the 5-NN walk of
 // knn_kernel<1, false, PRUNE>, then fit_query (line / plane fit, record write, Huber-weighted packet
 // at the linearisation pose) on the neighbours held in registers -- knn_kernel + fit_eval_kernel
@@ -1501,9 +1753,14 @@ __device__ __forceinline__ void store_kept(const BatchView& bv, int b, int e, si
     int kid[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) kid[j] = key_bits(k[j]) < kSentinel ? (int)(uint32_t)key_bits(k[j]) : -1;
-    int* mp = bv.memo_nbr + memo_idx(b, 0, e, F);
-    *reinterpret_cast<int4*>(mp) = make_int4(kid[0], kid[1], kid[2], kid[3]);
-    mp[4] = kid[4];
+    if constexpr (kMemoAos) {   // one 32-B record: words 0-3 as one 16-B store
+        int* mp = bv.memo_nbr + memo_idx(b, 0, e, F);
+        *reinterpret_cast<int4*>(mp) = make_int4(kid[0], kid[1], kid[2], kid[3]);
+        mp[4] = kid[4];
+    } else {                    // planar A/B layout: word j of position e at memo_idx(b, j, e, F)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) bv.memo_nbr[memo_idx(b, j, e, F)] = kid[j];
+    }
 }
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void dense_pass1_kernel(
     GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, int gx, int remap, unsigned* p2count) {
@@ -1659,6 +1916,89 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FIT ? 3 : L
     }
 }
 
+// LMSF_P2_TEAM = 0 | 2 | 4 | 8 (VERDICT r04 #3a): pass 2's walk with a team of T lanes per listed query instead of
+// one.  r04's one-lane walk ran at lane utilisation 0.36: a few queries walk up to 25 first-pass rows (each two
+// dependent offset loads, then its candidates) while their wave-mates are done.  Here lane t of a team takes rows
+// t, t + T, ... of the same nearest-first order, each lane keeps its own 5 keys, and after every step of T rows the
+// team's bound becomes min(pass-1 bound, the smallest of the lanes' 5th keys) -- never below the team's true 5th
+// key, so the pruning stays exact; the lanes' keys are merged at the end (knn_kernel's team merge).  Same kept 5.
+// Measured r05 (one box, C5 pairs/s): one lane 4,163; T = 2 4,052; T = 4 3,975; T = 8 3,784 -- the team's shared
+// bound prunes later than one lane's own 5th key, and the extra lanes walk rows the one-lane walk never enters.
+// One lane stays the default.
+#ifndef LMSF_P2_TEAM
+#define LMSF_P2_TEAM 0
+#endif
+__constant__ signed char kRing5c[25][2] = {{0, 0},  {0, -1}, {-1, 0}, {1, 0},  {0, 1},  {-1, -1}, {1, -1}, {-1, 1}, {1, 1},
+                                           {0, -2}, {-2, 0}, {2, 0},  {0, 2},  {-1, -2}, {1, -2}, {-2, -1}, {2, -1}, {-2, 1},
+                                           {2, 1},  {-1, 2}, {1, 2},  {-2, -2}, {2, -2}, {-2, 2}, {2, 2}};
+template <int T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_P2_WALK_WAVES))) void dense_pass2_team_kernel(
+    GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, const unsigned* p2count) {
+    const unsigned count = *p2count;
+    const size_t F = bv.feat_stride;
+    const int tl = threadIdx.x % T;
+    const unsigned teams = gridDim.x * (256 / T);
+    for (unsigned li = (blockIdx.x * 256 + threadIdx.x) / T; li < count; li += teams) {   // team-uniform
+        const size_t code = (size_t)(unsigned)bv.wl[li];
+        const float bound = bv.wlim[li];
+        const int b = (int)(code / F), e = (int)(code - (size_t)b * F);
+        const int ne = bv.n_edge[b];
+        const size_t ppos = (size_t)b * F + e;
+        const float4 p = bv.featp[ppos];
+        const bool is_edge = __float_as_int(p.w) < ne;
+        const GridView gf = pick_grid(is_edge, fe, fs);
+        const bool fine = LMSF_PASS2_FINE && gf.n > 0 && gf.sy == 2;
+        const GridView g = pick_grid(fine, gf, pick_grid(is_edge, ge, gs));
+        const float3 w = associate(load_pose(bv.st[b].x), p);
+        const double sentinel = key_as_double(kSentinel);
+        double k[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) k[j] = sentinel;
+        const float4* rp = g.pts;
+        const int nrows = fine ? 25 : 9;
+        const DenseQuery<2> dq(g, w);
+        const int xa = dq.xa, xb = dq.xb;
+        float tb = bound;   // the team's bound
+#pragma unroll 1
+        for (int i0 = 0; i0 < nrows; i0 += T) {
+            const int i = i0 + tl;
+            if (i < nrows) {
+                const float d4 = fminf(tb, key_d2(k[4]));
+                const int dyo = fine ? (int)kRing5c[i][0] : (kDenseRowOrder[i] % 3) - 1;
+                const int dzo = fine ? (int)kRing5c[i][1] : (kDenseRowOrder[i] / 3) - 1;
+                const float lb = dq.lb(dyo, dzo);
+                const uint32_t* row;
+                int sa, sb;
+                if (lb <= d4 && dq.row(g, dyo, dzo, row)) {
+                    dense_window(g, w, d4 * kDenseCull, lb, xa, xb, sa, sb);
+                    if (sa <= sb) {
+                        const uint32_t a = row[sa];
+                        dense_run(k, rp, a, row[sb + 1] - a, w);
+                    }
+                }
+            }
+            float m = key_d2(k[4]);
+#pragma unroll
+            for (int o = T / 2; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o, T));
+            tb = fminf(tb, m);
+        }
+        double res[5];
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {   // team merge: the owning lane pops its head (keys are unique)
+            double mn = k[0];
+#pragma unroll
+            for (int o = T / 2; o >= 1; o >>= 1) mn = key_min(mn, __shfl_xor(mn, o, T));
+            res[r] = mn;
+            if (key_bits(k[0]) == key_bits(mn)) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) k[j] = k[j + 1];
+                k[4] = sentinel;
+            }
+        }
+        if (tl == 0) store_kept(bv, b, e, F, res);
+    }
+}
+
 // The fit of dense_pass2_kernel<false>'s queries (same list, same order): the kept 5 from the memo record.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void dense_fit2_kernel(
     GridView ge, GridView gs, BatchView bv, const unsigned* p2count) {
@@ -1674,9 +2014,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
         const bool is_edge = qq < ne;
         const GridView g = pick_grid(is_edge, ge, gs);   // orig: the caller-order map either way
         const float3 w = associate(load_pose(bv.st[b].x), p);
-        const int* mp = bv.memo_nbr + memo_idx(b, 0, e, F);
-        const int4 m0 = *reinterpret_cast<const int4*>(mp);
-        const int kid[5] = {m0.x, m0.y, m0.z, m0.w, mp[4]};
+        int kid[5];
+        if constexpr (kMemoAos) {
+            const int* mp = bv.memo_nbr + memo_idx(b, 0, e, F);
+            const int4 m0 = *reinterpret_cast<const int4*>(mp);
+            kid[0] = m0.x; kid[1] = m0.y; kid[2] = m0.z; kid[3] = m0.w; kid[4] = mp[4];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) kid[j] = bv.memo_nbr[memo_idx(b, j, e, F)];
+        }
         double k[5];
 #pragma unroll
         for (int j = 0; j < 5; ++j) k[j] = kid[j] >= 0 ? key_as_double((uint64_t)(uint32_t)kid[j]) : key_as_double(kSentinel);
@@ -1789,14 +2135,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_EVAL_W
 // sync[2 b] counts arrivals of slot b across launches; sync[2 b + 1] holds the count at the start of the
 // next launch (written by block 0 after the last wait of this one).
 
-__device__ __forceinline__ void coherent_store_f64(double* p, double v) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double coherent_load_f64(const double* p) {
-    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<double*>(p)),
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
 
 // Every block of the slot arrives once; returns when all nblk of this barrier have (count reaches target).
 __device__ __forceinline__ void slot_barrier(unsigned* cnt, unsigned target, int* err, unsigned spin_limit) {
@@ -1851,6 +2189,7 @@ __device__ void reduce_coherent(const BatchView& bv, int b, int p0, int np, doub
 constexpr bool kLoopCtlWave = LMSF_LOOP_CTL_WAVE != 0;
 __global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, unsigned* sync, int* err,
                                                       unsigned spin_limit) {
+    stamp_if(bv.stamp_end, blockIdx.x == 0 && blockIdx.y == 0);   // the search launch before it has drained
     const int b = blockIdx.y, part = blockIdx.x, nblk = gridDim.x;
     __shared__ SolveState sS;
     __shared__ double tot[kPacket];
@@ -2122,8 +2461,18 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
             if (e != hipSuccess) return e;
             // grid-stride over the list (~10% of the queries on C5): 8 blocks per CU
             if (LMSF_P2_SPLITFIT) {
-                hipLaunchKernelGGL(dense_pass2_kernel<false>, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge, fine_surf,
-                                   bv, (const unsigned*)bv.p2count);
+                static const int team = ab_int("LMSF_P2_TEAM", LMSF_P2_TEAM);
+                const unsigned* cnt = bv.p2count;
+                switch (team) {
+                    case 2: hipLaunchKernelGGL(dense_pass2_team_kernel<2>, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
+                                               fine_surf, bv, cnt); break;
+                    case 4: hipLaunchKernelGGL(dense_pass2_team_kernel<4>, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
+                                               fine_surf, bv, cnt); break;
+                    case 8: hipLaunchKernelGGL(dense_pass2_team_kernel<8>, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
+                                               fine_surf, bv, cnt); break;
+                    default: hipLaunchKernelGGL(dense_pass2_kernel<false>, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
+                                                fine_surf, bv, cnt); break;
+                }
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
                 hipLaunchKernelGGL(dense_fit2_kernel, dim3(2048), dim3(256), 0, s, edge, surf, bv, (const unsigned*)bv.p2count);

@@ -59,6 +59,7 @@ __global__ void state_init_kernel(BatchView bv, const double* poses) {
 #endif
 constexpr int kCtlMode = LMSF_CTL_MODE;
 __global__ __launch_bounds__(kBeginThreads) LMSF_CTL_ATTR void lm_begin_kernel(BatchView bv) {
+    stamp_if(bv.stamp_end, blockIdx.x == 0);   // the search launch before it has drained (single-scan launches)
     const int b = blockIdx.x;
     const int nq = bv.n_edge[b] + bv.n_surf[b];
 #ifdef LMSF_STEP_PROFILE

@@ -218,6 +218,13 @@ hipError_t launch_knn(const GridView& edge, const GridView& surf, const GridView
                       const BatchView& bv, int skip_converged, hipStream_t s, bool memo = false);
 hipError_t launch_fit_eval(const GridView& edge, const GridView& surf, const BatchView& bv, int solver,
                            hipStream_t s);
+// Single-scan Ceres-LM launches: the search, the fit, the records and the first evaluation in one launch
+// (k_match.hip track_match_kernel; its packets are fit_eval_kernel<1>'s count, one per 256 positions).  ticket:
+// [B][track_ticket_words(F)] counters, zeroed once (the kernel re-arms them).
+bool track_fused_enabled();
+__host__ __device__ size_t track_ticket_words(size_t feat_stride);
+hipError_t launch_track_match(const GridView& edge, const GridView& surf, const GridView& edge2, const GridView& surf2,
+                              const BatchView& bv, unsigned* ticket, hipStream_t s);
 hipError_t launch_lm_begin(const BatchView& bv, hipStream_t s);
 // One LM inner iteration: evaluation at the candidate, then the step control.
 hipError_t launch_lm_eval_step(const BatchView& bv, int outer, int is_last, hipStream_t s);
