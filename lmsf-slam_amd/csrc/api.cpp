@@ -787,6 +787,8 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
         if (fused) {
             BatchView bvo = bv;
             bvo.memo = batch_memo(o) ? 1 : 0;
+            // dense maps: the outer iteration before the memo pass keeps 6 exact keys and leaves the anchors
+            bvo.anchor = memo_on && !c->count27 && o == memo_from - 1 ? 1 : 0;
             HIPCHK(c, launch_match_fit(ge, gs, bvo, s, fe, fs));
         }
         else {   // single-scan launches: the 8-lane search, with the slot memo under the Ceres-LM solver
@@ -2171,6 +2173,10 @@ lmsf_status ctx_window_target(lmsf_ctx* c, int kind, size_t n_max, float4** orig
     *orig = reinterpret_cast<float4*>(m.orig);
     *bb = m.d_bb;
     return LMSF_OK;
+}
+
+lmsf_status ctx_window_reserve(lmsf_ctx* c, int kind, size_t n, hipStream_t s) {
+    return grid_reserve(c, c->map[kind], n, s);
 }
 
 lmsf_status ctx_window_build(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s) {

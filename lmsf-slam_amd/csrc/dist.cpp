@@ -213,9 +213,14 @@ lmsf_status lmsf_group_exchange_keyframes(lmsf_group* g, const double pose[16], 
     if (!g->custom) {
         LCHK(hipSetDevice(g->device));
         LCHK(ncclGroupStart());
-        if (rows[0]) LCHK(ncclAllGather(feat, g_edge, (size_t)rows[0] * 4, ncclFloat32, g->comm, g->stream));
-        if (rows[1]) LCHK(ncclAllGather(feat + cap * 4, g_surf, (size_t)rows[1] * 4, ncclFloat32, g->comm, g->stream));
-        LCHK(ncclGroupEnd());
+        // a failed enqueue inside the group still closes it (an early return left the RCCL group open on
+        // this rank, misordering its later collectives against the other ranks')
+        bool enq = true;
+        if (rows[0]) enq = ok(ncclAllGather(feat, g_edge, (size_t)rows[0] * 4, ncclFloat32, g->comm, g->stream));
+        if (enq && rows[1])
+            enq = ok(ncclAllGather(feat + cap * 4, g_surf, (size_t)rows[1] * 4, ncclFloat32, g->comm, g->stream));
+        const bool closed = ok(ncclGroupEnd());
+        if (!enq || !closed) return LMSF_ERR_HIP;
         LCHK(hipStreamSynchronize(g->stream));
         return LMSF_OK;
     }

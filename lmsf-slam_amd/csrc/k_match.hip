@@ -860,7 +860,7 @@ __device__ __forceinline__ double coherent_load_f64(const double* p) {
 //      count) and the sums do not depend on which block came last.
 // Records and the memo state stay by slot (the single-scan layout lmsf_match / capture read).
 #ifndef LMSF_TRACK_FUSED
-#define LMSF_TRACK_FUSED 1
+#define LMSF_TRACK_FUSED 0
 #endif
 constexpr int kTrackPos = 64;     // search positions per block (one 8-lane team each)
 constexpr int kTrackGroup = 4;    // blocks per packet: 256 positions
@@ -1708,17 +1708,19 @@ __device__ __forceinline__ void dense_window(const GridView& gg, const float3 w,
     sb = min(xb, (int)floor(((double)w.x + r) * gg.sx) - gg.ox);
 }
 
-__device__ __forceinline__ void key_insert(double (&k)[5], double x) {
+template <int NK>
+__device__ __forceinline__ void key_insert(double (&k)[NK], double x) {
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < NK; ++i) {
         const double lo = key_min(k[i], x);
         x = key_max(k[i], x);
         k[i] = lo;
     }
 }
 
-// One row's candidates [a, a + len) of pts into the kept 5 keys k.
-__device__ __forceinline__ void dense_run(double (&k)[5], const float4* __restrict__ rp, uint32_t a, uint32_t len, const float3 w) {
+// One row's candidates [a, a + len) of pts into the kept NK keys k.
+template <int NK>
+__device__ __forceinline__ void dense_run(double (&k)[NK], const float4* __restrict__ rp, uint32_t a, uint32_t len, const float3 w) {
     uint32_t c = 0;
     for (; c + LMSF_FUSED_UNROLL <= len; c += LMSF_FUSED_UNROLL) {
         float4 m[LMSF_FUSED_UNROLL];
@@ -1749,7 +1751,9 @@ __device__ __forceinline__ void dense_run(double (&k)[5], const float4* __restri
 constexpr int kDenseRowOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // own row, faces, corners (knn_walk's kOrder)
 constexpr float kDenseCull = 1.0f + 1e-5f;                       // knn_walk's kCullLim
 
-__device__ __forceinline__ void store_kept(const BatchView& bv, int b, int e, size_t F, const double (&k)[5]) {
+// The kept 5 indices (-1: none) in key order, for the fit kernel, in the position's memo record.
+template <int NK>
+__device__ __forceinline__ void store_kept(const BatchView& bv, int b, int e, size_t F, const double (&k)[NK]) {
     int kid[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) kid[j] = key_bits(k[j]) < kSentinel ? (int)(uint32_t)key_bits(k[j]) : -1;
@@ -1762,6 +1766,47 @@ __device__ __forceinline__ void store_kept(const BatchView& bv, int b, int e, si
         for (int j = 0; j < 5; ++j) bv.memo_nbr[memo_idx(b, j, e, F)] = kid[j];
     }
 }
+
+// The memo anchor of an exact 6-key search at w (match_fit_kernel's, for the sparse maps' memo pass): the 5
+// indices, s6 (capped at 1 m), the smallest consecutive gap, and prevw = (w, s6 - s5); gap -1: fewer than 5.
+__device__ __forceinline__ void store_anchor(const BatchView& bv, int b, int pos, size_t F, const float3 w,
+                                             const double (&k)[6]) {
+    float gap = -1.f;
+    if (key_bits(k[4]) < kSentinel) {
+        const double s6 = sqrt((double)fminf(key_d2(k[5]), 1.0f));
+        double sj = sqrt((double)key_d2(k[0])), gord = 1.0;
+#pragma unroll
+        for (int j = 1; j < 5; ++j) {
+            const double sn = sqrt((double)key_d2(k[j]));
+            gord = fmin(gord, sn - sj);
+            sj = sn;
+        }
+        gap = (float)(s6 - sj);
+        const int w5 = __float_as_int((float)s6), w6 = __float_as_int((float)fmin(gord, s6 - sj));
+        if constexpr (kMemoAos) {
+            int* mp = bv.memo_nbr + memo_idx(b, 0, pos, F);
+            *reinterpret_cast<int4*>(mp) = make_int4((int)(uint32_t)key_bits(k[0]), (int)(uint32_t)key_bits(k[1]),
+                                                     (int)(uint32_t)key_bits(k[2]), (int)(uint32_t)key_bits(k[3]));
+            *reinterpret_cast<int4*>(mp + 4) = make_int4((int)(uint32_t)key_bits(k[4]), w5, w6, 0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) bv.memo_nbr[memo_idx(b, j, pos, F)] = (int)(uint32_t)key_bits(k[j]);
+            bv.memo_nbr[memo_idx(b, 5, pos, F)] = w5;
+            bv.memo_nbr[memo_idx(b, 6, pos, F)] = w6;
+        }
+    }
+    bv.prevw[(size_t)b * F + pos] = make_float4(w.x, w.y, w.z, gap);
+}
+
+template <int NK>
+__device__ __forceinline__ void first5(const double (&k)[NK], double (&k5)[5]) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) k5[j] = k[j];
+}
+
+// NK = 5, or 6 in the outer iteration before the dense memo starts (BatchView::anchor): the 6th-nearest key is then
+// exact too (rows pruned with it), and complete queries leave the memo anchor.
+template <int NK>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void dense_pass1_kernel(
     GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, int gx, int remap, unsigned* p2count) {
     int bx, b;
@@ -1782,9 +1827,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
     const GridView g = pick_grid(is_edge, pick_grid(fe.n > 0, fe, ge), pick_grid(fs.n > 0, fs, gs));
     const float3 w = associate(load_pose(bv.st[b].x), p);
     const double sentinel = key_as_double(kSentinel);
-    double k[5];
+    double k[NK];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) k[j] = sentinel;
+    for (int j = 0; j < NK; ++j) k[j] = sentinel;
     unsigned int c27 = 0;
     if (valid) {
         // rows resolved up front: the 18 offset loads in flight together
@@ -1815,22 +1860,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
             const uint32_t ln = ln_[i];
-            if (!ln || lb_[i] > key_d2(k[4])) continue;
+            if (!ln || lb_[i] > key_d2(k[NK - 1])) continue;
             dense_run(k, rp, st_[i], ln, w);
         }
     }
-    // complete (5th key within lim1: nothing nearer lies outside the scanned ball) -> fit; else -> pass-2 list
-    const bool p2 = valid && key_d2(k[4]) > g.lim1;
+    // complete (NK-th key within lim1: nothing nearer lies outside the scanned ball) -> fit; else -> pass-2 list
+    const bool p2 = valid && key_d2(k[NK - 1]) > g.lim1;
     const unsigned long long m2 = __ballot(p2);
     int base2 = 0;
     if (lane == 0 && m2) base2 = (int)atomicAdd(p2count, (unsigned)__popcll(m2));
     base2 = __shfl(base2, 0, 64);
-    if (p2) {   // pass 2 from scratch on the 1 m grid, bounded by this 5th key (the 5 nearest lie within it)
+    if (p2) {   // pass 2 from scratch, bounded by this NK-th key (the NK nearest lie within it)
         const int at = base2 + __popcll(m2 & below);
         bv.wl[at] = (int)((size_t)b * F + e);
-        bv.wlim[at] = key_d2(k[4]);
+        bv.wlim[at] = key_d2(k[NK - 1]);
     } else if (valid) {
-        dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);   // g.orig: the caller-order map either way
+        if constexpr (NK == 6) store_anchor(bv, b, e, F, w, k);
+        double k5[5];
+        first5(k, k5);
+        dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k5);   // g.orig: the caller-order map either way
     }
     if (bv.n27) {   // accounting runs: the 27-cell candidates (of the first-pass grid) and the queries
         unsigned int qn = valid ? 1u : 0u;
@@ -1860,15 +1908,91 @@ constexpr int kRing5[25][2] = {{0, 0},  {0, -1}, {-1, 0}, {1, 0},  {0, 1},  {-1,
 #define LMSF_PASS2_FINE 1
 #endif
 
+// The bounded pruned walk of pass 2 (and of the dense memo pass's listed searches): the NK nearest of w within
+// `bound` (a squared distance at least the true NK-th key's), on the first-pass grid's 5 x 5 rows when the kind has
+// one (sy = 2), else the 1 m grid's 3 x 3.
+// A bound within one first-pass cell (bound x margin <= (1 / sy)^2) is walked in pass 1's form: the query's 3 x 3 rows
+// hold the whole ball (its cell +- one cell of 1 / sy m in y and z, +-1 m of x-slices), their offsets resolved up
+// front in one batch of loads, rows entered nearest first while their bound is within the current NK-th key.
+// (r05: pass 2 and the dense memo's searches walked the 25 rows one dependent offset pair at a time -- C5 iteration 0
+// pass 2 3.4 ms, the memo's listed searches 2.2-5.0 ms per dispatch.)
+template <int NK>
+__device__ __forceinline__ void dense_ball_walk(const GridView& g, const float3 w, float lim, double (&k)[NK]) {
+    uint32_t st_[9], ln_[9];
+    float lb_[9];
+    const DenseQuery<1> dq(g, w);
+    const int xa = dq.xa, xb = dq.xb;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        st_[i] = 0;
+        ln_[i] = 0;
+        const int dyo = (kDenseRowOrder[i] % 3) - 1, dzo = (kDenseRowOrder[i] / 3) - 1;
+        const float lb = dq.lb(dyo, dzo);
+        lb_[i] = lb;
+        const uint32_t* row;
+        int sa, sb;
+        if (lb > lim || !dq.row(g, dyo, dzo, row)) continue;
+        dense_window(g, w, lim, lb, xa, xb, sa, sb);
+        if (sa <= sb) {
+            st_[i] = row[sa];
+            ln_[i] = row[sb + 1] - st_[i];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const uint32_t ln = ln_[i];
+        if (!ln || lb_[i] > key_d2(k[NK - 1])) continue;
+        dense_run(k, g.pts, st_[i], ln, w);
+    }
+}
+
+template <int NK>
+__device__ __forceinline__ const GridView dense_bounded_walk(const GridView& ge, const GridView& gs, const GridView& fe,
+                                                             const GridView& fs, bool is_edge, const float3 w, float bound,
+                                                             double (&k)[NK]) {
+    const GridView gf = pick_grid(is_edge, fe, fs);
+    const bool fine = LMSF_PASS2_FINE && gf.n > 0 && gf.sy == 2;
+    const GridView g = pick_grid(fine, gf, pick_grid(is_edge, ge, gs));
+#pragma unroll
+    for (int j = 0; j < NK; ++j) k[j] = key_as_double(kSentinel);
+    if (fine && bound * kDenseCull <= 0.25f) {   // within one 0.5 m first-pass cell
+        dense_ball_walk(g, w, bound * kDenseCull, k);
+        return g;
+    }
+    const float4* rp = g.pts;
+    const int nrows = fine ? 25 : 9;
+    const DenseQuery<2> dq(g, w);   // the 1 m grid's 3 x 3 rows are its inner ring
+    const int xa = dq.xa, xb = dq.xb;
+#pragma unroll 1
+    for (int i = 0; i < nrows; ++i) {
+        const float d4 = fminf(bound, key_d2(k[NK - 1]));
+        const uint32_t* row;
+        int sa, sb;
+        const int dyo = fine ? kRing5[i][0] : (kDenseRowOrder[i] % 3) - 1;
+        const int dzo = fine ? kRing5[i][1] : (kDenseRowOrder[i] / 3) - 1;
+        const float lb = dq.lb(dyo, dzo);
+        if (lb > d4) continue;   // ahead of the row's address and offsets
+        if (!dq.row(g, dyo, dzo, row)) continue;
+        dense_window(g, w, d4 * kDenseCull, lb, xa, xb, sa, sb);
+        if (sa > sb) continue;
+        const uint32_t a = row[sa];
+        dense_run(k, rp, a, row[sb + 1] - a, w);
+    }
+    return g;
+}
+
 // LMSF_P2_SPLITFIT: pass 2 as a walk kernel (no fit: few registers, more waves to hide its row-by-row offset
 // latency; the kept 5 indices left in the position's memo record) and a fit kernel over the same list.
+// (r05: a team of 2 / 4 / 8 lanes per listed query -- rows dealt to the lanes, the team's bound shared after every
+// step -- measured 4,052 / 3,975 / 3,784 vs 4,163 C5 pairs/s for one lane: the shared bound prunes later than one
+// lane's own key, and the extra lanes walk rows one lane never enters.  Not kept.)
 #ifndef LMSF_P2_SPLITFIT
 #define LMSF_P2_SPLITFIT 1
 #endif
 #ifndef LMSF_P2_WALK_WAVES
 #define LMSF_P2_WALK_WAVES 6
 #endif
-template <bool FIT>
+template <bool FIT, int NK>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FIT ? 3 : LMSF_P2_WALK_WAVES))) void dense_pass2_kernel(
     GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, const unsigned* p2count) {
     const unsigned count = *p2count;
@@ -1882,120 +2006,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FIT ? 3 : L
         const float4 p = bv.featp[ppos];
         const int qq = __float_as_int(p.w);
         const bool is_edge = qq < ne;
-        const GridView gf = pick_grid(is_edge, fe, fs);
-        const bool fine = LMSF_PASS2_FINE && gf.n > 0 && gf.sy == 2;
-        const GridView g = pick_grid(fine, gf, pick_grid(is_edge, ge, gs));
         const float3 w = associate(load_pose(bv.st[b].x), p);
-        double k[5];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) k[j] = key_as_double(kSentinel);
-        const float4* rp = g.pts;
-        const int nrows = fine ? 25 : 9;
-        const DenseQuery<2> dq(g, w);   // the 1 m grid's 3 x 3 rows are its inner ring
-        const int xa = dq.xa, xb = dq.xb;
-#pragma unroll 1
-        for (int i = 0; i < nrows; ++i) {
-            const float d4 = fminf(bound, key_d2(k[4]));
-            const uint32_t* row;
-            int sa, sb;
-            const int dyo = fine ? kRing5[i][0] : (kDenseRowOrder[i] % 3) - 1;
-            const int dzo = fine ? kRing5[i][1] : (kDenseRowOrder[i] / 3) - 1;
-            const float lb = dq.lb(dyo, dzo);
-            if (lb > d4) continue;   // ahead of the row's address and offsets
-            if (!dq.row(g, dyo, dzo, row)) continue;
-            dense_window(g, w, d4 * kDenseCull, lb, xa, xb, sa, sb);
-            if (sa > sb) continue;
-            const uint32_t a = row[sa];
-            dense_run(k, rp, a, row[sb + 1] - a, w);
-        }
+        double k[NK];
+        const GridView g = dense_bounded_walk<NK>(ge, gs, fe, fs, is_edge, w, bound, k);
         if constexpr (FIT) {
-            dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);
+            double k5[5];
+            first5(k, k5);
+            dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k5);
         } else {   // the kept indices (-1: none) for the fit kernel, in key order
             store_kept(bv, b, e, F, k);
         }
-    }
-}
-
-// LMSF_P2_TEAM = 0 | 2 | 4 | 8 (VERDICT r04 #3a): pass 2's walk with a team of T lanes per listed query instead of
-// one.  r04's one-lane walk ran at lane utilisation 0.36: a few queries walk up to 25 first-pass rows (each two
-// dependent offset loads, then its candidates) while their wave-mates are done.  Here lane t of a team takes rows
-// t, t + T, ... of the same nearest-first order, each lane keeps its own 5 keys, and after every step of T rows the
-// team's bound becomes min(pass-1 bound, the smallest of the lanes' 5th keys) -- never below the team's true 5th
-// key, so the pruning stays exact; the lanes' keys are merged at the end (knn_kernel's team merge).  Same kept 5.
-// Measured r05 (one box, C5 pairs/s): one lane 4,163; T = 2 4,052; T = 4 3,975; T = 8 3,784 -- the team's shared
-// bound prunes later than one lane's own 5th key, and the extra lanes walk rows the one-lane walk never enters.
-// One lane stays the default.
-#ifndef LMSF_P2_TEAM
-#define LMSF_P2_TEAM 0
-#endif
-__constant__ signed char kRing5c[25][2] = {{0, 0},  {0, -1}, {-1, 0}, {1, 0},  {0, 1},  {-1, -1}, {1, -1}, {-1, 1}, {1, 1},
-                                           {0, -2}, {-2, 0}, {2, 0},  {0, 2},  {-1, -2}, {1, -2}, {-2, -1}, {2, -1}, {-2, 1},
-                                           {2, 1},  {-1, 2}, {1, 2},  {-2, -2}, {2, -2}, {-2, 2}, {2, 2}};
-template <int T>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_P2_WALK_WAVES))) void dense_pass2_team_kernel(
-    GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, const unsigned* p2count) {
-    const unsigned count = *p2count;
-    const size_t F = bv.feat_stride;
-    const int tl = threadIdx.x % T;
-    const unsigned teams = gridDim.x * (256 / T);
-    for (unsigned li = (blockIdx.x * 256 + threadIdx.x) / T; li < count; li += teams) {   // team-uniform
-        const size_t code = (size_t)(unsigned)bv.wl[li];
-        const float bound = bv.wlim[li];
-        const int b = (int)(code / F), e = (int)(code - (size_t)b * F);
-        const int ne = bv.n_edge[b];
-        const size_t ppos = (size_t)b * F + e;
-        const float4 p = bv.featp[ppos];
-        const bool is_edge = __float_as_int(p.w) < ne;
-        const GridView gf = pick_grid(is_edge, fe, fs);
-        const bool fine = LMSF_PASS2_FINE && gf.n > 0 && gf.sy == 2;
-        const GridView g = pick_grid(fine, gf, pick_grid(is_edge, ge, gs));
-        const float3 w = associate(load_pose(bv.st[b].x), p);
-        const double sentinel = key_as_double(kSentinel);
-        double k[5];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) k[j] = sentinel;
-        const float4* rp = g.pts;
-        const int nrows = fine ? 25 : 9;
-        const DenseQuery<2> dq(g, w);
-        const int xa = dq.xa, xb = dq.xb;
-        float tb = bound;   // the team's bound
-#pragma unroll 1
-        for (int i0 = 0; i0 < nrows; i0 += T) {
-            const int i = i0 + tl;
-            if (i < nrows) {
-                const float d4 = fminf(tb, key_d2(k[4]));
-                const int dyo = fine ? (int)kRing5c[i][0] : (kDenseRowOrder[i] % 3) - 1;
-                const int dzo = fine ? (int)kRing5c[i][1] : (kDenseRowOrder[i] / 3) - 1;
-                const float lb = dq.lb(dyo, dzo);
-                const uint32_t* row;
-                int sa, sb;
-                if (lb <= d4 && dq.row(g, dyo, dzo, row)) {
-                    dense_window(g, w, d4 * kDenseCull, lb, xa, xb, sa, sb);
-                    if (sa <= sb) {
-                        const uint32_t a = row[sa];
-                        dense_run(k, rp, a, row[sb + 1] - a, w);
-                    }
-                }
-            }
-            float m = key_d2(k[4]);
-#pragma unroll
-            for (int o = T / 2; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o, T));
-            tb = fminf(tb, m);
-        }
-        double res[5];
-#pragma unroll
-        for (int r = 0; r < 5; ++r) {   // team merge: the owning lane pops its head (keys are unique)
-            double mn = k[0];
-#pragma unroll
-            for (int o = T / 2; o >= 1; o >>= 1) mn = key_min(mn, __shfl_xor(mn, o, T));
-            res[r] = mn;
-            if (key_bits(k[0]) == key_bits(mn)) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) k[j] = k[j + 1];
-                k[4] = sentinel;
-            }
-        }
-        if (tl == 0) store_kept(bv, b, e, F, res);
+        if constexpr (NK == 6) store_anchor(bv, b, e, F, w, k);   // the same 5 indices, then s6 and the gaps
     }
 }
 
@@ -2027,6 +2048,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
 #pragma unroll
         for (int j = 0; j < 5; ++j) k[j] = kid[j] >= 0 ? key_as_double((uint64_t)(uint32_t)kid[j]) : key_as_double(kSentinel);
         dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k);
+    }
+}
+
+// ---------------------------------------------------------------- dense maps: the query memo (r05)
+// VERDICT r04 #3b: C5 re-associated every feature in all 5 outer iterations.  tools/memo_model.py C5 (oracle kd-tree
+// + Ceres trace on one C5 scan): the memo test serves 33% of the queries in outer iteration 2 (reuse 12%, refit 21%),
+// 91% in 3 and 99% in 4, and the misses' bounded re-search (radius s6 + d) holds ~6-7 candidates against ~12-14 in
+// pass 1's first-pass ball.  So on dense maps too: outer iteration memo_from - 1 runs the two passes with 6 exact keys
+// and leaves every position's anchor (store_anchor, the sparse memo's record); iterations >= memo_from run
+// match_memo_kernel (unchanged: it reads only the anchors and the records by position), then this kernel over the
+// scan's lists: searches walk the first-pass grid's rows bounded by min(1 m, s6 + d) (dense_bounded_walk, 6 keys --
+// exact, the 6 nearest at w0 lie within s6 + d of w), refresh the anchor and fit; refits fit the reordered stored 5.
+// Records by search position, as every dense pass.
+// Grid (G, B): blockIdx.y = scan, its G blocks grid-stride over the scan's lists (r05 first form: one block per 256
+// positions, gx * B = 256k blocks on C5, most of them empty past iteration 2 -- ~2 ms per dispatch of block
+// launches alone).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void dense_memo_search_kernel(
+    GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv) {
+    const int b = blockIdx.y;
+    const size_t F = bv.feat_stride;
+    const int* cnt = bv.wcount + (size_t)b * memo_blocks(F);
+    const int total_s = cnt[0], total = total_s + cnt[1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) bv.n_search[b] = total;
+    const int ne = bv.n_edge[b];
+    const Pose P = load_pose(bv.st[b].x);
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+        const bool walk = e < total_s;
+        const int pos = walk ? bv.wl[(size_t)b * F + e] : bv.wl[(size_t)b * F + F - 1 - (e - total_s)];
+        const size_t ppos = (size_t)b * F + pos;
+        const float4 p = bv.featp[ppos];
+        const int qq = __float_as_int(p.w);
+        const bool is_edge = qq < ne;
+        const float3 w = associate(P, p);
+        double k5[5];
+        GridView g = pick_grid(is_edge, ge, gs);
+        if (walk) {
+            double k[6];
+            g = dense_bounded_walk<6>(ge, gs, fe, fs, is_edge, w, bv.wlim[(size_t)b * F + e], k);
+            store_anchor(bv, b, pos, F, w, k);
+            first5(k, k5);
+        } else {   // refit: the memo pass left the 5 neighbours in their order at w (key bits: index only)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) k5[j] = key_as_double((uint64_t)(uint32_t)bv.memo_nbr[memo_idx(b, j, pos, F)]);
+        }
+        dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k5);
     }
 }
 
@@ -2452,33 +2518,44 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
     const int remap = knn_remap();
     if (match_fit_prune(edge, surf)) {
         static const bool split = ab_int("LMSF_DENSE_SPLIT", LMSF_DENSE_SPLIT) != 0;
-        if (split && kLinEval && bv.p2count && (size_t)bv.B * bv.feat_stride < ((size_t)1 << 31)) {
+        if (split && kLinEval && kListAtomic && bv.memo && bv.wcount) {   // dense memo pass + its listed searches
+            const hipError_t e = hipMemsetAsync(bv.wcount, 0, (size_t)bv.B * memo_blocks(bv.feat_stride) * sizeof(int), s);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(match_memo_kernel, grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
+            // ~2048 blocks over all scans (8 per CU), each scan's list grid-strided by its blocks
+            const int G = std::max(1, std::min(gx, std::max(4, 2048 / std::max(bv.B, 1))));
+            hipLaunchKernelGGL(dense_memo_search_kernel, dim3(G, bv.B), dim3(256), 0, s, edge, surf, fine_edge, fine_surf,
+                               bv);
+        } else if (split && kLinEval && bv.p2count && (size_t)bv.B * bv.feat_stride < ((size_t)1 << 31)) {
             hipError_t e = hipMemsetAsync(bv.p2count, 0, sizeof(unsigned), s);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(dense_pass1_kernel, grid, dim3(256), 0, s, edge, surf, fine_edge, fine_surf, bv, gx, remap,
-                               bv.p2count);
+            const unsigned* cnt = bv.p2count;
+            // the outer iteration before the memo: 6 exact keys, anchors left for the memo pass
+            if (bv.anchor)
+                hipLaunchKernelGGL(dense_pass1_kernel<6>, grid, dim3(256), 0, s, edge, surf, fine_edge, fine_surf, bv, gx,
+                                   remap, bv.p2count);
+            else
+                hipLaunchKernelGGL(dense_pass1_kernel<5>, grid, dim3(256), 0, s, edge, surf, fine_edge, fine_surf, bv, gx,
+                                   remap, bv.p2count);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
             // grid-stride over the list (~10% of the queries on C5): 8 blocks per CU
             if (LMSF_P2_SPLITFIT) {
-                static const int team = ab_int("LMSF_P2_TEAM", LMSF_P2_TEAM);
-                const unsigned* cnt = bv.p2count;
-                switch (team) {
-                    case 2: hipLaunchKernelGGL(dense_pass2_team_kernel<2>, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
-                                               fine_surf, bv, cnt); break;
-                    case 4: hipLaunchKernelGGL(dense_pass2_team_kernel<4>, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
-                                               fine_surf, bv, cnt); break;
-                    case 8: hipLaunchKernelGGL(dense_pass2_team_kernel<8>, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
-                                               fine_surf, bv, cnt); break;
-                    default: hipLaunchKernelGGL(dense_pass2_kernel<false>, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
-                                                fine_surf, bv, cnt); break;
-                }
+                if (bv.anchor)
+                    hipLaunchKernelGGL((dense_pass2_kernel<false, 6>), dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
+                                       fine_surf, bv, cnt);
+                else
+                    hipLaunchKernelGGL((dense_pass2_kernel<false, 5>), dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
+                                       fine_surf, bv, cnt);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
-                hipLaunchKernelGGL(dense_fit2_kernel, dim3(2048), dim3(256), 0, s, edge, surf, bv, (const unsigned*)bv.p2count);
+                hipLaunchKernelGGL(dense_fit2_kernel, dim3(2048), dim3(256), 0, s, edge, surf, bv, cnt);
+            } else if (bv.anchor) {
+                hipLaunchKernelGGL((dense_pass2_kernel<true, 6>), dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
+                                   fine_surf, bv, cnt);
             } else {
-                hipLaunchKernelGGL(dense_pass2_kernel<true>, dim3(2048), dim3(256), 0, s, edge, surf, fine_edge, fine_surf,
-                                   bv, (const unsigned*)bv.p2count);
+                hipLaunchKernelGGL((dense_pass2_kernel<true, 5>), dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
+                                   fine_surf, bv, cnt);
             }
         } else {
             hipLaunchKernelGGL((match_fit_kernel<true, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);

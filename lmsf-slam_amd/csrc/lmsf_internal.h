@@ -178,6 +178,8 @@ struct BatchView {
     unsigned long long* stamp_start;
     unsigned long long* stamp_end;
     unsigned* p2count;       // dense maps: entries of the pass-2 work list in wl (dense_pass1_kernel)
+    int anchor;              // dense maps: this outer iteration keeps 6 exact keys and leaves the memo anchors
+                             //   (the one before the dense memo pass starts, k_match.hip dense_memo_search_kernel)
 };
 
 __device__ __forceinline__ void stamp_if(unsigned long long* at, bool first_block) {
@@ -388,6 +390,8 @@ lmsf_status ctx_window_finish(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s
 // for a producer that fills both on the stage stream (the tracker's voxel filter); then
 // ctx_window_stage(c, kind, nullptr, n_max, nullptr, s) only reads them back.
 lmsf_status ctx_window_target(lmsf_ctx* c, int kind, size_t n_max, float4** orig, int** bb, hipStream_t s);
+// The window grid's point buffers sized for n points ahead of the first commit (tracker creation).
+lmsf_status ctx_window_reserve(lmsf_ctx* c, int kind, size_t n, hipStream_t s);
 // ... or, instead of that read-back, the whole grid build on s (no host wait; ctx_window_finish then only
 // takes the box read-back and sets the view).
 lmsf_status ctx_window_build(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s);

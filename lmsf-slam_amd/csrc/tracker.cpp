@@ -473,6 +473,20 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
         lmsf_tracker_destroy(t);
         return LMSF_ERR_HIP;
     }
+    // A window never exceeds window_frames x the slot capacity: its voxel-filter workspace and grid points are
+    // sized for that here, so keyframe commits never grow them (r05: growths inside the first frames -- the window
+    // filling up -- cost C3 ~15% over a 20-frame run).  LMSF_OPT_GROWTH_TEST keeps the grow-on-demand path instead.
+    if (!ctx_option(ctx, LMSF_OPT_GROWTH_TEST)) {
+        const size_t wmax = (size_t)t->cap * (size_t)cfg->window_frames;
+        for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) {
+            const bool ok = (t->win[kind].leaf > 0 ? t->voxel[kind].reserve(wmax, ctx_stream(ctx)) == hipSuccess : true) &&
+                            ctx_window_reserve(ctx, kind, wmax, ctx_stream(ctx)) == LMSF_OK;
+            if (!ok) {
+                lmsf_tracker_destroy(t);
+                return LMSF_ERR_HIP;
+            }
+        }
+    }
     t->origin = t->curr = t->prev = t->motion = t->last_kf = iso_identity();
     ctx_add_settle(ctx, [](void* p) { return settle(static_cast<lmsf_tracker*>(p)); }, t);
     *out = t;

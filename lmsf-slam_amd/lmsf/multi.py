@@ -99,8 +99,8 @@ class KeyframeExchange:
     def __init__(self, cap: int, world: int, device=None):
         import torch
         self.cap, self.world, self.device = cap, world, device
-        self.info = torch.zeros((world, 19), dtype=torch.float64, device=device)
-        self.own = torch.zeros(19, dtype=torch.float64, device=device)
+        self.info = torch.zeros((world, 20), dtype=torch.float64, device=device)
+        self.own = torch.zeros(20, dtype=torch.float64, device=device)
         self.gbuf = torch.zeros(world * 2 * cap * 4, dtype=torch.float32, device=device)
         self.payload_bytes = 0      # feature bytes this rank received, summed over steps
         self.steps = 0
@@ -108,7 +108,7 @@ class KeyframeExchange:
     def exchange(self, pose, update_type, n_edge, n_surf, feat):
         import torch.distributed as dist
         import torch
-        vec = np.concatenate([np.asarray(pose, dtype=np.float64).ravel(), [update_type, n_edge, n_surf]])
+        vec = np.concatenate([np.asarray(pose, dtype=np.float64).ravel(), [update_type, n_edge, n_surf, self.cap]])
         self.steps += 1
         if self.world <= 1:   # one stream: nothing to exchange; the caller adds its own keyframe from its context
             return [(0, None, None, np.asarray(pose, dtype=np.float64).reshape(4, 4))] if update_type else []
@@ -119,6 +119,11 @@ class KeyframeExchange:
         if not kf.any():
             return []
         me, ms = int(allinfo[kf, 17].max()), int(allinfo[kf, 18].max())
+        # every rank sends me / ms rows of its own buffer: they must fit the smallest one, counts non-negative -- the
+        # C library's all-rank check (lmsf_group_exchange_keyframes), raised alike on every rank from the same info
+        if me > allinfo[:, 19].min() or ms > allinfo[:, 19].min() or (allinfo[kf, 17:19] < 0).any():
+            raise ValueError(f"keyframe exchange: counts ({me}, {ms}) exceed the smallest rank capacity "
+                             f"{int(allinfo[:, 19].min())} or are negative")
         W, cap = self.world, self.cap
         ge = self.gbuf[:W * me * 4].view(W, me, 4)
         gs = self.gbuf[W * me * 4:W * (me + ms) * 4].view(W, ms, 4)

@@ -139,7 +139,8 @@ def test_c5_fullsize_pruned_batch(lib, oracle_mt, c5_workload):
     ctx.kernel_stats_reset(timing=True)
     poses, stats = ctx.batch_run(wl.guess[:n])
     ks = ctx.kernel_stats()
-    assert ks.fused_launches == 5 and ks.reused_queries == 0          # pruned dense-map walk: no memo
+    # dense-map memo (r05): outer iterations 2-4 reuse / refit most queries (tools/memo_model.py C5: 33 / 91 / 99%)
+    assert ks.fused_launches == 5 and ks.reused_queries + ks.refit_queries > 0.3 * ks.queries
     reg = _oracle_reg(oracle_mt, wl, 5)
     for i in range(n):
         e, s, _, _ = oracle_mt.extract(wl.scans[i], **c["extract"])

@@ -99,7 +99,14 @@ def _worker_c45(rank, world, port, out_q):
         pose[0, 3] = 100 * rank + step
         got = xchg.exchange(pose, typ, ne if typ else 0, ns if typ else 0, feat)
         log.append([(q, fe.numpy().copy(), fs.numpy().copy(), P.copy()) for q, fe, fs, P in got])
-    out_q.put((rank, allp, et.numpy(), st.numpy(), log, xchg.payload_bytes))
+    # a count above a rank's capacity is refused on every rank alike, before any feature gather
+    payload = xchg.payload_bytes
+    try:
+        xchg.exchange(np.eye(4), 1, 1, cap + 3 if rank == 1 else 1, torch.zeros((2 * cap, 4), dtype=torch.float32))
+        refused = False
+    except ValueError:
+        refused = True
+    out_q.put((rank, allp, et.numpy(), st.numpy(), log, payload, refused))
     dist.destroy_process_group()
 
 
@@ -118,7 +125,8 @@ def test_gloo_world2_pairs_map_and_keyframe_exchange():
     rng = np.random.default_rng(0)
     e0 = rng.random((11, 4)).astype(np.float32)
     s0 = rng.random((23, 4)).astype(np.float32)
-    for rank, allp, et, st, log, payload in res:
+    assert all(r[6] for r in res)                 # both ranks refused the over-capacity exchange
+    for rank, allp, et, st, log, payload, _ in res:
         # features gathered at the keyframing ranks' largest counts: step 0 (3 + 3 rows), step 2 (3 + 5 rows),
         # 2 ranks x 16 B per row -- not 2 x 2 cap rows per exchange
         assert payload == 2 * (3 + 3) * 16 + 2 * (3 + 5) * 16
