@@ -104,6 +104,9 @@ def parse(argv=None):
                     help="torch.distributed backend of the ranks (nccl = RCCL); gloo: CPU rehearsal of the launcher; "
                          "gloo-gpu: rehearsal of the N-rank GPU path on a box with fewer GPUs (rank r on GPU r mod "
                          "the device count, gloo collectives on the GPU tensors; the line is marked as a rehearsal)")
+    ap.add_argument("--dump", default=None, metavar="DIR",
+                    help="C4: each rank writes its per-step poses and update types to DIR/c4_rank<r>.npz (the multi-rank "
+                         "parity test replays them against oracle trackers)")
     ap.add_argument("--launch-check", action="store_true",
                     help="no GPU work: ranks join the process group, run the C2 pose all-gather on CPU tensors and "
                          "print the line skeleton (CPU test of the --gpus launcher)")
@@ -756,25 +759,37 @@ def run_batch(args, d):
 
 
 # ----------------------------------------------------------------------------- C4: stitched multi-stream tracking
+def c4_stream(rank, world, n, cols, workers=1):
+    """Rank `rank`'s C4 stream: ground truth and synthetic scans (8 m/s at 10 Hz, its own start on the road)."""
+    from lmsf import synth
+    c = synth.CONFIGS["C4"]
+    k = c["k"]
+    start = 8.0 * rank if world <= 8 else 64.0 * rank / world
+    truth = synth.trajectory(n, 3000 + k + rank, step=0.8, start_x=start)
+    scans = make_scans([(1000 + k, truth[i], 2000 + k + 97 * i + 7717 * rank, cols, c["elev"]) for i in range(n)], workers)
+    return truth, scans
+
+
+def c4_map(map_points):
+    """The shared C4 prior map (generated on rank 0 and broadcast)."""
+    from lmsf import synth
+    c = synth.CONFIGS["C4"]
+    k = c["k"]
+    scene = synth.make_scene(1000 + k, road_length=80.0)
+    return synth.make_map(scene, map_points, 1000 + k + 7, center_x=(0.0, 80.0), radius=c["radius"])
+
+
 def run_streams(args, d):
     import numpy as np
     from lmsf import multi, synth
-    c = synth.CONFIGS["C4"]
-    k = c["k"]
     world, rank = d.world, d.rank
     n = args.warmup + args.steps
-    scene = synth.make_scene(1000 + k, road_length=80.0)
-    step_m = 0.8                                                # 8 m/s at 10 Hz
-    start = 8.0 * rank if world <= 8 else 64.0 * rank / world
-    truth = synth.trajectory(n, 3000 + k + rank, step=step_m, start_x=start)
-    scans = make_scans([(1000 + k, truth[i], 2000 + k + 97 * i + 7717 * rank, args.cols, c["elev"]) for i in range(n)],
-                       args.workers)
+    truth, scans = c4_stream(rank, world, n, args.cols, args.workers)
     d.init()
     torch = d.torch
     from lmsf import _lib
     scans_dev = [torch.from_numpy(s).to(d.dev) for s in scans]
-    em_t, sm_t = shared_map(d, lambda: synth.make_map(scene, args.map_points, 1000 + k + 7, center_x=(0.0, 80.0),
-                                                      radius=c["radius"]))
+    em_t, sm_t = shared_map(d, lambda: c4_map(args.map_points))
     max_pts = max(len(s) for s in scans)
     ctx = _lib.Context(device=d.gpu, max_batch=1, max_scan_points=max_pts + 64, max_features=max_pts + 64,
                        schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer)
@@ -790,7 +805,7 @@ def run_streams(args, d):
     cap = max_pts + 64
     fbuf = torch.zeros((2 * cap, 4), dtype=torch.float32, device=d.dev)       # [edges | surfs] of own scan
     xchg = multi.KeyframeExchange(cap, world, d.dev)
-    state = {"i": 0, "kf": 0, "err": [], "xchg_s": 0.0, "poses": []}
+    state = {"i": 0, "kf": 0, "err": [], "xchg_s": 0.0, "poses": [], "types": []}
 
     phases = collections.defaultdict(float) if os.environ.get("LMSF_BENCH_PHASES") else None
 
@@ -834,10 +849,16 @@ def run_streams(args, d):
         Tt[:3, 3] = truth[i][4:]
         state["err"].append(float(np.linalg.norm(P[:3, 3] - Tt[:3, 3])))
         state["poses"].append(P.copy())
+        state["types"].append(int(r.update_type))
         state["i"] += 1
         return P
 
     elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, [ctx], not args.no_n27)
+    if args.dump:   # every step of this rank, warm-up included (the stream from its first scan)
+        os.makedirs(args.dump, exist_ok=True)
+        np.savez(os.path.join(args.dump, f"c4_rank{rank}.npz"), poses=np.stack(state["poses"]),
+                 types=np.asarray(state["types"]), world=world, cols=args.cols, map_points=args.map_points,
+                 outer=args.outer)
     if phases is not None:
         nst = state["i"]
         print("phases ms/step: " + "  ".join(f"{k} {1e3 * v / nst:.3f}" for k, v in phases.items()), file=sys.stderr)
