@@ -131,6 +131,18 @@ __global__ __launch_bounds__(256) void ring_offsets_kernel(ExtractView ev) {
     if (E == 0 && threadIdx.x == 0) ev.ring_start[(size_t)b * (kMaxRings + 1) + ev.n_scans] = 0;
 }
 
+// LMSF_SCATTER_BITS (A/B): the multisplit's in-wave ranking by ring-id bit ballots (1) or by a leader loop over the
+// distinct rings of the wave (0, r04).
+#ifndef LMSF_SCATTER_BITS
+#define LMSF_SCATTER_BITS 1
+#endif
+constexpr bool kScatterBits = LMSF_SCATTER_BITS != 0;
+// LMSF_CONCAT_LDS (A/B): concat_kernel's ring lookup of a position by binary search over the ring starts staged in
+// LDS (1) or read from global memory (0, r04: 7 dependent L2 round trips per position on a 128-ring scan).
+#ifndef LMSF_CONCAT_LDS
+#define LMSF_CONCAT_LDS 1
+#endif
+
 // Stable multisplit of one tile into ring order (input order preserved inside each ring).
 __global__ __launch_bounds__(256) void ring_scatter_kernel(ExtractView ev) {
     __shared__ int wcnt[4][kMaxRings];
@@ -147,6 +159,7 @@ __global__ __launch_bounds__(256) void ring_scatter_kernel(ExtractView ev) {
     float4* out = ev.ring_pts + (size_t)b * ev.raw_stride;
     int* osrc = ev.ring_src + (size_t)b * ev.raw_stride;
     (void)nt;
+    const int ring_bits = ev.n_scans <= 1 ? 0 : 32 - __clz(ev.n_scans - 1);
     for (int c0 = 0; c0 < kTile; c0 += 256) {
         for (int k = threadIdx.x; k < 4 * kMaxRings; k += 256) wcnt[k / kMaxRings][k % kMaxRings] = 0;
         __syncthreads();
@@ -154,14 +167,31 @@ __global__ __launch_bounds__(256) void ring_scatter_kernel(ExtractView ev) {
         const int r = i < n ? (int)rid[i] : -1;
         const float4 pt = r >= 0 ? raw[i] : make_float4(0, 0, 0, 0);   // in flight across the rank pass
         int rank = 0;
-        unsigned long long remaining = __ballot(r >= 0);
-        while (remaining) {
-            const int leader = __ffsll((long long)remaining) - 1;
-            const int rl = __shfl(r, leader, 64);
-            const unsigned long long m = __ballot(r == rl);
-            if (r == rl) rank = __popcll(m & lanemask_lt(lane));
-            if (lane == leader) wcnt[wave][rl] = __popcll(m);
-            remaining &= ~m;
+        if constexpr (kScatterBits) {
+            // the lanes of my ring by one ballot per ring-id bit (k_sort.hip's digit ranking): ceil(log2 n_scans)
+            // ballots, where the leader loop below takes one round per distinct ring in the wave -- up to 64 on a
+            // 128-beam scan stored column by column
+            const unsigned long long lt = lanemask_lt(lane);
+            unsigned long long peers = __ballot(r >= 0);
+            for (int bit = 0; bit < ring_bits; ++bit) {
+                const bool set = ((r >> bit) & 1) != 0;
+                const unsigned long long m = __ballot(set);
+                peers &= set ? m : ~m;
+            }
+            if (r >= 0) {
+                rank = __popcll(peers & lt);
+                if ((peers & lt) == 0ull) wcnt[wave][r] = __popcll(peers);
+            }
+        } else {
+            unsigned long long remaining = __ballot(r >= 0);
+            while (remaining) {
+                const int leader = __ffsll((long long)remaining) - 1;
+                const int rl = __shfl(r, leader, 64);
+                const unsigned long long m = __ballot(r == rl);
+                if (r == rl) rank = __popcll(m & lanemask_lt(lane));
+                if (lane == leader) wcnt[wave][rl] = __popcll(m);
+                remaining &= ~m;
+            }
         }
         __syncthreads();
         if (r >= 0) {
@@ -666,9 +696,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_RF_WAV
 
 // Concatenate per-ring stages: edges of ring 0..N-1, then surfs of ring 0..N-1 (FX:124-125 order).
 __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
-    __shared__ int epre[kMaxRings + 1], spre[kMaxRings + 1];
+    __shared__ int epre[kMaxRings + 1], spre[kMaxRings + 1], srs[kMaxRings + 1];
     const int b = blockIdx.y;
     const int nr = ev.n_scans;
+    if (LMSF_CONCAT_LDS)
+        for (int r = threadIdx.x; r <= nr; r += 256) srs[r] = ev.ring_start[(size_t)b * (kMaxRings + 1) + r];
 #ifdef LMSF_CONCAT_SERIAL   // A/B build: r02 first-half prologue (one thread sums the ring counts)
     if (threadIdx.x == 0) {
         int e = 0, s = 0;
@@ -712,7 +744,7 @@ __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
     }
     __syncthreads();
     const int ne = epre[nr];
-    const int* rs = ev.ring_start + (size_t)b * (kMaxRings + 1);
+    const int* rs = LMSF_CONCAT_LDS ? srs : ev.ring_start + (size_t)b * (kMaxRings + 1);
     // Every feature position of the rings, in ring order: its feature slot (edges of ring 0..N-1, then surfs,
     // each ring's in the reference's emission order -- the ring-local index ring_features_kernel packed into the
     // position's code) and its place in the fused search's order (edges of ring 0..N-1 then surfs, each ring's in
