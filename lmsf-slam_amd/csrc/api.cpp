@@ -176,6 +176,8 @@ struct lmsf_ctx {
     int* wl = nullptr;                // [B][F] memo pass work lists
     float* wlim = nullptr;            // [B][F] their search radii^2
     int* wcount = nullptr;            // [B][F / 256 + 1] their counts
+    int* wl2 = nullptr;               // [B][F] dense maps: pass-2 list of the memo iterations (with the first-pass grid)
+    float* wlim2 = nullptr;
     int* n_search = nullptr;          // [B] positions searched by the last fused launch
     float4* rec_p = nullptr;          // records: point + kind / values / edge tail (BatchView)
     RecV* rec_v = nullptr;
@@ -338,6 +340,8 @@ struct lmsf_ctx {
         v.memo_nbr = memo_nbr;
         v.wl = wl;
         v.wlim = wlim;
+        v.wl2 = wl2;
+        v.wlim2 = wlim2;
         v.memo_bound = opt[LMSF_OPT_MEMO_BOUND];
         v.memo_refit = opt[LMSF_OPT_MEMO_REFIT];
         v.memo_exact = opt[LMSF_OPT_MEMO_EXACT];
@@ -680,6 +684,14 @@ lmsf_status build_fine(lmsf_ctx* c, int kind) {
     size_t tb = f.scan_tmp_bytes;
     HIPCHK(c, exclusive_scan_u32(f.counts, f.off, cells + 1, f.scan_tmp, tb, s));
     HIPCHK(c, launch_map_scatter(m.orig, m.n, f.cell, f.off, f.fill, f.pts, 0, c->d_error + 17, s));
+    if (!c->wl2) {   // the dense memo iterations' pass-2 list (none: they take the bounded walk)
+        if (galloc(&c->wl2, (size_t)c->B * c->F, s) != hipSuccess || galloc(&c->wlim2, (size_t)c->B * c->F, s) != hipSuccess) {
+            gfree(c->wl2, s); gfree(c->wlim2, s);
+            c->wl2 = nullptr;
+            c->wlim2 = nullptr;
+            (void)hipGetLastError();
+        }
+    }
     f.orig = m.orig;
     f.orig_borrowed = true;
     f.lim1 = m.lim1;
@@ -744,6 +756,12 @@ lmsf_status sync_slot0_features(lmsf_ctx* c) {
 }
 
 // Enqueue the registration of slots [0, nb): outer iterations of match + solver control.
+// Dense maps (the C5 regime): the outer iteration the query memo starts at (r05 A/B, tools/memo_model.py C5: the memo
+// serves 33% of the queries in iteration 2, 69% in 3, 84% in 4 on the box).
+#ifndef LMSF_DENSE_MEMO_FROM
+#define LMSF_DENSE_MEMO_FROM 3
+#endif
+
 // Called by enqueue_solve only, after the maps were resolved there (never inside a stream capture: the first-pass
 // grid build and lim1 read back to the host).
 lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
@@ -787,8 +805,16 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
         if (fused) {
             BatchView bvo = bv;
             bvo.memo = batch_memo(o) ? 1 : 0;
-            // dense maps: the outer iteration before the memo pass keeps 6 exact keys and leaves the anchors
-            bvo.anchor = memo_on && !c->count27 && o == memo_from - 1 ? 1 : 0;
+            // dense maps: the memo from outer iteration dense_from (A/B LMSF_DENSE_MEMO_FROM; > iterations: never); the
+            // iteration before it keeps 6 exact keys and leaves the anchors
+            if (match_fit_prune(ge, gs)) {
+                static const int dense_from = ab_int("LMSF_DENSE_MEMO_FROM", LMSF_DENSE_MEMO_FROM);
+                const int from = std::max(dense_from, 1);
+                bvo.memo = o >= from && !c->count27 && memo_on ? 1 : 0;
+                bvo.anchor = memo_on && !c->count27 && o == from - 1 ? 1 : 0;
+            } else {
+                bvo.anchor = 0;
+            }
             HIPCHK(c, launch_match_fit(ge, gs, bvo, s, fe, fs));
         }
         else {   // single-scan launches: the 8-lane search, with the slot memo under the Ceres-LM solver
@@ -1075,6 +1101,8 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (c->ev_pre) hipEventDestroy(c->ev_pre);
     if (c->ev_pre_after) hipEventDestroy(c->ev_pre_after);
     if (c->pre_stream) hipStreamDestroy(c->pre_stream);
+    gfree(c->wl2, c->stream);
+    gfree(c->wlim2, c->stream);
     if (c->stream) hipStreamSynchronize(c->stream);   // the stream-ordered frees above
     hipFree(c->cap_rec);
     hipFree(c->cap_nn);

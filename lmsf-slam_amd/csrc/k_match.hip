@@ -1804,6 +1804,44 @@ __device__ __forceinline__ void first5(const double (&k)[NK], double (&k5)[5]) {
     for (int j = 0; j < 5; ++j) k5[j] = k[j];
 }
 
+// Pass 1 of one query on grid g (its kind's first-pass grid, else its 1 m grid): the 9 rows' offsets resolved up front
+// (the 18 loads in flight together), each trimmed to the first-pass ball sqrt(lim1), walked nearest row first while
+// a row's yz-gap bound is within the current NK-th key.
+template <int NK>
+__device__ __forceinline__ void dense_first_pass(const GridView& g, const float3 w, int count27, double (&k)[NK],
+                                                 unsigned int& c27) {
+    uint32_t st_[9], ln_[9];
+    float lb_[9];
+    const float lim1 = g.lim1 * kDenseCull;
+    const DenseQuery<1> dq(g, w);
+    const int xa = dq.xa, xb = dq.xb;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        st_[i] = 0;
+        ln_[i] = 0;
+        const int dyo = (kDenseRowOrder[i] % 3) - 1, dzo = (kDenseRowOrder[i] / 3) - 1;
+        const float lb = dq.lb(dyo, dzo);
+        lb_[i] = lb;
+        const uint32_t* row;
+        int sa, sb;
+        if (!dq.row(g, dyo, dzo, row)) continue;
+        if (count27) c27 += row[xb + 1] - row[xa];
+        if (lb > lim1) continue;
+        dense_window(g, w, lim1, lb, xa, xb, sa, sb);
+        if (sa <= sb) {
+            st_[i] = row[sa];
+            ln_[i] = row[sb + 1] - st_[i];
+        }
+    }
+    const float4* rp = g.pts;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const uint32_t ln = ln_[i];
+        if (!ln || lb_[i] > key_d2(k[NK - 1])) continue;
+        dense_run(k, rp, st_[i], ln, w);
+    }
+}
+
 // NK = 5, or 6 in the outer iteration before the dense memo starts (BatchView::anchor): the 6th-nearest key is then
 // exact too (rows pruned with it), and complete queries leave the memo anchor.
 template <int NK>
@@ -1831,39 +1869,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_
 #pragma unroll
     for (int j = 0; j < NK; ++j) k[j] = sentinel;
     unsigned int c27 = 0;
-    if (valid) {
-        // rows resolved up front: the 18 offset loads in flight together
-        uint32_t st_[9], ln_[9];
-        float lb_[9];
-        const float lim1 = g.lim1 * kDenseCull;
-        const DenseQuery<1> dq(g, w);
-        const int xa = dq.xa, xb = dq.xb;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            st_[i] = 0;
-            ln_[i] = 0;
-            const int dyo = (kDenseRowOrder[i] % 3) - 1, dzo = (kDenseRowOrder[i] / 3) - 1;
-            const float lb = dq.lb(dyo, dzo);
-            lb_[i] = lb;
-            const uint32_t* row;
-            int sa, sb;
-            if (!dq.row(g, dyo, dzo, row)) continue;
-            if (bv.count27) c27 += row[xb + 1] - row[xa];
-            if (lb > lim1) continue;
-            dense_window(g, w, lim1, lb, xa, xb, sa, sb);
-            if (sa <= sb) {
-                st_[i] = row[sa];
-                ln_[i] = row[sb + 1] - st_[i];
-            }
-        }
-        const float4* rp = g.pts;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            const uint32_t ln = ln_[i];
-            if (!ln || lb_[i] > key_d2(k[NK - 1])) continue;
-            dense_run(k, rp, st_[i], ln, w);
-        }
-    }
+    if (valid) dense_first_pass(g, w, bv.count27, k, c27);
     // complete (NK-th key within lim1: nothing nearer lies outside the scanned ball) -> fit; else -> pass-2 list
     const bool p2 = valid && key_d2(k[NK - 1]) > g.lim1;
     const unsigned long long m2 = __ballot(p2);
@@ -1906,6 +1912,9 @@ constexpr int kRing5[25][2] = {{0, 0},  {0, -1}, {-1, 0}, {1, 0},  {0, 1},  {-1,
                                {2, 1},  {-1, 2}, {1, 2},  {-2, -2}, {2, -2}, {-2, 2}, {2, 2}};
 #ifndef LMSF_PASS2_FINE
 #define LMSF_PASS2_FINE 1
+#endif
+#ifndef LMSF_P2_INNER
+#define LMSF_P2_INNER 0
 #endif
 
 // The bounded pruned walk of pass 2 (and of the dense memo pass's listed searches): the NK nearest of w within
@@ -1959,12 +1968,16 @@ __device__ __forceinline__ const GridView dense_bounded_walk(const GridView& ge,
         dense_ball_walk(g, w, bound * kDenseCull, k);
         return g;
     }
+    // LMSF_P2_INNER (A/B): a larger ball's inner 3 x 3 rows also resolved up front (windows at the bound), then the
+    // outer ring's 16 rows one by one (their yz-gap bound is >= 0.25 m^2: pruned once the kept keys are nearer)
+    const bool inner = LMSF_P2_INNER && fine;
+    if (inner) dense_ball_walk(g, w, bound * kDenseCull, k);
     const float4* rp = g.pts;
     const int nrows = fine ? 25 : 9;
     const DenseQuery<2> dq(g, w);   // the 1 m grid's 3 x 3 rows are its inner ring
     const int xa = dq.xa, xb = dq.xb;
 #pragma unroll 1
-    for (int i = 0; i < nrows; ++i) {
+    for (int i = inner ? 9 : 0; i < nrows; ++i) {
         const float d4 = fminf(bound, key_d2(k[NK - 1]));
         const uint32_t* row;
         int sa, sb;
@@ -1992,14 +2005,17 @@ __device__ __forceinline__ const GridView dense_bounded_walk(const GridView& ge,
 #ifndef LMSF_P2_WALK_WAVES
 #define LMSF_P2_WALK_WAVES 6
 #endif
+// wl / wlim: the pass-2 list (bv.wl / bv.wlim, or bv.wl2 / bv.wlim2 in the memo iterations, whose per-scan lists
+// occupy wl), p2count entries.
 template <bool FIT, int NK>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FIT ? 3 : LMSF_P2_WALK_WAVES))) void dense_pass2_kernel(
-    GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, const unsigned* p2count) {
+    GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, const unsigned* p2count, const int* wl,
+    const float* wlim) {
     const unsigned count = *p2count;
     const size_t F = bv.feat_stride;
     for (unsigned li = blockIdx.x * 256 + threadIdx.x; li < count; li += gridDim.x * 256) {
-        const size_t code = (size_t)(unsigned)bv.wl[li];
-        const float bound = bv.wlim[li];
+        const size_t code = (size_t)(unsigned)wl[li];
+        const float bound = wlim[li];
         const int b = (int)(code / F), e = (int)(code - (size_t)b * F);
         const int ne = bv.n_edge[b];
         const size_t ppos = (size_t)b * F + e;
@@ -2022,11 +2038,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FIT ? 3 : L
 
 // The fit of dense_pass2_kernel<false>'s queries (same list, same order): the kept 5 from the memo record.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void dense_fit2_kernel(
-    GridView ge, GridView gs, BatchView bv, const unsigned* p2count) {
+    GridView ge, GridView gs, BatchView bv, const unsigned* p2count, const int* wl) {
     const unsigned count = *p2count;
     const size_t F = bv.feat_stride;
     for (unsigned li = blockIdx.x * 256 + threadIdx.x; li < count; li += gridDim.x * 256) {
-        const size_t code = (size_t)(unsigned)bv.wl[li];
+        const size_t code = (size_t)(unsigned)wl[li];
         const int b = (int)(code / F), e = (int)(code - (size_t)b * F);
         const int ne = bv.n_edge[b];
         const size_t ppos = (size_t)b * F + e;
@@ -2063,8 +2079,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
 // Records by search position, as every dense pass.
 // Grid (G, B): blockIdx.y = scan, its G blocks grid-stride over the scan's lists (r05 first form: one block per 256
 // positions, gx * B = 256k blocks on C5, most of them empty past iteration 2 -- ~2 ms per dispatch of block
-// launches alone).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void dense_memo_search_kernel(
+// launches alone).  As pass 2, a walk kernel (few registers: more waves to hide the walk's latency; the kept 5 and
+// the refreshed anchor left in the position's memo record) and a fit kernel over the searches and the refits
+// (LMSF_MEMO_SPLITFIT; 0: one kernel, fit inline).
+#ifndef LMSF_MEMO_SPLITFIT
+#define LMSF_MEMO_SPLITFIT 0
+#endif
+template <bool FIT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FIT ? 3 : LMSF_P2_WALK_WAVES))) void dense_memo_search_kernel(
     GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv) {
     const int b = blockIdx.y;
     const size_t F = bv.feat_stride;
@@ -2073,7 +2095,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
     if (blockIdx.x == 0 && threadIdx.x == 0) bv.n_search[b] = total;
     const int ne = bv.n_edge[b];
     const Pose P = load_pose(bv.st[b].x);
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < (FIT ? total : total_s); e += gridDim.x * 256) {
         const bool walk = e < total_s;
         const int pos = walk ? bv.wl[(size_t)b * F + e] : bv.wl[(size_t)b * F + F - 1 - (e - total_s)];
         const size_t ppos = (size_t)b * F + pos;
@@ -2081,18 +2103,145 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
         const int qq = __float_as_int(p.w);
         const bool is_edge = qq < ne;
         const float3 w = associate(P, p);
-        double k5[5];
-        GridView g = pick_grid(is_edge, ge, gs);
         if (walk) {
             double k[6];
-            g = dense_bounded_walk<6>(ge, gs, fe, fs, is_edge, w, bv.wlim[(size_t)b * F + e], k);
-            store_anchor(bv, b, pos, F, w, k);
-            first5(k, k5);
-        } else {   // refit: the memo pass left the 5 neighbours in their order at w (key bits: index only)
+            const GridView g = dense_bounded_walk<6>(ge, gs, fe, fs, is_edge, w, bv.wlim[(size_t)b * F + e], k);
+            if constexpr (FIT) {
+                store_anchor(bv, b, pos, F, w, k);
+                double k5[5];
+                first5(k, k5);
+                dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k5);
+            } else {
+                store_kept(bv, b, pos, F, k);        // -1s when fewer than 5 were found
+                store_anchor(bv, b, pos, F, w, k);   // the same 5 indices, then s6 and the gaps
+            }
+        } else if constexpr (FIT) {   // refit: the memo pass left the 5 neighbours in their order at w
+            double k5[5];
 #pragma unroll
             for (int j = 0; j < 5; ++j) k5[j] = key_as_double((uint64_t)(uint32_t)bv.memo_nbr[memo_idx(b, j, pos, F)]);
+            dense_finish(pick_grid(is_edge, ge, gs), bv, ppos, p, is_edge, (size_t)b * F + qq, w, k5);
         }
-        dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k5);
+    }
+}
+
+// The fit of dense_memo_search_kernel<false>'s searches and of the memo pass's refits: the 5 from the memo record.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void dense_memo_fit_kernel(GridView ge,
+                                                                                                    GridView gs,
+                                                                                                    BatchView bv) {
+    const int b = blockIdx.y;
+    const size_t F = bv.feat_stride;
+    const int* cnt = bv.wcount + (size_t)b * memo_blocks(F);
+    const int total_s = cnt[0], total = total_s + cnt[1];
+    const int ne = bv.n_edge[b];
+    const Pose P = load_pose(bv.st[b].x);
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+        const int pos = e < total_s ? bv.wl[(size_t)b * F + e] : bv.wl[(size_t)b * F + F - 1 - (e - total_s)];
+        const size_t ppos = (size_t)b * F + pos;
+        const float4 p = bv.featp[ppos];
+        const int qq = __float_as_int(p.w);
+        const bool is_edge = qq < ne;
+        int kid[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) kid[j] = bv.memo_nbr[memo_idx(b, j, pos, F)];
+        double k5[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) k5[j] = kid[j] >= 0 ? key_as_double((uint64_t)(uint32_t)kid[j]) : key_as_double(kSentinel);
+        dense_finish(pick_grid(is_edge, ge, gs), bv, ppos, p, is_edge, (size_t)b * F + qq, associate(P, p), k5);
+    }
+}
+
+// LMSF_MEMO_PASS1 (default 1): the memo pass's listed searches run pass 1 (the first-pass ball, 9 rows resolved up
+// front, 6 keys) instead of the walk bounded by min(1 m, s6 + d): a query the ball completes (6th key within lim1) is
+// fitted and re-anchored here, the rest go to the pass-2 list in wl2 (bounded by the smaller of its 6th key and
+// s6 + d, both at least the true 6th); refits are fitted from the memo record.  (r05: the s6 + d walk took ~2x pass
+// 1's time per query -- its balls are larger than the first-pass ball.)
+#ifndef LMSF_MEMO_PASS1
+#define LMSF_MEMO_PASS1 1
+#endif
+// The scans' lists flattened: a block first scans the B lists' lengths into LDS (s_pre, B + 1 ints of dynamic LDS),
+// then grid-strides over all entries (r05 first form: G blocks per scan, so the scan with the longest list --
+// the pair that moved most -- set the kernel's length: ~2x pass 1's time per entry).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_FUSED_WAVES))) void dense_pass1_listed_kernel(
+    GridView ge, GridView gs, GridView fe, GridView fs, BatchView bv, unsigned* p2count) {
+    extern __shared__ int s_pre[];
+    __shared__ int s_wave[4];
+    const size_t F = bv.feat_stride;
+    const int B = bv.B;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // s_pre[b] = entries of the lists before scan b, 256 scans per round
+    int run = 0;
+    for (int b0 = 0; b0 < B; b0 += 256) {
+        const int b = b0 + threadIdx.x;
+        int c = 0;
+        if (b < B) {
+            const int* cnt = bv.wcount + (size_t)b * memo_blocks(F);
+            c = cnt[0] + cnt[1];
+            if (blockIdx.x == 0) bv.n_search[b] = c;
+        }
+        int inc = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += t;
+        }
+        if (lane == 63) s_wave[wave] = inc;
+        __syncthreads();
+        int before = run;
+#pragma unroll
+        for (int w4 = 0; w4 < 4; ++w4) before += w4 < wave ? s_wave[w4] : 0;
+        if (b < B) s_pre[b] = before + inc - c;
+        run += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) s_pre[B] = run;
+    __syncthreads();
+    const int total_all = s_pre[B];
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int g_e = blockIdx.x * 256 + threadIdx.x; g_e < total_all; g_e += gridDim.x * 256) {
+        int lo = 0, hi = B - 1;   // the last scan whose entries start at or before g_e
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_pre[mid] <= g_e) lo = mid;
+            else hi = mid - 1;
+        }
+        const int b = lo, e = g_e - s_pre[b];
+        const int total_s = bv.wcount[(size_t)b * memo_blocks(F)];
+        const bool walk = e < total_s;
+        const int pos = walk ? bv.wl[(size_t)b * F + e] : bv.wl[(size_t)b * F + F - 1 - (e - total_s)];
+        const size_t ppos = (size_t)b * F + pos;
+        const float4 p = bv.featp[ppos];
+        const int qq = __float_as_int(p.w);
+        const bool is_edge = qq < bv.n_edge[b];
+        const float3 w = associate(load_pose(bv.st[b].x), p);
+        const GridView g = pick_grid(is_edge, pick_grid(fe.n > 0, fe, ge), pick_grid(fs.n > 0, fs, gs));
+        double k[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) k[j] = key_as_double(kSentinel);
+        bool p2 = false;
+        if (walk) {
+            unsigned int c27 = 0;
+            dense_first_pass(g, w, 0, k, c27);
+            p2 = key_d2(k[5]) > g.lim1;
+        } else {   // refit: the memo pass left the 5 neighbours in their order at w (key bits: index only)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) k[j] = key_as_double((uint64_t)(uint32_t)bv.memo_nbr[memo_idx(b, j, pos, F)]);
+        }
+        // the incomplete searches to the pass-2 list (one atomic per wave: its first active lane)
+        const unsigned long long act = __ballot(1), m2 = __ballot(p2);
+        const int leader = __ffsll((long long)act) - 1;
+        int base2 = 0;
+        if (lane == leader && m2) base2 = (int)atomicAdd(p2count, (unsigned)__popcll(m2));
+        base2 = __shfl(base2, leader, 64);
+        if (p2) {
+            const int at = base2 + __popcll(m2 & below);
+            bv.wl2[at] = (int)ppos;
+            bv.wlim2[at] = fminf(key_d2(k[5]), bv.wlim[(size_t)b * F + e]);
+        } else {
+            if (walk) store_anchor(bv, b, pos, F, w, k);
+            double k5[5];
+            first5(k, k5);
+            dense_finish(g, bv, ppos, p, is_edge, (size_t)b * F + qq, w, k5);
+        }
     }
 }
 
@@ -2519,13 +2668,28 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
     if (match_fit_prune(edge, surf)) {
         static const bool split = ab_int("LMSF_DENSE_SPLIT", LMSF_DENSE_SPLIT) != 0;
         if (split && kLinEval && kListAtomic && bv.memo && bv.wcount) {   // dense memo pass + its listed searches
-            const hipError_t e = hipMemsetAsync(bv.wcount, 0, (size_t)bv.B * memo_blocks(bv.feat_stride) * sizeof(int), s);
+            hipError_t e = hipMemsetAsync(bv.wcount, 0, (size_t)bv.B * memo_blocks(bv.feat_stride) * sizeof(int), s);
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(match_memo_kernel, grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
             // ~2048 blocks over all scans (8 per CU), each scan's list grid-strided by its blocks
             const int G = std::max(1, std::min(gx, std::max(4, 2048 / std::max(bv.B, 1))));
-            hipLaunchKernelGGL(dense_memo_search_kernel, dim3(G, bv.B), dim3(256), 0, s, edge, surf, fine_edge, fine_surf,
-                               bv);
+            if (LMSF_MEMO_PASS1 && bv.wl2 && bv.p2count && bv.B <= 8192) {   // (B + 1) ints of LDS
+                if ((e = hipMemsetAsync(bv.p2count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
+                // all scans' entries flattened over ~8 blocks per CU
+                hipLaunchKernelGGL(dense_pass1_listed_kernel, dim3(2048), dim3(256), (size_t)(bv.B + 1) * sizeof(int), s,
+                                   edge, surf, fine_edge, fine_surf, bv, bv.p2count);
+                const unsigned* cnt = bv.p2count;
+                hipLaunchKernelGGL((dense_pass2_kernel<false, 6>), dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
+                                   fine_surf, bv, cnt, (const int*)bv.wl2, (const float*)bv.wlim2);
+                hipLaunchKernelGGL(dense_fit2_kernel, dim3(2048), dim3(256), 0, s, edge, surf, bv, cnt, (const int*)bv.wl2);
+            } else if (LMSF_MEMO_SPLITFIT) {
+                hipLaunchKernelGGL(dense_memo_search_kernel<false>, dim3(G, bv.B), dim3(256), 0, s, edge, surf, fine_edge,
+                                   fine_surf, bv);
+                hipLaunchKernelGGL(dense_memo_fit_kernel, dim3(G, bv.B), dim3(256), 0, s, edge, surf, bv);
+            } else {
+                hipLaunchKernelGGL(dense_memo_search_kernel<true>, dim3(G, bv.B), dim3(256), 0, s, edge, surf, fine_edge,
+                                   fine_surf, bv);
+            }
         } else if (split && kLinEval && bv.p2count && (size_t)bv.B * bv.feat_stride < ((size_t)1 << 31)) {
             hipError_t e = hipMemsetAsync(bv.p2count, 0, sizeof(unsigned), s);
             if (e != hipSuccess) return e;
@@ -2543,19 +2707,19 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
             if (LMSF_P2_SPLITFIT) {
                 if (bv.anchor)
                     hipLaunchKernelGGL((dense_pass2_kernel<false, 6>), dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
-                                       fine_surf, bv, cnt);
+                                       fine_surf, bv, cnt, (const int*)bv.wl, (const float*)bv.wlim);
                 else
                     hipLaunchKernelGGL((dense_pass2_kernel<false, 5>), dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
-                                       fine_surf, bv, cnt);
+                                       fine_surf, bv, cnt, (const int*)bv.wl, (const float*)bv.wlim);
                 e = hipGetLastError();
                 if (e != hipSuccess) return e;
-                hipLaunchKernelGGL(dense_fit2_kernel, dim3(2048), dim3(256), 0, s, edge, surf, bv, cnt);
+                hipLaunchKernelGGL(dense_fit2_kernel, dim3(2048), dim3(256), 0, s, edge, surf, bv, cnt, (const int*)bv.wl);
             } else if (bv.anchor) {
                 hipLaunchKernelGGL((dense_pass2_kernel<true, 6>), dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
-                                   fine_surf, bv, cnt);
+                                   fine_surf, bv, cnt, (const int*)bv.wl, (const float*)bv.wlim);
             } else {
                 hipLaunchKernelGGL((dense_pass2_kernel<true, 5>), dim3(2048), dim3(256), 0, s, edge, surf, fine_edge,
-                                   fine_surf, bv, cnt);
+                                   fine_surf, bv, cnt, (const int*)bv.wl, (const float*)bv.wlim);
             }
         } else {
             hipLaunchKernelGGL((match_fit_kernel<true, false>), grid, dim3(256), 0, s, edge, surf, bv, gx, remap);

@@ -178,6 +178,8 @@ struct BatchView {
     unsigned long long* stamp_start;
     unsigned long long* stamp_end;
     unsigned* p2count;       // dense maps: entries of the pass-2 work list in wl (dense_pass1_kernel)
+    int* wl2;                // dense maps: the pass-2 list of the memo iterations (wl holds the memo pass's lists), B F
+    float* wlim2;
     int anchor;              // dense maps: this outer iteration keeps 6 exact keys and leaves the memo anchors
                              //   (the one before the dense memo pass starts, k_match.hip dense_memo_search_kernel)
 };

@@ -1,7 +1,12 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "extract or prefetch or ingest or c1 or smoke" > gpurun_out/gpu_tests.log 2>&1
-rc=$?; echo "tests_rc=$rc"; tail -2 gpurun_out/gpu_tests.log; case $rc in 0) ;; *) exit $rc;; esac
-NO_TESTS=1 VARIANTS="x00 x11" CFG=C5 OUT=xtrace5 bash tools/gpu_trace_variants.sh || exit $?
-NO_TESTS=1 VARIANTS="x00 x11" CFG=C2 OUT=xtrace2 bash tools/gpu_trace_variants.sh || exit $?
-ROUNDS=1 CONFIGS="C5 C2" VARIANTS="x00 x11" bash tools/gpu_ab_lib.sh || exit $?
+export LMSF_LIB=lmsf-slam_amd/ab/liblmsf_ab.so
+for r in 1 2; do
+for e in 2 3 4 99; do
+for a in "--pipeline 1" "--pipeline 3"; do
+LMSF_DENSE_MEMO_FROM=$e timeout -k 10 300 python bench.py --config C5 --no-cpu $a > gpurun_out/p.json 2> gpurun_out/p.err
+rc=$?; echo "from $e [$a] r$r rc=$rc $(python3 -c "import json; d=json.loads([l for l in open('gpurun_out/p.json') if l.startswith('{')][-1]); print(d['value'], d['roofline']['avg_launch_ms'])")"
+case $rc in 0) ;; *) exit $rc;; esac
+done
+done
+done
