@@ -264,7 +264,8 @@ def kernel_name(ks, dense=False):
     if ks.launches and ks.fused_launches == ks.launches and dense:
         return ("dense_pass1_kernel + dense_pass2_kernel + dense_fit2_kernel (dense map: first pass on the 0.5 m "
                 "first-pass grid with the fit of the queries it completes, bounded pass-2 walk of the listed rest, "
-                "their fit; one outer iteration)")
+                "their fit; from outer iteration 3 match_memo_kernel first and dense_pass1_listed_kernel over its "
+                "misses in place of the full first pass; one outer iteration)")
     if ks.launches and ks.fused_launches == ks.launches:
         return ("match_memo_kernel + match_fit_kernel (query memo pass from outer iteration 2, then the fused 5-NN "
                 "search + line/plane fit + record write of the queries it lists; one outer iteration)")

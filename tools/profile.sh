@@ -1,11 +1,11 @@
-# Profiles (ROUND, default r04) of one bench configuration (CFG, default C2): kernel trace + stats of the bench
+# Profiles (ROUND, default r05) of one bench configuration (CFG, default C2): kernel trace + stats of the bench
 # command, then PMC passes (each counter set in a run of its own; --kernel-trace only beside --pmc):
 # HBM traffic (FETCH_SIZE, WRITE_SIZE), L2 hit/miss, and an SQ pass (wave cycles, waits, instruction
 # mix).  PMC runs use one context stream (device-wide counters) and skip the untimed n27 step.
 set -u
 R="$GRAFT_REPO_ROOT"
 CFG=${CFG:-C2}
-O="$R/gpurun_out/${ROUND:-r04}/$CFG"
+O="$R/gpurun_out/${ROUND:-r05}/$CFG"
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 if [ -z "${SKIP_TRACE:-}" ]; then
