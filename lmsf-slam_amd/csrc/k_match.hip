@@ -2335,10 +2335,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_EVAL_W
 
 // ---------------------------------------------------------------- single-scan LM loop in one launch
 // The Ceres LM of one outer iteration (lm_begin + 4 x (lm_eval + lm_step), 9 launches) as one launch for
-// contexts whose whole grid is co-resident (tracking: one scan, ~70 blocks on 256 CUs; kLoopMaxBlocks).  Every block keeps
+// contexts whose whole grid is co-resident (tracking: one scan, 128 blocks for 64k feature slots; kLoopMaxBlocks).  Every block keeps
 // its own LDS copy of the slot's SolveState and runs the one-lane control on identical inputs (the same
 // packets summed in the same order), so all copies stay equal and no block waits for another's step: a
-// block evaluates its 1024 records at the candidate, publishes its packet, and one arrive / wait on a
+// block evaluates its kLoopBlock records at the candidate, publishes its packet, and one arrive / wait on a
 // per-slot counter later every block reduces every packet itself.
 //
 // Cross-block visibility (MI355X_MICROARCH.md, correctness boundaries: per-XCD L2s are not coherent):
@@ -2408,16 +2408,27 @@ __global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, u
     const int b = blockIdx.y, part = blockIdx.x, nblk = gridDim.x;
     __shared__ SolveState sS;
     __shared__ double tot[kPacket];
+#ifdef LMSF_STEP_PROFILE   // diagnostics build (tools/build_variant.sh): phase stamps of slot 0, first and last block
+    unsigned long long tp[24];
+    int ntp = 0;
+    const bool prof = b == 0 && (part == 0 || part == nblk - 1) && threadIdx.x == 0;
+#define LOOP_STAMP() do { if (prof && ntp < 24) tp[ntp++] = wall_clock64(); } while (0)
+#else
+#define LOOP_STAMP() do {} while (0)
+#endif
+    LOOP_STAMP();
     state_copy(sS, bv.st[b]);
     const int nq = bv.n_edge[b] + bv.n_surf[b];
     // lm_begin: the first evaluation's packets (fit_eval), IterationZero and the first step
     reduce_parts(bv, b, (nq + bv.part_q - 1) / bv.part_q, tot);   // ends with a barrier: sS is in place
+    LOOP_STAMP();
     if constexpr (kLoopCtlWave) {
         if (threadIdx.x < 64) wv::lm_begin(sS, tot);
     } else if (threadIdx.x == 0) {
         lm_begin_apply(sS, tot);
     }
     __syncthreads();
+    LOOP_STAMP();
     const unsigned base = sync[2 * b + 1];
     unsigned nbar = 0;
     const int pbuf = bv.max_parts / 2;   // packet buffers [pbuf, pbuf + 2 nblk): above the fit packets
@@ -2434,17 +2445,17 @@ __global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, u
 #pragma unroll
         for (int k = 0; k < kPacket; ++k) P[k] = 0.0;
         // lm_eval_kernel's form: the records' loads in flight together, then evaluated
-        const int q0 = part * kEvalBlock + threadIdx.x;
+        const int q0 = part * kLoopBlock + threadIdx.x;
         auto rec_at = [&](int k) { return rbase + (q0 + k * 256 < nq ? q0 + k * 256 : 0); };
-        float4 rp[kEvalPerThread];
-        RecV rv[kEvalPerThread];
+        float4 rp[kLoopPerThread];
+        RecV rv[kLoopPerThread];
 #pragma unroll
-        for (int k = 0; k < kEvalPerThread; ++k) {
+        for (int k = 0; k < kLoopPerThread; ++k) {
             rp[k] = bv.rec_p[rec_at(k)];
             rv[k] = bv.rec_v[rec_at(k)];
         }
 #pragma unroll
-        for (int k = 0; k < kEvalPerThread; ++k) {
+        for (int k = 0; k < kLoopPerThread; ++k) {
             const bool edge = __float_as_int(rp[k].w) == LMSF_EDGE;
             eval_record(Ps, q0 + k * 256 < nq, rp[k], rv[k], edge ? bv.rec_e[rec_at(k)] : make_double2(0.0, 0.0), P);
         }
@@ -2465,15 +2476,19 @@ __global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, u
                 coherent_store_f64(slotp + e, ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e]);
             }
         }
+        LOOP_STAMP();
         ++nbar;
         slot_barrier(&sync[2 * b], base + nbar * (unsigned)nblk, err, spin_limit);
+        LOOP_STAMP();
         reduce_coherent(bv, b, pbuf + (i & 1) * nblk, nblk, tot);
+        LOOP_STAMP();
         if constexpr (kLoopCtlWave) {
             if (threadIdx.x < 64) wv::lm_step(sS, tot, outer, last);
         } else if (threadIdx.x == 0) {
             lm_step_apply(sS, tot, outer, last);
         }
         __syncthreads();
+        LOOP_STAMP();
     }
     if (nbar == 0) {   // no wait yet: make sure every block has read st before block 0 rewrites it
         ++nbar;
@@ -2483,9 +2498,19 @@ __global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, u
         state_copy(bv.st[b], sS);
         if (threadIdx.x == 0) sync[2 * b + 1] = base + nbar * (unsigned)nblk;
     }
+#ifdef LMSF_STEP_PROFILE
+    if (prof) {   // x10 ns: begin reduce, begin apply, then per inner iteration eval, barrier, reduce, step
+        unsigned d[18];
+        for (int j = 0; j < 18; ++j) d[j] = j + 1 < ntp ? (unsigned)(tp[j + 1] - tp[j]) : 0u;
+        printf("lm_loop o%d blk%d/%d nq %d: %u %u | %u %u %u %u | %u %u %u %u | %u %u %u %u | %u %u %u %u\n", outer, part,
+               nblk, nq, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10], d[11], d[12], d[13], d[14],
+               d[15], d[16], d[17]);
+    }
+#endif
+#undef LOOP_STAMP
 }
 
-int lm_loop_blocks(const BatchView& bv) { return (bv.feat_stride + kEvalBlock - 1) / kEvalBlock; }
+int lm_loop_blocks(const BatchView& bv) { return (bv.feat_stride + kLoopBlock - 1) / kLoopBlock; }
 
 hipError_t launch_lm_loop(const BatchView& bv, int outer, unsigned* sync, int* err, unsigned spin_limit,
                           hipStream_t s) {

@@ -20,6 +20,14 @@ constexpr int kFitBlockMax = 256 * kFitMaxPerThread;
 #endif
 constexpr int kEvalPerThread = LMSF_EVAL_PER_THREAD;   // records per thread in the LM evaluation kernel
 constexpr int kEvalBlock = 256 * kEvalPerThread;
+// Records per thread of the single-scan LM loop (lm_loop_kernel; A/B).  2 puts a C3 / C4 scan's evaluation on twice
+// the CUs (128 blocks instead of 64 for 64k feature slots): C4 1,371 / 1,385 vs 1,372 / 1,365 scans/s, C3 1,296 /
+// 1,330 vs 1,377 / 1,357 frames/s (r05, alternating) -- the evaluation is not what bounds the loop.
+#ifndef LMSF_LOOP_PER_THREAD
+#define LMSF_LOOP_PER_THREAD 4
+#endif
+constexpr int kLoopPerThread = LMSF_LOOP_PER_THREAD;
+constexpr int kLoopBlock = 256 * kLoopPerThread;
 // Workspace growth: when a request exceeds the capacity, allocate 1.5x (a growing or jittering
 // request -- the keyframe window, a varying scan size -- then reallocates rarely: hipFree
 // synchronises the device and costs ~0.5 ms on the tracking path).
