@@ -713,12 +713,14 @@ lmsf_status ctx_settle(lmsf_ctx* c) {
 lmsf_status resolve_all_lim1(lmsf_ctx* c, size_t query_slots) {
     lmsf_status rs = ctx_settle(c);
     if (rs) return rs;
-    if (knn_team_for(query_slots) != 1) return LMSF_OK;   // the 8-lane walk never prunes
+    // the first-pass radius of dense maps: the pruned one-lane walks and, on dense priors, the 8-lane team walk
+    // (one read-back per map build: a prior's is taken at the first launch after set_prior_map)
     for (DevMap* ms : {c->map, c->prior})
         for (int k = 0; k < 3; ++k) {
             lmsf_status rc = resolve_lim1(c, ms[k]);
             if (rc) return rc;
         }
+    if (knn_team_for(query_slots) != 1) return LMSF_OK;
     if (c->cfg.solver == LMSF_SOLVER_CERES_LM)   // the fused batch path's dense first pass
         for (int k : {LMSF_EDGE, LMSF_SURF}) {
             lmsf_status rc = build_fine(c, k);

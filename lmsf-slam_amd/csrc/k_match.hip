@@ -78,6 +78,11 @@ constexpr bool kKnnRowsFirst = LMSF_KNN_ROWS_FIRST != 0;
 #define LMSF_KNN_LB_SKIP 1
 #endif
 constexpr bool kLbSkip = LMSF_KNN_LB_SKIP != 0;   // rows-first walk: nearest rows first, rows beyond the kept keys skipped
+// First-pass radius^2 of the pruned team walk as a multiple of the map's lim1 (its 6th key, the slot memo's, lies
+// farther out than the one-lane walk's 5th)
+#ifndef LMSF_TEAM_R1X
+#define LMSF_TEAM_R1X 2
+#endif
 
 template <int T>
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
@@ -218,6 +223,38 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
             k[i] = lo;
         }
     };
+    // row rr -> its (grid, dy, dz) geometry; false when the row lies outside the grid
+    auto row_geo = [&](int rr, const uint32_t*& row, int& xa, int& xb, float& lb, int& ox, int& sx) {
+        const GridView gg = pick_grid(TWO && rr >= 9, g2, g);
+        ox = gg.ox;
+        sx = gg.sx;
+        const int r9 = rr % 9, dyo = (r9 % 3) - 1, dzo = (r9 / 3) - 1;
+        const float fxs = fx * (float)gg.sx;
+        const bool inside = gg.n > 0 && fxs >= (float)(gg.ox - 2 * gg.sx) && fxs <= (float)(gg.ox + gg.nx + gg.sx) &&
+                            fy >= (float)(gg.oy - 2) && fy <= (float)(gg.oy + gg.ny + 1) &&
+                            fz >= (float)(gg.oz - 2) && fz <= (float)(gg.oz + gg.nz + 1);
+        if (!inside) return false;
+        const int cxs = (int)fxs - gg.ox, cy = (int)fy - gg.oy + dyo, cz = (int)fz - gg.oz + dzo;
+        xa = max(cxs - gg.sx, 0);
+        xb = min(cxs + 2 * gg.sx - 1, gg.nx - 1);
+        if (cy < 0 || cy >= gg.ny || cz < 0 || cz >= gg.nz || xa > xb) return false;
+        row = gg.off + ((size_t)cz * gg.ny + cy) * gg.nx;
+        const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
+        const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
+        const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
+        lb = gy * gy + gz * gz;
+        return true;
+    };
+    // slices of [xa, xb] meeting [w.x - r, w.x + r], r = sqrt(lim - lb) (empty when lim < lb)
+    auto window = [&](float lim, float lb, int xa, int xb, int ox, int sx, int& sa, int& sb) {
+        const float rem = lim - lb;
+        sa = 1;
+        sb = 0;
+        if (rem < 0.f) return;
+        const double r = (double)sqrtf(rem);
+        sa = max(xa, (int)floor(((double)w.x - r) * sx) - ox);
+        sb = min(xb, (int)floor(((double)w.x + r) * sx) - ox);
+    };
     if constexpr (T == 1 && !PRUNE && kKnnRowsFirst) {
         // all rows resolved first (2 x NR offset loads in one batch, one latency instead of NR), then
         // walked with RU candidate loads in flight
@@ -301,38 +338,6 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
             }
             for (; c < len; ++c) consider(rp[a + c], (uint32_t)(a + c) | tag);
         };
-        // row rr -> its (grid, dy, dz) geometry; false when the row lies outside the grid
-        auto row_geo = [&](int rr, const uint32_t*& row, int& xa, int& xb, float& lb, int& ox, int& sx) {
-            const GridView gg = pick_grid(TWO && rr >= 9, g2, g);
-            ox = gg.ox;
-            sx = gg.sx;
-            const int r9 = rr % 9, dyo = (r9 % 3) - 1, dzo = (r9 / 3) - 1;
-            const float fxs = fx * (float)gg.sx;
-            const bool inside = gg.n > 0 && fxs >= (float)(gg.ox - 2 * gg.sx) && fxs <= (float)(gg.ox + gg.nx + gg.sx) &&
-                                fy >= (float)(gg.oy - 2) && fy <= (float)(gg.oy + gg.ny + 1) &&
-                                fz >= (float)(gg.oz - 2) && fz <= (float)(gg.oz + gg.nz + 1);
-            if (!inside) return false;
-            const int cxs = (int)fxs - gg.ox, cy = (int)fy - gg.oy + dyo, cz = (int)fz - gg.oz + dzo;
-            xa = max(cxs - gg.sx, 0);
-            xb = min(cxs + 2 * gg.sx - 1, gg.nx - 1);
-            if (cy < 0 || cy >= gg.ny || cz < 0 || cz >= gg.nz || xa > xb) return false;
-            row = gg.off + ((size_t)cz * gg.ny + cy) * gg.nx;
-            const float ylo = fy + (float)dyo, zlo = fz + (float)dzo;
-            const float gy = fmaxf(0.f, fmaxf(ylo - w.y, w.y - (ylo + 1.f)));
-            const float gz = fmaxf(0.f, fmaxf(zlo - w.z, w.z - (zlo + 1.f)));
-            lb = gy * gy + gz * gz;
-            return true;
-        };
-        // slices of [xa, xb] meeting [w.x - r, w.x + r], r = sqrt(lim - lb) (empty when lim < lb)
-        auto window = [&](float lim, float lb, int xa, int xb, int ox, int sx, int& sa, int& sb) {
-            const float rem = lim - lb;
-            sa = 1;
-            sb = 0;
-            if (rem < 0.f) return;
-            const double r = (double)sqrtf(rem);
-            sa = max(xa, (int)floor(((double)w.x - r) * sx) - ox);
-            sb = min(xb, (int)floor(((double)w.x + r) * sx) - ox);
-        };
         constexpr int kOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // own row, faces, corners
         auto row_of = [&](int i) { return kOrder[TWO ? i / 2 : i] + ((TWO && (i & 1)) ? 9 : 0); };
         const float lim1 = g.lim1 * kCullLim;   // both grids of a kind share the first-pass radius
@@ -390,45 +395,137 @@ __device__ __forceinline__ void knn_walk(const GridView& g, const GridView& g2, 
     } else {
         // lane l resolves rows l, l + T, ...; the team shares them by shuffles
         constexpr int REPS = (NR + T - 1) / T;
-        int rs_[REPS], rl_[REPS];
+        // the team strides over the flattened candidates of the rows' ranges [rs_, rs_ + rl_) (entry rep of lane l:
+        // row l + rep T)
+        auto walk_rows = [&](const int (&rs_)[REPS], const int (&rl_)[REPS]) {
+            int st[NR], pre[NR + 1];
+            pre[0] = 0;
 #pragma unroll
-        for (int rep = 0; rep < REPS; ++rep) {
-            rs_[rep] = 0;
-            rl_[rep] = 0;
-            float lbr;
-            if (lane + rep * T < NR) resolve_row(lane + rep * T, rs_[rep], rl_[rep], lbr);
-        }
-        int st[NR], pre[NR + 1];
-        pre[0] = 0;
+            for (int r = 0; r < NR; ++r) {
+                st[r] = __shfl(rs_[r / T], r % T, T);
+                pre[r + 1] = pre[r] + __shfl(rl_[r / T], r % T, T);
+            }
+            const int total = pre[NR];
+            // current row r: candidates [rpre, rend) map to pts[rbase + (v - rpre)]
+            int r = 0, rpre = 0, rend = pre[1], rbase = st[0];
+            const float4* rpts = g.pts;
+            uint32_t rtag = 0;
+            for (int v = lane; v < total; v += T) {
+                while (v >= rend) {
+                    ++r;
+                    rpre = rend;
+                    int e = pre[NR], s0 = st[NR - 1];
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            st[r] = __shfl(rs_[r / T], r % T, T);
-            pre[r + 1] = pre[r] + __shfl(rl_[r / T], r % T, T);
-        }
-        const int total = pre[NR];
-        // current row r: candidates [rpre, rend) map to pts[rbase + (v - rpre)]
-        int r = 0, rpre = 0, rend = pre[1], rbase = st[0];
-        const float4* rpts = g.pts;
-        uint32_t rtag = 0;
-        for (int v = lane; v < total; v += T) {
-            while (v >= rend) {
-                ++r;
-                rpre = rend;
-                int e = pre[NR], s0 = st[NR - 1];
-#pragma unroll
-                for (int j = NR - 1; j >= 1; --j) {   // static-index selects keep pre[]/st[] in registers
-                    e = (r + 1 == j) ? pre[j] : e;
-                    s0 = (r == j - 1) ? st[j - 1] : s0;
+                    for (int j = NR - 1; j >= 1; --j) {   // static-index selects keep pre[]/st[] in registers
+                        e = (r + 1 == j) ? pre[j] : e;
+                        s0 = (r == j - 1) ? st[j - 1] : s0;
+                    }
+                    rend = e;
+                    rbase = s0;
+                    if (TWO && r == 9) {
+                        rpts = g2.pts;
+                        rtag = kGridBit;
+                    }
                 }
-                rend = e;
-                rbase = s0;
-                if (TWO && r == 9) {
-                    rpts = g2.pts;
-                    rtag = kGridBit;
+                const int pos = rbase + (v - rpre);
+                consider(rpts[pos], (uint32_t)pos | rtag);
+            }
+        };
+        int rs_[REPS], rl_[REPS];
+        if constexpr (!PRUNE) {
+#pragma unroll
+            for (int rep = 0; rep < REPS; ++rep) {
+                rs_[rep] = 0;
+                rl_[rep] = 0;
+                float lbr;
+                if (lane + rep * T < NR) resolve_row(lane + rep * T, rs_[rep], rl_[rep], lbr);
+            }
+            walk_rows(rs_, rl_);
+        } else {
+            // Pruned team walk (dense priors, single-scan launches): pass 1 walks every row meeting the first-pass
+            // ball (radius^2 r1 = min(lim1, lim)) trimmed to it; the team's NK-th key d4 (its lanes' lists merged)
+            // ends the search when it lies within lim1 (no point outside the scanned ball can displace it) or
+            // when the ball was the whole search radius; else pass 2 walks the rows with yz-gap^2 <= d4, trimmed
+            // to d4 (kCullLim margin) minus the slices pass 1 scanned -- the one-lane pruned walk's rules, with
+            // the bound shared by the team once, between the passes.
+            const float l1 = fminf(g.lim1 * (float)LMSF_TEAM_R1X, 1.f);   // the team's first-pass radius^2
+            const float r1 = fminf(l1 * kCullLim, lim);
+#pragma unroll
+            for (int rep = 0; rep < REPS; ++rep) {
+                rs_[rep] = 0;
+                rl_[rep] = 0;
+                const int rr = lane + rep * T;
+                const uint32_t* row;
+                int xa, xb, ox, sx;
+                float lb;
+                if (rr < NR && row_geo(rr, row, xa, xb, lb, ox, sx)) {
+                    if (count27) c27 += row[xb + 1] - row[xa];
+                    int sa, sb;
+                    if (lb <= r1) {
+                        window(r1, lb, xa, xb, ox, sx, sa, sb);
+                        if (sa <= sb) {
+                            rs_[rep] = (int)row[sa];
+                            rl_[rep] = (int)(row[sb + 1] - row[sa]);
+                        }
+                    }
                 }
             }
-            const int pos = rbase + (v - rpre);
-            consider(rpts[pos], (uint32_t)pos | rtag);
+            walk_rows(rs_, rl_);
+            // the team's NK-th key (a copy of the lists merged: NK rounds of team-min, the owner pops)
+            double kk[NK];
+#pragma unroll
+            for (int j = 0; j < NK; ++j) kk[j] = k[j];
+            double kth = kk[0];
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                kth = kk[0];
+#pragma unroll
+                for (int o = T / 2; o >= 1; o >>= 1) kth = key_min(kth, __shfl_xor(kth, o, T));
+                if (key_bits(kk[0]) == key_bits(kth)) {
+#pragma unroll
+                    for (int j = 0; j + 1 < NK; ++j) kk[j] = kk[j + 1];
+                    kk[NK - 1] = key_as_double(kSentinel);
+                }
+            }
+            const float d4 = key_d2(kth);
+            if (!(d4 <= l1) && !(lim <= l1 * kCullLim)) {
+                const float b2 = fminf(d4 * kCullLim, lim);
+                int qs_[REPS], ql_[REPS];   // right-hand segments (left-hand ones in rs_ / rl_)
+#pragma unroll
+                for (int rep = 0; rep < REPS; ++rep) {
+                    rs_[rep] = 0;
+                    rl_[rep] = 0;
+                    qs_[rep] = 0;
+                    ql_[rep] = 0;
+                    const int rr = lane + rep * T;
+                    const uint32_t* row;
+                    int xa, xb, ox, sx;
+                    float lb;
+                    if (rr < NR && row_geo(rr, row, xa, xb, lb, ox, sx) && !(lb > d4)) {
+                        int sa, sb, ta = 1, tb = 0;
+                        window(b2, lb, xa, xb, ox, sx, sa, sb);
+                        if (lb <= r1) window(r1, lb, xa, xb, ox, sx, ta, tb);
+                        if (ta > tb) {
+                            if (sa <= sb) {
+                                rs_[rep] = (int)row[sa];
+                                rl_[rep] = (int)(row[sb + 1] - row[sa]);
+                            }
+                        } else {
+                            const int l1 = min(sb, ta - 1), r0 = max(sa, tb + 1);
+                            if (sa <= l1) {
+                                rs_[rep] = (int)row[sa];
+                                rl_[rep] = (int)(row[l1 + 1] - row[sa]);
+                            }
+                            if (r0 <= sb) {
+                                qs_[rep] = (int)row[r0];
+                                ql_[rep] = (int)(row[sb + 1] - row[r0]);
+                            }
+                        }
+                    }
+                }
+                walk_rows(rs_, rl_);
+                walk_rows(qs_, ql_);
+            }
         }
     }
 }
@@ -468,6 +565,10 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
     constexpr int NK = MEMO ? 6 : 5;
     __shared__ unsigned long long blk_n27;
     __shared__ unsigned int blk_q, blk_r;
+#ifdef LMSF_STEP_PROFILE   // diagnostics build: block start / walk start / walk end / end stamps of sampled blocks
+    __shared__ unsigned long long kt[4];
+    if (threadIdx.x == 0) { kt[0] = wall_clock64(); kt[1] = kt[2] = 0; }
+#endif
     stamp_if(bv.stamp_start, blockIdx.x == 0);
     int bx, b;
     block_coords(remap, gx, bx, b);
@@ -537,12 +638,18 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
             }
         }
         unsigned int c27 = 0;
+#ifdef LMSF_STEP_PROFILE
+        if (threadIdx.x == 0) kt[1] = wall_clock64();
+#endif
         if (!reuse) {
             const double sentinel = key_as_double(kSentinel);
             double k[NK];   // ascending kept keys
 #pragma unroll
             for (int j = 0; j < NK; ++j) k[j] = sentinel;
             knn_walk<T, TWO, PRUNE, kKnnUnroll, NK>(g, g2, w, lane, bv.count27, k, c27, lim);
+#ifdef LMSF_STEP_PROFILE
+            if (threadIdx.x == 0) kt[2] = wall_clock64();
+#endif
             // merge: NK rounds of team-min; the owning lane pops its head (keys are unique)
             double res[NK];
 #pragma unroll
@@ -591,6 +698,10 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
         }
     }
     __syncthreads();
+#ifdef LMSF_STEP_PROFILE
+    if (threadIdx.x == 0 && (blockIdx.x % 97) == 0)
+        printf("knnblk %d %llu %llu %llu %llu\n", blockIdx.x, kt[0], kt[1], kt[2], (unsigned long long)wall_clock64());
+#endif
     if (threadIdx.x == 0 && bv.n27 && blk_q) {
         // 64 counter shards on separate 128-B lines: one word serialises ~1e5 block updates
         unsigned long long* shard = bv.n27 + (size_t)(blockIdx.x & (kCounterShards - 1)) * 16;
@@ -2609,9 +2720,18 @@ static void launch_knn_t(int T, bool prune, bool memo, dim3 grid, const GridView
                          int remap, hipStream_t s) {
 #define LMSF_KNN(TT, PP) hipLaunchKernelGGL((knn_kernel<TT, TWO, PP>), grid, dim3(256), 0, s, edge, surf, edge2, surf2, bv, \
                                             skip_converged, gx, remap)
-    if (memo && T == 8) {   // the team walk never prunes
-        hipLaunchKernelGGL((knn_kernel<8, TWO, false, true>), grid, dim3(256), 0, s, edge, surf, edge2, surf2, bv,
-                           skip_converged, gx, remap);
+    // The memo team walk on dense maps: pruned with LMSF_TEAM_PRUNE=1 (A/B; exact, but C4's search launch took 54.6-58
+    // vs 52 us unpruned at first-pass radii of 1-8 x lim1: the walks shortened -- slowest team 22-28 vs 34-48 us,
+    // r05 block stamps -- but the launch is set by its blocks' start beside the concurrent extraction and by the
+    // memo / row-resolution latencies both forms share).
+    if (memo && T == 8) {
+        static const bool team_prune = ab_int("LMSF_TEAM_PRUNE", 0) != 0;
+        if (prune && team_prune)
+            hipLaunchKernelGGL((knn_kernel<8, TWO, true, true>), grid, dim3(256), 0, s, edge, surf, edge2, surf2, bv,
+                               skip_converged, gx, remap);
+        else
+            hipLaunchKernelGGL((knn_kernel<8, TWO, false, true>), grid, dim3(256), 0, s, edge, surf, edge2, surf2, bv,
+                               skip_converged, gx, remap);
         return;
     }
     switch (T) {
