@@ -508,6 +508,28 @@ def test_batch_memo_dense(lib, oracle_mod, dense_workload):
     assert dt <= POSE_TOL and dr <= POSE_TOL
 
 
+def test_batch_dense_wide_extent(lib, dense_workload):
+    """a dense map whose first-pass grid would exceed the cell limit.  Two far points stretch the
+    surf map to 4,000 x 100 x 100 m: its 1 m grid has 1.6e8 cells (4 x-slices per metre), the 0.5 m first-pass grid
+    would need 1.3e9 > 2^30 -- it is refused (recorded against the map build, not retried per launch) and the first
+    pass runs on the 1 m grid.  Both launches on the wide map equal the compact map's poses bit for bit (the far
+    points are never within 1 m of a query: the same neighbour sets and records)."""
+    wl = dense_workload
+    ctx = _ctx(lib, schedule=1, max_iterations=5, max_batch=16)
+    ctx.set_map(lib.EDGE, wl.edge_map)
+    ctx.set_map(lib.SURF, wl.surf_map)
+    ctx.load_scans([wl.scans[0]] * 16)
+    rng = np.random.default_rng(9)
+    from lmsf import synth
+    guesses = np.stack([synth.perturb(wl.truth[0], rng) for _ in range(16)])
+    ref, _ = ctx.batch_run(guesses)
+    far = np.array([[2000.0, 50.0, 50.0, 0.0], [-2000.0, -50.0, -50.0, 0.0]], np.float32)
+    ctx.set_map(lib.SURF, np.concatenate([wl.surf_map, far]))
+    wide, _ = ctx.batch_run(guesses)
+    wide2, _ = ctx.batch_run(guesses)
+    assert np.array_equal(wide, ref) and np.array_equal(wide2, ref)
+
+
 def test_edge_cases(lib, oracle_mod, small_workload):
     wl = small_workload
     ctx = _ctx(lib)
