@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <climits>
 #include <type_traits>
 
 #include "lmsf_internal.h"
@@ -142,11 +143,23 @@ constexpr bool kScatterBits = LMSF_SCATTER_BITS != 0;
 #ifndef LMSF_CONCAT_LDS
 #define LMSF_CONCAT_LDS 1
 #endif
+// LMSF_SCATTER_LDS (A/B): ring_scatter_kernel stages its tile in LDS in ring-major order and writes each ring's run of
+// the tile contiguously (1), or stores every point straight to its ring position (0, r04: on a column-major 128-beam
+// scan a wave's 64 stores then land in 64 rings, 16 B each).
+#ifndef LMSF_SCATTER_LDS
+#define LMSF_SCATTER_LDS 1
+#endif
+constexpr bool kScatterLds = LMSF_SCATTER_LDS != 0;
 
 // Stable multisplit of one tile into ring order (input order preserved inside each ring).
 __global__ __launch_bounds__(256) void ring_scatter_kernel(ExtractView ev) {
     __shared__ int wcnt[4][kMaxRings];
     __shared__ int running[kMaxRings];
+    // kScatterLds: the tile's points in ring-major order (lstart: the tile's exclusive ring prefix), their
+    // destinations and source indices
+    __shared__ float4 s_pt[kScatterLds ? kTile : 1];
+    __shared__ int s_dst[kScatterLds ? kTile : 1], s_src[kScatterLds ? kTile : 1];
+    __shared__ int lstart[kMaxRings];
     const int b = blockIdx.y, t = blockIdx.x;
     const int n = ev.raw_count[b];
     if (t * kTile >= n) return;
@@ -159,6 +172,36 @@ __global__ __launch_bounds__(256) void ring_scatter_kernel(ExtractView ev) {
     float4* out = ev.ring_pts + (size_t)b * ev.raw_stride;
     int* osrc = ev.ring_src + (size_t)b * ev.raw_stride;
     (void)nt;
+    int tile_total = 0;
+    if constexpr (kScatterLds) {   // the tile's ring counts (lstart as a histogram first), then their prefix
+        for (int r = threadIdx.x; r < kMaxRings; r += 256) lstart[r] = 0;
+        __syncthreads();
+        for (int k = threadIdx.x; k < kTile; k += 256) {
+            const int i = t * kTile + k;
+            const int r = i < n ? (int)rid[i] : -1;
+            if (r >= 0) atomicAdd(&lstart[r], 1);
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {   // exclusive scan over the rings by one wave
+            int acc = 0;
+            for (int r0 = 0; r0 < ev.n_scans; r0 += 64) {
+                const int r = r0 + lane;
+                const int c = r < ev.n_scans ? lstart[r] : 0;
+                int x = c;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(x, o, 64);
+                    if (lane >= o) x += y;
+                }
+                if (r < ev.n_scans) lstart[r] = acc + x - c;
+                acc += __shfl(x, 63, 64);
+            }
+            if (lane == 0) wcnt[0][0] = acc;   // the tile's total (wcnt is cleared before its first use below)
+        }
+        __syncthreads();
+        tile_total = wcnt[0][0];
+        __syncthreads();
+    }
     const int ring_bits = ev.n_scans <= 1 ? 0 : 32 - __clz(ev.n_scans - 1);
     for (int c0 = 0; c0 < kTile; c0 += 256) {
         for (int k = threadIdx.x; k < 4 * kMaxRings; k += 256) wcnt[k / kMaxRings][k % kMaxRings] = 0;
@@ -198,13 +241,27 @@ __global__ __launch_bounds__(256) void ring_scatter_kernel(ExtractView ev) {
             int base = running[r];
             for (int w = 0; w < wave; ++w) base += wcnt[w][r];
             const int dst = toff[(size_t)r * ev.n_tiles + t] + base + rank;
-            out[dst] = pt;
-            osrc[dst] = i;
+            if constexpr (kScatterLds) {
+                const int lp = lstart[r] + base + rank;
+                s_pt[lp] = pt;
+                s_dst[lp] = dst;
+                s_src[lp] = i;
+            } else {
+                out[dst] = pt;
+                osrc[dst] = i;
+            }
         }
         __syncthreads();
         for (int rr = threadIdx.x; rr < ev.n_scans; rr += 256)
             running[rr] += wcnt[0][rr] + wcnt[1][rr] + wcnt[2][rr] + wcnt[3][rr];
         __syncthreads();
+    }
+    if constexpr (kScatterLds) {   // each ring's run of the tile to consecutive ring positions
+        for (int j = threadIdx.x; j < tile_total; j += 256) {
+            const int dst = s_dst[j];
+            out[dst] = s_pt[j];
+            osrc[dst] = s_src[j];
+        }
     }
 }
 
@@ -788,6 +845,174 @@ __global__ __launch_bounds__(256) void concat_kernel(ExtractView ev) {
     }
 }
 
+// concat_kernel's placement with one workgroup per (sector, ring, scan) (LMSF_CONCAT_SECTOR, A/B): a sector's edge
+// picks and its surfs each occupy one contiguous range of the ring's emission order (the greedy pick and the surf
+// compaction run sector by sector), so the block stages the sector's points in LDS by their emission index and
+// writes feat / feat_src as contiguous runs -- where the grid-stride form stores every point to its slot, a wave's
+// 64 stores spread over the sector's curvature permutation.  The search-order outputs (fslot / featp, by rank:
+// ring order) and qslot (by position) are written directly.  Results are the same placements.
+#ifndef LMSF_CONCAT_SECTOR
+#define LMSF_CONCAT_SECTOR 1
+#endif
+constexpr int kCatPer = kSortMax / 256;   // positions per thread (a sector holds at most kSortMax)
+constexpr int kCatStage = 1024;           // surfs staged per sector (larger sectors store the rest directly)
+__global__ __launch_bounds__(256) void concat_sector_kernel(ExtractView ev) {
+    __shared__ float4 s_pt[kCatStage];
+    __shared__ int s_src[kCatStage];
+    __shared__ float4 e_pt[64];
+    __shared__ int e_src[64];
+    __shared__ int s_min[2], s_cnt[2];   // [0] edges, [1] surfs: smallest emission index and count in the sector
+    __shared__ int pre[4];               // epre[r], epre[r + 1], spre[r], spre[r + 1]
+    __shared__ int tot[2];               // ne, ns of the scan
+    const int r = blockIdx.x / 6, k = blockIdx.x % 6, b = blockIdx.y;
+    const int nr = ev.n_scans;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int* rs = ev.ring_start + (size_t)b * (kMaxRings + 1);
+    if (r >= nr) return;
+    const int start = rs[r], size = rs[r + 1] - start;
+    // this ring's prefixes and the scan's totals: the edge / surf counts of the rings before r (wave 0 / wave 1)
+    if (wave < 2) {
+        const int* cnt = (wave == 0 ? ev.ring_edge_cnt : ev.ring_surf_cnt) + (size_t)b * kMaxRings;
+        int below = 0, all = 0, mine = 0;
+        for (int r0 = lane; r0 < nr; r0 += 64) {
+            const int c = cnt[r0];
+            all += c;
+            below += r0 < r ? c : 0;
+            mine += r0 == r ? c : 0;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            below += __shfl_xor(below, o, 64);
+            all += __shfl_xor(all, o, 64);
+            mine += __shfl_xor(mine, o, 64);
+        }
+        if (lane == 0) {
+            pre[2 * wave] = below;
+            pre[2 * wave + 1] = below + mine;
+            tot[wave] = all;
+            s_min[wave] = INT_MAX;
+            s_cnt[wave] = 0;
+        }
+    }
+    __syncthreads();
+    const int ne = tot[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ev.n_edge[b] = tot[0];
+        ev.n_surf[b] = tot[1];
+        ev.n_pos[b] = rs[nr];
+    }
+    int* qs = ev.qslot + (size_t)b * ev.raw_stride + start;
+    // positions outside the sectors (and whole rings the features kernel skipped) hold no feature
+    bool ring_ok = size >= 20 && size <= kRingMax;
+    int s0 = 0, n = 0;
+    if (ring_ok) {   // ring_features_kernel's bound: a ring whose first or last sector exceeds kSortMax has no features
+        int a0, n0, a5, n5;
+        sector_bounds(size, 0, a0, n0);
+        sector_bounds(size, 5, a5, n5);
+        ring_ok = n0 <= kSortMax && n5 <= kSortMax;
+        sector_bounds(size, k, s0, n);
+    }
+    if (!ring_ok) {
+        if (k == 0)
+            for (int j = threadIdx.x; j < size; j += 256) qs[j] = -1;
+        return;
+    }
+    if (k == 0)
+        for (int j = threadIdx.x; j < s0; j += 256) qs[j] = -1;
+    if (k == 5)
+        for (int j = s0 + n + threadIdx.x; j < size; j += 256) qs[j] = -1;
+    const int* qc = ev.qcode + (size_t)b * ev.raw_stride + start + s0;
+    const float4* rp = ev.ring_pts + (size_t)b * ev.raw_stride + start + s0;
+    const int* rsrc = ev.ring_src + (size_t)b * ev.raw_stride + start + s0;
+    int code[kCatPer];
+    int mn[2] = {INT_MAX, INT_MAX}, ct[2] = {0, 0};
+#pragma unroll
+    for (int u = 0; u < kCatPer; ++u) {
+        const int i = threadIdx.x + 256 * u;
+        code[u] = i < n ? qc[i] : -1;
+        if (code[u] >= 0) {
+            const int kind = (code[u] & kQSurf) ? 1 : 0;
+            mn[kind] = min(mn[kind], code[u] & kQCodeMask);
+            ++ct[kind];
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {   // per wave, then one LDS atomic per wave and kind
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            mn[d] = min(mn[d], __shfl_xor(mn[d], o, 64));
+            ct[d] += __shfl_xor(ct[d], o, 64);
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            if (ct[d]) {
+                atomicMin(&s_min[d], mn[d]);
+                atomicAdd(&s_cnt[d], ct[d]);
+            }
+        }
+    }
+    __syncthreads();
+    int* fs = ev.fslot + (size_t)b * ev.feat_stride;
+    float4* fp = ev.featp + (size_t)b * ev.feat_stride;
+    const int ecap = pre[1] - pre[0], scap = pre[3] - pre[2];   // the ring's kept counts (capacity drops)
+#pragma unroll
+    for (int u = 0; u < kCatPer; ++u) {
+        const int i = threadIdx.x + 256 * u;
+        if (i >= n) continue;
+        const int c = code[u];
+        int slot = -1;
+        if (c >= 0) {
+            const bool surf = (c & kQSurf) != 0;
+            const int l = c & kQCodeMask, rank = (c >> kQRankShift) & kQCodeMask;
+            const float4 q = rp[i];
+            const int src = rsrc[i];
+            int o = -1;
+            if (surf) {
+                if (l < scap) { slot = ne + pre[2] + l; o = ne + pre[2] + rank; }
+                if (l - s_min[1] < kCatStage) {
+                    s_pt[l - s_min[1]] = q;
+                    s_src[l - s_min[1]] = src;
+                } else if (slot >= 0 && slot < ev.feat_stride) {   // beyond the staging: stored directly
+                    ev.feat[(size_t)b * ev.feat_stride + slot] = q;
+                    ev.feat_src[(size_t)b * ev.feat_stride + slot] = src;
+                }
+            } else {
+                if (l < ecap) { slot = pre[0] + l; o = pre[0] + rank; }
+                if (l - s_min[0] < 64) {
+                    e_pt[l - s_min[0]] = q;
+                    e_src[l - s_min[0]] = src;
+                }
+            }
+            if (slot >= 0 && slot < ev.feat_stride && o < ev.feat_stride) {
+                fs[o] = slot;
+                fp[o] = make_float4(q.x, q.y, q.z, __int_as_float(slot));
+            }
+        }
+        qs[s0 + i] = slot;
+    }
+    __syncthreads();
+    float4* feat = ev.feat + (size_t)b * ev.feat_stride;
+    int* fsrc = ev.feat_src + (size_t)b * ev.feat_stride;
+    for (int j = threadIdx.x; j < min(s_cnt[1], kCatStage); j += 256) {   // the sector's surfs: s_min .. + count
+        const int l = s_min[1] + j;
+        const int slot = ne + pre[2] + l;
+        if (l < scap && slot < ev.feat_stride) {
+            feat[slot] = s_pt[j];
+            fsrc[slot] = s_src[j];
+        }
+    }
+    for (int j = threadIdx.x; j < min(s_cnt[0], 64); j += 256) {
+        const int l = s_min[0] + j;
+        const int slot = pre[0] + l;
+        if (l < ecap && slot < ev.feat_stride) {
+            feat[slot] = e_pt[j];
+            fsrc[slot] = e_src[j];
+        }
+    }
+}
+
 hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
     hipLaunchKernelGGL(ring_count_kernel, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(ring_offsets_kernel, dim3(ev.B), dim3(256), 0, s, ev);
@@ -800,7 +1025,10 @@ hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
         return v >= 1 && v <= 1024 ? v : 256;
     }();
     const int cblocks = min(cmax, (ev.raw_stride + 255) / 256);
-    hipLaunchKernelGGL(concat_kernel, dim3(max(cblocks, 1), ev.B), dim3(256), 0, s, ev);
+    if (LMSF_CONCAT_SECTOR)
+        hipLaunchKernelGGL(concat_sector_kernel, dim3(ev.n_scans * 6, ev.B), dim3(256), 0, s, ev);
+    else
+        hipLaunchKernelGGL(concat_kernel, dim3(max(cblocks, 1), ev.B), dim3(256), 0, s, ev);
     return hipGetLastError();
 }
 
