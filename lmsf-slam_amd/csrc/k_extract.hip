@@ -144,14 +144,17 @@ constexpr bool kScatterBits = LMSF_SCATTER_BITS != 0;
 #define LMSF_CONCAT_LDS 1
 #endif
 // LMSF_SCATTER_LDS (A/B): ring_scatter_kernel stages its tile in LDS in ring-major order and writes each ring's run of
-// the tile contiguously (1), or stores every point straight to its ring position (0, r04: on a column-major 128-beam
-// scan a wave's 64 stores then land in 64 rings, 16 B each).
+// the tile contiguously for scans of more than kScatterLdsRings rings (1), or stores every point straight to its ring
+// position (0, r04: on a column-major 128-beam scan a wave's 64 stores then land in 64 rings, 16 B each).  16-beam
+// scans keep the direct stores: a 256-point chunk already writes 16-point runs per ring, and the staging's extra
+// pass and 51 KB of LDS made C2's scatter slower (81 -> 104 us per 128 scans).
 #ifndef LMSF_SCATTER_LDS
 #define LMSF_SCATTER_LDS 1
 #endif
-constexpr bool kScatterLds = LMSF_SCATTER_LDS != 0;
+constexpr int kScatterLdsRings = 32;
 
 // Stable multisplit of one tile into ring order (input order preserved inside each ring).
+template <bool kScatterLds>
 __global__ __launch_bounds__(256) void ring_scatter_kernel(ExtractView ev) {
     __shared__ int wcnt[4][kMaxRings];
     __shared__ int running[kMaxRings];
@@ -1016,7 +1019,10 @@ __global__ __launch_bounds__(256) void concat_sector_kernel(ExtractView ev) {
 hipError_t launch_extract(const ExtractView& ev, hipStream_t s) {
     hipLaunchKernelGGL(ring_count_kernel, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(ring_offsets_kernel, dim3(ev.B), dim3(256), 0, s, ev);
-    hipLaunchKernelGGL(ring_scatter_kernel, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
+    if (LMSF_SCATTER_LDS && ev.n_scans > kScatterLdsRings)
+        hipLaunchKernelGGL(ring_scatter_kernel<true>, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
+    else
+        hipLaunchKernelGGL(ring_scatter_kernel<false>, dim3(ev.n_tiles, ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(sector_sort_kernel, dim3(ev.n_scans * 6, ev.B), dim3(256), 0, s, ev);
     hipLaunchKernelGGL(ring_features_kernel, dim3(ev.n_scans, ev.B), dim3(256), 0, s, ev);
     // blocks per scan (LMSF_CONCAT_BLOCKS, A/B; default 256: ~one feature and one position per thread)
