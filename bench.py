@@ -106,7 +106,8 @@ def parse(argv=None):
                          "the device count, gloo collectives on the GPU tensors; the line is marked as a rehearsal)")
     ap.add_argument("--dump", default=None, metavar="DIR",
                     help="C4: each rank writes its per-step poses and update types to DIR/c4_rank<r>.npz (the multi-rank "
-                         "parity test replays them against oracle trackers)")
+                         "parity test replays them against oracle trackers); C2: its units' scans (seeds, truth), "
+                         "guesses, last-step poses and all-gathered poses to DIR/c2_rank<r>.npz")
     ap.add_argument("--launch-check", action="store_true",
                     help="no GPU work: ranks join the process group, run the C2 pose all-gather on CPU tensors and "
                          "print the line skeleton (CPU test of the --gpus launcher)")
@@ -623,6 +624,13 @@ def run_batch(args, d):
         return poses
 
     elapsed, _, mean_n27 = timed(d, step, args.warmup, args.steps, ctxs, not args.no_n27)
+    if args.dump and cfg == "C2":   # the multi-rank parity test (tests/test_gpu_multirank.py) replays these
+        os.makedirs(args.dump, exist_ok=True)
+        g = gathered.cpu().numpy() if world > 1 else poses[None].copy()
+        np.savez(os.path.join(args.dump, f"c2_rank{rank}.npz"), poses=poses, gathered=g, guesses=guesses,
+                 truth_u=truth_u, unit_scan=np.asarray(unit_scan),
+                 seeds=np.asarray([2000 + k + 97 * (rank * U + i) for i in range(U)]), world=world, cols=args.cols,
+                 map_points=args.map_points)
     enqueue_ms = float(np.median(enqueue_s)) * 1e3
     timed_coll = coll_s[args.warmup:args.warmup + args.steps]   # timed() runs the warmups first
     collective_ms = round(1e3 * float(np.mean(timed_coll)), 4) if timed_coll and world > 1 else 0.0

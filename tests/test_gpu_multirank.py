@@ -1,4 +1,4 @@
-"""The N-rank GPU data path pinned numerically on a one-GPU box.
+"""The N-rank GPU data path pinned numerically on a one-GPU box (C2 added in r05).
 
 `bench.py --gpus 2 --dist-backend gloo-gpu --config C4` runs the C4 configuration (BASELINE configs[3]) as two
 ranks on the box's GPU: the launcher starts `torch.distributed.run` as a child process, rank 0 broadcasts the shared
@@ -73,3 +73,49 @@ def test_c4_two_rank_rehearsal_matches_oracle_trackers(oracle_mod, tmp_path):
                 ot.commit()
         keyframes += len(kfs)
     assert keyframes >= 2
+
+
+def test_c2_two_rank_rehearsal_matches_oracle(oracle_mod, tmp_path):
+    """The default configuration's N-rank path (scan-sharded C2, poses all-gathered after every step) as two gloo-gpu
+    ranks on the box's GPU: each rank's own poses reach both ranks unchanged (the all-gather), and the first units of
+    each rank -- its own scans (rank-dependent seeds) at its own guesses -- match the oracle's registration."""
+    from conftest import pose_err
+    sys.path.insert(0, REPO)
+    import bench
+    from lmsf import synth
+    map_points, cols, batch, unique = 200_000, 1024, 8, 4
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo-gpu", "--config",
+           "C2", "--steps", "2", "--warmup", "1", "--batch", str(batch), "--unique-scans", str(unique), "--streams", "1",
+           "--map-points", str(map_points), "--cols", str(cols), "--no-cpu", "--no-n27", "--h2d", "off", "--workers",
+           "1", "--dump", str(tmp_path)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1 and '"n_gpus": 2' in line[0] and "rehearsal" in line[0]
+    dumps = [np.load(tmp_path / f"c2_rank{q}.npz") for q in range(2)]
+    for q in range(2):
+        assert dumps[q]["gathered"].shape == (2, batch, 7)
+        for o in range(2):
+            assert np.array_equal(dumps[o]["gathered"][q], dumps[q]["poses"]), (q, o)
+    c = synth.CONFIGS["C2"]
+    k = c["k"]
+    scene = synth.make_scene(1000 + k, road_length=80.0)
+    em, sm = synth.make_map(scene, map_points, 1000 + k + 7, center_x=(0.0, 80.0), radius=c["radius"])
+    for q in range(2):
+        dm = dumps[q]
+        for i in range(2):   # units 0 and 1: scans 0 and 1 of rank q
+            u = int(dm["unit_scan"][i])
+            scan = bench.make_scans([(1000 + k, dm["truth_u"][u], int(dm["seeds"][u]), cols, c["elev"])], 1)[0]
+            e, s, _, _ = oracle_mod.extract(scan, **c["extract"])
+            reg = oracle_mod.Registration()
+            reg.set_map(1, em)
+            reg.set_map(2, sm)
+            reg.set_scan(1, e)
+            reg.set_scan(2, s)
+            reg.set_fixed_schedule(True)
+            reg.set_max_iterations(5)
+            ox, _, _ = reg.solve(dm["guesses"][i])
+            dt, dr = pose_err(dm["poses"][i], ox)
+            assert dt <= POSE_TOL and dr <= POSE_TOL, (q, i, dt, dr)
