@@ -51,7 +51,10 @@ DEFAULTS = {   # per configuration: batch (scans per launch), map points, column
     # r02 (tools/gpu_ab_batch.sh, 128 slots per context): 256 x 2 streams 22.37-22.39k scans/s, 384 x 3
     # 22.84k, 512 x 4 23.06-23.13k, 768 x 6 23.07k, 1024 x 8 22.92k, 1024 x 4 (256 per context) 22.92k,
     # 512 x 8 (64 per context) 22.27k: four contexts of 128 fill the chip's gaps best (22 ms per step)
-    "C2": dict(batch=512, map_points=1_000_000, cols=4096, steps=40, warmup=2, streams=4),
+    # r05 (two boxes, alternating, 512 scans per step): 2 contexts of 256 28.35-28.38k / 27.91-28.11k scans/s, 4 of
+    # 128 27.98-28.08k / 27.70-27.72k, 3 27.84-28.00k, 6 27.85-28.01k, 8 27.66-27.68k, 1 27.50-27.55k -- with the
+    # r03-r05 per-launch savings (wave LM control, memo lists) two larger launches now overlap best
+    "C2": dict(batch=512, map_points=1_000_000, cols=4096, steps=40, warmup=2, streams=2),
     "C3": dict(batch=1, map_points=0, cols=4096, steps=20, warmup=3),
     "C4": dict(batch=1, map_points=5_000_000, cols=4096, steps=20, warmup=3),
     # C5: launches of 125 taken in turn by 3 contexts (r04 A/B, two rounds each: 1 context 3,836 pairs/s, 2 4,104,

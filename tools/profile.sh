@@ -13,7 +13,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/trace" -o run --output
 rc=$?; echo "trace $CFG rc=$rc"; case $rc in 0) ;; *) exit $rc;; esac
 fi
 case $CFG in
-  C2) PMC_ARGS="--steps 2 --warmup 1 --streams 1 --batch 128" ;;
+  C2) PMC_ARGS="--steps 2 --warmup 1 --streams 1 --batch 256" ;;   # one context of the default launch (2 x 256)
   C5) PMC_ARGS="--steps 1 --warmup 1 --streams 1 --pipeline 1" ;;
   *)  PMC_ARGS="--steps 6 --warmup 2" ;;
 esac
