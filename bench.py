@@ -58,7 +58,8 @@ DEFAULTS = {   # per configuration: batch (scans per launch), map points, column
     "C3": dict(batch=1, map_points=0, cols=4096, steps=20, warmup=3),
     "C4": dict(batch=1, map_points=5_000_000, cols=4096, steps=20, warmup=3),
     # C5: launches of 125 taken in turn by 3 contexts (r04 A/B, two rounds each: 1 context 3,836 pairs/s, 2 4,104,
-    # 3 4,114-4,169, 4 4,138-4,149, 8 4,083-4,108): a launch's LM-control phases overlap the next one's search
+    # 3 4,114-4,169, 4 4,138-4,149, 8 4,083-4,108): a launch's LM-control phases overlap the next one's search.
+    # r05 re-check: 2 4,264-4,270, 2 x 250 scans 4,287-4,300, 3 4,321-4,327, 4 4,341-4,356 -- 3 kept (4 within 0.5%)
     "C5": dict(batch=125, map_points=10_000_000, cols=2048, steps=2, warmup=1, pipeline=3),
 }
 
