@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cfloat>
+#include <cmath>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -2000,11 +2001,14 @@ lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int3
                              0, c->stream));
         HIPCHK(c, launch_fit_eval(ge, gs, bv, LMSF_SOLVER_CERES_LM, c->stream));
     }
-    std::vector<float4> rp(out ? nq : 0);
+    // the device records (k_match.hip store_record): points packed to 3 floats, the kind by position (edges first)
+    // and NaN in v[3] when unmatched (LMSF_REC44); else float4 points with the kind in w
+    const size_t qb = rec44_layout() ? 3 * sizeof(float) : sizeof(float4);
+    std::vector<unsigned char> rpb(out ? nq * qb : 0);
     std::vector<RecV> rv(out ? nq : 0);
     std::vector<double2> re(out ? nq : 0);
     if (nq && out) {
-        HIPCHK(c, hipMemcpyAsync(rp.data(), c->rec_p, nq * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(rpb.data(), c->rec_p, nq * qb, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(rv.data(), c->rec_v, nq * sizeof(RecV), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipMemcpyAsync(re.data(), c->rec_e, nq * sizeof(double2), hipMemcpyDeviceToHost, c->stream));
     }
@@ -2018,8 +2022,11 @@ lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int3
         if (i >= nq) return c->fail(LMSF_ERR_HIP, "search order out of range");
         lmsf_record& r = out[i];
         std::memset(&r, 0, sizeof r);
-        r.px = rp[j].x; r.py = rp[j].y; r.pz = rp[j].z;
-        std::memcpy(&r.kind, &rp[j].w, sizeof r.kind);
+        float q[4];
+        std::memcpy(q, rpb.data() + j * qb, qb);
+        r.px = q[0]; r.py = q[1]; r.pz = q[2];
+        if (qb == sizeof(float4)) std::memcpy(&r.kind, &q[3], sizeof r.kind);
+        else r.kind = std::isnan(rv[j].v[3]) ? 0 : (j < (size_t)c->slot0_ne ? LMSF_EDGE : LMSF_SURF);
         if (r.kind != 0) {
             r.v0[0] = rv[j].v[0]; r.v0[1] = rv[j].v[1]; r.v0[2] = rv[j].v[2]; r.v1[0] = rv[j].v[3];
         }

@@ -805,42 +805,51 @@ __device__ __forceinline__ void block_reduce_packet(double* P, double* out) {
     }
 }
 
-// Split record store / load (BatchView: rec_p, rec_v, rec_e).  Readers test the kind first, so the
-// value arrays of unmatched slots are never read (lmsf_match zero-fills them on the host).
+// Split record store / load (BatchView: rec_p, rec_v, rec_e).
+// LMSF_REC44 (default): the record's point is packed to 12 B in rec_p's memory (rec_p then holds
+// float3s) and the kind is the position's -- edges come before surfs both in slot order and in the fused path's
+// search order -- with NaN in v[3] marking an unmatched record (a matched one's D / b.x is finite): an LM
+// evaluation then reads 44 B per surf record and 60 B per edge record instead of 48 / 64.  0 (A/B builds): the
+// float4 point with the kind in w, whose unmatched records' value arrays are never read.
+#ifndef LMSF_REC44
+#define LMSF_REC44 1
+#endif
+struct RecQ { float x, y, z; };
+bool rec44_layout() { return LMSF_REC44 != 0; }
 __device__ __forceinline__ void store_record(const BatchView& bv, size_t slot, float4 p, int kind, const d3& v0, double v1x,
                                              double v1y, double v1z) {
-    bv.rec_p[slot] = make_float4(p.x, p.y, p.z, __int_as_float(kind));
+    if (LMSF_REC44) reinterpret_cast<RecQ*>(bv.rec_p)[slot] = RecQ{p.x, p.y, p.z};
+    else bv.rec_p[slot] = make_float4(p.x, p.y, p.z, __int_as_float(kind));
     if (kind != 0) {
         RecV v;
         v.v[0] = v0.x; v.v[1] = v0.y; v.v[2] = v0.z; v.v[3] = v1x;
         bv.rec_v[slot] = v;
         if (kind == LMSF_EDGE) bv.rec_e[slot] = make_double2(v1y, v1z);
+    } else if (LMSF_REC44) {
+        bv.rec_v[slot].v[3] = __longlong_as_double(0x7ff8000000000000ll);   // NaN: no correspondence
     }
+}
+
+// The record at slot (its position `local` in the slot's order, ne edges first): the point with the kind in w,
+// and the values in v (unspecified when the kind is 0).  Both loads are issued before either is used.
+__device__ __forceinline__ float4 load_record(const BatchView& bv, size_t slot, int local, int ne, RecV& v) {
+    v = bv.rec_v[slot];
+    if (LMSF_REC44) {
+        const RecQ q = reinterpret_cast<const RecQ*>(bv.rec_p)[slot];
+        const int kind = isnan(v.v[3]) ? 0 : local < ne ? LMSF_EDGE : LMSF_SURF;
+        return make_float4(q.x, q.y, q.z, __int_as_float(kind));
+    }
+    return bv.rec_p[slot];
 }
 
 // Residual + Jacobian of one stored record at pose Ps (edge_factor.hpp:33-61, surf_factor.hpp:32-56);
 // false when the slot holds no correspondence.
-__device__ __forceinline__ bool record_residual(const BatchView& bv, size_t slot, const Pose& Ps, double& res, double* J) {
-    const float4 p = bv.rec_p[slot];
+__device__ __forceinline__ bool record_residual(const BatchView& bv, size_t slot, int local, int ne, const Pose& Ps,
+                                                double& res, double* J) {
+    RecV v;
+    const float4 p = load_record(bv, slot, local, ne, v);
     const int kind = __float_as_int(p.w);
     if (kind == 0) return false;
-    const RecV v = bv.rec_v[slot];
-    const d3 pp = mk((double)p.x, (double)p.y, (double)p.z);
-    if (kind == LMSF_EDGE) {
-        const double2 e = bv.rec_e[slot];
-        res = edge_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), mk(v.v[3], e.x, e.y), J);
-    } else {
-        res = surf_residual(Ps, pp, mk(v.v[0], v.v[1], v.v[2]), v.v[3], J);
-    }
-    return true;
-}
-
-__device__ __forceinline__ bool record_residual_kind(const BatchView& bv, size_t slot, const Pose& Ps, double& res,
-                                                    double* J, int& kind) {
-    const float4 p = bv.rec_p[slot];
-    kind = __float_as_int(p.w);
-    if (kind == 0) return false;
-    const RecV v = bv.rec_v[slot];
     const d3 pp = mk((double)p.x, (double)p.y, (double)p.z);
     if (kind == LMSF_EDGE) {
         const double2 e = bv.rec_e[slot];
@@ -1302,8 +1311,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_MEMO_W
 #pragma unroll
             for (int j = 0; j < 7; ++j) mw[j] = bv.memo_nbr[memo_idx(b, j, i, F)];
         }
-        const float4 rp = bv.rec_p[pos];
-        const RecV rv = bv.rec_v[pos];
+        RecV rv;
+        const float4 rp = load_record(bv, pos, i, ne, rv);
         if (q >= 0 && q < nq && pw.w >= 0.f) {
             const size_t slot = pos;
             const float3 w = associate(Ps, p);
@@ -2401,26 +2410,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_EVAL_W
     for (int i = 0; i < kPacket; ++i) P[i] = 0.0;
     const size_t base = (size_t)b * bv.feat_stride;
     const int q0 = blockIdx.x * kEvalBlock + threadIdx.x;
-    auto slot_of = [&](int k) { return base + (q0 + k * 256 < nq ? q0 + k * 256 : 0); };
+    const int ne = bv.n_edge[b];
+    auto loc_of = [&](int k) { return q0 + k * 256 < nq ? q0 + k * 256 : 0; };
+    auto slot_of = [&](int k) { return base + loc_of(k); };
+    auto rec_of = [&](int k, RecV& v) { return load_record(bv, slot_of(k), loc_of(k), ne, v); };
 #if LMSF_EVAL_PIPE
     // Software pipeline, one record per step: rec_p / rec_v of record k + 2 and rec_e of record k + 1
     // (edges only; its kind arrived a step earlier) are in flight while record k is evaluated.
     const double2 ez = make_double2(0.0, 0.0);
-    float4 p0 = bv.rec_p[slot_of(0)], p1 = p0;
-    RecV v0 = bv.rec_v[slot_of(0)], v1 = v0;
-    if (kEvalPerThread > 1) {
-        p1 = bv.rec_p[slot_of(1)];
-        v1 = bv.rec_v[slot_of(1)];
-    }
+    RecV v0, v1;
+    float4 p0 = rec_of(0, v0), p1 = p0;
+    v1 = v0;
+    if (kEvalPerThread > 1) p1 = rec_of(1, v1);
     double2 e0 = __float_as_int(p0.w) == LMSF_EDGE ? bv.rec_e[slot_of(0)] : ez;
 #pragma unroll
     for (int k = 0; k < kEvalPerThread; ++k) {
         float4 pn = p1;
         RecV vn = v1;
-        if (k + 2 < kEvalPerThread) {
-            pn = bv.rec_p[slot_of(k + 2)];
-            vn = bv.rec_v[slot_of(k + 2)];
-        }
+        if (k + 2 < kEvalPerThread) pn = rec_of(k + 2, vn);
         double2 en = ez;
         if (k + 1 < kEvalPerThread && __float_as_int(p1.w) == LMSF_EDGE) en = bv.rec_e[slot_of(k + 1)];
         eval_record<LIN>(Ps, q0 + k * 256 < nq, p0, v0, e0, P);
@@ -2431,10 +2438,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMSF_EVAL_W
     float4 rp[kEvalPerThread];
     RecV rv[kEvalPerThread];
 #pragma unroll
-    for (int k = 0; k < kEvalPerThread; ++k) {
-        rp[k] = bv.rec_p[slot_of(k)];
-        rv[k] = bv.rec_v[slot_of(k)];
-    }
+    for (int k = 0; k < kEvalPerThread; ++k) rp[k] = rec_of(k, rv[k]);
 #pragma unroll
     for (int k = 0; k < kEvalPerThread; ++k) {
         const bool edge = __float_as_int(rp[k].w) == LMSF_EDGE;
@@ -2557,14 +2561,12 @@ __global__ __launch_bounds__(256) void lm_loop_kernel(BatchView bv, int outer, u
         for (int k = 0; k < kPacket; ++k) P[k] = 0.0;
         // lm_eval_kernel's form: the records' loads in flight together, then evaluated
         const int q0 = part * kLoopBlock + threadIdx.x;
-        auto rec_at = [&](int k) { return rbase + (q0 + k * 256 < nq ? q0 + k * 256 : 0); };
+        auto loc_at = [&](int k) { return q0 + k * 256 < nq ? q0 + k * 256 : 0; };
+        auto rec_at = [&](int k) { return rbase + loc_at(k); };
         float4 rp[kLoopPerThread];
         RecV rv[kLoopPerThread];
 #pragma unroll
-        for (int k = 0; k < kLoopPerThread; ++k) {
-            rp[k] = bv.rec_p[rec_at(k)];
-            rv[k] = bv.rec_v[rec_at(k)];
-        }
+        for (int k = 0; k < kLoopPerThread; ++k) rp[k] = load_record(bv, rec_at(k), loc_at(k), bv.n_edge[b], rv[k]);
 #pragma unroll
         for (int k = 0; k < kLoopPerThread; ++k) {
             const bool edge = __float_as_int(rp[k].w) == LMSF_EDGE;
@@ -2643,7 +2645,7 @@ __global__ __launch_bounds__(256) void eval_at_kernel(BatchView bv, const double
         const int q = blockIdx.x * kEvalBlock + k * 256 + threadIdx.x;
         if (q < nq) {
             double J[6], res;
-            if (record_residual(bv, (size_t)q, Ps, res, J)) huber_accumulate(P, res, J);
+            if (record_residual(bv, (size_t)q, q, bv.n_edge[0], Ps, res, J)) huber_accumulate(P, res, J);
         }
     }
     block_reduce_packet(P, bv.partials + (size_t)blockIdx.x * kPacket);
@@ -2661,7 +2663,8 @@ __global__ __launch_bounds__(256) void capture_kernel(BatchView bv, int b, int b
     const size_t pos = (size_t)b * bv.feat_stride + i;
     const int q = by_pos ? __float_as_int(bv.featp[pos].w) : i;
     if (q < 0 || q >= nq) return;
-    const float4 p = bv.rec_p[pos];
+    RecV v;
+    const float4 p = load_record(bv, pos, i, bv.n_edge[b], v);
     lmsf_record r;
     r.px = p.x;
     r.py = p.y;
@@ -2670,7 +2673,6 @@ __global__ __launch_bounds__(256) void capture_kernel(BatchView bv, int b, int b
     r.v0[0] = r.v0[1] = r.v0[2] = 0.0;
     r.v1[0] = r.v1[1] = r.v1[2] = 0.0;
     if (r.kind != 0) {
-        const RecV v = bv.rec_v[pos];
         r.v0[0] = v.v[0];
         r.v0[1] = v.v[1];
         r.v0[2] = v.v[2];

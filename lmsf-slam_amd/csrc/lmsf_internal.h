@@ -408,6 +408,7 @@ lmsf_status ctx_window_build(lmsf_ctx* c, int kind, size_t n_max, hipStream_t s)
 // The window's points in window order (the grid's unsorted source) after a finished commit.
 const float4* ctx_window_points(const lmsf_ctx* c, int kind);
 int grid_slices();
+bool rec44_layout();                    // records with 12-B points, kind by position (k_match.hip LMSF_REC44)
 int* ctx_fault_word(lmsf_ctx* c);       // the context's device fault word (d_error[17])
 int ctx_option(const lmsf_ctx* c, int option);
 lmsf_status ctx_slot0_features(lmsf_ctx* c, const float4** d_feat, int64_t* ne, int64_t* ns);
