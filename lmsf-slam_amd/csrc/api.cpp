@@ -2002,7 +2002,7 @@ lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int3
         HIPCHK(c, launch_fit_eval(ge, gs, bv, LMSF_SOLVER_CERES_LM, c->stream));
     }
     // the device records (k_match.hip store_record): points packed to 3 floats, the kind by position (edges first)
-    // and NaN in v[3] when unmatched (LMSF_REC44); else float4 points with the kind in w
+    // and the kRecNone NaN in v[3] when unmatched (LMSF_REC44); else float4 points with the kind in w
     const size_t qb = rec44_layout() ? 3 * sizeof(float) : sizeof(float4);
     std::vector<unsigned char> rpb(out ? nq * qb : 0);
     std::vector<RecV> rv(out ? nq : 0);
@@ -2026,7 +2026,11 @@ lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int3
         std::memcpy(q, rpb.data() + j * qb, qb);
         r.px = q[0]; r.py = q[1]; r.pz = q[2];
         if (qb == sizeof(float4)) std::memcpy(&r.kind, &q[3], sizeof r.kind);
-        else r.kind = std::isnan(rv[j].v[3]) ? 0 : (j < (size_t)c->slot0_ne ? LMSF_EDGE : LMSF_SURF);
+        else {
+            long long bits;
+            std::memcpy(&bits, &rv[j].v[3], sizeof bits);
+            r.kind = bits == 0x7ff8dead0000beefll ? 0 : (j < (size_t)c->slot0_ne ? LMSF_EDGE : LMSF_SURF);   // kRecNone
+        }
         if (r.kind != 0) {
             r.v0[0] = rv[j].v[0]; r.v0[1] = rv[j].v[1]; r.v0[2] = rv[j].v[2]; r.v1[0] = rv[j].v[3];
         }

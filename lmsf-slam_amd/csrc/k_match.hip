@@ -808,13 +808,15 @@ __device__ __forceinline__ void block_reduce_packet(double* P, double* out) {
 // Split record store / load (BatchView: rec_p, rec_v, rec_e).
 // LMSF_REC44 (default): the record's point is packed to 12 B in rec_p's memory (rec_p then holds
 // float3s) and the kind is the position's -- edges come before surfs both in slot order and in the fused path's
-// search order -- with NaN in v[3] marking an unmatched record (a matched one's D / b.x is finite): an LM
+// search order -- with a NaN of a payload arithmetic never produces (kRecNone) in v[3] marking an unmatched record (a
+// degenerate fit's own NaN stays a matched record, as the oracle evaluates it): an LM
 // evaluation then reads 44 B per surf record and 60 B per edge record instead of 48 / 64.  0 (A/B builds): the
 // float4 point with the kind in w, whose unmatched records' value arrays are never read.
 #ifndef LMSF_REC44
 #define LMSF_REC44 1
 #endif
 struct RecQ { float x, y, z; };
+constexpr long long kRecNone = 0x7ff8dead0000beefll;   // quiet NaN with a payload: "no correspondence"
 bool rec44_layout() { return LMSF_REC44 != 0; }
 __device__ __forceinline__ void store_record(const BatchView& bv, size_t slot, float4 p, int kind, const d3& v0, double v1x,
                                              double v1y, double v1z) {
@@ -826,7 +828,7 @@ __device__ __forceinline__ void store_record(const BatchView& bv, size_t slot, f
         bv.rec_v[slot] = v;
         if (kind == LMSF_EDGE) bv.rec_e[slot] = make_double2(v1y, v1z);
     } else if (LMSF_REC44) {
-        bv.rec_v[slot].v[3] = __longlong_as_double(0x7ff8000000000000ll);   // NaN: no correspondence
+        bv.rec_v[slot].v[3] = __longlong_as_double(kRecNone);
     }
 }
 
@@ -836,7 +838,7 @@ __device__ __forceinline__ float4 load_record(const BatchView& bv, size_t slot, 
     v = bv.rec_v[slot];
     if (LMSF_REC44) {
         const RecQ q = reinterpret_cast<const RecQ*>(bv.rec_p)[slot];
-        const int kind = isnan(v.v[3]) ? 0 : local < ne ? LMSF_EDGE : LMSF_SURF;
+        const int kind = __double_as_longlong(v.v[3]) == kRecNone ? 0 : local < ne ? LMSF_EDGE : LMSF_SURF;
         return make_float4(q.x, q.y, q.z, __int_as_float(kind));
     }
     return bv.rec_p[slot];
