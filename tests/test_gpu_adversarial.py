@@ -1,0 +1,153 @@
+"""GPU parity on SURVEY §7's hard parts: the adversarial fixture (tests/golden/adversarial.npz,
+tests/adversarial_fixture.py) merged into the synthetic background, run through every search path --
+
+* `knn8`:  the single-scan 8-lane `knn_kernel<8>` with the slot memo + `fit_eval` + the LM loop (3 x 70k slots),
+* `fused`: the batch path's fused `match_fit_kernel` with the query memo (`match_memo_kernel`, listed searches),
+* `dense`: the same on a dense background (the C5 regime): first-pass grid `dense_pass1` / `dense_pass2` /
+           `dense_fit2`, the dense memo from outer iteration 3 and its listed passes --
+
+over 5 outer iterations (`lmsf_batch_capture`): the records (kRecNone unmatched markers included; NaN fields
+compared by NaN-ness, adversarial_fixture.canon) and the 5-NN indices after every outer iteration equal the
+oracle's fresh match at the pose the GPU matched at, the per-iteration poses equal the oracle's, and the slot
+whose record is a degenerate NaN fit keeps its guess like the oracle.  REG/FeatureMatch/EdgeFeatureMatch.hpp:38-84,
+surfFeatureMatch.hpp:37-85, ceres_factor/edge_factor.hpp:41-57, ceres_edgeSurfFeatureRegistration.hpp:105-125."""
+import numpy as np
+import pytest
+
+import adversarial_fixture as af
+from conftest import pose_err
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from lmsf import _lib
+    _lib.load()
+    return _lib
+
+
+@pytest.fixture(scope="module")
+def adv(oracle_mod, small_workload):
+    from lmsf import synth
+    fx = af.load()
+    wl = small_workload
+    scan = wl.scans[0]
+    assert af.scan_sha(scan) == str(fx["scan_sha"]), "synthetic scan 0 changed: regenerate the fixture"
+    e, s, _, _ = oracle_mod.extract(scan)
+    sets, ts = af.sets_from_fixture(fx, e, s)
+    planted, first = af.planted_maps(sets)
+    truth = wl.truth[0]
+    sparse = {k: af.combined_map(planted, af.to_lidar(bg, truth), sets, k) for k, bg in ((1, wl.edge_map), (2, wl.surf_map))}
+    dw = synth.make_workload("C2", n_scans=1, map_points=1_000_000, radius=30.0, road_length=20.0)
+    assert np.array_equal(dw.truth[0], truth)
+    dense = {k: af.combined_map(planted, af.to_lidar(bg, truth), sets, k) for k, bg in ((1, dw.edge_map), (2, dw.surf_map))}
+    guesses = np.stack([af.pose(t) for t in ts])
+    return dict(fx=fx, scan=scan, e=e, s=s, sets=sets, maps={"sparse": sparse, "dense": dense}, guesses=guesses)
+
+
+def _slice_density(m):
+    p = m[:, :3].astype(np.float32)
+    c = np.stack([np.floor(p[:, 0] * 4), np.floor(p[:, 1]), np.floor(p[:, 2])], 1).astype(np.int64)
+    return len(p) / len(np.unique(c, axis=0))
+
+
+def _oracle(oracle_mod, maps, e, s):
+    reg = oracle_mod.Registration()
+    reg.set_map(1, maps[1])
+    reg.set_map(2, maps[2])
+    reg.set_scan(1, e)
+    reg.set_scan(2, s)
+    reg.set_fixed_schedule(True)
+    reg.set_max_iterations(5)
+    return reg
+
+
+def _same_records(grec, gnn, orec, onn, what):
+    assert len(grec) == len(orec), what
+    found = gnn >= 0
+    assert np.array_equal(gnn[found], onn[found]), (what, int((gnn[found] != onn[found]).sum()))
+    assert found[orec["kind"] > 0].all(), what                 # a record needs its 5 found within 1 m
+    a, b = af.canon(grec), af.canon(orec)
+    if a.tobytes() != b.tobytes():
+        diff = np.nonzero((a.view(np.uint8).reshape(len(a), -1) != b.view(np.uint8).reshape(len(b), -1)).any(1))[0]
+        raise AssertionError(f"{what}: {len(diff)} records differ, first {diff[:5]}: gpu {grec[diff[:2]]} "
+                             f"oracle {orec[diff[:2]]}")
+
+
+def _planted_rows(adv, slot):
+    """(record row, fixture row) of every planted query of `slot` (records: edges first, slot order)."""
+    ne = len(adv["e"])
+    return [((st[2] if st[1] == 1 else ne + st[2]), k) for k, st in enumerate(adv["sets"]) if st[0] == slot]
+
+
+PATHS = {"knn8": ("sparse", 70000), "fused": ("sparse", 1 << 19), "dense": ("dense", 1 << 19)}
+
+
+@pytest.mark.parametrize("path", list(PATHS))
+def test_adversarial_batch_parity(lib, oracle_mod, adv, path):
+    which, F = PATHS[path]
+    maps = adv["maps"][which]
+    assert (_slice_density(maps[2]) >= 8) == (which == "dense")
+    e, s, g = adv["e"], adv["s"], adv["guesses"]
+    ctx = lib.Context(max_batch=3, max_scan_points=70000, max_features=F, schedule=1, max_iterations=5)
+    ctx.set_map(lib.EDGE, maps[1])
+    ctx.set_map(lib.SURF, maps[2])
+    ctx.load_scans([adv["scan"]] * 3)
+    ctx.batch_capture([0, 1, 2])
+    ctx.kernel_stats_reset(timing=True)
+    poses, stats = ctx.batch_run(g)
+    ks = ctx.kernel_stats()
+    assert ks.fused_launches == (0 if path == "knn8" else 5), path
+    assert ks.reused_queries > 0                                 # the memo served queries beside the corner cases
+    reg = _oracle(oracle_mod, maps, e, s)
+    fx = adv["fx"]
+    for slot in range(3):
+        for it in range(5):
+            grec, gnn, gpose = ctx.batch_records(slot, it)
+            orec, onn = reg.match(gpose)
+            _same_records(grec, gnn, orec, onn, f"{path} slot {slot} outer iteration {it}")
+            if it == 0:   # the planted queries at the guess: the committed oracle vectors (planted points alone)
+                assert np.array_equal(gpose, g[slot])
+                for row, k in _planted_rows(adv, slot):
+                    assert af.canon(grec[row:row + 1]).tobytes() == af.canon(fx["rec"][k:k + 1]).tobytes(), \
+                        (path, str(fx["label"][k]))
+                    f = gnn[row] >= 0
+                    assert np.array_equal(gnn[row][f], fx["nn"][k][f]), (path, str(fx["label"][k]))
+        ox, otr, ost = reg.solve(g[slot])
+        gtr = ctx.batch_trace(slot)
+        assert gtr.shape == otr.shape == (5, 7), (path, slot)
+        for a, b in zip(gtr, otr):
+            dt, dr = pose_err(a, b)
+            assert dt <= POSE_TOL and dr <= POSE_TOL, (path, slot, dt, dr)
+        assert (stats[slot].edge_matches, stats[slot].surf_matches) == (ost.edge_matches, ost.surf_matches)
+    # the degenerate NaN record (slot 2) stops the LM at its guess, as in the oracle
+    assert np.array_equal(poses[2], g[2]) and all(np.array_equal(t, g[2]) for t in ctx.batch_trace(2))
+    if path != "knn8":    # memo on / off: the same poses bit for bit
+        ctx.batch_capture([])
+        ctx.set_option(lib.OPT_QUERY_MEMO, 0)
+        try:
+            poses0, _ = ctx.batch_run(g)
+        finally:
+            ctx.set_option(lib.OPT_QUERY_MEMO, 1)
+        assert np.array_equal(poses0, poses), path
+
+
+@pytest.mark.parametrize("path", list(PATHS))
+def test_adversarial_single_match(lib, oracle_mod, adv, path):
+    """lmsf_match (SetInputSource + one Match at a pose) on the device-extracted scan at each slot's guess:
+    8-lane teams (70k slots) or the one-lane search + fit (2^19 slots; the pruned walk on the dense map)."""
+    which, F = PATHS[path]
+    maps = adv["maps"][which]
+    ctx = lib.Context(max_batch=1, max_scan_points=70000, max_features=F)
+    ctx.set_map(lib.EDGE, maps[1])
+    ctx.set_map(lib.SURF, maps[2])
+    assert ctx.extract(adv["scan"]) == (len(adv["e"]), len(adv["s"]))
+    reg = _oracle(oracle_mod, maps, adv["e"], adv["s"])
+    for slot in range(3):
+        g = adv["guesses"][slot]
+        grec, gnn = ctx.match(g, len(adv["e"]) + len(adv["s"]))
+        orec, onn = reg.match(g)
+        _same_records(grec, gnn, orec, onn, f"{path} match slot {slot}")
