@@ -816,7 +816,6 @@ __device__ __forceinline__ void block_reduce_packet(double* P, double* out) {
 #define LMSF_REC44 1
 #endif
 struct RecQ { float x, y, z; };
-constexpr long long kRecNone = 0x7ff8dead0000beefll;   // quiet NaN with a payload: "no correspondence"
 bool rec44_layout() { return LMSF_REC44 != 0; }
 __device__ __forceinline__ void store_record(const BatchView& bv, size_t slot, float4 p, int kind, const d3& v0, double v1x,
                                              double v1y, double v1z) {
@@ -1178,9 +1177,12 @@ __global__ __launch_bounds__(512) void track_match_kernel(GridView ge, GridView 
     const int members = min(kTrackGroup, nblk - grp * kTrackGroup);
     unsigned* tk = ticket + (size_t)b * track_ticket_words(F) + grp;
     unsigned mine = 0;
-    if (lane == 0) mine = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // acq_rel ticket: this block's packet stores are released before its arrival, and the last
+    // arrival acquires every earlier member's packet before it sums them
+    if (lane == 0) mine = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     mine = __shfl(mine, 0, 64);
     if ((int)mine + 1 != members) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the whole wave, not only lane 0, reads after the acquire
     // the group's last block: its packets summed in block order into the group packet, the ticket re-armed
     if (lane < kPacket) {
         double t = 0.0;
@@ -2822,7 +2824,8 @@ hipError_t launch_match_fit(const GridView& edge, const GridView& surf, const Ba
             hipLaunchKernelGGL(match_memo_kernel, grid, dim3(256), 0, s, edge, surf, bv, gx, remap);
             // ~2048 blocks over all scans (8 per CU), each scan's list grid-strided by its blocks
             const int G = std::max(1, std::min(gx, std::max(4, 2048 / std::max(bv.B, 1))));
-            if (LMSF_MEMO_PASS1 && bv.wl2 && bv.p2count && bv.B <= 8192) {   // (B + 1) ints of LDS
+            if (LMSF_MEMO_PASS1 && bv.wl2 && bv.p2count && bv.B <= 8192 &&   // (B + 1) ints of LDS; wl2 holds b * F + pos as int
+                (size_t)bv.B * bv.feat_stride < ((size_t)1 << 31)) {
                 if ((e = hipMemsetAsync(bv.p2count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
                 // all scans' entries flattened over ~8 blocks per CU
                 hipLaunchKernelGGL(dense_pass1_listed_kernel, dim3(2048), dim3(256), (size_t)(bv.B + 1) * sizeof(int), s,

@@ -82,6 +82,10 @@ constexpr int kCounterShards = 64;   // candidate / query counters, 16 u64 (128 
 constexpr int kMemoWords = 7;        // memo words per search position: 5 neighbour indices, s6, order gap
 constexpr int kMemoStride = 8;       // memo_nbr allocation per search position (the AoS layout's 32-B record)
 constexpr int kCaptureIters = 10;    // outer iterations kept per captured slot (lmsf_batch_capture)
+// v[3] of an unmatched record (LMSF_REC44, k_match.hip store_record; decoded by lmsf_match / lmsf_batch_records):
+// a quiet NaN whose low payload bits no arithmetic on float map points produces (a float NaN widened to double has
+// its 29 low bits 0), so a degenerate fit's own NaN stays a matched record
+constexpr long long kRecNone = 0x7ff8dead0000beefll;
 
 // Tuning knobs measured by A/B builds.  The shipped library reads no environment:
 // ab_int returns the default unless the library was built with -DLMSF_AB (tools/build_variant.sh), which
@@ -410,6 +414,7 @@ const float4* ctx_window_points(const lmsf_ctx* c, int kind);
 int grid_slices();
 bool rec44_layout();                    // records with 12-B points, kind by position (k_match.hip LMSF_REC44)
 int* ctx_fault_word(lmsf_ctx* c);       // the context's device fault word (d_error[17])
+uint64_t ctx_fault_seq(const lmsf_ctx* c);   // device faults reported so far (LMSF_ERR_HIP "device look-back fault")
 int ctx_option(const lmsf_ctx* c, int option);
 lmsf_status ctx_slot0_features(lmsf_ctx* c, const float4** d_feat, int64_t* ne, int64_t* ns);
 

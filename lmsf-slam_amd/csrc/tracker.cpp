@@ -162,6 +162,7 @@ struct lmsf_tracker {
     bool quit = false, staging = false;
     lmsf_status job_rc[2] = {LMSF_OK, LMSF_OK};
     size_t fin_n[3] = {0, 0, 0};  // per kind: the window size a worker's grid finish found
+    uint64_t fault_seen = 0;      // ctx_fault_seq when the maps were last (re)built
 };
 
 namespace {
@@ -352,8 +353,31 @@ lmsf_status commit(lmsf_tracker* t) {
     return commit_finish(t);
 }
 
-// A deferred commit completed before anything that reads or rewrites the windows or the map.
-lmsf_status settle(lmsf_tracker* t) { return commit_finish(t); }
+// A deferred commit completed before anything that reads or rewrites the windows or the map.  A device fault
+// reported since the maps were built (a look-back / scatter check in a voxel filter or grid build: a faulted filter
+// leaves its window empty, k_voxel.hip) means a grid the context searches may be empty or partial, and that report
+// failed only one call: the priors and every window are rebuilt here from the tracker's own copies (the keyframe
+// slots are written by the transforms, never by a filter) before anything reads the map again.
+lmsf_status settle(lmsf_tracker* t) {
+    lmsf_status rc = commit_finish(t);
+    if (rc) return rc;
+    const uint64_t seq = ctx_fault_seq(t->ctx);
+    if (seq == t->fault_seen) return LMSF_OK;
+    t->fault_seen = seq;
+    bool any = false;
+    for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) {
+        Window& w = t->win[kind];
+        if (w.prior_n) {
+            rc = ctx_set_prior_device(t->ctx, kind, w.prior, w.prior_n);
+            if (rc) return rc;
+        }
+        if (w.count > 0 || w.prior_n) {
+            w.dirty = true;
+            any = true;
+        }
+    }
+    return any ? commit(t) : LMSF_OK;
+}
 
 // updateLocalMap (:205-232) with the current scan's features (context slot 0).
 lmsf_status update_local_map(lmsf_tracker* t, const Iso& T) {
@@ -488,6 +512,7 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
         }
     }
     t->origin = t->curr = t->prev = t->motion = t->last_kf = iso_identity();
+    t->fault_seen = ctx_fault_seq(ctx);
     ctx_add_settle(ctx, [](void* p) { return settle(static_cast<lmsf_tracker*>(p)); }, t);
     *out = t;
     return LMSF_OK;

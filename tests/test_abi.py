@@ -221,6 +221,16 @@ def test_shipped_library_reads_no_environment_knobs(lib):
         assert len(re.findall(r"\bgetenv\s*\(", text)) == (1 if f == "lmsf_internal.h" else 0), f
 
 
+def test_library_never_drains_the_device(lib):
+    """no call of the shipped library waits for the whole device (other contexts' and other
+    libraries' streams) -- context creation zeroes its words on its own stream, growths are stream-ordered
+    pool allocations; the library imports no hipDeviceSynchronize / hipMemset (null-stream) at all."""
+    und = {t.split("@")[0] for t in subprocess.run(["nm", "-D", "-u", lib.LIB_PATH], capture_output=True,
+                                                    text=True).stdout.split()}
+    assert "hipDeviceSynchronize" not in und and "hipMemset" not in und
+    assert "hipMemsetAsync" in und and "hipStreamSynchronize" in und
+
+
 def test_set_option_validates(lib):
     """lmsf_set_option: known options, 0 | 1 only (no device needed for the argument checks)."""
     L = lib.load()

@@ -73,6 +73,32 @@ def test_roofline_measured_and_model():
     assert r3["achieved"] is None and r3["frac"] is None and r3["basis"].startswith("untimed")
 
 
+def test_roofline_bound_from_committed_valu_pass():
+    """the line's `bound` is the roof the committed counters show -- VALU issue for the C2 / C5
+    batch searches (busy >= 0.75), latency for the single-scan C3 / C4 launches -- with the VALU pass beside the
+    HBM fraction; the 8(d) model is marked invalid once its strict all-query sum exceeds the HBM peak."""
+    bench = _bench_module()
+    ks = types.SimpleNamespace(launches=10, total_ms=10.0, queries=1_000_000, reused_queries=400_000,
+                               fused_launches=10, n27_sum=0)
+    for cfg, bound, kernel in (("C2", "valu", "match_fit_kernel"), ("C5", "valu", "dense_pass1_kernel"),
+                               ("C4", "latency", "knn_kernel"), ("C3", "latency", "knn_kernel")):
+        tj = bench.load_traffic(os.path.join(REPO, "profiles", f"traffic_{cfg}.json"), config=cfg)
+        r = bench.knn_roofline(ks, 50.0, tj, 0.02, "n")
+        assert r["bound"] == bound and r["valu"]["kernels"][0]["kernel"] == kernel, cfg
+        assert r["frac_basis"].startswith("HBM") and r["frac"] is not None
+        assert os.path.exists(os.path.join(REPO, r["valu"]["source"]))
+    assert bench.binding_roof(None, 0.7) == "hbm" and bench.binding_roof(None, None) == "hbm"
+    # slow launches: both 8(d) forms far below the peak, the model stands
+    slow = types.SimpleNamespace(**dict(vars(ks), total_ms=1000.0))
+    r = bench.knn_roofline(slow, 50.0, None, 0.02, "n")
+    assert r["model"]["valid"] is True and r["model"]["strict"]["exceeds_peak"] is False
+    # 99% memo reuse: 2.6 MB searched-only per 10-us launch fits, the strict 1M x 1,032 B = 103 MB (10 TB/s) does not
+    mid = types.SimpleNamespace(**dict(vars(ks), total_ms=0.1, reused_queries=990_000))
+    r = bench.knn_roofline(mid, 50.0, None, 10.0, "n")
+    assert r["model"]["exceeds_peak"] is False and r["model"]["strict"]["exceeds_peak"] is True
+    assert r["model"]["valid"] is False and r["model"]["frac"] is None and "strict" in r["model"]["invalid_reason"]
+
+
 def test_load_traffic_matches_workload(tmp_path):
     bench = _bench_module()
     p = tmp_path / "t.json"

@@ -944,8 +944,10 @@ def test_lookback_fault_flagged(lib, oracle_mod, sequence_workload, inject):
     """The device look-back checks (radix.h) catch what r04's null-stream memset race produced, injected into the
     window voxel filter's first radix pass (LMSF_OPT_FAULT_INJECT): a stale prefix that puts a tile's scatter outside
     the pairs (1) and a look-back word of another allocation (2).  Nothing is written or read outside the buffers,
-    the next Solve fails with LMSF_ERR_HIP "device look-back fault", the fault word is cleared by that report, and
-    the next commit (look-back words re-zeroed) tracks exactly as a tracker that never faulted."""
+    the next Solve fails with LMSF_ERR_HIP "device look-back fault", the fault word is cleared by that report, a
+    retried Solve with no re-commit finds the windows rebuilt from the keyframe slots (the faulted filter
+    had left its window empty) and tracks as a tracker that never faulted, and so does the next commit (look-back words
+    re-zeroed)."""
     from conftest import pose_matrix
     wl = sequence_workload
     e, s, _, _ = oracle_mod.extract(wl.scans[0], n_scans=wl.n_scans)
@@ -966,6 +968,12 @@ def test_lookback_fault_flagged(lib, oracle_mod, sequence_workload, inject):
     ref_ctx.extract(wl.scans[1])
     ref_pose, _ = ref_ctx.solve(guess)
 
+    ref2_ctx = _ctx(lib, n_scans=wl.n_scans)      # the faulted commit's window (2 keyframes), never faulted
+    ref2_t = tracker(ref2_ctx)
+    ref2_t.commit_map()
+    ref2_ctx.extract(wl.scans[1])
+    ref2_pose, _ = ref2_ctx.solve(guess)
+
     ctx = _ctx(lib, n_scans=wl.n_scans)
     t = tracker(ctx)
     ctx.set_option(lib.OPT_FAULT_INJECT, inject)
@@ -975,13 +983,53 @@ def test_lookback_fault_flagged(lib, oracle_mod, sequence_workload, inject):
     with pytest.raises(lib.LmsfError, match="device look-back fault") as ei:
         ctx.solve(guess)
     assert ei.value.code == lib.ERR_HIP
+    pose2, _ = ctx.solve(guess)                   # retried without a commit: the windows were rebuilt
+    assert np.array_equal(pose2, ref2_pose)
     t.add_keyframe(e, s, T0)                      # window = 3 copies, as the reference tracker's
     t.commit_map()
     ctx.extract(wl.scans[1])
     pose, _ = ctx.solve(guess)
     assert np.array_equal(pose, ref_pose)
-    for x in (t, ref_t):
+    for x in (t, ref_t, ref2_t):
         x.close()
+
+
+def test_context_created_beside_running_batch(lib, small_workload):
+    """a context is zeroed on its own stream at creation (no hipDeviceSynchronize), so creating one
+    while another context's batch runs neither waits for that batch nor disturbs it: the batch's poses equal a
+    batch run alone bit for bit, the new context registers, and (when the batch is long enough to tell) its creation
+    returned well before the batch finished."""
+    import time
+    wl = small_workload
+    n, B = len(wl.scans), 256
+    ctx = _ctx(lib, schedule=1, max_iterations=5, max_batch=B)
+    ctx.set_map(lib.EDGE, wl.edge_map)
+    ctx.set_map(lib.SURF, wl.surf_map)
+    ctx.load_scans([wl.scans[i % n] for i in range(B)])
+    guesses = np.stack([wl.guess[i % n] for i in range(B)])
+    ref, _ = ctx.batch_run(guesses)
+    t0 = time.perf_counter()
+    ctx.batch_run(guesses)
+    dur = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    _ctx(lib, max_batch=1).close()
+    idle = time.perf_counter() - t0
+    ctx.batch_launch(guesses)
+    t0 = time.perf_counter()
+    other = _ctx(lib, max_batch=1)
+    busy = time.perf_counter() - t0
+    poses, _ = ctx.batch_wait(B)
+    assert np.array_equal(poses, ref)
+    other.set_map(lib.EDGE, wl.edge_map)
+    other.set_map(lib.SURF, wl.surf_map)
+    other.extract(wl.scans[0])
+    other.set_schedule(lib.SCHEDULE_FIXED)
+    other.set_max_iterations(5)
+    x, st = other.solve(wl.guess[0])
+    dt, dr = pose_err(x, ref[0])              # the 8-lane single-scan path: same registration, other sum order
+    assert st.surf_matches > 0 and dt <= POSE_TOL and dr <= POSE_TOL
+    if dur > 4 * idle:
+        assert busy < idle + 0.5 * dur, (busy, idle, dur)
 
 
 def test_lm_loop_fault_recovery(lib, oracle_mod, small_workload):
