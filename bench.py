@@ -108,6 +108,10 @@ def parse(argv=None):
                     help="torch.distributed backend of the ranks (nccl = RCCL); gloo: CPU rehearsal of the launcher; "
                          "gloo-gpu: rehearsal of the N-rank GPU path on a box with fewer GPUs (rank r on GPU r mod "
                          "the device count, gloo collectives on the GPU tensors; the line is marked as a rehearsal)")
+    ap.add_argument("--dist-impl", default="auto", choices=("auto", "torch", "c"),
+                    help="the N-rank exchanges: c = the shipped C library (liblmsf_dist.so: its RCCL communicator on "
+                         "the nccl backend, its protocol over host collectives on gloo), torch = torch.distributed "
+                         "(lmsf/multi.py); auto = c (VERDICT r05 #5: the code a C / C++ caller links)")
     ap.add_argument("--dump", default=None, metavar="DIR",
                     help="C4: each rank writes its per-step poses and update types to DIR/c4_rank<r>.npz (the multi-rank "
                          "parity test replays them against oracle trackers); C2: its units' scans (seeds, truth), "
@@ -147,13 +151,19 @@ def launch_ranks(argv, n):
 
 
 class Dist:
-    def __init__(self, backend="nccl"):
+    def __init__(self, backend="nccl", impl="auto"):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.gpu = self.local                             # the device this rank registers on
         self.backend = backend
-        self.torch = self.dist = self.dev = None
+        self.impl = "c" if impl == "auto" else impl
+        self.torch = self.dist = self.dev = self.coll = None
+
+    def _collectives(self):
+        from lmsf import multi
+        self.coll = multi.make_collectives(self.impl, self.world, self.dev, self.gpu)
+        return self
 
     def init(self):
         """Bind the GPU and join the process group (after the host-side input generation)."""
@@ -167,13 +177,13 @@ class Dist:
             if self.world > 1:
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 dist.init_process_group("gloo")
-            return self
+            return self._collectives()
         if self.backend != "nccl":                        # CPU rehearsal (gloo)
             self.dev = torch.device("cpu")
             if self.world > 1:
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 dist.init_process_group(self.backend)
-            return self
+            return self._collectives()
         if self.world > 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             torch.cuda.set_device(self.local)
@@ -181,7 +191,7 @@ class Dist:
         else:
             torch.cuda.set_device(0)
         self.dev = torch.device("cuda", self.local)
-        return self
+        return self._collectives()
 
     def sync(self):
         if self.dev is not None and self.dev.type == "cuda":
@@ -192,6 +202,8 @@ class Dist:
             self.dist.barrier()
 
     def close(self):
+        if self.coll is not None:
+            self.coll.close()
         if self.world > 1 and self.dist is not None and self.dist.is_initialized():
             self.dist.destroy_process_group()
 
@@ -229,8 +241,7 @@ def timed(d, step, warmup, steps, ctxs, count_n27=True):
     d.barrier()
     elapsed = time.perf_counter() - t0
     if d.world > 1:
-        from lmsf import multi
-        elapsed = multi.max_over_ranks(elapsed, d.dev)
+        elapsed = d.coll.max(elapsed)
     if mean_n27 is None:
         stats = [c.kernel_stats() for c in ctxs]   # keep the timed launches' accounting
         mean_n27 = counted()
@@ -258,9 +269,8 @@ def shared_map(d, make):
     if d.world == 1:
         e, s = make()
         return torch.from_numpy(e).to(d.dev), torch.from_numpy(s).to(d.dev)
-    from lmsf import multi
     e, s = make() if d.rank == 0 else (None, None)
-    return multi.broadcast_map(e, s, d.dev)
+    return d.coll.broadcast_map(e, s)
 
 
 def kernel_name(ks, dense=False):
@@ -454,6 +464,8 @@ def apply_options(args, ctxs):
 def line(args, d, metric, value, unit, elapsed, scaling, workload, extra_cfg, roofline, cpu, **extra):
     if args.opt:
         extra_cfg = dict(extra_cfg, options=list(args.opt))
+    if d.world > 1:               # which code ran the exchanges
+        extra_cfg = dict(extra_cfg, dist_impl=d.coll.impl)
     if d.backend == "gloo-gpu":   # ranks share GPUs: a correctness rehearsal, not a scaling measurement
         extra_cfg = dict(extra_cfg, rehearsal=f"{d.world} ranks on {d.torch.cuda.device_count()} GPU(s), gloo")
     out = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": d.world, "steps": args.steps,
@@ -535,14 +547,14 @@ def make_scans(jobs, workers):
     return out
 
 
-def exchange_poses(cfg, poses, gathered, pairs, world, dev):
-    """The C2 / C5 collective section: the RCCL all-gather of every rank's 6-DoF poses."""
-    from lmsf import multi
-    if world <= 1:
+def exchange_poses(cfg, poses, gathered, pairs, coll):
+    """The C2 / C5 collective section: the RCCL all-gather of every rank's 6-DoF poses, through the
+    shipped C library (lmsf_group_allgather_poses) or torch.distributed (--dist-impl)."""
+    if coll.world <= 1:
         return poses
     if cfg == "C2":
-        return multi.gather_poses(poses, gathered, dev)
-    return multi.gather_pair_poses(poses, pairs, world, dev)
+        return coll.gather_poses(poses, gathered)
+    return coll.gather_pair_poses(poses, pairs)
 
 
 def run_launch_check(args, d):
@@ -553,15 +565,15 @@ def run_launch_check(args, d):
     n = 4
     poses = np.stack([np.full(7, 1000.0 * d.rank + i) for i in range(n)])
     gathered = torch.zeros((d.world, n, 7), dtype=torch.float64)
-    g = exchange_poses("C2", poses, gathered, 0, d.world, d.dev)
+    g = exchange_poses("C2", poses, gathered, 0, d.coll)
     g = g.numpy() if hasattr(g, "numpy") else np.asarray(g)[None]
     ok = all(np.array_equal(g[r], np.stack([np.full(7, 1000.0 * r + i) for i in range(n)])) for r in range(d.world))
     if d.world > 1:
-        from lmsf import multi
-        ok = multi.max_over_ranks(0.0 if ok else 1.0, d.dev) == 0.0
+        ok = d.coll.max(0.0 if ok else 1.0) == 0.0
     if d.rank == 0:
         print(json.dumps({"metric": "launch-check", "value": 0.0, "unit": "scans/s", "n_gpus": d.world,
-                          "steps": args.steps, "warmup": args.warmup, "backend": d.backend, "gather_ok": bool(ok)}))
+                          "steps": args.steps, "warmup": args.warmup, "backend": d.backend, "gather_ok": bool(ok),
+                          "dist_impl": d.coll.impl}))
     return 0 if ok else 4
 
 
@@ -631,7 +643,7 @@ def run_batch(args, d):
                 ctxs[ci].batch_launch(guesses[a:a + m])
                 enq += time.perf_counter() - t_enq
         t_c = time.perf_counter()
-        exchange_poses(cfg, poses, gathered, args.pairs, world, d.dev)
+        exchange_poses(cfg, poses, gathered, args.pairs, d.coll)
         coll_s.append(time.perf_counter() - t_c)
         enqueue_s.append(enq)
         return poses
@@ -676,7 +688,7 @@ def run_batch(args, d):
                 poses[a:a + m], st = cx.batch_wait(m)
                 matches[a:a + m] = [s.edge_matches + s.surf_matches for s in st]
         t_c = time.perf_counter()
-        exchange_poses(cfg, poses, gathered, args.pairs, world, d.dev)
+        exchange_poses(cfg, poses, gathered, args.pairs, d.coll)
         coll_s.append(time.perf_counter() - t_c)
         enqueue_s.append(enq)
         return poses
@@ -734,7 +746,7 @@ def run_batch(args, d):
         d.barrier()
         el2 = time.perf_counter() - t0
         if world > 1:
-            el2 = multi.max_over_ranks(el2, d.dev)
+            el2 = d.coll.max(el2)
         stream_in["on"] = False
         copy_ms = None
         if stream_in["shadow"] is not None:   # DMA time of the uploads alone: ms per step (link-bound if ~ step)
@@ -871,7 +883,7 @@ def run_streams(args, d):
     map_points = int(em_t.shape[0] + sm_t.shape[0])
     cap = max_pts + 64
     fbuf = torch.zeros((2 * cap, 4), dtype=torch.float32, device=d.dev)       # [edges | surfs] of own scan
-    xchg = multi.KeyframeExchange(cap, world, d.dev)
+    xchg = d.coll.keyframe_exchange(cap)
     state = {"i": 0, "kf": 0, "err": [], "xchg_s": 0.0, "poses": [], "types": []}
 
     phases = collections.defaultdict(float) if os.environ.get("LMSF_BENCH_PHASES") else None
@@ -1071,7 +1083,7 @@ def main(argv=None):
         args.workers = max(1, min(16, (host_cpu()[1] or 1)))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(argv, args.gpus)          # before anything touches the GPU
-    d = Dist(args.dist_backend)
+    d = Dist(args.dist_backend, args.dist_impl)
     if d.world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={d.world}", file=sys.stderr)
         return 3

@@ -248,3 +248,208 @@ class CGroup:
         d = self.C.c_double(v)
         rc = self.L.lmsf_group_max(self.h, self.C.byref(d))
         return rc, d.value
+
+
+class RcclGroup(CGroup):
+    """lmsf_group over RCCL (lmsf_group_create): the shipped C library's own communicator on this rank's GPU, the
+    code a C / C++ caller of include/lmsf/lmsf_dist.h links.  Rank 0's unique id reaches the other ranks over the
+    current torch.distributed group (one 128-byte broadcast before any collective of the library).  Cloud and
+    keyframe buffers are device memory of that GPU (torch tensors' data pointers); poses and the max are host."""
+
+    def __init__(self, device_index, lib_path=None):
+        import ctypes as C
+        import os
+        import torch
+        import torch.distributed as dist
+        from . import _lib
+        _lib._share_torch_hip_runtime()     # one HIP runtime and torch's RCCL (same SONAME) in the process
+        L = C.CDLL(lib_path or os.path.join(_lib.PKG_ROOT, "liblmsf_dist.so"))
+        P = C.c_void_p
+        L.lmsf_group_unique_id.argtypes = [P]
+        L.lmsf_group_create.argtypes = [C.c_int32, C.c_int32, C.c_int32, P, C.POINTER(P)]
+        L.lmsf_group_destroy.argtypes = [P]
+        L.lmsf_group_destroy.restype = None
+        L.lmsf_group_allgather_poses.argtypes = [P, P, C.c_int32, P]
+        L.lmsf_group_broadcast_cloud.argtypes = [P, C.c_int32, P, C.c_size_t, C.POINTER(C.c_size_t)]
+        L.lmsf_group_exchange_keyframes.argtypes = [P, P, C.c_int32, C.c_int64, C.c_int64, P, C.c_size_t, P, P,
+                                                    P, C.POINTER(C.c_int32)]
+        L.lmsf_group_max.argtypes = [P, C.POINTER(C.c_double)]
+        for f in ("lmsf_group_unique_id", "lmsf_group_create", "lmsf_group_allgather_poses", "lmsf_group_broadcast_cloud",
+                  "lmsf_group_exchange_keyframes", "lmsf_group_max"):
+            getattr(L, f).restype = C.c_int32
+        self.C, self.L = C, L
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.gather_bytes = []
+        uid = np.zeros(128, np.uint8)
+        if self.rank == 0 and L.lmsf_group_unique_id(uid.ctypes.data) != 0:
+            raise RuntimeError("lmsf_group_unique_id failed")
+        bdev = torch.device("cuda", device_index) if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.from_numpy(uid).to(bdev)
+        dist.broadcast(t, 0)
+        uid = np.ascontiguousarray(t.cpu().numpy())
+        h = P()
+        rc = L.lmsf_group_create(int(device_index), self.world, self.rank, uid.ctypes.data, C.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"lmsf_group_create: {rc}")
+        self.h = h
+
+
+class Collectives:
+    """The exchanges of the N-rank paths over torch.distributed (`impl` "torch": the functions
+    above).  world <= 1: no collective at all."""
+
+    impl = "torch"
+
+    def __init__(self, world, device=None):
+        self.world, self.device = world, device
+
+    def gather_poses(self, poses, gathered):
+        return gather_poses(poses, gathered, self.device)
+
+    def gather_pair_poses(self, poses, n_pairs):
+        return gather_pair_poses(poses, n_pairs, self.world, self.device)
+
+    def max(self, v):
+        return max_over_ranks(v, self.device)
+
+    def broadcast_map(self, edge, surf):
+        return broadcast_map(edge, surf, self.device)
+
+    def keyframe_exchange(self, cap):
+        return KeyframeExchange(cap, self.world, self.device)
+
+    def close(self):
+        pass
+
+
+class CCollectives(Collectives):
+    """The same exchanges through the shipped C library (liblmsf_dist.so, include/lmsf/lmsf_dist.h): its RCCL
+    communicator on the rank's GPU ("c-rccl", device buffers), or -- ranks on gloo (the CPU and gloo-gpu
+    rehearsals) -- its protocol over torch.distributed host collectives ("c-transport", host buffers).  Results
+    are returned in the torch implementation's forms, so the bench paths do not depend on which one runs."""
+
+    def __init__(self, world, device=None, device_index=None, rccl=True):
+        super().__init__(world, device)
+        self.rccl = rccl
+        self.impl = "c-rccl" if rccl else "c-transport"
+        self.g = RcclGroup(device_index) if rccl else CGroup()
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what}: lmsf status {rc}")
+
+    def gather_poses(self, poses, gathered):
+        rc, allp = self.g.allgather_poses(poses)
+        self._check(rc, "lmsf_group_allgather_poses")
+        import torch
+        gathered.copy_(torch.from_numpy(allp))
+        return gathered
+
+    def gather_pair_poses(self, poses, n_pairs):
+        per = -(-n_pairs // self.world)
+        buf = np.zeros((per, 7))
+        buf[:len(poses)] = poses
+        rc, allp = self.g.allgather_poses(buf)
+        self._check(rc, "lmsf_group_allgather_poses")
+        res = np.zeros((n_pairs, 7))
+        for r in range(self.world):
+            idx = pair_partition(n_pairs, r, self.world)
+            res[idx] = allp[r, :len(idx)]
+        return res
+
+    def max(self, v):
+        rc, m = self.g.max(float(v))
+        self._check(rc, "lmsf_group_max")
+        return m
+
+    def broadcast_map(self, edge, surf):
+        """Rank 0's maps into every rank's buffers with lmsf_group_broadcast_cloud (row counts first, by
+        lmsf_group_max, so every rank sizes its buffer)."""
+        import torch
+        out = []
+        for src in (edge, surf):
+            n = int(self.max(float(len(src)) if self.g.rank == 0 else 0.0))
+            on = self.device if self.rccl else torch.device("cpu")
+            if self.g.rank == 0:
+                t = torch.as_tensor(np.ascontiguousarray(src, dtype=np.float32)).to(on).contiguous()
+            else:
+                t = torch.empty((n, 4), dtype=torch.float32, device=on)
+            if self.rccl:
+                torch.cuda.synchronize(self.device)   # torch's upload / allocation done before the library's stream reads
+            self._check(self._bcast(t, n), "lmsf_group_broadcast_cloud")
+            out.append(t.to(self.device) if self.device is not None else t)
+        return out[0], out[1]
+
+    def _bcast(self, t, n):
+        C = self.g.C
+        nn = C.c_size_t(n)
+        if self.rccl:
+            return self.g.L.lmsf_group_broadcast_cloud(self.g.h, 0, C.c_void_p(t.data_ptr()) if n else None, n,
+                                                       C.byref(nn))
+        a = t.numpy()
+        rc, _ = self.g.broadcast_cloud(0, a if n else None, n)
+        return rc
+
+    def keyframe_exchange(self, cap):
+        return CKeyframeExchange(self, cap)
+
+    def close(self):
+        self.g.close()
+
+
+class CKeyframeExchange:
+    """KeyframeExchange's interface on lmsf_group_exchange_keyframes: (pose, update type, counts) of every rank,
+    then -- only when some rank keyframed -- the features at the keyframing ranks' largest counts; returns
+    [(rank, edge_view, surf_view, pose4x4)] for the keyframed streams in rank order."""
+
+    def __init__(self, coll, cap):
+        import torch
+        self.coll, self.cap, self.world = coll, cap, coll.world
+        on = coll.device if coll.rccl else torch.device("cpu")
+        self.gbuf = torch.zeros((coll.world * 2 * cap, 4), dtype=torch.float32, device=on)
+        self.hfeat = None if coll.rccl else torch.zeros((2 * cap, 4), dtype=torch.float32)
+        if coll.rccl:
+            torch.cuda.synchronize(coll.device)       # the zeroed buffer before the library's stream writes it
+        self.payload_bytes = 0
+        self.steps = 0
+
+    def exchange(self, pose, update_type, n_edge, n_surf, feat):
+        self.steps += 1
+        if self.world <= 1:
+            return [(0, None, None, np.asarray(pose, dtype=np.float64).reshape(4, 4))] if update_type else []
+        g = self.coll.g
+        C = g.C
+        P = np.ascontiguousarray(pose, dtype=np.float64).reshape(16)
+        info = np.zeros((self.world, 19))
+        rows = np.zeros(2, np.int64)
+        anyk = C.c_int32(0)
+        if self.coll.rccl:
+            fptr, gptr = C.c_void_p(feat.data_ptr()), C.c_void_p(self.gbuf.data_ptr())
+        else:
+            if update_type:
+                self.hfeat[:n_edge].copy_(feat[:n_edge])
+                self.hfeat[self.cap:self.cap + n_surf].copy_(feat[self.cap:self.cap + n_surf])
+            fptr, gptr = C.c_void_p(self.hfeat.data_ptr()), C.c_void_p(self.gbuf.data_ptr())
+        rc = g.L.lmsf_group_exchange_keyframes(g.h, P.ctypes.data, int(update_type), int(n_edge), int(n_surf), fptr,
+                                               self.cap, info.ctypes.data, gptr, rows.ctypes.data, C.byref(anyk))
+        if rc != 0:
+            raise ValueError(f"lmsf_group_exchange_keyframes: status {rc} (counts above the smallest rank capacity?)")
+        if not anyk.value:
+            return []
+        W, re_, rs = self.world, int(rows[0]), int(rows[1])
+        self.payload_bytes += W * (re_ + rs) * 16
+        out = []
+        for q in range(W):
+            if info[q, 16] > 0:
+                ne, ns = int(info[q, 17]), int(info[q, 18])
+                e0, s0 = q * re_, W * re_ + q * rs
+                out.append((q, self.gbuf[e0:e0 + ne], self.gbuf[s0:s0 + ns], info[q, :16].reshape(4, 4)))
+        return out
+
+
+def make_collectives(impl, world, device=None, device_index=None):
+    """impl "torch" | "c" (the shipped C library: RCCL on the nccl backend, its host transport on gloo)."""
+    if impl == "c" and world > 1:
+        import torch.distributed as dist
+        return CCollectives(world, device, device_index, rccl=dist.get_backend() == "nccl")
+    return Collectives(world, device)

@@ -19,12 +19,16 @@ def _run(args, env=None, timeout=180):
     return subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, timeout=timeout, env=e)
 
 
-def test_gpus2_launches_two_ranks_and_gathers():
-    r = _run(["--gpus", "2", "--launch-check", "--dist-backend", "gloo"])
+@pytest.mark.parametrize("impl,expect", [("auto", "c-transport"), ("torch", "torch")])
+def test_gpus2_launches_two_ranks_and_gathers(impl, expect):
+    """The launcher's ranks run the C2 pose all-gather and the max-over-ranks through the shipped C library
+    (--dist-impl auto = c: liblmsf_dist.so's protocol, here over gloo host collectives; RCCL on the nccl backend)
+    or torch.distributed; the line names which."""
+    r = _run(["--gpus", "2", "--launch-check", "--dist-backend", "gloo", "--dist-impl", impl])
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1                       # rank 0 only
-    assert lines[0]["n_gpus"] == 2 and lines[0]["gather_ok"] is True
+    assert lines[0]["n_gpus"] == 2 and lines[0]["gather_ok"] is True and lines[0]["dist_impl"] == expect
 
 
 def test_world_size_mismatch_fails():

@@ -3,8 +3,9 @@
 `bench.py --gpus 2 --dist-backend gloo-gpu --config C4` runs the C4 configuration (BASELINE configs[3]) as two
 ranks on the box's GPU: the launcher starts `torch.distributed.run` as a child process, rank 0 broadcasts the shared
 prior map, and every step all-gathers (pose, update type, feature counts) and -- when a stream keyframes -- the
-feature payloads, so both replicas append every stream's keyframes in rank order (lmsf/multi.py KeyframeExchange,
-the protocol liblmsf_dist.so runs over RCCL on a multi-GPU node).  Each rank dumps its per-step poses and update
+feature payloads, so both replicas append every stream's keyframes in rank order.  Since r06 the exchanges run in
+the shipped C library (liblmsf_dist.so, lmsf_group_exchange_keyframes / _broadcast_cloud / _allgather_poses / _max:
+bench.py --dist-impl c, the default) -- over RCCL on a multi-GPU node, over its host transport on gloo here.  Each rank dumps its per-step poses and update
 types (`--dump`); here two oracle trackers (oracle/tracker.py) consume the same two streams and the same keyframe
 stream, and each rank's tracking must equal its oracle replica's: update decisions exactly, poses <= 1e-4 m / rad
 (north_star) at every step.  RCCL itself only runs on the driver's 8-GPU node; gloo carries the collectives here.
@@ -37,6 +38,7 @@ def test_c4_two_rank_rehearsal_matches_oracle_trackers(oracle_mod, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(line) == 1 and '"n_gpus": 2' in line[0] and "rehearsal" in line[0]
+    assert '"dist_impl": "c-transport"' in line[0]      # the shipped C library's exchanges
     dumps = [np.load(tmp_path / f"c4_rank{q}.npz") for q in range(2)]
     n = steps + warmup
     assert all(len(dm["poses"]) == n for dm in dumps)
@@ -94,6 +96,7 @@ def test_c2_two_rank_rehearsal_matches_oracle(oracle_mod, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(line) == 1 and '"n_gpus": 2' in line[0] and "rehearsal" in line[0]
+    assert '"dist_impl": "c-transport"' in line[0]      # the shipped C library's exchanges
     dumps = [np.load(tmp_path / f"c2_rank{q}.npz") for q in range(2)]
     for q in range(2):
         assert dumps[q]["gathered"].shape == (2, batch, 7)

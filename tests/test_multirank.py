@@ -67,8 +67,9 @@ def test_gloo_world2_pose_allgather():
             np.testing.assert_array_equal(buf[r2], expect)
 
 
-def _worker_c45(rank, world, port, out_q):
-    """C5 pair partition + padded pose gather; C4 map broadcast + keyframe exchange."""
+def _worker_c45(rank, world, port, out_q, impl="torch"):
+    """C5 pair partition + padded pose gather; C4 map broadcast + keyframe exchange -- through torch.distributed or
+    the shipped C library's protocol (multi.CCollectives over gloo host collectives: bench.py --dist-impl c)."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lmsf-slam_amd"))
     import torch
@@ -77,17 +78,18 @@ def _worker_c45(rank, world, port, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    coll = multi.make_collectives(impl, world)
     # C5: 7 pairs, rank r owns i = r, r + 2, ...; pose of pair i = i
     mine = multi.pair_partition(7, rank, world)
-    allp = multi.gather_pair_poses(np.stack([np.full(7, float(i)) for i in mine]), 7, world)
+    allp = coll.gather_pair_poses(np.stack([np.full(7, float(i)) for i in mine]), 7)
     # C4: rank 0's map replicated
     rng = np.random.default_rng(0)
     e0 = rng.random((11, 4)).astype(np.float32)
     s0 = rng.random((23, 4)).astype(np.float32)
-    et, st = multi.broadcast_map(e0 if rank == 0 else None, s0 if rank == 0 else None)
+    et, st = coll.broadcast_map(e0 if rank == 0 else None, s0 if rank == 0 else None)
     # C4 keyframe exchange over 3 steps: step 0 both keyframe, step 1 none, step 2 only rank 1
     cap = 8
-    xchg = multi.KeyframeExchange(cap, world)
+    xchg = coll.keyframe_exchange(cap)
     log = []
     for step, kf in enumerate([(1, 1), (0, 0), (0, 2)]):
         typ = kf[rank]
@@ -106,16 +108,18 @@ def _worker_c45(rank, world, port, out_q):
         refused = False
     except ValueError:
         refused = True
-    out_q.put((rank, allp, et.numpy(), st.numpy(), log, payload, refused))
+    out_q.put((rank, allp, et.numpy(), st.numpy(), log, payload, refused, coll.impl, coll.max(float(rank + 3))))
+    coll.close()
     dist.destroy_process_group()
 
 
-def test_gloo_world2_pairs_map_and_keyframe_exchange():
+@pytest.mark.parametrize("impl", ["torch", "c"])
+def test_gloo_world2_pairs_map_and_keyframe_exchange(impl):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_c45, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_c45, args=(r, 2, port, q, impl)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
@@ -126,7 +130,8 @@ def test_gloo_world2_pairs_map_and_keyframe_exchange():
     e0 = rng.random((11, 4)).astype(np.float32)
     s0 = rng.random((23, 4)).astype(np.float32)
     assert all(r[6] for r in res)                 # both ranks refused the over-capacity exchange
-    for rank, allp, et, st, log, payload, _ in res:
+    assert all(r[7] == ("c-transport" if impl == "c" else "torch") and r[8] == 4.0 for r in res)
+    for rank, allp, et, st, log, payload, *_ in res:
         # features gathered at the keyframing ranks' largest counts: step 0 (3 + 3 rows), step 2 (3 + 5 rows),
         # 2 ranks x 16 B per row -- not 2 x 2 cap rows per exchange
         assert payload == 2 * (3 + 3) * 16 + 2 * (3 + 5) * 16
