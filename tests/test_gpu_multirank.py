@@ -122,3 +122,46 @@ def test_c2_two_rank_rehearsal_matches_oracle(oracle_mod, tmp_path):
             ox, _, _ = reg.solve(dm["guesses"][i])
             dt, dr = pose_err(dm["poses"][i], ox)
             assert dt <= POSE_TOL and dr <= POSE_TOL, (q, i, dt, dr)
+
+
+_RCCL_ONE_RANK = r"""
+import os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(sys.argv[1], "lmsf-slam_amd"))
+import torch
+import torch.distributed as dist
+from lmsf import multi
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[2])
+torch.cuda.set_device(0)
+dev = torch.device("cuda", 0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+coll = multi.CCollectives(1, dev, 0, rccl=True)
+poses = np.arange(35, dtype=np.float64).reshape(5, 7)
+g = coll.gather_poses(poses, torch.zeros((1, 5, 7), dtype=torch.float64, device=dev))
+assert np.array_equal(g.cpu().numpy()[0], poses)
+assert coll.max(3.5) == 3.5
+rng = np.random.default_rng(1)
+e0, s0 = rng.random((11, 4)).astype(np.float32), rng.random((23, 4)).astype(np.float32)
+e, s = coll.broadcast_map(e0, s0)
+assert e.device.type == "cuda" and e.cpu().numpy().tobytes() == e0.tobytes() and s.cpu().numpy().tobytes() == s0.tobytes()
+assert coll.impl == "c-rccl"
+coll.close()
+dist.destroy_process_group()
+print("rccl group ok")
+"""
+
+
+def test_rccl_group_in_python_one_rank():
+    """bench.py's --dist-impl c on the nccl backend: multi.CCollectives creates liblmsf_dist.so's own RCCL
+    communicator (rank 0's unique id broadcast over torch.distributed, lmsf_group_create on the rank's GPU) beside
+    torch's, with torch's librccl serving both (one RCCL and one HIP runtime in the process), and runs the pose
+    all-gather, the max and the device-memory map broadcast through it (one rank: the box has one GPU)."""
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-c", _RCCL_ONE_RANK, REPO, str(port)], capture_output=True, text=True,
+                       timeout=180, env=env)
+    assert r.returncode == 0 and "rccl group ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
