@@ -59,7 +59,7 @@ static void front_end(Algorithm::PointCloudProcessBase<P, P>& extract, Algorithm
 }
 
 int main(int argc, char** argv) {
-    if (argc != 16) {
+    if (argc != 15) {
         std::fprintf(stderr, "usage: %s scan edge_map surf_map out_dir qx qy qz qw tx ty tz voxel near far\n", argv[0]);
         return 2;
     }
