@@ -147,6 +147,14 @@ struct lmsf_ctx {
     int opt[LMSF_OPT_COUNT] = {1, 1, 1, 1, 1, 0, 1, 1, 0, 0, 0};   // lmsf_set_option (defaults: lmsf.h)
     bool loop_off_once = false;       // the re-run of a faulted LM loop (9-launch form, direct launches)
     uint64_t fault_seq = 0;           // device faults reported so far (report_fault): trackers rebuild their maps after one
+    // prior-grid pass of the next Solve's outer iteration 0 (ctx_presearch: enqueued before a tracker's window rebuild
+    // is joined, so it runs beside it); used by the next lmsf_solve at the same pose, dropped by any other call
+    double* pre_keys = nullptr;       // [B][F][6]
+    double* h_pre_pose = nullptr;     // pinned / device copies of its pose (never the caller's h_poses / d_poses, which
+    double* d_pre_pose = nullptr;     //   a map consumer settling inside its own call has just uploaded)
+    hipEvent_t ev_pre_pose = nullptr; // that upload done: h_pre_pose reusable
+    bool pre_valid = false, pre_use = false;
+    double pre_pose[7] = {0, 0, 0, 0, 0, 0, 0};
     int64_t loop_recoveries = 0;
     int last_launch_iters = 0;        // outer iterations of the last batch launch (its re-run after a loop fault)
     int last_launch_n = 0;            // and its slots
@@ -372,6 +380,7 @@ struct lmsf_ctx {
         v.n_pos = n_pos;
         v.pos_stride = R;
         v.p2count = reinterpret_cast<unsigned*>(d_error + 48);
+        v.pre_keys = pre_keys;
         return v;
     }
 
@@ -834,7 +843,10 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
             BatchView bvk = bv;
             bvk.stamp_start = st0;
             bvk.memo = !gn && o > 0 && !c->count27 && memo_on ? 1 : 0;
-            if (track) {   // search + fit + first evaluation in one launch (k_match.hip track_match_kernel)
+            if (o == 0 && c->pre_use && !track) {   // the window pass after ctx_presearch's prior pass
+                c->pre_use = false;
+                HIPCHK(c, launch_knn_split(2, ge2, gs2, ge, gs, bvk, s));
+            } else if (track) {   // search + fit + first evaluation in one launch (k_match.hip track_match_kernel)
                 HIPCHK(c, launch_track_match(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{},
                                              gs2.n ? gs : GridView{}, bvk, c->d_ticket, s));
             } else {
@@ -1121,6 +1133,10 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     hipFree(c->cap_rec);
     hipFree(c->cap_nn);
     hipFree(c->cap_pose);
+    hipFree(c->pre_keys);
+    hipFree(c->d_pre_pose);
+    if (c->h_pre_pose) hipHostFree(c->h_pre_pose);
+    if (c->ev_pre_pose) hipEventDestroy(c->ev_pre_pose);
     c->voxel.release();
     hipFree(c->vox_in);
     hipFree(c->vox_out);
@@ -1273,6 +1289,7 @@ lmsf_status lmsf_set_map(lmsf_ctx* c, int32_t kind, const float* xyzi, size_t n)
     HIPCHK(c, hipSetDevice(c->cfg.device));
     lmsf_status rs = ctx_settle(c);
     if (rs) return rs;
+    c->pre_valid = false;
     return build_map(c, kind, xyzi, n);
 }
 
@@ -1280,6 +1297,7 @@ lmsf_status lmsf_set_scan(lmsf_ctx* c, int32_t kind, const float* xyzi, size_t n
     if (!c || (kind != LMSF_EDGE && kind != LMSF_SURF)) return LMSF_ERR_ARG;
     if (n && !xyzi) return c->fail(LMSF_ERR_ARG, "null scan pointer");
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    c->pre_valid = false;
     if (c->features_on_device) {  // keep the other kind extracted on the device
         const int other = kind == LMSF_EDGE ? LMSF_SURF : LMSF_EDGE;
         const int64_t no = other == LMSF_EDGE ? c->slot0_ne : c->slot0_ns;
@@ -1332,9 +1350,13 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     rc = sync_slot0_features(c);
     if (rc) return rc;
     const int iters = outer_iterations_for_solve(c);
+    // the prior pass enqueued by ctx_presearch at this exact pose serves outer iteration 0 (nothing invalidated it)
+    c->pre_use = c->pre_valid && std::memcmp(pose, c->pre_pose, sizeof c->pre_pose) == 0;
+    c->pre_valid = false;
     std::memcpy(c->h_poses, pose, 7 * sizeof(double));
     HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
     rc = enqueue_solve(c, 1, iters);
+    c->pre_use = false;
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -1490,6 +1512,7 @@ lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf
     if (!c || (n && !xyzi)) return LMSF_ERR_ARG;
     if (n > (size_t)c->R) return c->fail(LMSF_ERR_CAPACITY, "%zu points exceed max_scan_points %d", n, c->R);
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    c->pre_valid = false;
     if (c->pre_pending && xyzi == c->pre_src && n == c->pre_n) {   // prefetched: adopt its outputs
         c->pre_pending = false;
         lmsf_status rj = join_prefetch(c);
@@ -1502,10 +1525,13 @@ lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf
         // whatever slot 0 held before, so it is refused (LMSF_ERR_STATE) until the next scan load
         c->raw_loaded = 0;
         c->raw_adopted = true;
-        lmsf_status rc = ctx_settle(c);
-        if (rc) return rc;
+        // a deferred tracker commit completes here (its settle hook first enqueues the next Solve's prior-grid pass,
+        // ctx_presearch, to run beside the window rebuild); the caller's next prefetch then follows the rebuild
+        // (r06 A/B: settling only at the Solve put the prefetch beside the rebuild -- C3 1.2k vs 1.66k frames/s)
         HIPCHK(c, hipEventSynchronize(c->ev_pre));
-        return adopt_counts(c, c->h_pre + 4, counts);
+        lmsf_status rc = adopt_counts(c, c->h_pre + 4, counts);
+        if (rc) return rc;
+        return ctx_settle(c);
     }
     {
         lmsf_status rd = drop_prefetch(c);
@@ -1764,6 +1790,7 @@ lmsf_status lmsf_batch_load_scans(lmsf_ctx* c, const float* xyzi, const int64_t*
 
 // sync = false: the caller synchronises the stream before h_counts is written again
 static lmsf_status load_scans(lmsf_ctx* c, const float* xyzi, const int64_t* counts, int32_t n, bool sync) {
+    c->pre_valid = false;
     if (!c || !counts || n < 1 || n > c->B) return LMSF_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->cfg.device));
     if (c->raw_pending) {   // a streamed upload not yet consumed: this copy replaces it, after it
@@ -1939,6 +1966,7 @@ lmsf_status lmsf_set_option(lmsf_ctx* c, int32_t option, int32_t value) {
     if (!c || option < 0 || option >= LMSF_OPT_COUNT) return LMSF_ERR_ARG;
     if (value != 0 && value != 1 && !(option == LMSF_OPT_FAULT_INJECT && value == 2)) return LMSF_ERR_ARG;
     c->opt[option] = value;
+    c->pre_valid = false;
     return LMSF_OK;
 }
 
@@ -2194,7 +2222,57 @@ void ctx_remove_settle(lmsf_ctx* c, void* arg) {
 }
 
 // SetInputSource from device-resident points (local-map rebuild without a host round trip).
+// The prior-grid pass of the next single-scan Solve's outer iteration 0 at pose x (r06): state init and
+// knn_kernel SPLIT 1 on the context stream, enqueued by a tracker before it joins its keyframe window rebuild (settle),
+// so the walk over the static prior -- most of iteration 0's search on C4's 5M-point prior -- runs beside the rebuild
+// and only the window pass waits for it.  Best effort: LMSF_OK without enqueueing anything when the next Solve would
+// not take the 8-lane memo search on a prior + window map (then that Solve searches as before).
+lmsf_status ctx_presearch(lmsf_ctx* c, const double x[7]) {
+    if (c->pre_valid && std::memcmp(x, c->pre_pose, sizeof c->pre_pose) == 0) return LMSF_OK;   // already enqueued
+    c->pre_valid = false;
+    if (c->cfg.solver != LMSF_SOLVER_CERES_LM || !c->opt[LMSF_OPT_QUERY_MEMO] || c->count27 || c->opt[LMSF_OPT_GRAPH] ||
+        c->prior[LMSF_EDGE].n == 0 || c->prior[LMSF_SURF].n == 0 || knn_team_for((size_t)c->F) != 8 ||
+        fit_per_thread_default() != 1 || track_fused_enabled() || !c->cap_slots.empty() || c->loop_off_once)
+        return LMSF_OK;
+    static const bool on = ab_int("LMSF_PRESEARCH", 1) != 0;   // A/B builds: 0 = the one-launch TWO walk
+    // extracted features only (on the device, or enqueued ahead on the context stream); host features upload later
+    if (!on || !c->features_on_device || c->scan_dirty) return LMSF_OK;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    lmsf_status rc = LMSF_OK;
+    for (int k : {LMSF_EDGE, LMSF_SURF}) {
+        rc = resolve_lim1(c, c->prior[k]);
+        if (rc) return rc;
+    }
+    if (!c->pre_keys) {
+        HIPCHK(c, dalloc(&c->pre_keys, (size_t)c->B * c->F * 6));
+        HIPCHK(c, dalloc(&c->d_pre_pose, 7));
+        HIPCHK(c, hipHostMalloc((void**)&c->h_pre_pose, 7 * sizeof(double), hipHostMallocDefault));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_pre_pose, hipEventDisableTiming));
+    } else {
+        HIPCHK(c, hipEventSynchronize(c->ev_pre_pose));   // the previous presearch's upload has left h_pre_pose
+    }
+    hipStream_t s = c->stream;
+    std::memcpy(c->h_pre_pose, x, 7 * sizeof(double));
+    HIPCHK(c, hipMemcpyAsync(c->d_pre_pose, c->h_pre_pose, 7 * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipEventRecord(c->ev_pre_pose, s));
+    BatchView bv = c->bview(1);
+    HIPCHK(c, launch_state_init(bv, c->d_pre_pose, s));
+    bv.n27 = nullptr;    // the window pass counts the queries
+    bv.memo = 0;
+    const bool t = c->timing && c->ev_used + 2 <= 2 * kEventPairs;   // the pass's span joins the search time
+    bv.stamp_start = t ? c->d_stamps + c->ev_used : nullptr;
+    HIPCHK(c, launch_knn_split(1, c->prior[LMSF_EDGE].view(), c->prior[LMSF_SURF].view(), GridView{}, GridView{}, bv, s));
+    if (t) {
+        HIPCHK(c, launch_stamp(c->d_stamps + c->ev_used + 1, s));
+        c->ev_used += 2;
+    }
+    std::memcpy(c->pre_pose, x, sizeof c->pre_pose);
+    c->pre_valid = true;
+    return LMSF_OK;
+}
+
 lmsf_status ctx_set_prior_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n) {
+    c->pre_valid = false;
     if (n == 0) {
         c->prior[kind].n = 0;
     } else {

@@ -559,10 +559,17 @@ __device__ __forceinline__ void key_cswap(double& a, double& b) {
 // recomputed from nnp (points + indices) and sorted: when the order is unchanged nnp already holds this
 // search's answer and the walk is skipped (fit_eval refits from it); otherwise the walk covers only
 // min(1 m, s6 + d) (match_memo_kernel's argument, DESIGN.md "Query memo").
-template <int T, bool TWO, bool PRUNE, bool MEMO = false>
+// SPLIT (r06, tracking contexts with a prior map: outer iteration 0 of a Solve in two launches): 1 walks the prior
+// grid only (ge / gs) and leaves the team's NK kept keys in bv.pre_keys -- enqueued before the keyframe window's
+// rebuild is joined, so it runs beside that rebuild; 2 walks the window grid only (ge2 / gs2), its lane 0 seeded
+// with those keys and every row trimmed to the prior's NK-th key (+ 1e-5, the memo bound's margin: every window
+// point that can enter the kept NK lies within it), then the usual merge, neighbours and memo anchor.  Keys carry
+// global indices, so the result is the one-launch TWO walk's over [prior | window] exactly.
+template <int T, bool TWO, bool PRUNE, bool MEMO = false, int SPLIT = 0>
 __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, GridView ge2, GridView gs2, BatchView bv,
                                                   int skip_converged, int gx, int remap) {
     constexpr int NK = MEMO ? 6 : 5;
+    static_assert(SPLIT == 0 || (!TWO && !PRUNE && T > 1), "split walks: plain team walks of one grid each");
     __shared__ unsigned long long blk_n27;
     __shared__ unsigned int blk_q, blk_r;
 #ifdef LMSF_STEP_PROFILE   // diagnostics build: block start / walk start / walk end / end stamps of sampled blocks
@@ -591,7 +598,7 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
     if (active) {
         const bool is_edge = q < ne;
         const GridView g = pick_grid(is_edge, ge, gs);
-        const GridView g2 = pick_grid(is_edge, ge2, gs2);
+        const GridView g2 = pick_grid(is_edge, ge2, gs2);   // SPLIT 2: the walked window, g the prior
         const Pose P = load_pose(bv.st[b].x);
         const size_t slot = (size_t)b * bv.feat_stride + q;
         const float4 p = bv.feat[slot];
@@ -646,7 +653,22 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
             double k[NK];   // ascending kept keys
 #pragma unroll
             for (int j = 0; j < NK; ++j) k[j] = sentinel;
-            knn_walk<T, TWO, PRUNE, kKnnUnroll, NK>(g, g2, w, lane, bv.count27, k, c27, lim);
+            if constexpr (SPLIT == 2) {   // the prior's kept keys, in lane 0's list
+                const double* pk = bv.pre_keys + slot * 6;
+                double pre[NK];
+#pragma unroll
+                for (int j = 0; j < NK; ++j) pre[j] = pk[j];
+                lim = fminf(kFullLim, key_d2(pre[NK - 1]) + 1e-5f);
+                if (lane == 0) {
+#pragma unroll
+                    for (int j = 0; j < NK; ++j) k[j] = pre[j];
+                }
+                knn_walk<T, false, false, kKnnUnroll, NK>(g2, g2, w, lane, 0, k, c27, lim);
+            } else if constexpr (SPLIT == 1) {
+                knn_walk<T, false, false, kKnnUnroll, NK>(g, g, w, lane, 0, k, c27, lim);
+            } else {
+                knn_walk<T, TWO, PRUNE, kKnnUnroll, NK>(g, g2, w, lane, bv.count27, k, c27, lim);
+            }
 #ifdef LMSF_STEP_PROFILE
             if (threadIdx.x == 0) kt[2] = wall_clock64();
 #endif
@@ -664,24 +686,29 @@ __global__ __launch_bounds__(256) void knn_kernel(GridView ge, GridView gs, Grid
                     k[NK - 1] = sentinel;
                 }
             }
+            if constexpr (SPLIT == 1) {   // the prior pass leaves its keys; the window pass writes the results
+#pragma unroll
+                for (int i = 0; i < NK; ++i)
+                    if (i % T == lane) bv.pre_keys[slot * 6 + i] = res[i];
+            }
             // every rank written (lane i % T writes rank i; teams smaller than 5 write several): the
             // neighbour point (from the caller-order copy, w = its map index), so the fit reads 80
             // contiguous bytes.  Indices below g.n belong to g, the rest to g2 (its points carry P + j).
 #pragma unroll
             for (int i = 0; i < 5; ++i) {
-                if (i % T == lane) {
+                if (SPLIT != 1 && i % T == lane) {
                     float4 o = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
                     const uint64_t kb = key_bits(res[i]);
                     if (kb < kSentinel) {
                         const uint32_t idx = (uint32_t)kb;
-                        const bool second = TWO && idx >= (uint32_t)g.n;
+                        const bool second = (TWO || SPLIT == 2) && idx >= (uint32_t)g.n;
                         const float4 m = second ? g2.orig[idx - (uint32_t)g.n] : g.orig[idx];
                         o = make_float4(m.x, m.y, m.z, __int_as_float((int)idx));
                     }
                     nn_out[i] = o;
                 }
             }
-            if (MEMO && lane == 0) {   // the anchor of this full search
+            if (MEMO && SPLIT != 1 && lane == 0) {   // the anchor of this full search
                 float gap = -1.f;
                 if (key_bits(res[4]) < kSentinel) {
                     const double s6 = sqrt((double)fminf(key_d2(res[NK - 1]), 1.0f));
@@ -2040,6 +2067,13 @@ constexpr int kRing5[25][2] = {{0, 0},  {0, -1}, {-1, 0}, {1, 0},  {0, 1},  {-1,
 #ifndef LMSF_P2_INNER
 #define LMSF_P2_INNER 0
 #endif
+// LMSF_P2_BALL2 (A/B): a pass-2 query whose bound exceeds one first-pass cell first walks the 0.5 m
+// ball in pass 1's form (its 3 x 3 rows' offsets up front, windows at 0.25 m^2): when its NK-th key lies within the
+// ball it is complete there; else the 25 rows continue bounded by min(bound, NK-th key), the inner rows minus the
+// slices the ball scanned (outer iteration 0's displaced queries, which walked up to 1 m at lane utilisation 0.23).
+#ifndef LMSF_P2_BALL2
+#define LMSF_P2_BALL2 0
+#endif
 
 // The bounded pruned walk of pass 2 (and of the dense memo pass's listed searches): the NK nearest of w within
 // `bound` (a squared distance at least the true NK-th key's), on the first-pass grid's 5 x 5 rows when the kind has
@@ -2091,6 +2125,44 @@ __device__ __forceinline__ const GridView dense_bounded_walk(const GridView& ge,
     if (fine && bound * kDenseCull <= 0.25f) {   // within one 0.5 m first-pass cell
         dense_ball_walk(g, w, bound * kDenseCull, k);
         return g;
+    }
+    if constexpr (LMSF_P2_BALL2) {
+        if (fine) {
+            constexpr float kBall = 0.25f;   // (1 / sy)^2: the 3 x 3 rows hold every point within 0.5 m
+            dense_ball_walk(g, w, kBall * kDenseCull, k);
+            if (key_d2(k[NK - 1]) <= kBall) return g;   // every point nearer than the NK-th was in the scanned ball
+            const DenseQuery<2> dq(g, w);
+            const int xa = dq.xa, xb = dq.xb;
+#pragma unroll 1
+            for (int i = 0; i < 25; ++i) {
+                const float d4 = fminf(bound, key_d2(k[NK - 1]));
+                const uint32_t* row;
+                int sa, sb;
+                const int dyo = kRing5[i][0], dzo = kRing5[i][1];
+                const float lb = dq.lb(dyo, dzo);
+                if (lb > d4) continue;
+                if (!dq.row(g, dyo, dzo, row)) continue;
+                dense_window(g, w, d4 * kDenseCull, lb, xa, xb, sa, sb);
+                if (sa > sb) continue;
+                int ta = 1, tb = 0;   // the ball's slices of an inner row (scanned unless pruned: then lb > d4 here too)
+                if (i < 9 && !(lb > kBall * kDenseCull)) dense_window(g, w, kBall * kDenseCull, lb, xa, xb, ta, tb);
+                if (ta > tb) {
+                    const uint32_t a = row[sa];
+                    dense_run(k, g.pts, a, row[sb + 1] - a, w);
+                } else {
+                    const int l1 = min(sb, ta - 1), r0 = max(sa, tb + 1);
+                    if (sa <= l1) {
+                        const uint32_t a = row[sa];
+                        dense_run(k, g.pts, a, row[l1 + 1] - a, w);
+                    }
+                    if (r0 <= sb) {
+                        const uint32_t a = row[r0];
+                        dense_run(k, g.pts, a, row[sb + 1] - a, w);
+                    }
+                }
+            }
+            return g;
+        }
     }
     // LMSF_P2_INNER (A/B): a larger ball's inner 3 x 3 rows also resolved up front (windows at the bound), then the
     // outer ring's 16 rows one by one (their yz-gap bound is >= 0.25 m^2: pruned once the kept keys are nearer)
@@ -2754,6 +2826,23 @@ static void launch_knn_t(int T, bool prune, bool memo, dim3 grid, const GridView
         default: LMSF_KNN(16, false); break;
     }
 #undef LMSF_KNN
+}
+
+// Outer iteration 0 of a single-scan Solve on a prior + window map in two launches (knn_kernel SPLIT): pass 1
+// (prior grids edge / surf) or pass 2 (windows edge2 / surf2, seeded from pass 1's keys).  8-lane teams, memo form.
+hipError_t launch_knn_split(int pass, const GridView& edge, const GridView& surf, const GridView& edge2,
+                            const GridView& surf2, const BatchView& bv, hipStream_t s) {
+    const int T = 8, remap = knn_remap();
+    const int span = (bv.qslot && bv.pos_stride > bv.feat_stride) ? bv.pos_stride : bv.feat_stride;
+    const int gx = (span + (256 / T) - 1) / (256 / T);
+    const dim3 grid(gx * bv.B);
+    if (pass == 1)
+        hipLaunchKernelGGL((knn_kernel<8, false, false, true, 1>), grid, dim3(256), 0, s, edge, surf, edge2, surf2, bv, 0,
+                           gx, remap);
+    else
+        hipLaunchKernelGGL((knn_kernel<8, false, false, true, 2>), grid, dim3(256), 0, s, edge, surf, edge2, surf2, bv, 0,
+                           gx, remap);
+    return hipGetLastError();
 }
 
 hipError_t launch_knn(const GridView& edge, const GridView& surf, const GridView& edge2, const GridView& surf2,

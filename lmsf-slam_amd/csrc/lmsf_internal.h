@@ -194,6 +194,7 @@ struct BatchView {
     float* wlim2;
     int anchor;              // dense maps: this outer iteration keeps 6 exact keys and leaves the memo anchors
                              //   (the one before the dense memo pass starts, k_match.hip dense_memo_search_kernel)
+    double* pre_keys;        // [B][feat_stride][6] kept keys of the prior-grid pass (knn_kernel SPLIT 1 -> 2)
 };
 
 __device__ __forceinline__ void stamp_if(unsigned long long* at, bool first_block) {
@@ -230,6 +231,8 @@ hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, void*
 // edge2 / surf2: optional second grid per kind (n = 0: none), searched as if concatenated after
 // the first (its points carry global indices).
 // memo: keep the per-slot anchors (and, with bv.memo, reuse unchanged 5-NN sets) -- 8-lane sparse launches.
+hipError_t launch_knn_split(int pass, const GridView& edge, const GridView& surf, const GridView& edge2,
+                            const GridView& surf2, const BatchView& bv, hipStream_t s);
 hipError_t launch_knn(const GridView& edge, const GridView& surf, const GridView& edge2, const GridView& surf2,
                       const BatchView& bv, int skip_converged, hipStream_t s, bool memo = false);
 hipError_t launch_fit_eval(const GridView& edge, const GridView& surf, const BatchView& bv, int solver,
@@ -392,6 +395,8 @@ void ctx_remove_settle(lmsf_ctx* c, void* arg);
 // map of a kind = [prior | window]: the prior grid is built once (static), the window grid at every
 // keyframe commit with indices offset by the prior size; n == 0 clears that part.
 lmsf_status ctx_set_prior_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n);
+// the prior-grid pass of the next Solve's outer iteration 0 at pose x, beside a window rebuild (best effort)
+lmsf_status ctx_presearch(lmsf_ctx* c, const double x[7]);
 lmsf_status ctx_set_window_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n);
 // host wait of the single-scan paths (spins on hipStreamQuery unless LMSF_SPIN_SYNC=0)
 hipError_t stream_wait(hipStream_t s);

@@ -353,6 +353,18 @@ lmsf_status commit(lmsf_tracker* t) {
     return commit_finish(t);
 }
 
+// The prior-grid pass of the next Solve at the motion-model prediction (:125-129; deltaT given: that delta) -- the pose
+// register_pose will pass -- enqueued on the context stream before a pending keyframe rebuild is joined into it, so
+// it runs beside the rebuild (api.cpp ctx_presearch).
+lmsf_status presearch_prediction(lmsf_tracker* t, const double* deltaT) {
+    const Iso pred = (deltaT == nullptr || is_identity16(deltaT)) ? iso_mul(t->prev, t->motion)
+                                                                  : iso_mul(t->prev, iso_from16(deltaT));
+    double x[7];
+    quat_from_R(pred.R, x);
+    x[4] = pred.t[0]; x[5] = pred.t[1]; x[6] = pred.t[2];
+    return ctx_presearch(t->ctx, x);
+}
+
 // A deferred commit completed before anything that reads or rewrites the windows or the map.  A device fault
 // reported since the maps were built (a look-back / scatter check in a voxel filter or grid build: a faulted filter
 // leaves its window empty, k_voxel.hip) means a grid the context searches may be empty or partial, and that report
@@ -513,7 +525,16 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
     }
     t->origin = t->curr = t->prev = t->motion = t->last_kf = iso_identity();
     t->fault_seen = ctx_fault_seq(ctx);
-    ctx_add_settle(ctx, [](void* p) { return settle(static_cast<lmsf_tracker*>(p)); }, t);
+    // the context's map consumers (and extractions) settle a deferred commit; with one pending, the next Solve's
+    // prior-grid pass is enqueued first so it overlaps the rebuild
+    ctx_add_settle(ctx, [](void* p) {
+        lmsf_tracker* tk = static_cast<lmsf_tracker*>(p);
+        if (tk->init && (tk->pending || tk->staging)) {
+            lmsf_status rp = presearch_prediction(tk, nullptr);
+            if (rp) return rp;
+        }
+        return settle(tk);
+    }, t);
     *out = t;
     return LMSF_OK;
 }
@@ -524,6 +545,10 @@ namespace {
 
 // Solve (:107-160) on the features currently in the context's slot 0.
 lmsf_status solve_current(lmsf_tracker* t, double timestamp, double deltaT[16], lmsf_tracker_result* res) {
+    if (t->init) {   // the prediction below, as register_pose will pass it (a no-op when the settle hook enqueued it)
+        lmsf_status rp = presearch_prediction(t, deltaT);
+        if (rp) return rp;
+    }
     lmsf_status rc0 = settle(t);   // a deferred keyframe commit completes before the search reads the map
     if (rc0) return rc0;
     lmsf_tracker_result r;

@@ -849,7 +849,8 @@ def test_tracker_shared_map_streams(lib, oracle_mod, sequence_workload):
                 rec_a, nn_a = ctxs[0].match(wl.truth[streams[0][step]], nq[0])
                 gts[0].local_map(lib.EDGE)
                 rec_b, nn_b = ctxs[0].match(wl.truth[streams[0][step]], nq[0])
-                assert rec_a.tobytes() == rec_b.tobytes() and (nn_a == nn_b).all()
+                same = rec_a.tobytes() == rec_b.tobytes() and bool((nn_a == nn_b).all())   # no byte-string diff
+                assert same, "a match right after commit_map differs from one after the completed commit"
             assert len(gts[s].local_map(lib.SURF)) == len(ots[s].local_map(2))
     # replica 0 added stream 0's keyframes from its context and stream 1's from tensors, replica 1 the reverse
     np.testing.assert_allclose(gts[0].local_map(lib.SURF), gts[1].local_map(lib.SURF), atol=0)
