@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
@@ -160,6 +162,7 @@ struct lmsf_tracker {
     std::condition_variable cv;
     int job[2] = {0, 0};          // kind to stage on aux[i] (0: none)
     bool quit = false, staging = false;
+    std::atomic<unsigned> posted{0};   // jobs posted (spinning workers watch it before they sleep on cv)
     lmsf_status job_rc[2] = {LMSF_OK, LMSF_OK};
     size_t fin_n[3] = {0, 0, 0};  // per kind: the window size a worker's grid finish found
     uint64_t fault_seen = 0;      // ctx_fault_seq when the maps were last (re)built
@@ -295,10 +298,25 @@ lmsf_status finish_kind(lmsf_tracker* t, int kind, hipStream_t ks) {
 // Worker i: stage, then finish, of the kind posted for aux[i].  Both halves run here, so the two kinds' host
 // waits and grid builds proceed side by side (r03 trace: one thread finishing both put the edge grid's
 // ~5 launches behind the surf grid's) and the caller's thread only joins.
+// Before sleeping on the condition variable a worker polls for LMSF_WORKER_SPIN_US (A/B knob; commits come once per
+// scan, ~0.7 ms apart on C4): a condition-variable wake-up put ~25 us between commit_map and the rebuild's first
+// kernel (r06 C4 trace).
+#ifndef LMSF_WORKER_SPIN_US
+#define LMSF_WORKER_SPIN_US 0
+#endif
 void worker_main(lmsf_tracker* t, int i, int device) {
     hipSetDevice(device);
+    static const int spin_us = ab_int("LMSF_WORKER_SPIN_US", LMSF_WORKER_SPIN_US);
     std::unique_lock<std::mutex> lk(t->mu);
     for (;;) {
+        if (spin_us > 0 && t->job[i] == 0 && !t->quit) {
+            const unsigned seen = t->posted.load(std::memory_order_acquire);
+            lk.unlock();
+            const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
+            while (t->posted.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() < until) {
+            }
+            lk.lock();
+        }
         t->cv.wait(lk, [t, i] { return t->job[i] != 0 || t->quit; });
         if (t->quit) return;
         const int kind = t->job[i];
@@ -483,8 +501,13 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
     t->cfg = *cfg;
     t->cap = ctx_feature_capacity(ctx);
     if (hipSetDevice(ctx_device(ctx)) != hipSuccess) { delete t; return LMSF_ERR_HIP; }
-    if (hipStreamCreateWithFlags(&t->aux[0], hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&t->aux[1], hipStreamNonBlocking) != hipSuccess ||
+    // LMSF_AUX_PRIORITY (A/B): the window rebuild's streams at the device's highest priority, so the rebuild -- the
+    // critical path between two Solves -- takes CUs ahead of the next Solve's prior-grid pass running beside it
+    static const bool aux_hi = ab_int("LMSF_AUX_PRIORITY", 0) != 0;
+    int prio_lo = 0, prio_hi = 0;
+    if (aux_hi) (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (hipStreamCreateWithPriority(&t->aux[0], hipStreamNonBlocking, aux_hi ? prio_hi : 0) != hipSuccess ||
+        hipStreamCreateWithPriority(&t->aux[1], hipStreamNonBlocking, aux_hi ? prio_hi : 0) != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_join[LMSF_EDGE], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_join[LMSF_SURF], hipEventDisableTiming) != hipSuccess) {
@@ -736,6 +759,7 @@ lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t) {
         for (int kind : {LMSF_SURF, LMSF_EDGE})
             if (t->ks[kind]) t->job[t->ks[kind] == t->aux[0] ? 0 : 1] = kind;
         t->staging = true;
+        t->posted.fetch_add(1u, std::memory_order_release);
     }
     t->cv.notify_all();
     t->pending = true;
