@@ -153,6 +153,10 @@ struct lmsf_ctx {
     double* h_pre_pose = nullptr;     // pinned / device copies of its pose (never the caller's h_poses / d_poses, which
     double* d_pre_pose = nullptr;     //   a map consumer settling inside its own call has just uploaded)
     hipEvent_t ev_pre_pose = nullptr; // that upload done: h_pre_pose reusable
+    uint64_t st_epoch = 0;            // launches that (re)wrote the slots' SolveState (state init, solves, matches)
+    uint64_t pre_st_epoch = ~0ull;    // st_epoch right after ctx_presearch's state init
+    bool skip_state_init = false;     // this enqueue_solve: st already initialised at its pose by ctx_presearch
+    bool pose_skipped = false;        // d_poses not uploaded for that solve (a loop recovery uploads it first)
     bool pre_valid = false, pre_use = false;
     double pre_pose[7] = {0, 0, 0, 0, 0, 0, 0};
     int64_t loop_recoveries = 0;
@@ -939,8 +943,9 @@ lmsf_status enqueue_solve(lmsf_ctx* c, int nb, int iters, bool recover = false) 
     }
     hipStream_t s = c->stream;
     // direct launches: graphs off, timing events not yet collected, or a record capture
+    ++c->st_epoch;
     if (!c->opt[LMSF_OPT_GRAPH] || c->ev_used != 0 || !c->cap_slots.empty() || c->loop_off_once) {
-        HIPCHK(c, launch_state_init(c->bview(nb), c->d_poses, s));
+        if (!c->skip_state_init) HIPCHK(c, launch_state_init(c->bview(nb), c->d_poses, s));
         return enqueue_register(c, nb, iters);
     }
     std::vector<unsigned char> key = solve_key(c, nb, iters);
@@ -1012,6 +1017,10 @@ lmsf_status collect_timing(lmsf_ctx* c, bool lazy = false) {
 // unfaulted run gives (tests/test_gpu_parity.py::test_lm_loop_fault_recovery).
 lmsf_status loop_recover(lmsf_ctx* c, int nb, int iters) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->pose_skipped) {   // the solve ran from ctx_presearch's state: its pose, for the re-run's state init
+        HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        c->pose_skipped = false;
+    }
     HIPCHK(c, hipMemsetAsync(c->d_lmsync, 0, 2 * (size_t)c->B * sizeof(unsigned), c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_error + 16, 0, sizeof(int), c->stream));
     c->h_pack[3] = 0;
@@ -1353,9 +1362,16 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     // the prior pass enqueued by ctx_presearch at this exact pose serves outer iteration 0 (nothing invalidated it)
     c->pre_use = c->pre_valid && std::memcmp(pose, c->pre_pose, sizeof c->pre_pose) == 0;
     c->pre_valid = false;
+    // ... and when nothing rewrote the SolveState since, its state init too (the pose upload and the init kernel
+    // sat between the window join and the first search)
+    const bool keep_state = c->pre_use && c->st_epoch == c->pre_st_epoch && !c->opt[LMSF_OPT_GRAPH];
     std::memcpy(c->h_poses, pose, 7 * sizeof(double));
-    HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (!keep_state)
+        HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    c->pose_skipped = keep_state;
+    c->skip_state_init = keep_state;
     rc = enqueue_solve(c, 1, iters);
+    c->skip_state_init = false;
     c->pre_use = false;
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
@@ -2031,6 +2047,7 @@ lmsf_status lmsf_match(lmsf_ctx* c, const double pose[7], lmsf_record* out, int3
     if (rc) return rc;
     BatchView bv = c->bview(1);
     bv.write_nn = 1;
+    ++c->st_epoch;
     HIPCHK(c, launch_state_init(bv, c->d_poses, c->stream));
     const GridView ge = c->map[LMSF_EDGE].view(), gs = c->map[LMSF_SURF].view();
     const GridView ge2 = c->prior[LMSF_EDGE].view(), gs2 = c->prior[LMSF_SURF].view();
@@ -2257,6 +2274,7 @@ lmsf_status ctx_presearch(lmsf_ctx* c, const double x[7]) {
     HIPCHK(c, hipEventRecord(c->ev_pre_pose, s));
     BatchView bv = c->bview(1);
     HIPCHK(c, launch_state_init(bv, c->d_pre_pose, s));
+    c->pre_st_epoch = ++c->st_epoch;
     bv.n27 = nullptr;    // the window pass counts the queries
     bv.memo = 0;
     const bool t = c->timing && c->ev_used + 2 <= 2 * kEventPairs;   // the pass's span joins the search time
