@@ -9,7 +9,9 @@ Usage: python tools/traffic.py <fetch_dir> <write_dir> <hitmiss_dir> <kernels> <
        kernels: comma-separated name substrings of the kernels one "launch" (one outer iteration of the
        neighbour search) runs, the first naming the kernel that runs exactly once per launch (e.g.
        match_fit_kernel,match_memo_kernel: the memo pass runs in outer iterations > 0 only); per-launch
-       figures = sums over all their dispatches / dispatches of the first.
+       figures = sums over all their dispatches / dispatches of the first ("a|b": either name counts: the tracking
+       search's outer iterations are knn_kernel<..., 0> launches, iteration 0 a prior pass <..., 1> beside the
+       keyframe rebuild and a window pass <..., 2>, counted once).
        (k=v: the workload the passes ran -- config, batch, streams, map_points, unique_scans, profile)
 """
 import csv
@@ -30,7 +32,7 @@ def per_launch(d, kernels, counter):
         if r["Counter_Name"] != counter or not any(k in r["Kernel_Name"] for k in kernels):
             continue
         tot += float(r["Counter_Value"])
-        if kernels[0] in r["Kernel_Name"]:
+        if any(k in r["Kernel_Name"] for k in kernels[0].split("|")):
             first.add(r["Dispatch_Id"])
     return tot, len(first)
 
@@ -43,7 +45,7 @@ def mean_duration_us(d, kernels):
     for r in csv.DictReader(open(files[0])):
         if any(k in r["Kernel_Name"] for k in kernels):
             tot += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-            n += kernels[0] in r["Kernel_Name"]
+            n += any(k in r["Kernel_Name"] for k in kernels[0].split("|"))
     return tot / n / 1e3 if n else None
 
 
