@@ -266,7 +266,9 @@ __global__ __launch_bounds__(256) void gn_accum_kernel(BatchView bv) {
     const int q = blockIdx.x * fb + chunk * 256 + threadIdx.x;
     const size_t slot = (size_t)b * bv.feat_stride + q;
     const double* gr = bv.gn_rows + slot * 4;
-    const bool valid = q < nq && gr[3] >= 0.0;
+    // unmatched rows carry -1; a matched row's residual is >= 0 or NaN (a degenerate fit, e.g. the edge of two equal
+    // points: 0/0), and a NaN row is a match that poisons the normal equations, as in the reference (kind != 0)
+    const bool valid = q < nq && !(gr[3] < 0.0);
     const bool is_edge = q < ne;
     __syncthreads();   // previous chunk's wcnt / base reads are complete
     const unsigned long long me = __ballot(valid && is_edge), ms = __ballot(valid && !is_edge);

@@ -108,6 +108,9 @@ struct lmsfo_map {
     void knn(const float* q, int k, Key* best) const {
         for (int i = 0; i < k; ++i) best[i] = {std::numeric_limits<float>::infinity(), INT32_MAX};
         if (nodes.empty()) return;
+        // a non-finite query (a NaN pose) has a NaN or +inf distance to every point: no key is ever less than
+        // the empty slots, and box_d2's NaN would walk the whole tree to find that out
+        if (!(std::isfinite(q[0]) && std::isfinite(q[1]) && std::isfinite(q[2]))) return;
         int stack[128];
         int sp = 0;
         stack[sp++] = 0;

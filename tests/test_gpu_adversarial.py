@@ -151,3 +151,48 @@ def test_adversarial_single_match(lib, oracle_mod, adv, path):
         grec, gnn = ctx.match(g, len(adv["e"]) + len(adv["s"]))
         orec, onn = reg.match(g)
         _same_records(grec, gnn, orec, onn, f"{path} match slot {slot}")
+
+
+def _same_traces(gtr, otr, what):
+    """Per-outer-iteration poses: equal NaN pattern (a NaN record poisons Gauss-Newton's normal equations on both
+    sides), else within POSE_TOL."""
+    assert gtr.shape == otr.shape, (what, gtr.shape, otr.shape)
+    for a, b in zip(gtr, otr):
+        assert np.array_equal(np.isnan(a), np.isnan(b)), (what, a, b)
+        if not np.isnan(a).any():
+            dt, dr = pose_err(a, b)
+            assert dt <= POSE_TOL and dr <= POSE_TOL, (what, dt, dr)
+
+
+def test_adversarial_gauss_newton(lib, oracle_mod, adv):
+    """The GN variant (REG/edgeSurfFeatureRegistration.hpp:218-330: JᵀJ by colPivHouseholderQr, the degeneracy
+    projection from SelfAdjointEigenSolver<MatrixXd> at iteration 0, its convergence test) on the adversarial scene,
+    every slot to convergence: the records after every outer iteration equal the oracle's at the GPU's pose, and the
+    per-iteration poses (NaN pattern included: the origin slot's NaN record) equal the oracle GN's."""
+    maps = adv["maps"]["sparse"]
+    e, s, g = adv["e"], adv["s"], adv["guesses"]
+    ctx = lib.Context(max_batch=3, max_scan_points=70000, max_features=70000, solver=lib.SOLVER_GN, schedule=1,
+                      max_iterations=5)
+    ctx.set_map(lib.EDGE, maps[1])
+    ctx.set_map(lib.SURF, maps[2])
+    ctx.load_scans([adv["scan"]] * 3)
+    ctx.batch_capture([0, 1, 2])
+    poses, stats = ctx.batch_run(g)
+    reg = oracle_mod.Registration(oracle_mod.SOLVER_GN)
+    reg.set_map(1, maps[1])
+    reg.set_map(2, maps[2])
+    reg.set_scan(1, e)
+    reg.set_scan(2, s)
+    reg.set_fixed_schedule(True)
+    reg.set_max_iterations(5)
+    for slot in range(3):
+        gtr = ctx.batch_trace(slot)
+        for it in range(len(gtr)):
+            grec, gnn, gpose = ctx.batch_records(slot, it)
+            if np.isnan(gpose).any():
+                break
+            orec, onn = reg.match(gpose)
+            _same_records(grec, gnn, orec, onn, f"GN slot {slot} outer iteration {it}")
+        ox, otr, ost = reg.solve(g[slot])
+        _same_traces(gtr, otr, f"GN slot {slot}")
+        assert stats[slot].termination == ost.termination, (slot, stats[slot].termination, ost.termination)
