@@ -128,6 +128,27 @@ hipError_t lmsf::stream_wait(hipStream_t s) {
     }
 }
 
+#ifdef LMSF_HOST_PROFILE
+namespace {
+struct HProfTable {
+    std::atomic<long long> ns[32] = {}, calls[32] = {};
+    std::atomic<const char*> name[32] = {};
+    ~HProfTable() {
+        for (int i = 0; i < 32; ++i)
+            if (calls[i])
+                fprintf(stderr, "hprof %2d %-28s calls %8lld  mean %9.2f us  total %10.3f ms\n", i, name[i].load(),
+                        calls[i].load(), 1e-3 * ns[i] / calls[i], 1e-6 * ns[i]);
+    }
+};
+HProfTable g_hprof;
+}  // namespace
+void lmsf::hprof_add(int id, const char* name, long long ns) {
+    g_hprof.name[id] = name;
+    g_hprof.ns[id] += ns;
+    g_hprof.calls[id] += 1;
+}
+#endif
+
 namespace {
 
 template <typename T>
@@ -1350,6 +1371,7 @@ lmsf_status lmsf_set_extract_params(lmsf_ctx* c, const lmsf_extract_params* p) {
 
 lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     if (!c || !pose) return LMSF_ERR_ARG;
+    HPROF(5, "solve total");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     lmsf_status rc = ctx_settle(c);   // a deferred tracker commit may be the first map of this context
     if (rc) return rc;
@@ -1370,13 +1392,19 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
         HIPCHK(c, hipMemcpyAsync(c->d_poses, c->h_poses, 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
     c->pose_skipped = keep_state;
     c->skip_state_init = keep_state;
-    rc = enqueue_solve(c, 1, iters);
+    {
+        HPROF(11, "solve enqueue");
+        rc = enqueue_solve(c, 1, iters);
+    }
     c->skip_state_init = false;
     c->pre_use = false;
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, stream_wait(c->stream));
+    {
+        HPROF(6, "solve wait");
+        HIPCHK(c, stream_wait(c->stream));
+    }
     if (c->h_pack[4]) return report_fault(c, c->h_pack[4]);
     rc = collect_timing(c, true);
     if (rc) return rc;
@@ -1436,6 +1464,7 @@ static lmsf_status drop_prefetch(lmsf_ctx* c) {
 
 // The extraction of (pre_src, pre_n) on pre_stream into the alternate output set (worker thread).
 static lmsf_status enqueue_prefetch(lmsf_ctx* c) {
+    HPROF(4, "prefetch worker enqueue");
     hipStream_t s = c->pre_stream;
     const size_t n = c->pre_n;
     HIPCHK(c, hipStreamWaitEvent(s, c->ev_pre_after, 0));
@@ -1480,6 +1509,7 @@ static void prefetch_worker(lmsf_ctx* c) {
 
 lmsf_status lmsf_prefetch_features(lmsf_ctx* c, const float* xyzi, size_t n) {
     if (!c || (n && !xyzi)) return LMSF_ERR_ARG;
+    HPROF(3, "prefetch call");
     if (n > (size_t)c->R) return c->fail(LMSF_ERR_CAPACITY, "%zu points exceed max_scan_points %d", n, c->R);
     HIPCHK(c, hipSetDevice(c->cfg.device));
     if (c->pre_pending) {   // replaced: its outputs are never adopted
@@ -1526,6 +1556,7 @@ lmsf_status lmsf_prefetch_features(lmsf_ctx* c, const float* xyzi, size_t n) {
 
 lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf_feature_counts* counts) {
     if (!c || (n && !xyzi)) return LMSF_ERR_ARG;
+    HPROF(0, "extract total");
     if (n > (size_t)c->R) return c->fail(LMSF_ERR_CAPACITY, "%zu points exceed max_scan_points %d", n, c->R);
     HIPCHK(c, hipSetDevice(c->cfg.device));
     c->pre_valid = false;
@@ -1544,9 +1575,13 @@ lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf
         // a deferred tracker commit completes here (its settle hook first enqueues the next Solve's prior-grid pass,
         // ctx_presearch, to run beside the window rebuild); the caller's next prefetch then follows the rebuild
         // (r06 A/B: settling only at the Solve put the prefetch beside the rebuild -- C3 1.2k vs 1.66k frames/s)
-        HIPCHK(c, hipEventSynchronize(c->ev_pre));
+        {
+            HPROF(1, "extract ev_pre sync");
+            HIPCHK(c, hipEventSynchronize(c->ev_pre));
+        }
         lmsf_status rc = adopt_counts(c, c->h_pre + 4, counts);
         if (rc) return rc;
+        HPROF(2, "extract settle");
         return ctx_settle(c);
     }
     {

@@ -101,6 +101,27 @@ inline int ab_int(const char* name, int def) {
 #endif
 }
 
+// Host-time probes of a diagnostics build (-DLMSF_HOST_PROFILE, tools/build_variant.sh): HPROF(id, name) adds the
+// wall time from there to the end of the enclosing block to bucket id; the table is printed to stderr at exit.
+// Empty in every other build.
+#ifdef LMSF_HOST_PROFILE
+}  // namespace lmsf
+#include <chrono>
+namespace lmsf {
+void hprof_add(int id, const char* name, long long ns);
+struct HProf {
+    int id;
+    const char* name;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~HProf() {
+        hprof_add(id, name, std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
+#define HPROF(id, name) HProf hprof_##id{id, name}
+#else
+#define HPROF(id, name) do {} while (0)
+#endif
+
 // Dense cell grid over one feature map: cell = floor(coord) - origin, 1 m cells (the match
 // radius: search_thresh_ = 1.0 squared metres, REG/FeatureMatch/FeatureMatchBase.hpp:29).
 struct GridView {

@@ -277,6 +277,7 @@ lmsf_status commit_stage(lmsf_tracker* t) {
 // Wait until the workers have enqueued the posted rebuild (no GPU wait); their status.
 lmsf_status join_worker(lmsf_tracker* t) {
     if (!t->staging) return LMSF_OK;
+    HPROF(8, "join_worker wait");
     std::unique_lock<std::mutex> lk(t->mu);
     t->cv.wait(lk, [t] { return !t->job[0] && !t->job[1]; });
     t->staging = false;
@@ -321,8 +322,15 @@ void worker_main(lmsf_tracker* t, int i, int device) {
         if (t->quit) return;
         const int kind = t->job[i];
         lk.unlock();
-        lmsf_status rc = commit_stage_kind(t, kind, t->aux[i]);
-        if (!rc) rc = finish_kind(t, kind, t->aux[i]);
+        lmsf_status rc;
+        {
+            HPROF(9, "worker stage");
+            rc = commit_stage_kind(t, kind, t->aux[i]);
+        }
+        if (!rc) {
+            HPROF(10, "worker finish");
+            rc = finish_kind(t, kind, t->aux[i]);
+        }
         lk.lock();
         t->job_rc[i] = rc;
         t->job[i] = 0;
@@ -389,6 +397,7 @@ lmsf_status presearch_prediction(lmsf_tracker* t, const double* deltaT) {
 // failed only one call: the priors and every window are rebuilt here from the tracker's own copies (the keyframe
 // slots are written by the transforms, never by a filter) before anything reads the map again.
 lmsf_status settle(lmsf_tracker* t) {
+    HPROF(12, "tracker settle");
     lmsf_status rc = commit_finish(t);
     if (rc) return rc;
     const uint64_t seq = ctx_fault_seq(t->ctx);
@@ -553,6 +562,7 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
     ctx_add_settle(ctx, [](void* p) {
         lmsf_tracker* tk = static_cast<lmsf_tracker*>(p);
         if (tk->init && (tk->pending || tk->staging)) {
+            HPROF(7, "settle hook presearch");
             lmsf_status rp = presearch_prediction(tk, nullptr);
             if (rp) return rp;
         }
@@ -568,6 +578,7 @@ namespace {
 
 // Solve (:107-160) on the features currently in the context's slot 0.
 lmsf_status solve_current(lmsf_tracker* t, double timestamp, double deltaT[16], lmsf_tracker_result* res) {
+    HPROF(15, "tracker solve total");
     if (t->init) {   // the prediction below, as register_pose will pass it (a no-op when the settle hook enqueued it)
         lmsf_status rp = presearch_prediction(t, deltaT);
         if (rp) return rp;
@@ -721,6 +732,7 @@ lmsf_status lmsf_tracker_add_keyframe_extracted(lmsf_tracker* t, const double po
     int64_t ne, ns;
     lmsf_status rc = ctx_slot0_features(t->ctx, &feat, &ne, &ns);
     if (rc) return rc;
+    HPROF(14, "add_keyframe_extracted push");
     const Iso T = iso_from16(pose);
     rc = push_frame(t, LMSF_EDGE, feat, ne, T);
     if (rc) return rc;
@@ -731,6 +743,7 @@ lmsf_status lmsf_tracker_add_keyframe_extracted(lmsf_tracker* t, const double po
 // work the caller enqueues on the context in between (the next scan's extraction) runs beside it.
 lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t) {
     if (!t) return LMSF_ERR_ARG;
+    HPROF(13, "commit_map call");
     if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
     lmsf_status rc = settle(t);
     if (rc) return rc;
