@@ -268,6 +268,7 @@ struct lmsf_ctx {
     const float* pre_src = nullptr;
     size_t pre_n = 0;
     bool pre_pending = false;
+    bool pre_held = false;            // a prefetch not yet posted: it follows the next Solve's kernels (release_prefetch)
     // the prefetch's enqueues (~12 API calls) are made by a worker thread of the context, so that the caller's
     // next call (the Solve it overlaps) is enqueued at once instead of behind them
     std::thread pre_worker;
@@ -1197,6 +1198,9 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     delete c;
 }
 
+#ifndef LMSF_CTX_PRIORITY
+#define LMSF_CTX_PRIORITY 1
+#endif
 lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
     if (!cfg || !out) return LMSF_ERR_ARG;
     *out = nullptr;
@@ -1222,7 +1226,16 @@ lmsf_status lmsf_ctx_create(const lmsf_config* cfg, lmsf_ctx** out) {
         if ((expr) != hipSuccess) return bail(LMSF_ERR_HIP); \
     } while (0)
     CHK(hipSetDevice(cfg->device));
-    CHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    {
+        // A single-scan context's stream (its Solves) at the device's highest priority, ahead of the prefetch
+        // extraction and the tracker's window rebuilds running beside it (r06, three rounds on each of two boxes,
+        // alternating: C4 1,474 / 1,488 / 1,494 and 1,499 / 1,486 / 1,464 vs 1,465 / 1,466 / 1,484 and 1,468 / 1,447
+        // / 1,449 scans/s; C3 within its noise).  A/B builds: LMSF_CTX_PRIORITY=0 for the default priority.
+        static const bool hi = ab_int("LMSF_CTX_PRIORITY", LMSF_CTX_PRIORITY) != 0;
+        int lo = 0, top = 0;
+        if (hi && c->B == 1) (void)hipDeviceGetStreamPriorityRange(&lo, &top);
+        CHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi && c->B == 1 ? top : 0));
+    }
     const size_t B = c->B, F = c->F, R = c->R;
     CHK(dalloc(&c->feat, B * F));
     CHK(dalloc(&c->feat_src, B * F));
@@ -1369,6 +1382,8 @@ lmsf_status lmsf_set_extract_params(lmsf_ctx* c, const lmsf_extract_params* p) {
     return LMSF_OK;
 }
 
+static lmsf_status release_prefetch(lmsf_ctx* c);
+
 lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     if (!c || !pose) return LMSF_ERR_ARG;
     HPROF(5, "solve total");
@@ -1398,6 +1413,8 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     }
     c->skip_state_init = false;
     c->pre_use = false;
+    if (rc) return rc;
+    rc = release_prefetch(c);   // a held prefetch follows this Solve's kernels
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -1443,8 +1460,25 @@ static lmsf_status adopt_counts(lmsf_ctx* c, const int* hc, lmsf_feature_counts*
     return LMSF_OK;
 }
 
+// A held prefetch posted to its worker, ordered after everything enqueued on the context so far.
+static lmsf_status release_prefetch(lmsf_ctx* c) {
+    if (!c->pre_held) return LMSF_OK;
+    c->pre_held = false;
+    HIPCHK(c, hipEventRecord(c->ev_pre_after, c->stream));
+    {
+        std::lock_guard<std::mutex> lk(c->pre_mu);
+        c->pre_job = true;
+    }
+    c->pre_cv.notify_all();
+    return LMSF_OK;
+}
+
 // The prefetch worker's enqueues, done (their status; the worker thread stays for the next prefetch).
 static lmsf_status join_prefetch(lmsf_ctx* c) {
+    {
+        lmsf_status rr = release_prefetch(c);
+        if (rr) return rr;
+    }
     std::unique_lock<std::mutex> lk(c->pre_mu);
     c->pre_cv.wait(lk, [c] { return !c->pre_job; });
     const lmsf_status rc = c->pre_rc;
@@ -1537,21 +1571,19 @@ lmsf_status lmsf_prefetch_features(lmsf_ctx* c, const float* xyzi, size_t n) {
         HIPCHK(c, hipStreamCreateWithFlags(&c->pre_stream, hipStreamNonBlocking));
         c->pre_worker = std::thread(prefetch_worker, c);
     }
-    // after everything enqueued on the context so far: the last extraction (shared scratch) and the readers of
-    // the output set this one overwrites (a keyframe transform of the features before the last)
-    HIPCHK(c, hipEventRecord(c->ev_pre_after, c->stream));
     c->h_pre[0] = (int)n;
     c->h_pre[2] = 0;
     c->h_pre[3] = 0;
     c->pre_src = xyzi;
     c->pre_n = n;
     c->pre_pending = true;
-    {
-        std::lock_guard<std::mutex> lk(c->pre_mu);
-        c->pre_job = true;
-    }
-    c->pre_cv.notify_all();
-    return LMSF_OK;
+    // after everything enqueued on the context so far: the last extraction (shared scratch) and the readers of
+    // the output set this one overwrites (a keyframe transform of the features before the last).  A/B builds
+    // (LMSF_PREFETCH_AFTER_SOLVE=1): held until the next Solve has enqueued its kernels, so the extraction runs in the
+    // GPU's idle time after that Solve (the pose read-back and the keyframe hand-off) instead of beside its searches
+    static const bool hold = ab_int("LMSF_PREFETCH_AFTER_SOLVE", 0) != 0;
+    c->pre_held = true;
+    return hold ? LMSF_OK : release_prefetch(c);
 }
 
 lmsf_status lmsf_extract_features(lmsf_ctx* c, const float* xyzi, size_t n, lmsf_feature_counts* counts) {
