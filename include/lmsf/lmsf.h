@@ -296,6 +296,8 @@ typedef struct {
                                * the 9-launch form (results as without the fault) */
     int64_t buffer_growths;   /* map-grid buffer growths since the context was created (not reset: the
                                * growth test checks that a tracker's window grids were regrown) */
+    int64_t split_searches;   /* Solves whose outer iteration 0 ran in two passes: the prior grids' walk enqueued
+                               * beside a tracker's keyframe window rebuild, then the window's (same results) */
 } lmsf_kernel_stats;
 lmsf_status lmsf_kernel_stats_get(lmsf_ctx* ctx, lmsf_kernel_stats* out);
 lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* ctx, int32_t mode);

@@ -181,6 +181,7 @@ struct lmsf_ctx {
     bool pre_valid = false, pre_use = false;
     double pre_pose[7] = {0, 0, 0, 0, 0, 0, 0};
     int64_t loop_recoveries = 0;
+    int64_t split_searches = 0;       // Solves whose outer iteration 0 took ctx_presearch's prior pass (kernel stats)
     int last_launch_iters = 0;        // outer iterations of the last batch launch (its re-run after a loop fault)
     int last_launch_n = 0;            // and its slots
     // record capture (lmsf_batch_capture): device rows [n_cap][kCaptureIters][F] of the captured slots
@@ -871,6 +872,7 @@ lmsf_status enqueue_register(lmsf_ctx* c, int nb, int iters) {
             bvk.memo = !gn && o > 0 && !c->count27 && memo_on ? 1 : 0;
             if (o == 0 && c->pre_use && !track) {   // the window pass after ctx_presearch's prior pass
                 c->pre_use = false;
+                c->split_searches++;
                 HIPCHK(c, launch_knn_split(2, ge2, gs2, ge, gs, bvk, s));
             } else if (track) {   // search + fit + first evaluation in one launch (k_match.hip track_match_kernel)
                 HIPCHK(c, launch_track_match(ge2.n ? ge2 : ge, gs2.n ? gs2 : gs, ge2.n ? ge : GridView{},
@@ -2237,6 +2239,7 @@ lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* c, int32_t mode) {
     c->fused_launches = 0;
     c->knn_queries = 0;
     c->loop_recoveries = 0;
+    c->split_searches = 0;
     HIPCHK(c, hipMemsetAsync(c->d_n27, 0, kCounterShards * 16 * sizeof(unsigned long long), c->stream));
     return LMSF_OK;
 }
@@ -2264,6 +2267,7 @@ lmsf_status lmsf_kernel_stats_get(lmsf_ctx* c, lmsf_kernel_stats* out) {
     out->reused_queries = (int64_t)r;
     out->refit_queries = (int64_t)rf;
     out->loop_recoveries = c->loop_recoveries;
+    out->split_searches = c->split_searches;
     int64_t g = 0;
     for (DevMap* ms : {c->map, c->prior, c->fine})
         for (int k = 0; k < 3; ++k) g += ms[k].growths;
@@ -2316,7 +2320,7 @@ lmsf_status ctx_presearch(lmsf_ctx* c, const double x[7]) {
     c->pre_valid = false;
     if (c->cfg.solver != LMSF_SOLVER_CERES_LM || !c->opt[LMSF_OPT_QUERY_MEMO] || c->count27 || c->opt[LMSF_OPT_GRAPH] ||
         c->prior[LMSF_EDGE].n == 0 || c->prior[LMSF_SURF].n == 0 || knn_team_for((size_t)c->F) != 8 ||
-        fit_per_thread_default() != 1 || track_fused_enabled() || !c->cap_slots.empty() || c->loop_off_once)
+        fit_per_thread_default() != 1 || track_fused_enabled() || c->loop_off_once)
         return LMSF_OK;
     static const bool on = ab_int("LMSF_PRESEARCH", 1) != 0;   // A/B builds: 0 = the one-launch TWO walk
     // extracted features only (on the device, or enqueued ahead on the context stream); host features upload later

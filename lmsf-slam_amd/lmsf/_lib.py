@@ -53,7 +53,7 @@ class KernelStats(C.Structure):
     _fields_ = [("launches", C.c_int64), ("total_ms", C.c_double), ("queries", C.c_int64), ("n27_sum", C.c_int64),
                 ("fused_launches", C.c_int64), ("reused_queries", C.c_int64),
                 ("refit_queries", C.c_int64), ("loop_recoveries", C.c_int64),
-                ("buffer_growths", C.c_int64)]
+                ("buffer_growths", C.c_int64), ("split_searches", C.c_int64)]
 
 
 class ExtractParams(C.Structure):

@@ -196,3 +196,55 @@ def test_adversarial_gauss_newton(lib, oracle_mod, adv):
         ox, otr, ost = reg.solve(g[slot])
         _same_traces(gtr, otr, f"GN slot {slot}")
         assert stats[slot].termination == ost.termination, (slot, stats[slot].termination, ost.termination)
+
+
+def test_tracker_split_search_ties(lib, oracle_mod, adv):
+    """A tracker Solve whose outer iteration 0 runs split (ctx_presearch: the prior grids' walk enqueued beside the
+    keyframe window rebuild, then the window pass seeded with its keys; knn_kernel SPLIT 1 / 2) on the adversarial
+    scene as the prior map and a keyframe of exact copies of every planted point as the window (identity pose, no
+    voxel filter): every planted candidate ties across the two grids at equal d^2, so each query's kept keys interleave
+    prior and window points and only the index order (prior first) decides them.  The records and 5-NN indices after
+    every outer iteration equal the oracle's fresh match over [prior | window] at the GPU's pose, and the poses follow
+    the oracle's registration (LidarTrackerLocalMap.hpp:125-133 / ceres_edgeSurfFeatureRegistration.hpp:100-125)."""
+    maps = adv["maps"]["sparse"]
+    planted, _ = af.planted_maps(adv["sets"])
+    g = adv["guesses"][0]
+    T0 = np.eye(4)
+    T0[:3, 3] = g[4:]
+    ctx = lib.Context(max_batch=1, max_scan_points=70000, max_features=70000)
+    tr = lib.Tracker(ctx, manual_map_update=True, leaf_edge=0.0, leaf_surf=0.0)
+    tr.set_initial_pose(T0)
+    tr.set_prior_map(lib.EDGE, maps[1])
+    tr.set_prior_map(lib.SURF, maps[2])
+    ctx.extract(adv["scan"])
+    _, r0 = tr.solve_extracted(0.0)
+    assert r0.initialized
+    tr.add_keyframe(planted[1], planted[2], np.eye(4))
+    tr.commit_map()
+    ctx.batch_capture([0])
+    ctx.kernel_stats_reset()
+    ctx.extract(adv["scan"])       # settles the commit: the prior pass at the prediction T0 goes first
+    _, r = tr.solve_extracted(0.1)
+    assert ctx.kernel_stats().split_searches == 1
+    assert (r.local_map_edge, r.local_map_surf) == (len(maps[1]) + len(planted[1]), len(maps[2]) + len(planted[2]))
+    reg = oracle_mod.Registration()
+    for k in (1, 2):
+        reg.set_map(k, np.concatenate([maps[k], planted[k]], 0))
+    reg.set_scan(1, adv["e"])
+    reg.set_scan(2, adv["s"])
+    ox, otr, ost = reg.solve(g)
+    n = r.solve.outer_iterations
+    assert n == len(otr), (n, otr.shape)
+    window_nn = 0
+    for it in range(min(n, 10)):
+        grec, gnn, gpose = ctx.batch_records(0, it)
+        if it == 0:
+            assert np.array_equal(gpose, g)
+        else:
+            dt, dr = pose_err(gpose, otr[it - 1])
+            assert dt <= POSE_TOL and dr <= POSE_TOL, (it, dt, dr)
+        orec, onn = reg.match(gpose)
+        _same_records(grec, gnn, orec, onn, f"split tracker outer iteration {it}")
+        ne = len(adv["e"])
+        window_nn += int((gnn[:ne] >= len(maps[1])).sum() + (gnn[ne:] >= len(maps[2])).sum())
+    assert window_nn > 0                                        # window points won places in the kept sets
