@@ -873,7 +873,9 @@ def run_streams(args, d):
     ctx = _lib.Context(device=d.gpu, max_batch=1, max_scan_points=max_pts + 64, max_features=max_pts + 64,
                        schedule=_lib.SCHEDULE_FIXED, max_iterations=args.outer)
     apply_options(args, [ctx])
-    tr = _lib.Tracker(ctx, manual_map_update=True)
+    # keyframe lookahead (lmsf_tracker_config.keyframe_lookahead) only for one stream: with several, the keyframes of
+    # lower ranks are appended before this rank's own and would undo it at every step
+    tr = _lib.Tracker(ctx, manual_map_update=True, keyframe_lookahead=(world == 1))
     T0 = np.eye(4)
     T0[:3, :3] = synth.quat_to_mat(truth[0][:4])
     T0[:3, 3] = truth[0][4:]

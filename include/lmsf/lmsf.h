@@ -298,6 +298,8 @@ typedef struct {
                                * growth test checks that a tracker's window grids were regrown) */
     int64_t split_searches;   /* Solves whose outer iteration 0 ran in two passes: the prior grids' walk enqueued
                                * beside a tracker's keyframe window rebuild, then the window's (same results) */
+    int64_t lookahead_solves; /* Solves during which a tracker's keyframe lookahead was enqueued
+                               * (lmsf_tracker_config.keyframe_lookahead) */
 } lmsf_kernel_stats;
 lmsf_status lmsf_kernel_stats_get(lmsf_ctx* ctx, lmsf_kernel_stats* out);
 lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* ctx, int32_t mode);
@@ -324,6 +326,13 @@ typedef struct {
                                   lmsf_tracker_commit_map (multi-stream map stitching) */
     double leaf_edge;          /* VoxelGrid leaf of the keyframe window, per kind (build-defined: */
     double leaf_surf;          /* 0.2 / 0.4 m, LOAM's mapping resolutions; 0 = no downsampling) */
+    int32_t keyframe_lookahead; /* 1 (default): when the motion-model prediction already passes the keyframe
+                                  gate, the window rebuild with this scan's features at the Solve's result is
+                                  started on the device while the Solve runs; a keyframe of exactly that pose and
+                                  those features (the tracker's own, lmsf_tracker_add_keyframe_extracted with
+                                  lmsf_tracker_pose, or the automatic update) adopts it, anything else undoes it.
+                                  Results are identical either way.  0 for callers that append other streams'
+                                  keyframes first (the lookahead would be undone every time) */
 } lmsf_tracker_config;
 
 #define LMSF_UPDATE_NONE 0    /* LocalMapUpdataType NO_UPDATA */

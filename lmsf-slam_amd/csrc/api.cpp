@@ -182,6 +182,7 @@ struct lmsf_ctx {
     double pre_pose[7] = {0, 0, 0, 0, 0, 0, 0};
     int64_t loop_recoveries = 0;
     int64_t split_searches = 0;       // Solves whose outer iteration 0 took ctx_presearch's prior pass (kernel stats)
+    int64_t post_solves = 0;          // Solves that ran an armed post-solve call (kernel stats)
     int last_launch_iters = 0;        // outer iterations of the last batch launch (its re-run after a loop fault)
     int last_launch_n = 0;            // and its slots
     // record capture (lmsf_batch_capture): device rows [n_cap][kCaptureIters][F] of the captured slots
@@ -306,9 +307,15 @@ struct lmsf_ctx {
     std::vector<float> host_scan[3];  // SetInputTarget copies (slot 0)
     bool scan_dirty = false;
     bool features_on_device = false;  // slot 0 features came from lmsf_extract_features
+    uint64_t feat_seq = 0;            // bumped whenever slot 0's features change (ctx_feature_seq)
     // trackers on this context with a deferred keyframe commit (lmsf_tracker_commit_map): completed
     // before any map consumer of the context (resolve_all_lim1) or a map replacement
     std::vector<std::pair<lmsf_status (*)(void*), void*>> settle_hooks;
+    // armed for one lmsf_solve: called once its kernels and its result's read-back are enqueued, before the host
+    // waits (a tracker's keyframe lookahead enqueues the next window rebuild there); the wait is then on ev_solved
+    lmsf_status (*post_solve)(void*) = nullptr;
+    void* post_solve_arg = nullptr;
+    hipEvent_t ev_solved = nullptr;
     int64_t slot0_ne = 0, slot0_ns = 0;
     int last_outer = 0;
     int batch_done = 0;               // slots whose SolveState the last lmsf_batch_wait read back into h_st
@@ -1072,12 +1079,13 @@ lmsf_status report_fault(lmsf_ctx* c, int bits) {
     HIPCHK(c, hipMemsetAsync(c->d_error + 17, 0, sizeof(int), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     ++c->fault_seq;   // the grids built since the last report may be empty or partial (the settle hooks rebuild them)
-    return c->fail(LMSF_ERR_HIP, "device look-back fault (flags 0x%x:%s%s%s%s%s)", bits,
+    return c->fail(LMSF_ERR_HIP, "device look-back fault (flags 0x%x:%s%s%s%s%s%s)", bits,
                    bits & kFaultRadixScatter ? " radix scatter out of range" : "",
                    bits & kFaultLookbackWait ? " look-back wait exhausted" : "",
                    bits & kFaultForeignEpoch ? " foreign look-back epoch" : "",
                    bits & kFaultSegment ? " voxel segments out of range" : "",
-                   bits & kFaultGridScatter ? " grid scatter out of range" : "");
+                   bits & kFaultGridScatter ? " grid scatter out of range" : "",
+                   bits & kFaultStreamWait ? " stream flag wait exhausted" : "");
 }
 
 int outer_iterations_for_solve(lmsf_ctx* c) {
@@ -1159,6 +1167,7 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (c->h_pre) hipHostFree(c->h_pre);
     if (c->ev_pre) hipEventDestroy(c->ev_pre);
     if (c->ev_pre_after) hipEventDestroy(c->ev_pre_after);
+    if (c->ev_solved) hipEventDestroy(c->ev_solved);
     if (c->pre_stream) hipStreamDestroy(c->pre_stream);
     gfree(c->wl2, c->stream);
     gfree(c->wlim2, c->stream);
@@ -1355,6 +1364,7 @@ lmsf_status lmsf_set_scan(lmsf_ctx* c, int32_t kind, const float* xyzi, size_t n
     }
     c->host_scan[kind].assign(xyzi, xyzi + 4 * n);
     c->scan_dirty = true;
+    ++c->feat_seq;
     return LMSF_OK;
 }
 
@@ -1389,6 +1399,8 @@ static lmsf_status release_prefetch(lmsf_ctx* c);
 lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     if (!c || !pose) return LMSF_ERR_ARG;
     HPROF(5, "solve total");
+    const auto post = c->post_solve;   // armed for this call only, whatever its outcome
+    c->post_solve = nullptr;
     HIPCHK(c, hipSetDevice(c->cfg.device));
     lmsf_status rc = ctx_settle(c);   // a deferred tracker commit may be the first map of this context
     if (rc) return rc;
@@ -1420,7 +1432,16 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    {
+    if (post) {   // the armed call: work that follows this Solve on the device, enqueued while it runs
+        auto fn = post;
+        c->post_solves++;
+        if (!c->ev_solved) HIPCHK(c, hipEventCreateWithFlags(&c->ev_solved, hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(c->ev_solved, c->stream));
+        rc = fn(c->post_solve_arg);
+        if (rc) return rc;
+        HPROF(6, "solve wait");
+        HIPCHK(c, hipEventSynchronize(c->ev_solved));
+    } else {
         HPROF(6, "solve wait");
         HIPCHK(c, stream_wait(c->stream));
     }
@@ -1455,6 +1476,7 @@ static lmsf_status adopt_counts(lmsf_ctx* c, const int* hc, lmsf_feature_counts*
     c->slot0_ne = hc[0];
     c->slot0_ns = hc[1];
     c->features_on_device = true;
+    ++c->feat_seq;
     c->scan_dirty = false;
     c->host_scan[LMSF_EDGE].clear();
     c->host_scan[LMSF_SURF].clear();
@@ -1694,6 +1716,7 @@ lmsf_status lmsf_common_process(lmsf_ctx* c, const float* xyzi, size_t n, const 
     c->slot0_ne = 0;
     c->slot0_ns = m;
     c->features_on_device = true;
+    ++c->feat_seq;
     c->qorder_valid = false;          // slot order (no ring order for a filtered cloud)
     c->scan_dirty = false;
     c->host_scan[LMSF_EDGE].clear();
@@ -2002,6 +2025,7 @@ lmsf_status lmsf_batch_launch(lmsf_ctx* c, int32_t n, const double* poses) {
     if (c->cfg.solver == LMSF_SOLVER_CERES_LM && c->cfg.schedule == LMSF_SCHEDULE_REFERENCE_DECAY && iters > 2) --iters;
     iters = std::min(iters, kMaxOuter);
     c->features_on_device = false;
+    ++c->feat_seq;
     c->last_launch_iters = iters;
     c->last_launch_n = n;
     return enqueue_solve(c, n, iters);
@@ -2240,6 +2264,7 @@ lmsf_status lmsf_kernel_stats_reset(lmsf_ctx* c, int32_t mode) {
     c->knn_queries = 0;
     c->loop_recoveries = 0;
     c->split_searches = 0;
+    c->post_solves = 0;
     HIPCHK(c, hipMemsetAsync(c->d_n27, 0, kCounterShards * 16 * sizeof(unsigned long long), c->stream));
     return LMSF_OK;
 }
@@ -2268,6 +2293,7 @@ lmsf_status lmsf_kernel_stats_get(lmsf_ctx* c, lmsf_kernel_stats* out) {
     out->refit_queries = (int64_t)rf;
     out->loop_recoveries = c->loop_recoveries;
     out->split_searches = c->split_searches;
+    out->lookahead_solves = c->post_solves;
     int64_t g = 0;
     for (DevMap* ms : {c->map, c->prior, c->fine})
         for (int k = 0; k < 3; ++k) g += ms[k].growths;
@@ -2299,6 +2325,15 @@ bool ctx_features_on_device(const lmsf_ctx* c) { return c->features_on_device; }
 lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg) { return c->fail(code, "%s", msg); }
 
 void ctx_add_settle(lmsf_ctx* c, lmsf_status (*fn)(void*), void* arg) { c->settle_hooks.emplace_back(fn, arg); }
+
+void ctx_arm_post_solve(lmsf_ctx* c, lmsf_status (*fn)(void*), void* arg) {
+    c->post_solve = fn;
+    c->post_solve_arg = arg;
+}
+
+const double* ctx_solved_pose(const lmsf_ctx* c) { return c->st[0].x; }
+int64_t ctx_loop_recoveries(const lmsf_ctx* c) { return c->loop_recoveries; }
+uint64_t ctx_feature_seq(const lmsf_ctx* c) { return c->feat_seq; }
 
 void ctx_remove_settle(lmsf_ctx* c, void* arg) {
     auto& v = c->settle_hooks;

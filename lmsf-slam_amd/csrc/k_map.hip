@@ -108,9 +108,69 @@ __global__ void transform_kernel(const float4* in, int n, Affine34 M, float4* ou
     out[i] = o;
 }
 
+// Cross-stream ordering through a device flag instead of an event wait (tracker rebuild fork / join, A/B
+// LMSF_FLAG_SYNC): the producer stream ends its work with flag_signal (release: the kernels before it on that stream
+// have completed and released their writes at kernel end), the consumer stream runs flag_wait (one wave polling with
+// acquire loads) before the work that reads them.  A wait past its bound flags kFaultStreamWait in err and lets the
+// stream go on (reported as LMSF_ERR_HIP at the next read-back), so no configuration can hang the device.
+__global__ void flag_signal_kernel(uint32_t* flag, uint32_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void flag_wait_kernel(const uint32_t* flag, uint32_t v, int* err, unsigned spin_limit) {
+    if (threadIdx.x != 0) return;
+    unsigned spins = 0;
+    while ((int)(__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - v) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > spin_limit) {
+            if (err) atomicOr(err, kFaultStreamWait);
+            break;
+        }
+    }
+}
+
+hipError_t launch_flag_signal(uint32_t* flag, uint32_t v, hipStream_t s) {
+    hipLaunchKernelGGL(flag_signal_kernel, dim3(1), dim3(64), 0, s, flag, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_flag_wait(const uint32_t* flag, uint32_t v, int* err, hipStream_t s) {
+    hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, s, flag, v, err, 1u << 24);
+    return hipGetLastError();
+}
+
 hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(transform_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, M, out);
+    return hipGetLastError();
+}
+
+// The same transform at a pose the device holds (x = qx qy qz qw tx ty tz, a Solve's result): the matrix as the host
+// builds it (tracker.cpp R_from_quat, Eigen's toRotationMatrix; t = x[4..6]), then transform_kernel's arithmetic --
+// the same bits as launch_transform with the host's copy of that pose.
+__global__ void transform_pose_kernel(const float4* in, int n, const double* x, float4* out) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double qx = x[0], qy = x[1], qz = x[2], qw = x[3];
+    const double tx = 2 * qx, ty = 2 * qy, tz = 2 * qz, twx = tx * qw, twy = ty * qw, twz = tz * qw;
+    const double txx = tx * qx, txy = ty * qx, txz = tz * qx, tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    const double m[12] = {1 - (tyy + tzz), txy - twz, txz + twy, x[4],
+                          txy + twz, 1 - (txx + tzz), tyz - twx, x[5],
+                          txz - twy, tyz + twx, 1 - (txx + tyy), x[6]};
+    const float4 p = in[i];
+    const double px = p.x, py = p.y, pz = p.z;
+    float4 o;
+    o.x = (float)(m[0] * px + m[1] * py + m[2] * pz + m[3]);
+    o.y = (float)(m[4] * px + m[5] * py + m[6] * pz + m[7]);
+    o.z = (float)(m[8] * px + m[9] * py + m[10] * pz + m[11]);
+    o.w = p.w;
+    out[i] = o;
+}
+
+hipError_t launch_transform_pose(const float4* in, int n, const double* x, float4* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(transform_pose_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, x, out);
     return hipGetLastError();
 }
 

@@ -67,6 +67,7 @@ constexpr int kFaultLookbackWait = 2;   // a look-back wait exceeded its bound
 constexpr int kFaultForeignEpoch = 4;   // a look-back word newer than the running sort (memory of another allocation)
 constexpr int kFaultSegment = 8;        // the voxel segment pass counted more voxels than points
 constexpr int kFaultGridScatter = 16;   // a grid scatter computed a position outside [0, n)
+constexpr int kFaultStreamWait = 32;    // a cross-stream flag wait exceeded its bound (k_map.hip flag_wait_kernel)
 // Look-back epochs: one process-wide counter (never restarts, never 0), shared by every sort and scan.
 uint32_t next_lookback_epoch();
 constexpr int kRingMax = 8192;       // points per ring handled by the extraction kernel
@@ -344,6 +345,11 @@ hipError_t launch_extract(const ExtractView& ev, hipStream_t s);
 struct Affine34 { double m[12]; };   // row-major 3x4 of an Isometry3d matrix
 // pcl::transformPointCloud(cloud, out, Matrix4d) per point: float(m00 x + m01 y + m02 z + m03), double math
 hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hipStream_t s);
+// ... at the pose x[7] (qx qy qz qw tx ty tz) in device memory, its matrix built as the tracker's host code builds it
+hipError_t launch_transform_pose(const float4* in, int n, const double* x, float4* out, hipStream_t s);
+// flag <- v after the work enqueued on s so far; s waits until flag reaches v (wrap-safe), bounded (err |= kFaultStreamWait)
+hipError_t launch_flag_signal(uint32_t* flag, uint32_t v, hipStream_t s);
+hipError_t launch_flag_wait(const uint32_t* flag, uint32_t v, int* err, hipStream_t s);
 // Concatenation of up to kSlotTable device arrays (kernel-argument table, start[] exclusive prefix).
 constexpr int kSlotTable = 32;
 struct SlotTable {
@@ -413,6 +419,13 @@ lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg);
 // a tracker's deferred-commit completion, run by the context before its map consumers
 void ctx_add_settle(lmsf_ctx* c, lmsf_status (*fn)(void*), void* arg);
 void ctx_remove_settle(lmsf_ctx* c, void* arg);
+// fn(arg) once, inside the next lmsf_solve: after its kernels and its result's read-back are enqueued, before its
+// host wait (a tracker's keyframe lookahead); ctx_solved_pose: that Solve's result on the device (x[7]);
+// ctx_loop_recoveries: lmsf_kernel_stats' count (a recovered Solve re-ran after the armed call)
+void ctx_arm_post_solve(lmsf_ctx* c, lmsf_status (*fn)(void*), void* arg);
+const double* ctx_solved_pose(const lmsf_ctx* c);
+int64_t ctx_loop_recoveries(const lmsf_ctx* c);
+uint64_t ctx_feature_seq(const lmsf_ctx* c);   // changes whenever slot 0's features do
 // map of a kind = [prior | window]: the prior grid is built once (static), the window grid at every
 // keyframe commit with indices offset by the prior size; n == 0 clears that part.
 lmsf_status ctx_set_prior_device(lmsf_ctx* c, int kind, const float4* d_pts, size_t n);

@@ -148,6 +148,13 @@ struct lmsf_tracker {
     VoxelFilter voxel[3];       // per kind: the two windows are filtered concurrently
     hipStream_t aux[2] = {nullptr, nullptr};   // the windows' commits (surf, edge), beside the context stream
     hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
+    // LMSF_FLAG_SYNC (A/B): the fork / join orderings through device flags (k_map.hip flag_wait_kernel) instead of
+    // event waits, whose cross-queue wake-up measured 20-35 us per hop on the r06 C4 trace.  flags: [0] fork,
+    // [kind] join; the values last signalled.
+    uint32_t* flags = nullptr;
+    uint32_t fork_val = 0, join_val[3] = {0, 0, 0};
+    bool fork_flags = false, join_flags[3] = {false, false, false};   // the mode each mark used (its wait uses the same)
+    bool counted = false;         // in g_trackers
     hipStream_t ks[3] = {nullptr, nullptr, nullptr};   // staged commit: stream per kind (null: unchanged)
     size_t nmax[3] = {0, 0, 0};
     bool pending = false;                               // staged, not yet finished
@@ -166,11 +173,69 @@ struct lmsf_tracker {
     lmsf_status job_rc[2] = {LMSF_OK, LMSF_OK};
     size_t fin_n[3] = {0, 0, 0};  // per kind: the window size a worker's grid finish found
     uint64_t fault_seen = 0;      // ctx_fault_seq when the maps were last (re)built
+    // Keyframe lookahead (cfg.keyframe_lookahead, r06): when the motion-model prediction already passes the keyframe
+    // gate, the Solve's own features are transformed at its result on the device and the window rebuild is posted
+    // while the Solve runs (ctx_arm_post_solve), so the rebuild no longer waits for the pose read-back, the caller's
+    // decision and the hand-off to the workers.  The caller's keyframe of exactly that pose and those features adopts
+    // it; anything else rolls it back (the window state restored, the evicted frame's buffer kept aside, the window
+    // grid rebuilt).  Results are the same either way.
+    int look = 0;                 // kLookNone / kLookPosted / kLookAdopted
+    double look_pose[16];
+    bool look_pose_known = false;
+    uint64_t look_feat = 0;       // ctx_feature_seq of the features it transformed
+    int64_t look_recoveries = 0;  // ctx_loop_recoveries before the Solve (a recovered Solve re-ran after the transform)
+    float4* spare[3] = {nullptr, nullptr, nullptr};   // per kind: a slot buffer outside the ring
+    struct Undo { bool pushed; int slot, head, count, size; bool dirty; } undo[3] = {};
 };
 
 namespace {
 
 lmsf_status fail(lmsf_tracker* t, lmsf_status code, const char* msg) { return ctx_fail(t->ctx, code, msg); }
+
+// Trackers per device.  The flag waits and the keyframe lookahead are used while a tracker is the only one on its
+// device (r06 A/B: C4, one tracker per GPU, 1,579 / 1,578 / 1,541 scans/s with both vs 1,475 / 1,477 / 1,433 with
+// neither; C3's two trackers on one GPU 1,230 / 1,359 / 1,394 vs 1,346 / 1,369 / 1,374 frames/s): a spinning wait on a
+// hardware queue another tracker's streams share holds that tracker's work behind it (4 queues per process).
+std::atomic<int> g_trackers[64];
+bool sole_tracker(const lmsf_tracker* t) {
+    const int d = ctx_device(t->ctx);
+    return d < 0 || d >= 64 || g_trackers[d].load(std::memory_order_relaxed) == 1;
+}
+
+#ifndef LMSF_FLAG_SYNC
+#define LMSF_FLAG_SYNC 1
+#endif
+bool flag_sync(const lmsf_tracker* t) {
+    static const bool on = ab_int("LMSF_FLAG_SYNC", LMSF_FLAG_SYNC) != 0;
+    return on && sole_tracker(t);
+}
+
+// The fork point: everything enqueued on the context stream so far (the keyframe transforms) before the rebuilds.
+hipError_t fork_mark(lmsf_tracker* t) {
+    t->fork_flags = flag_sync(t);
+    hipError_t e = hipEventRecord(t->ev_fork, ctx_stream(t->ctx));
+    if (e == hipSuccess && t->fork_flags) e = launch_flag_signal(t->flags, ++t->fork_val, ctx_stream(t->ctx));
+    return e;
+}
+
+hipError_t fork_wait(lmsf_tracker* t, hipStream_t ks) {
+    return t->fork_flags ? launch_flag_wait(t->flags, t->fork_val, ctx_fault_word(t->ctx), ks)
+                         : hipStreamWaitEvent(ks, t->ev_fork, 0);
+}
+
+// The join of one kind's rebuild on ks into the context stream: marked on ks, waited for on the context stream.
+hipError_t join_mark(lmsf_tracker* t, int kind, hipStream_t ks) {
+    t->join_flags[kind] = t->fork_flags;
+    hipError_t e = hipEventRecord(t->ev_join[kind], ks);
+    if (e == hipSuccess && t->join_flags[kind]) e = launch_flag_signal(t->flags + kind, ++t->join_val[kind], ks);
+    return e;
+}
+
+hipError_t join_wait(lmsf_tracker* t, int kind) {
+    hipStream_t s = ctx_stream(t->ctx);
+    return t->join_flags[kind] ? launch_flag_wait(t->flags + kind, t->join_val[kind], ctx_fault_word(t->ctx), s)
+                               : hipStreamWaitEvent(s, t->ev_join[kind], 0);
+}
 
 #define TCHK(t, expr)                                               \
     do {                                                            \
@@ -218,7 +283,7 @@ lmsf_status push_frame(lmsf_tracker* t, int kind, const float4* src, int64_t n, 
 // One kind's half of commit_stage on stream ks (after ev_fork).
 lmsf_status commit_stage_kind(lmsf_tracker* t, int kind, hipStream_t ks) {
     Window& w = t->win[kind];
-    TCHK(t, hipStreamWaitEvent(ks, t->ev_fork, 0));
+    TCHK(t, fork_wait(t, ks));
     const int W = (int)w.slots.size();
     float4* dst = w.leaf > 0 ? w.wcat : w.concat;
     size_t nw = 0;
@@ -263,7 +328,7 @@ int assign_streams(lmsf_tracker* t) {
 }
 
 lmsf_status commit_stage(lmsf_tracker* t) {
-    TCHK(t, hipEventRecord(t->ev_fork, ctx_stream(t->ctx)));   // the keyframe transforms queued on the context
+    TCHK(t, fork_mark(t));   // the keyframe transforms queued on the context
     assign_streams(t);
     for (int kind : {LMSF_SURF, LMSF_EDGE}) {
         if (!t->ks[kind]) continue;
@@ -292,7 +357,7 @@ lmsf_status finish_kind(lmsf_tracker* t, int kind, hipStream_t ks) {
     if (!(t->win[kind].leaf > 0)) TCHK(t, stream_wait(ks));
     lmsf_status rc = ctx_window_finish(t->ctx, kind, t->nmax[kind], ks, &t->fin_n[kind]);
     if (rc) return rc;
-    TCHK(t, hipEventRecord(t->ev_join[kind], ks));
+    TCHK(t, join_mark(t, kind, ks));
     return LMSF_OK;
 }
 
@@ -350,7 +415,7 @@ lmsf_status commit_finish(lmsf_tracker* t) {
             w.window_n = t->fin_n[kind];
             w.total = w.prior_n + w.window_n;
             w.dirty = false;
-            TCHK(t, hipStreamWaitEvent(s, t->ev_join[kind], 0));
+            TCHK(t, join_wait(t, kind));
         }
         return LMSF_OK;
     }
@@ -367,8 +432,8 @@ lmsf_status commit_finish(lmsf_tracker* t) {
         w.window_n = n;
         w.total = w.prior_n + n;
         w.dirty = false;
-        TCHK(t, hipEventRecord(t->ev_join[kind], t->ks[kind]));
-        TCHK(t, hipStreamWaitEvent(s, t->ev_join[kind], 0));
+        TCHK(t, join_mark(t, kind, t->ks[kind]));
+        TCHK(t, join_wait(t, kind));
     }
     return LMSF_OK;
 }
@@ -391,6 +456,108 @@ lmsf_status presearch_prediction(lmsf_tracker* t, const double* deltaT) {
     return ctx_presearch(t->ctx, x);
 }
 
+enum { kLookNone = 0, kLookPosted = 1, kLookAdopted = 2 };
+
+// The posted half of lmsf_tracker_commit_map: each changed kind's rebuild enqueued on its aux stream by its worker
+// (A/B builds: on the caller's thread), after everything enqueued on the context stream so far (ev_fork).
+lmsf_status post_commit(lmsf_tracker* t) {
+    TCHK(t, fork_mark(t));
+    if (assign_streams(t) == 0) return LMSF_OK;
+    // A/B builds (diagnostics): the rebuild enqueued on the caller's thread instead of the two workers
+    static const bool inline_commit = ab_int("LMSF_COMMIT_INLINE", 0) != 0;
+    if (inline_commit) {
+        for (int i = 0; i < 2; ++i) {
+            const int kind = t->ks[LMSF_SURF] == t->aux[i] ? LMSF_SURF : t->ks[LMSF_EDGE] == t->aux[i] ? LMSF_EDGE : 0;
+            lmsf_status r = kind ? commit_stage_kind(t, kind, t->aux[i]) : LMSF_OK;
+            if (!r && kind) r = finish_kind(t, kind, t->aux[i]);
+            t->job_rc[i] = r;
+            t->job[i] = 0;
+        }
+        t->staging = true;
+        t->pending = true;
+        return LMSF_OK;
+    }
+    if (!t->worker[0].joinable())
+        for (int i = 0; i < 2; ++i) t->worker[i] = std::thread(worker_main, t, i, ctx_device(t->ctx));
+    {
+        std::lock_guard<std::mutex> lk(t->mu);
+        for (int kind : {LMSF_SURF, LMSF_EDGE})
+            if (t->ks[kind]) t->job[t->ks[kind] == t->aux[0] ? 0 : 1] = kind;
+        t->staging = true;
+        t->posted.fetch_add(1u, std::memory_order_release);
+    }
+    t->cv.notify_all();
+    t->pending = true;
+    return LMSF_OK;
+}
+
+// needUpdataLocalMap (:239-262) of pose T at timestamp: LMSF_UPDATE_TIME / _MOTION / _NONE.
+int gate_type(const lmsf_tracker* t, const Iso& T, double timestamp) {
+    if (timestamp - t->last_kf_time > t->cfg.time_interval) return LMSF_UPDATE_TIME;
+    const Iso d = iso_mul(iso_inverse(t->last_kf), T);
+    const double dt = std::sqrt(d.t[0] * d.t[0] + d.t[1] * d.t[1] + d.t[2] * d.t[2]);
+    double q[4];
+    quat_from_R(d.R, q);
+    const double qn = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    const double angle = std::acos(q[3] / qn) * 2;
+    return (dt > t->cfg.threshold_trans || angle > t->cfg.threshold_rot) ? LMSF_UPDATE_MOTION : LMSF_UPDATE_NONE;
+}
+
+// The lookahead (ctx_arm_post_solve, inside lmsf_solve before its wait): the context's slot-0 features of each kind
+// transformed at the Solve's device-resident result into the spare buffer, which takes the slot push_frame would
+// fill, and the rebuild posted.
+lmsf_status lookahead_post(void* p) {
+    lmsf_tracker* t = static_cast<lmsf_tracker*>(p);
+    const float4* feat;
+    int64_t ne, ns;
+    lmsf_status rc = ctx_slot0_features(t->ctx, &feat, &ne, &ns);
+    if (rc) return rc;
+    const float4* src[3] = {nullptr, feat, feat + ne};
+    const int64_t cnt[3] = {0, ne, ns};
+    for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) {
+        Window& w = t->win[kind];
+        auto& u = t->undo[kind];
+        u.pushed = false;
+        if (cnt[kind] == 0) continue;
+        if (cnt[kind] > t->cap) return fail(t, LMSF_ERR_CAPACITY, "keyframe larger than the tracker slot capacity");
+        const int W = (int)w.slots.size();
+        u = {true, w.count < W ? (w.head + w.count) % W : w.head, w.head, w.count, 0, w.dirty};
+        u.size = w.sizes[u.slot];
+        if (w.count < W) ++w.count;
+        else w.head = (w.head + 1) % W;
+        std::swap(w.slots[u.slot], t->spare[kind]);   // the evicted frame stays in the spare buffer until adopted
+        TCHK(t, launch_transform_pose(src[kind], (int)cnt[kind], ctx_solved_pose(t->ctx), w.slots[u.slot],
+                                      ctx_stream(t->ctx)));
+        w.sizes[u.slot] = (int)cnt[kind];
+        w.dirty = true;
+    }
+    t->look_feat = ctx_feature_seq(t->ctx);
+    t->look_pose_known = false;
+    t->look = kLookPosted;
+    return post_commit(t);
+}
+
+// A posted lookahead the caller did not adopt: its rebuild joined, the windows restored, and rebuilt.
+lmsf_status look_rollback(lmsf_tracker* t) {
+    t->look = kLookNone;
+    lmsf_status rc = commit_finish(t);
+    if (rc) return rc;
+    bool any = false;
+    for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) {
+        auto& u = t->undo[kind];
+        if (!u.pushed) continue;
+        u.pushed = false;
+        Window& w = t->win[kind];
+        std::swap(w.slots[u.slot], t->spare[kind]);
+        w.head = u.head;
+        w.count = u.count;
+        w.sizes[u.slot] = u.size;
+        w.dirty = true;   // the window grid holds the lookahead frame
+        any = true;
+    }
+    return any ? post_commit(t) : LMSF_OK;
+}
+
 // A deferred commit completed before anything that reads or rewrites the windows or the map.  A device fault
 // reported since the maps were built (a look-back / scatter check in a voxel filter or grid build: a faulted filter
 // leaves its window empty, k_voxel.hip) means a grid the context searches may be empty or partial, and that report
@@ -398,6 +565,11 @@ lmsf_status presearch_prediction(lmsf_tracker* t, const double* deltaT) {
 // slots are written by the transforms, never by a filter) before anything reads the map again.
 lmsf_status settle(lmsf_tracker* t) {
     HPROF(12, "tracker settle");
+    if (t->look == kLookPosted) {   // not adopted by the time anything else touches the windows or the map
+        lmsf_status rl = look_rollback(t);
+        if (rl) return rl;
+    }
+    t->look = kLookNone;
     lmsf_status rc = commit_finish(t);
     if (rc) return rc;
     const uint64_t seq = ctx_fault_seq(t->ctx);
@@ -462,11 +634,13 @@ lmsf_status lmsf_tracker_config_init(lmsf_tracker_config* cfg) {
     cfg->manual_map_update = 0;
     cfg->leaf_edge = 0.2;
     cfg->leaf_surf = 0.4;
+    cfg->keyframe_lookahead = 1;
     return LMSF_OK;
 }
 
 void lmsf_tracker_destroy(lmsf_tracker* t) {
     if (!t) return;
+    if (t->counted) g_trackers[ctx_device(t->ctx)].fetch_sub(1);
     hipSetDevice(ctx_device(t->ctx));
     // A deferred commit is completed first (a posted one joined from the workers): its staging already rewrote
     // the context's window grids (points, box read-back), so the context must not keep searching the old sizes
@@ -496,9 +670,11 @@ void lmsf_tracker_destroy(lmsf_tracker* t) {
             hipStreamDestroy(a);
         }
     if (t->ev_fork) hipEventDestroy(t->ev_fork);
+    hipFree(t->flags);
     for (hipEvent_t e : t->ev_join)
         if (e) hipEventDestroy(e);
     hipFree(t->stage);
+    for (float4* p : t->spare) hipFree(p);
     delete t;
 }
 
@@ -508,6 +684,7 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
     lmsf_tracker* t = new lmsf_tracker();
     t->ctx = ctx;
     t->cfg = *cfg;
+    t->cfg.keyframe_lookahead = ab_int("LMSF_LOOKAHEAD", cfg->keyframe_lookahead);   // A/B builds: an override
     t->cap = ctx_feature_capacity(ctx);
     if (hipSetDevice(ctx_device(ctx)) != hipSuccess) { delete t; return LMSF_ERR_HIP; }
     // LMSF_AUX_PRIORITY (A/B): the window rebuild's streams at the device's highest priority, so the rebuild -- the
@@ -519,7 +696,10 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
         hipStreamCreateWithPriority(&t->aux[1], hipStreamNonBlocking, aux_hi ? prio_hi : 0) != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_join[LMSF_EDGE], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&t->ev_join[LMSF_SURF], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&t->ev_join[LMSF_SURF], hipEventDisableTiming) != hipSuccess ||
+        hipMalloc((void**)&t->flags, 4 * sizeof(uint32_t)) != hipSuccess ||
+        hipMemsetAsync(t->flags, 0, 4 * sizeof(uint32_t), ctx_stream(ctx)) != hipSuccess ||
+        hipStreamSynchronize(ctx_stream(ctx)) != hipSuccess) {
         lmsf_tracker_destroy(t);
         return LMSF_ERR_HIP;
     }
@@ -537,6 +717,11 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
             return LMSF_ERR_HIP;
         }
     }
+    for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind)
+        if (hipMalloc((void**)&t->spare[kind], (size_t)t->cap * sizeof(float4)) != hipSuccess) {
+            lmsf_tracker_destroy(t);
+            return LMSF_ERR_HIP;
+        }
     if (hipMalloc((void**)&t->stage, (size_t)t->cap * sizeof(float4)) != hipSuccess) {
         lmsf_tracker_destroy(t);
         return LMSF_ERR_HIP;
@@ -568,6 +753,11 @@ lmsf_status lmsf_tracker_create(lmsf_ctx* ctx, const lmsf_tracker_config* cfg, l
         }
         return settle(tk);
     }, t);
+    const int dev = ctx_device(ctx);
+    if (dev >= 0 && dev < 64) {
+        g_trackers[dev].fetch_add(1);
+        t->counted = true;
+    }
     *out = t;
     return LMSF_OK;
 }
@@ -605,32 +795,46 @@ lmsf_status solve_current(lmsf_tracker* t, double timestamp, double deltaT[16], 
     } else {
         if (is_identity16(deltaT)) t->curr = iso_mul(t->prev, t->motion);   // :125-129
         else t->curr = iso_mul(t->prev, iso_from16(deltaT));
+        // the keyframe lookahead when the prediction already passes the gate (the window rebuild of this scan's
+        // features at the Solve's result is posted while the Solve runs)
+        const bool look = t->cfg.keyframe_lookahead && sole_tracker(t) && gate_type(t, t->curr, timestamp) != LMSF_UPDATE_NONE;
+        if (look) {
+            t->look_recoveries = ctx_loop_recoveries(t->ctx);
+            ctx_arm_post_solve(t->ctx, lookahead_post, t);
+        }
         rc = register_pose(t, t->curr, &r.solve);                      // :131
+        if (t->look == kLookPosted && (rc || ctx_loop_recoveries(t->ctx) != t->look_recoveries)) {
+            // a failed Solve, or one re-run after the lookahead read its first result: not a keyframe of this pose
+            lmsf_status rl = look_rollback(t);
+            if (!rc) rc = rl;
+        }
         if (rc) return rc;
+        if (t->look == kLookPosted) {
+            iso_to16(t->curr, t->look_pose);
+            t->look_pose_known = true;
+        }
         t->motion = iso_mul(iso_inverse(t->prev), t->curr);             // :133
         iso_to16(t->motion, deltaT);
         t->prev = t->curr;
-        // needUpdataLocalMap (:239-262)
-        int type = LMSF_UPDATE_NONE;
-        if (timestamp - t->last_kf_time > t->cfg.time_interval) {
-            type = LMSF_UPDATE_TIME;
-        } else {
-            const Iso d = iso_mul(iso_inverse(t->last_kf), t->curr);
-            const double dt = std::sqrt(d.t[0] * d.t[0] + d.t[1] * d.t[1] + d.t[2] * d.t[2]);
-            double q[4];
-            quat_from_R(d.R, q);
-            const double qn = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-            const double angle = std::acos(q[3] / qn) * 2;
-            if (dt > t->cfg.threshold_trans || angle > t->cfg.threshold_rot) type = LMSF_UPDATE_MOTION;
-        }
+        const int type = gate_type(t, t->curr, timestamp);             // needUpdataLocalMap (:239-262)
         r.update_type = type;
         if (type) {
             t->last_kf = t->curr;
             t->last_kf_time = timestamp;
             if (!manual) {
-                rc = update_local_map(t, t->curr);
-                if (rc) return rc;
+                if (t->look == kLookPosted && t->look_feat == ctx_feature_seq(t->ctx)) {
+                    t->look = kLookNone;   // updateLocalMap's frame: the lookahead's, completed as commit() would
+                    rc = commit_finish(t);
+                    if (rc) return rc;
+                } else {
+                    rc = update_local_map(t, t->curr);
+                    if (rc) return rc;
+                }
             }
+        }
+        if (!manual && t->look == kLookPosted) {   // no keyframe after all
+            rc = look_rollback(t);
+            if (rc) return rc;
         }
     }
     r.local_map_edge = (int64_t)t->win[LMSF_EDGE].total;
@@ -723,6 +927,11 @@ lmsf_status lmsf_tracker_add_keyframe(lmsf_tracker* t, const float* edge, size_t
 lmsf_status lmsf_tracker_add_keyframe_extracted(lmsf_tracker* t, const double pose[16]) {
     if (!t || !pose) return LMSF_ERR_ARG;
     if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    if (t->look == kLookPosted && t->look_pose_known && std::memcmp(pose, t->look_pose, sizeof t->look_pose) == 0 &&
+        t->look_feat == ctx_feature_seq(t->ctx)) {
+        t->look = kLookAdopted;   // this frame is in the window already, its rebuild posted
+        return LMSF_OK;
+    }
     {
         lmsf_status rs = settle(t);
         if (rs) return rs;
@@ -745,38 +954,15 @@ lmsf_status lmsf_tracker_commit_map(lmsf_tracker* t) {
     if (!t) return LMSF_ERR_ARG;
     HPROF(13, "commit_map call");
     if (hipSetDevice(ctx_device(t->ctx)) != hipSuccess) return LMSF_ERR_HIP;
+    if (t->look == kLookAdopted) {   // the adopted lookahead's rebuild is this commit, posted already
+        t->look = kLookNone;
+        return LMSF_OK;
+    }
     lmsf_status rc = settle(t);
     if (rc) return rc;
     // the keyframe transforms enqueued so far on the context stream, then each changed kind's rebuild enqueued
     // by its worker on its aux stream
-    TCHK(t, hipEventRecord(t->ev_fork, ctx_stream(t->ctx)));
-    if (assign_streams(t) == 0) return LMSF_OK;
-    // A/B builds (diagnostics): the rebuild enqueued on the caller's thread instead of the two workers
-    static const bool inline_commit = ab_int("LMSF_COMMIT_INLINE", 0) != 0;
-    if (inline_commit) {
-        for (int i = 0; i < 2; ++i) {
-            const int kind = t->ks[LMSF_SURF] == t->aux[i] ? LMSF_SURF : t->ks[LMSF_EDGE] == t->aux[i] ? LMSF_EDGE : 0;
-            lmsf_status r = kind ? commit_stage_kind(t, kind, t->aux[i]) : LMSF_OK;
-            if (!r && kind) r = finish_kind(t, kind, t->aux[i]);
-            t->job_rc[i] = r;
-            t->job[i] = 0;
-        }
-        t->staging = true;
-        t->pending = true;
-        return LMSF_OK;
-    }
-    if (!t->worker[0].joinable())
-        for (int i = 0; i < 2; ++i) t->worker[i] = std::thread(worker_main, t, i, ctx_device(t->ctx));
-    {
-        std::lock_guard<std::mutex> lk(t->mu);
-        for (int kind : {LMSF_SURF, LMSF_EDGE})
-            if (t->ks[kind]) t->job[t->ks[kind] == t->aux[0] ? 0 : 1] = kind;
-        t->staging = true;
-        t->posted.fetch_add(1u, std::memory_order_release);
-    }
-    t->cv.notify_all();
-    t->pending = true;
-    return LMSF_OK;
+    return post_commit(t);
 }
 
 lmsf_status lmsf_tracker_register(lmsf_tracker* t, const float* edge, size_t n_edge, const float* surf,

@@ -53,7 +53,8 @@ class KernelStats(C.Structure):
     _fields_ = [("launches", C.c_int64), ("total_ms", C.c_double), ("queries", C.c_int64), ("n27_sum", C.c_int64),
                 ("fused_launches", C.c_int64), ("reused_queries", C.c_int64),
                 ("refit_queries", C.c_int64), ("loop_recoveries", C.c_int64),
-                ("buffer_growths", C.c_int64), ("split_searches", C.c_int64)]
+                ("buffer_growths", C.c_int64), ("split_searches", C.c_int64),
+                ("lookahead_solves", C.c_int64)]
 
 
 class ExtractParams(C.Structure):
@@ -70,7 +71,7 @@ class CommonParams(C.Structure):
 class TrackerConfig(C.Structure):
     _fields_ = [("window_frames", C.c_int32), ("threshold_trans", C.c_double), ("threshold_rot", C.c_double),
                 ("time_interval", C.c_double), ("manual_map_update", C.c_int32), ("leaf_edge", C.c_double),
-                ("leaf_surf", C.c_double)]
+                ("leaf_surf", C.c_double), ("keyframe_lookahead", C.c_int32)]
 
 
 class IngestParams(C.Structure):
@@ -489,13 +490,14 @@ class Tracker:
     """lmsf_tracker: LidarTrackerLocalMap over a Context (poses are 4x4 row-major matrices)."""
 
     def __init__(self, ctx: Context, window_frames=10, threshold_trans=0.3, threshold_rot=0.1, time_interval=10.0,
-                 manual_map_update=False, leaf_edge=0.2, leaf_surf=0.4):
+                 manual_map_update=False, leaf_edge=0.2, leaf_surf=0.4, keyframe_lookahead=True):
         cfg = TrackerConfig()
         load().lmsf_tracker_config_init(C.byref(cfg))
         cfg.window_frames, cfg.threshold_trans = window_frames, threshold_trans
         cfg.threshold_rot, cfg.time_interval = threshold_rot, time_interval
         cfg.manual_map_update = int(bool(manual_map_update))
         cfg.leaf_edge, cfg.leaf_surf = leaf_edge, leaf_surf
+        cfg.keyframe_lookahead = int(bool(keyframe_lookahead))
         self.ctx = ctx
         h = C.c_void_p()
         ctx._check(load().lmsf_tracker_create(ctx.h, C.byref(cfg), C.byref(h)))

@@ -1220,3 +1220,55 @@ def test_dist_example(lib, oracle_mod, small_workload, tmp_path):
     ox, _, _ = reg.solve(g)
     dt, dr = pose_err(x, ox)
     assert dt <= POSE_TOL and dr <= POSE_TOL
+
+
+def test_tracker_keyframe_lookahead_exact(lib, oracle_mod, sequence_workload):
+    """The keyframe lookahead (lmsf_tracker_config.keyframe_lookahead: the window rebuild with the scan's features at
+    the Solve's device-resident result, posted while the Solve runs; used while the tracker is alone on its device,
+    with the flag-ordered fork / join) changes nothing: a manual-mode tracker on an extracted sequence, lookahead on and
+    off, gives bit-identical poses, decisions, map sizes and final local maps -- while the caller adopts it (its own
+    keyframe at lmsf_tracker_pose), skips a keyframe the gate asked for, appends host features instead, or appends at a
+    different pose (each of the last three undoes it), and where the prediction and the gate disagree (window of 3,
+    mixed decisions)."""
+    wl = sequence_workload
+
+    def run(look):
+        ctx = _ctx(lib, n_scans=wl.n_scans, max_batch=1)
+        tr = lib.Tracker(ctx, window_frames=3, manual_map_update=True, keyframe_lookahead=look)
+        ctx.kernel_stats_reset(timing=False)
+        steps = []
+        for i, scan in enumerate(wl.scans):
+            ctx.extract(scan)
+            _, r = tr.solve_extracted(wl.dt * i)
+            P = tr.pose()
+            if r.update_type:
+                if i == 3:
+                    pass                                          # the gate's keyframe skipped by the caller
+                elif i == 5:
+                    ge, _ = ctx.copy_features(lib.EDGE)
+                    gs, _ = ctx.copy_features(lib.SURF)
+                    tr.add_keyframe(ge, gs, P)                    # the same frame, as host data
+                    tr.commit_map()
+                elif i == 7:
+                    Q = P.copy()
+                    Q[0, 3] += 0.01
+                    tr.add_keyframe_extracted(Q)                  # another pose
+                    tr.commit_map()
+                else:
+                    tr.add_keyframe_extracted(P)
+                    tr.commit_map()
+            steps.append((P, r.update_type, r.local_map_edge, r.local_map_surf))
+        maps = [tr.local_map(k) for k in (lib.EDGE, lib.SURF)]
+        looks = ctx.kernel_stats().lookahead_solves
+        tr.close()
+        return steps, maps, looks
+
+    a, ma, la = run(True)
+    b, mb, lb = run(False)
+    assert la >= 3 and lb == 0, (la, lb)
+    for i, ((Pa, ta, ea, sa), (Pb, tb, eb, sb)) in enumerate(zip(a, b)):
+        assert np.array_equal(Pa, Pb), (i, Pa - Pb)
+        assert (ta, ea, sa) == (tb, eb, sb), i
+    assert 0 in [s[1] for s in a[1:]] and 1 in [s[1] for s in a[1:]]
+    for x, y in zip(ma, mb):
+        assert x.tobytes() == y.tobytes()
