@@ -311,11 +311,10 @@ struct lmsf_ctx {
     // trackers on this context with a deferred keyframe commit (lmsf_tracker_commit_map): completed
     // before any map consumer of the context (resolve_all_lim1) or a map replacement
     std::vector<std::pair<lmsf_status (*)(void*), void*>> settle_hooks;
-    // armed for one lmsf_solve: called once its kernels and its result's read-back are enqueued, before the host
-    // waits (a tracker's keyframe lookahead enqueues the next window rebuild there); the wait is then on ev_solved
+    // armed for one lmsf_solve: called once its kernels are enqueued, before its result's read-back and the host wait
+    // (a tracker's keyframe lookahead enqueues the next window rebuild there)
     lmsf_status (*post_solve)(void*) = nullptr;
     void* post_solve_arg = nullptr;
-    hipEvent_t ev_solved = nullptr;
     int64_t slot0_ne = 0, slot0_ns = 0;
     int last_outer = 0;
     int batch_done = 0;               // slots whose SolveState the last lmsf_batch_wait read back into h_st
@@ -1167,7 +1166,6 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (c->h_pre) hipHostFree(c->h_pre);
     if (c->ev_pre) hipEventDestroy(c->ev_pre);
     if (c->ev_pre_after) hipEventDestroy(c->ev_pre_after);
-    if (c->ev_solved) hipEventDestroy(c->ev_solved);
     if (c->pre_stream) hipStreamDestroy(c->pre_stream);
     gfree(c->wl2, c->stream);
     gfree(c->wlim2, c->stream);
@@ -1430,18 +1428,15 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     if (rc) return rc;
     rc = release_prefetch(c);   // a held prefetch follows this Solve's kernels
     if (rc) return rc;
+    if (post) {   // the armed call: work that follows this Solve on the device, enqueued while it runs -- ahead of
+                  // the result's read-back, whose copies would put ~20-40 us between the last search kernel and it
+        c->post_solves++;
+        rc = post(c->post_solve_arg);
+        if (rc) return rc;
+    }
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(SolveState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&c->h_pack[3], c->d_error + 16, 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    if (post) {   // the armed call: work that follows this Solve on the device, enqueued while it runs
-        auto fn = post;
-        c->post_solves++;
-        if (!c->ev_solved) HIPCHK(c, hipEventCreateWithFlags(&c->ev_solved, hipEventDisableTiming));
-        HIPCHK(c, hipEventRecord(c->ev_solved, c->stream));
-        rc = fn(c->post_solve_arg);
-        if (rc) return rc;
-        HPROF(6, "solve wait");
-        HIPCHK(c, hipEventSynchronize(c->ev_solved));
-    } else {
+    {
         HPROF(6, "solve wait");
         HIPCHK(c, stream_wait(c->stream));
     }

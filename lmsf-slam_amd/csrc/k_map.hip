@@ -148,7 +148,7 @@ hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hi
 // The same transform at a pose the device holds (x = qx qy qz qw tx ty tz, a Solve's result): the matrix as the host
 // builds it (tracker.cpp R_from_quat, Eigen's toRotationMatrix; t = x[4..6]), then transform_kernel's arithmetic --
 // the same bits as launch_transform with the host's copy of that pose.
-__global__ void transform_pose_kernel(const float4* in, int n, const double* x, float4* out) {
+__global__ void transform_pose_kernel(const float4* in, int n, const double* x, float4* out, int n0, float4* out1) {
 #pragma clang fp contract(off)
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -165,12 +165,21 @@ __global__ void transform_pose_kernel(const float4* in, int n, const double* x, 
     o.y = (float)(m[4] * px + m[5] * py + m[6] * pz + m[7]);
     o.z = (float)(m[8] * px + m[9] * py + m[10] * pz + m[11]);
     o.w = p.w;
-    out[i] = o;
+    if (i < n0) out[i] = o;
+    else out1[i - n0] = o;
 }
 
 hipError_t launch_transform_pose(const float4* in, int n, const double* x, float4* out, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(transform_pose_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, x, out);
+    hipLaunchKernelGGL(transform_pose_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, x, out, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_transform_pose2(const float4* in, int n0, int n1, const double* x, float4* out0, float4* out1,
+                                  hipStream_t s) {
+    const int n = n0 + n1;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(transform_pose_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, x, out0, n0, out1);
     return hipGetLastError();
 }
 

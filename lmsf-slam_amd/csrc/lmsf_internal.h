@@ -347,6 +347,9 @@ struct Affine34 { double m[12]; };   // row-major 3x4 of an Isometry3d matrix
 hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hipStream_t s);
 // ... at the pose x[7] (qx qy qz qw tx ty tz) in device memory, its matrix built as the tracker's host code builds it
 hipError_t launch_transform_pose(const float4* in, int n, const double* x, float4* out, hipStream_t s);
+// two clouds in one launch: in[0..n0) -> out0, in[n0..n0+n1) -> out1 (a scan's edge and surf features)
+hipError_t launch_transform_pose2(const float4* in, int n0, int n1, const double* x, float4* out0, float4* out1,
+                                  hipStream_t s);
 // flag <- v after the work enqueued on s so far; s waits until flag reaches v (wrap-safe), bounded (err |= kFaultStreamWait)
 hipError_t launch_flag_signal(uint32_t* flag, uint32_t v, hipStream_t s);
 hipError_t launch_flag_wait(const uint32_t* flag, uint32_t v, int* err, hipStream_t s);
@@ -419,7 +422,7 @@ lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg);
 // a tracker's deferred-commit completion, run by the context before its map consumers
 void ctx_add_settle(lmsf_ctx* c, lmsf_status (*fn)(void*), void* arg);
 void ctx_remove_settle(lmsf_ctx* c, void* arg);
-// fn(arg) once, inside the next lmsf_solve: after its kernels and its result's read-back are enqueued, before its
+// fn(arg) once, inside the next lmsf_solve: after its kernels are enqueued, before its result's read-back and its
 // host wait (a tracker's keyframe lookahead); ctx_solved_pose: that Solve's result on the device (x[7]);
 // ctx_loop_recoveries: lmsf_kernel_stats' count (a recovered Solve re-ran after the armed call)
 void ctx_arm_post_solve(lmsf_ctx* c, lmsf_status (*fn)(void*), void* arg);

@@ -512,28 +512,30 @@ lmsf_status lookahead_post(void* p) {
     int64_t ne, ns;
     lmsf_status rc = ctx_slot0_features(t->ctx, &feat, &ne, &ns);
     if (rc) return rc;
-    const float4* src[3] = {nullptr, feat, feat + ne};
     const int64_t cnt[3] = {0, ne, ns};
+    if (ne > t->cap || ns > t->cap) return fail(t, LMSF_ERR_CAPACITY, "keyframe larger than the tracker slot capacity");
+    float4* dst[3] = {nullptr, nullptr, nullptr};
     for (int kind = LMSF_EDGE; kind <= LMSF_SURF; ++kind) {
         Window& w = t->win[kind];
         auto& u = t->undo[kind];
         u.pushed = false;
         if (cnt[kind] == 0) continue;
-        if (cnt[kind] > t->cap) return fail(t, LMSF_ERR_CAPACITY, "keyframe larger than the tracker slot capacity");
         const int W = (int)w.slots.size();
         u = {true, w.count < W ? (w.head + w.count) % W : w.head, w.head, w.count, 0, w.dirty};
         u.size = w.sizes[u.slot];
         if (w.count < W) ++w.count;
         else w.head = (w.head + 1) % W;
         std::swap(w.slots[u.slot], t->spare[kind]);   // the evicted frame stays in the spare buffer until adopted
-        TCHK(t, launch_transform_pose(src[kind], (int)cnt[kind], ctx_solved_pose(t->ctx), w.slots[u.slot],
-                                      ctx_stream(t->ctx)));
+        dst[kind] = w.slots[u.slot];
         w.sizes[u.slot] = (int)cnt[kind];
         w.dirty = true;
     }
     t->look_feat = ctx_feature_seq(t->ctx);
     t->look_pose_known = false;
-    t->look = kLookPosted;
+    t->look = kLookPosted;   // from here a failure is undone by the caller (solve_current's look_rollback)
+    // both kinds in one launch (edges then surfs, as slot 0 holds them); a kind without features writes nothing
+    TCHK(t, launch_transform_pose2(feat, (int)ne, (int)ns, ctx_solved_pose(t->ctx), dst[LMSF_EDGE], dst[LMSF_SURF],
+                                   ctx_stream(t->ctx)));
     return post_commit(t);
 }
 
