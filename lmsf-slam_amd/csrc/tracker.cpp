@@ -155,6 +155,7 @@ struct lmsf_tracker {
     uint32_t fork_val = 0, join_val[3] = {0, 0, 0};
     bool fork_flags = false, join_flags[3] = {false, false, false};   // the mode each mark used (its wait uses the same)
     bool counted = false;         // in g_trackers
+    bool fin_defer[3] = {false, false, false};   // a worker left this kind's box read-back to commit_finish
     hipStream_t ks[3] = {nullptr, nullptr, nullptr};   // staged commit: stream per kind (null: unchanged)
     size_t nmax[3] = {0, 0, 0};
     bool pending = false;                               // staged, not yet finished
@@ -352,11 +353,16 @@ lmsf_status join_worker(lmsf_tracker* t) {
 // One kind's half of commit_finish on its stage stream: wait for the stage's read-back, enqueue the grid
 // build, mark its end for the context stream.
 lmsf_status finish_kind(lmsf_tracker* t, int kind, hipStream_t ks) {
-    // a device-built grid (filtered windows) needs only its box read-back, which the finish waits for itself:
-    // the rest of the build stays queued, and the context stream joins it on the device (ev_join)
-    if (!(t->win[kind].leaf > 0)) TCHK(t, stream_wait(ks));
-    lmsf_status rc = ctx_window_finish(t->ctx, kind, t->nmax[kind], ks, &t->fin_n[kind]);
-    if (rc) return rc;
+    // a device-built grid (filtered windows) is built whole on ks: only its box read-back is left, which the caller's
+    // thread takes after the join (commit_finish: the host wait -- then usually over -- stays off the workers, whose
+    // long waits behind a lookahead rebuild held the caller's enqueues: r06 host probes, 150 us per prefetch call);
+    // a staged window reads its box back here first and builds its grid on ks
+    t->fin_defer[kind] = t->win[kind].leaf > 0;
+    if (!t->fin_defer[kind]) {
+        TCHK(t, stream_wait(ks));
+        lmsf_status rc = ctx_window_finish(t->ctx, kind, t->nmax[kind], ks, &t->fin_n[kind]);
+        if (rc) return rc;
+    }
     TCHK(t, join_mark(t, kind, ks));
     return LMSF_OK;
 }
@@ -409,13 +415,20 @@ lmsf_status commit_finish(lmsf_tracker* t) {
         lmsf_status rj = join_worker(t);
         t->pending = false;
         if (rj) return rj;
+        for (int kind : {LMSF_SURF, LMSF_EDGE})
+            if (t->ks[kind]) TCHK(t, join_wait(t, kind));
         for (int kind : {LMSF_SURF, LMSF_EDGE}) {
             if (!t->ks[kind]) continue;
+            if (t->fin_defer[kind]) {   // its box read-back (an over-capacity grid is rebuilt on the context stream,
+                                        // after the join)
+                t->fin_defer[kind] = false;
+                lmsf_status rc = ctx_window_finish(t->ctx, kind, t->nmax[kind], s, &t->fin_n[kind]);
+                if (rc) return rc;
+            }
             Window& w = t->win[kind];
             w.window_n = t->fin_n[kind];
             w.total = w.prior_n + w.window_n;
             w.dirty = false;
-            TCHK(t, join_wait(t, kind));
         }
         return LMSF_OK;
     }
