@@ -171,9 +171,6 @@ struct lmsf_ctx {
     // prior-grid pass of the next Solve's outer iteration 0 (ctx_presearch: enqueued before a tracker's window rebuild
     // is joined, so it runs beside it); used by the next lmsf_solve at the same pose, dropped by any other call
     double* pre_keys = nullptr;       // [B][F][6]
-    double* h_pre_pose = nullptr;     // pinned / device copies of its pose (never the caller's h_poses / d_poses, which
-    double* d_pre_pose = nullptr;     //   a map consumer settling inside its own call has just uploaded)
-    hipEvent_t ev_pre_pose = nullptr; // that upload done: h_pre_pose reusable
     uint64_t st_epoch = 0;            // launches that (re)wrote the slots' SolveState (state init, solves, matches)
     uint64_t pre_st_epoch = ~0ull;    // st_epoch right after ctx_presearch's state init
     bool skip_state_init = false;     // this enqueue_solve: st already initialised at its pose by ctx_presearch
@@ -1174,9 +1171,6 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     hipFree(c->cap_nn);
     hipFree(c->cap_pose);
     hipFree(c->pre_keys);
-    hipFree(c->d_pre_pose);
-    if (c->h_pre_pose) hipHostFree(c->h_pre_pose);
-    if (c->ev_pre_pose) hipEventDestroy(c->ev_pre_pose);
     c->voxel.release();
     hipFree(c->vox_in);
     hipFree(c->vox_out);
@@ -2361,20 +2355,13 @@ lmsf_status ctx_presearch(lmsf_ctx* c, const double x[7]) {
         rc = resolve_lim1(c, c->prior[k]);
         if (rc) return rc;
     }
-    if (!c->pre_keys) {
-        HIPCHK(c, dalloc(&c->pre_keys, (size_t)c->B * c->F * 6));
-        HIPCHK(c, dalloc(&c->d_pre_pose, 7));
-        HIPCHK(c, hipHostMalloc((void**)&c->h_pre_pose, 7 * sizeof(double), hipHostMallocDefault));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_pre_pose, hipEventDisableTiming));
-    } else {
-        HIPCHK(c, hipEventSynchronize(c->ev_pre_pose));   // the previous presearch's upload has left h_pre_pose
-    }
+    if (!c->pre_keys) HIPCHK(c, dalloc(&c->pre_keys, (size_t)c->B * c->F * 6));
     hipStream_t s = c->stream;
-    std::memcpy(c->h_pre_pose, x, 7 * sizeof(double));
-    HIPCHK(c, hipMemcpyAsync(c->d_pre_pose, c->h_pre_pose, 7 * sizeof(double), hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipEventRecord(c->ev_pre_pose, s));
     BatchView bv = c->bview(1);
-    HIPCHK(c, launch_state_init(bv, c->d_pre_pose, s));
+    // the pose as a kernel argument (r06: its pinned upload, event and copy -> kernel transition cost ~20 us of host
+    // time per scan; never the caller's h_poses / d_poses, which a map consumer settling inside its own call has
+    // just uploaded)
+    HIPCHK(c, launch_state_init_pose(bv, x, s));
     c->pre_st_epoch = ++c->st_epoch;
     bv.n27 = nullptr;    // the window pass counts the queries
     bv.memo = 0;

@@ -20,12 +20,15 @@
 
 namespace lmsf {
 
-// Initialise slot states from host poses (qx qy qz qw tx ty tz).
-__global__ void state_init_kernel(BatchView bv, const double* poses) {
+struct Pose7 { double x[7]; };
+
+// Initialise slot states from poses (qx qy qz qw tx ty tz): poses [B][7] in device memory, or (p, one slot) a pose
+// passed by value -- no upload before the launch
+__global__ void state_init_kernel(BatchView bv, const double* poses, Pose7 p) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= bv.B) return;
     SolveState& S = bv.st[b];
-    for (int i = 0; i < 7; ++i) S.x[i] = poses[b * 7 + i];
+    for (int i = 0; i < 7; ++i) S.x[i] = poses ? poses[b * 7 + i] : p.x[i];
     S.inner_total = S.evals_total = S.outer_run = 0;
     S.gn_converged = 0;
     S.done = 1;
@@ -331,7 +334,15 @@ hipError_t launch_stamp(unsigned long long* out, hipStream_t s) {
 }
 
 hipError_t launch_state_init(const BatchView& bv, const double* poses, hipStream_t s) {
-    hipLaunchKernelGGL(state_init_kernel, dim3((bv.B + 63) / 64), dim3(64), 0, s, bv, poses);
+    hipLaunchKernelGGL(state_init_kernel, dim3((bv.B + 63) / 64), dim3(64), 0, s, bv, poses, Pose7{});
+    return hipGetLastError();
+}
+
+hipError_t launch_state_init_pose(const BatchView& bv, const double x[7], hipStream_t s) {
+    if (bv.B != 1) return hipErrorInvalidValue;
+    Pose7 p;
+    for (int i = 0; i < 7; ++i) p.x[i] = x[i];
+    hipLaunchKernelGGL(state_init_kernel, dim3(1), dim3(64), 0, s, bv, nullptr, p);
     return hipGetLastError();
 }
 

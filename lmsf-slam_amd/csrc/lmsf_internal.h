@@ -300,6 +300,8 @@ bool match_fit_prune(const GridView& edge, const GridView& surf);   // dense map
 hipError_t launch_capture(const BatchView& bv, int b, int by_pos, lmsf_record* rec, int32_t* nn, double* pose,
                           hipStream_t s);
 hipError_t launch_state_init(const BatchView& bv, const double* poses, hipStream_t s);
+// one slot (bv.B == 1) at a pose passed by value (no host-to-device copy before it)
+hipError_t launch_state_init_pose(const BatchView& bv, const double x[7], hipStream_t s);
 hipError_t launch_stamp(unsigned long long* out, hipStream_t s);   // wall clock after the stream's prior work
 // Standalone evaluation at one pose (diagnostics): packet of slot 0 into out29 (device).
 hipError_t launch_eval_at(const BatchView& bv, const double* pose_dev, double* out_dev, hipStream_t s);
