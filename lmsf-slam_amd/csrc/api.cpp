@@ -311,6 +311,7 @@ struct lmsf_ctx {
     // armed for one lmsf_solve: called once its kernels are enqueued, before its result's read-back and the host wait
     // (a tracker's keyframe lookahead enqueues the next window rebuild there)
     lmsf_status (*post_solve)(void*) = nullptr;
+    lmsf_status (*post_undo)(void*) = nullptr;   // called before a recovery re-run of that Solve
     void* post_solve_arg = nullptr;
     int64_t slot0_ne = 0, slot0_ns = 0;
     int last_outer = 0;
@@ -1392,7 +1393,9 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     if (!c || !pose) return LMSF_ERR_ARG;
     HPROF(5, "solve total");
     const auto post = c->post_solve;   // armed for this call only, whatever its outcome
+    const auto undo = c->post_undo;
     c->post_solve = nullptr;
+    c->post_undo = nullptr;
     HIPCHK(c, hipSetDevice(c->cfg.device));
     lmsf_status rc = ctx_settle(c);   // a deferred tracker commit may be the first map of this context
     if (rc) return rc;
@@ -1437,6 +1440,10 @@ lmsf_status lmsf_solve(lmsf_ctx* c, double pose[7], lmsf_solve_stats* stats) {
     if (c->h_pack[4]) return report_fault(c, c->h_pack[4]);
     rc = collect_timing(c, true);
     if (rc) return rc;
+    if (c->h_pack[3] && post && undo) {   // the armed call's work follows the faulted run: undone before the re-run
+        rc = undo(c->post_solve_arg);
+        if (rc) return rc;
+    }
     if (c->h_pack[3]) {
         rc = loop_recover(c, 1, iters);
         if (rc) return rc;
@@ -2315,8 +2322,9 @@ lmsf_status ctx_fail(lmsf_ctx* c, lmsf_status code, const char* msg) { return c-
 
 void ctx_add_settle(lmsf_ctx* c, lmsf_status (*fn)(void*), void* arg) { c->settle_hooks.emplace_back(fn, arg); }
 
-void ctx_arm_post_solve(lmsf_ctx* c, lmsf_status (*fn)(void*), void* arg) {
+void ctx_arm_post_solve(lmsf_ctx* c, lmsf_status (*fn)(void*), lmsf_status (*undo)(void*), void* arg) {
     c->post_solve = fn;
+    c->post_undo = undo;
     c->post_solve_arg = arg;
 }
 

@@ -427,7 +427,8 @@ void ctx_remove_settle(lmsf_ctx* c, void* arg);
 // fn(arg) once, inside the next lmsf_solve: after its kernels are enqueued, before its result's read-back and its
 // host wait (a tracker's keyframe lookahead); ctx_solved_pose: that Solve's result on the device (x[7]);
 // ctx_loop_recoveries: lmsf_kernel_stats' count (a recovered Solve re-ran after the armed call)
-void ctx_arm_post_solve(lmsf_ctx* c, lmsf_status (*fn)(void*), void* arg);
+// undo(arg): called before a recovery re-run of that Solve (the armed work must not run beside it)
+void ctx_arm_post_solve(lmsf_ctx* c, lmsf_status (*fn)(void*), lmsf_status (*undo)(void*), void* arg);
 const double* ctx_solved_pose(const lmsf_ctx* c);
 int64_t ctx_loop_recoveries(const lmsf_ctx* c);
 uint64_t ctx_feature_seq(const lmsf_ctx* c);   // changes whenever slot 0's features do

@@ -815,7 +815,9 @@ lmsf_status solve_current(lmsf_tracker* t, double timestamp, double deltaT[16], 
         const bool look = t->cfg.keyframe_lookahead && sole_tracker(t) && gate_type(t, t->curr, timestamp) != LMSF_UPDATE_NONE;
         if (look) {
             t->look_recoveries = ctx_loop_recoveries(t->ctx);
-            ctx_arm_post_solve(t->ctx, lookahead_post, t);
+            // a recovered Solve (lm_loop's bounded wait given up) re-runs only after the lookahead is undone and the
+            // restored window rebuilt and joined: the re-run must not search a window being rebuilt
+            ctx_arm_post_solve(t->ctx, lookahead_post, [](void* p) { return settle(static_cast<lmsf_tracker*>(p)); }, t);
         }
         rc = register_pose(t, t->curr, &r.solve);                      // :131
         if (t->look == kLookPosted && (rc || ctx_loop_recoveries(t->ctx) != t->look_recoveries)) {

@@ -1228,18 +1228,23 @@ def test_tracker_keyframe_lookahead_exact(lib, oracle_mod, sequence_workload):
     with the flag-ordered fork / join) changes nothing: a manual-mode tracker on an extracted sequence, lookahead on and
     off, gives bit-identical poses, decisions, map sizes and final local maps -- while the caller adopts it (its own
     keyframe at lmsf_tracker_pose), skips a keyframe the gate asked for, appends host features instead, or appends at a
-    different pose (each of the last three undoes it), and where the prediction and the gate disagree (window of 3,
-    mixed decisions)."""
+    different pose (each of the last three undoes it), where the prediction and the gate disagree (window of 3,
+    mixed decisions), and where the Solve is recovered (LMSF_OPT_LOOP_FAULT_TEST: the lookahead is undone and the
+    window rebuilt before the re-run)."""
     wl = sequence_workload
 
     def run(look):
         ctx = _ctx(lib, n_scans=wl.n_scans, max_batch=1)
         tr = lib.Tracker(ctx, window_frames=3, manual_map_update=True, keyframe_lookahead=look)
         ctx.kernel_stats_reset(timing=False)
-        steps = []
+        steps, faulted_look = [], []
         for i, scan in enumerate(wl.scans):
             ctx.extract(scan)
+            ctx.set_option(lib.OPT_LOOP_FAULT_TEST, 1 if i in (2, 6) else 0)   # recovered Solves (undo first)
+            l0 = ctx.kernel_stats().lookahead_solves
             _, r = tr.solve_extracted(wl.dt * i)
+            if i in (2, 6):
+                faulted_look.append(ctx.kernel_stats().lookahead_solves > l0)
             P = tr.pose()
             if r.update_type:
                 if i == 3:
@@ -1259,13 +1264,14 @@ def test_tracker_keyframe_lookahead_exact(lib, oracle_mod, sequence_workload):
                     tr.commit_map()
             steps.append((P, r.update_type, r.local_map_edge, r.local_map_surf))
         maps = [tr.local_map(k) for k in (lib.EDGE, lib.SURF)]
-        looks = ctx.kernel_stats().lookahead_solves
+        ks = ctx.kernel_stats()
         tr.close()
-        return steps, maps, looks
+        return steps, maps, ks.lookahead_solves, ks.loop_recoveries, faulted_look
 
-    a, ma, la = run(True)
-    b, mb, lb = run(False)
+    a, ma, la, ra, fa = run(True)
+    b, mb, lb, rb, _ = run(False)
     assert la >= 3 and lb == 0, (la, lb)
+    assert ra == rb == 2 and any(fa), (ra, rb, fa)      # a recovered Solve with its lookahead posted
     for i, ((Pa, ta, ea, sa), (Pb, tb, eb, sb)) in enumerate(zip(a, b)):
         assert np.array_equal(Pa, Pb), (i, Pa - Pb)
         assert (ta, ea, sa) == (tb, eb, sb), i
