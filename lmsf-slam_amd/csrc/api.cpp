@@ -312,6 +312,7 @@ struct lmsf_ctx {
     // (a tracker's keyframe lookahead enqueues the next window rebuild there)
     lmsf_status (*post_solve)(void*) = nullptr;
     lmsf_status (*post_undo)(void*) = nullptr;   // called before a recovery re-run of that Solve
+    hipEvent_t ev_side = nullptr, ev_side_done = nullptr;   // ctx_presearch on the prefetch stream (A/B)
     void* post_solve_arg = nullptr;
     int64_t slot0_ne = 0, slot0_ns = 0;
     int last_outer = 0;
@@ -1164,6 +1165,8 @@ void lmsf_ctx_destroy(lmsf_ctx* c) {
     if (c->h_pre) hipHostFree(c->h_pre);
     if (c->ev_pre) hipEventDestroy(c->ev_pre);
     if (c->ev_pre_after) hipEventDestroy(c->ev_pre_after);
+    if (c->ev_side) hipEventDestroy(c->ev_side);
+    if (c->ev_side_done) hipEventDestroy(c->ev_side_done);
     if (c->pre_stream) hipStreamDestroy(c->pre_stream);
     gfree(c->wl2, c->stream);
     gfree(c->wlim2, c->stream);
@@ -2347,6 +2350,9 @@ void ctx_remove_settle(lmsf_ctx* c, void* arg) {
 // so the walk over the static prior -- most of iteration 0's search on C4's 5M-point prior -- runs beside the rebuild
 // and only the window pass waits for it.  Best effort: LMSF_OK without enqueueing anything when the next Solve would
 // not take the 8-lane memo search on a prior + window map (then that Solve searches as before).
+#ifndef LMSF_PRESEARCH_SIDE
+#define LMSF_PRESEARCH_SIDE 0
+#endif
 lmsf_status ctx_presearch(lmsf_ctx* c, const double x[7]) {
     if (c->pre_valid && std::memcmp(x, c->pre_pose, sizeof c->pre_pose) == 0) return LMSF_OK;   // already enqueued
     c->pre_valid = false;
@@ -2365,6 +2371,19 @@ lmsf_status ctx_presearch(lmsf_ctx* c, const double x[7]) {
     }
     if (!c->pre_keys) HIPCHK(c, dalloc(&c->pre_keys, (size_t)c->B * c->F * 6));
     hipStream_t s = c->stream;
+    // A/B builds (LMSF_PRESEARCH_SIDE=1): on the prefetch stream (normal priority) after everything enqueued on the
+    // context stream so far, which then waits for it -- so the pass no longer takes the CUs ahead of the window
+    // rebuild it runs beside
+    static const bool side = ab_int("LMSF_PRESEARCH_SIDE", LMSF_PRESEARCH_SIDE) != 0;
+    if (side && c->pre_stream) {
+        if (!c->ev_side) {
+            HIPCHK(c, hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
+            HIPCHK(c, hipEventCreateWithFlags(&c->ev_side_done, hipEventDisableTiming));
+        }
+        HIPCHK(c, hipEventRecord(c->ev_side, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->pre_stream, c->ev_side, 0));
+        s = c->pre_stream;
+    }
     BatchView bv = c->bview(1);
     // the pose as a kernel argument (r06: its pinned upload, event and copy -> kernel transition cost ~20 us of host
     // time per scan; never the caller's h_poses / d_poses, which a map consumer settling inside its own call has
@@ -2379,6 +2398,10 @@ lmsf_status ctx_presearch(lmsf_ctx* c, const double x[7]) {
     if (t) {
         HIPCHK(c, launch_stamp(c->d_stamps + c->ev_used + 1, s));
         c->ev_used += 2;
+    }
+    if (s != c->stream) {   // every later use of the state or the keys on the context stream follows the pass
+        HIPCHK(c, hipEventRecord(c->ev_side_done, s));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_side_done, 0));
     }
     std::memcpy(c->pre_pose, x, sizeof c->pre_pose);
     c->pre_valid = true;
