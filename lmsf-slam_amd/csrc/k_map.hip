@@ -169,12 +169,6 @@ __global__ void transform_pose_kernel(const float4* in, int n, const double* x, 
     else out1[i - n0] = o;
 }
 
-hipError_t launch_transform_pose(const float4* in, int n, const double* x, float4* out, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(transform_pose_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, x, out, n, out);
-    return hipGetLastError();
-}
-
 hipError_t launch_transform_pose2(const float4* in, int n0, int n1, const double* x, float4* out0, float4* out1,
                                   hipStream_t s) {
     const int n = n0 + n1;

@@ -347,8 +347,7 @@ hipError_t launch_extract(const ExtractView& ev, hipStream_t s);
 struct Affine34 { double m[12]; };   // row-major 3x4 of an Isometry3d matrix
 // pcl::transformPointCloud(cloud, out, Matrix4d) per point: float(m00 x + m01 y + m02 z + m03), double math
 hipError_t launch_transform(const float4* in, int n, Affine34 M, float4* out, hipStream_t s);
-// ... at the pose x[7] (qx qy qz qw tx ty tz) in device memory, its matrix built as the tracker's host code builds it
-hipError_t launch_transform_pose(const float4* in, int n, const double* x, float4* out, hipStream_t s);
+// ... at the pose x[7] (qx qy qz qw tx ty tz) in device memory, its matrix built as the tracker's host code builds it;
 // two clouds in one launch: in[0..n0) -> out0, in[n0..n0+n1) -> out1 (a scan's edge and surf features)
 hipError_t launch_transform_pose2(const float4* in, int n0, int n1, const double* x, float4* out0, float4* out1,
                                   hipStream_t s);
