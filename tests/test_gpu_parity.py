@@ -1234,6 +1234,8 @@ def test_tracker_keyframe_lookahead_exact(lib, oracle_mod, sequence_workload):
     wl = sequence_workload
 
     def run(look):
+        import gc
+        gc.collect()   # earlier tests' unreferenced trackers gone: the lookahead needs its tracker alone on the device
         ctx = _ctx(lib, n_scans=wl.n_scans, max_batch=1)
         tr = lib.Tracker(ctx, window_frames=3, manual_map_update=True, keyframe_lookahead=look)
         ctx.kernel_stats_reset(timing=False)
