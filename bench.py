@@ -89,6 +89,10 @@ def parse(argv=None):
     ap.add_argument("--pairs", type=int, default=1000, help="C5: scan pairs in the whole job")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-lookahead", action="store_true",
+                    help="C3 / C4: trackers without the keyframe lookahead (lmsf_tracker_config.keyframe_lookahead = 0, "
+                         "event-ordered rebuilds) -- for PMC passes, whose serialised dispatches would stall its "
+                         "device-side flag waits")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="C3/C4: extract each scan only when its step starts (default: the next scan's extraction "
                          "runs beside the current registration, lmsf_prefetch_features)")
@@ -875,7 +879,7 @@ def run_streams(args, d):
     apply_options(args, [ctx])
     # keyframe lookahead (lmsf_tracker_config.keyframe_lookahead) only for one stream: with several, the keyframes of
     # lower ranks are appended before this rank's own and would undo it at every step
-    tr = _lib.Tracker(ctx, manual_map_update=True, keyframe_lookahead=(world == 1))
+    tr = _lib.Tracker(ctx, manual_map_update=True, keyframe_lookahead=(world == 1 and not args.no_lookahead))
     T0 = np.eye(4)
     T0[:3, :3] = synth.quat_to_mat(truth[0][:4])
     T0[:3, 3] = truth[0][4:]
@@ -1017,7 +1021,7 @@ def run_dual(args, d):
     max_pts = max(max(len(s) for s in ds.primary), max(len(s) for s in ds.sub))
     ctx = _lib.Context(device=d.gpu, max_batch=1, max_scan_points=max_pts + 64, max_features=max_pts + 64)
     apply_options(args, [ctx])
-    system = dual.DualLidarSystem(ctx, extrinsic=X0)
+    system = dual.DualLidarSystem(ctx, extrinsic=X0, keyframe_lookahead=not args.no_lookahead)
     state = {"i": 0, "poses": []}
 
     def step():

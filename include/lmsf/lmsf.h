@@ -332,7 +332,8 @@ typedef struct {
                                   those features (the tracker's own, lmsf_tracker_add_keyframe_extracted with
                                   lmsf_tracker_pose, or the automatic update) adopts it, anything else undoes it.
                                   Results are identical either way.  0 for callers that append other streams'
-                                  keyframes first (the lookahead would be undone every time) */
+                                  keyframes first (the lookahead would be undone every time), and under tools that
+                                  serialise kernel dispatches (its rebuild is ordered by device-side flag waits) */
 } lmsf_tracker_config;
 
 #define LMSF_UPDATE_NONE 0    /* LocalMapUpdataType NO_UPDATA */

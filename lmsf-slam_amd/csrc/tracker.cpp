@@ -206,9 +206,11 @@ bool sole_tracker(const lmsf_tracker* t) {
 #ifndef LMSF_FLAG_SYNC
 #define LMSF_FLAG_SYNC 1
 #endif
+// Only with the keyframe lookahead (flags alone measured neutral), so keyframe_lookahead = 0 also restores plain event
+// ordering -- e.g. under a tool that serialises kernel dispatches, where a spinning wait could hold its producer back.
 bool flag_sync(const lmsf_tracker* t) {
     static const bool on = ab_int("LMSF_FLAG_SYNC", LMSF_FLAG_SYNC) != 0;
-    return on && sole_tracker(t);
+    return on && t->cfg.keyframe_lookahead && sole_tracker(t);
 }
 
 // The fork point: everything enqueued on the context stream so far (the keyframe transforms) before the rebuilds.

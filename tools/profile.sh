@@ -15,7 +15,7 @@ fi
 case $CFG in
   C2) PMC_ARGS="--steps 2 --warmup 1 --streams 1 --batch 256" ;;   # one context of the default launch (2 x 256)
   C5) PMC_ARGS="--steps 1 --warmup 1 --streams 1 --pipeline 1" ;;
-  *)  PMC_ARGS="--steps 6 --warmup 2" ;;
+  *)  PMC_ARGS="--steps 6 --warmup 2 --no-lookahead" ;;   # C3 / C4: PMC passes serialise dispatches (flag waits)
 esac
 PMC_ARGS="$PMC_ARGS ${PMC_EXTRA:-}"   # e.g. C3 / C4: --opt LM_LOOP=0 --no-prefetch (the r04 C3 PMC pass faulted with both on)
 for ctr in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES" "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_CVT GRBM_GUI_ACTIVE"; do
